@@ -1,0 +1,265 @@
+/*
+ * deppy_hip.h — C-ABI of the MI355X-native batched dependency-resolution engine.
+ *
+ * This is the drop-in boundary for the `pkg/sat` hot path of timflannagan/deppy.
+ * The reference path is in-process Go:
+ *
+ *   sat.NewSolver(sat.WithInput(vars), sat.WithTracer(t))   pkg/sat/solve.go:121-146
+ *   (Solver).Solve(ctx) ([]Variable, error)                  pkg/sat/solve.go:32-34, 53-119
+ *
+ * A Go caller (pkg/solver/solver.go:42-47) reaches this library through a thin
+ * cgo shim.  Only plain pointers, sizes and int32/int64 arrays
+ * cross the boundary; no Go pointers are retained and no torch types appear.
+ *
+ * Three layers, each usable on its own:
+ *
+ *   1. Wire format  (dp_wire)  — the reference's []Variable with its
+ *      []Constraint lists, flattened into arrays of string-table indices.
+ *      dp_lower() restates newLitMapping (pkg/sat/lit_mapping.go:40-77) and
+ *      constraint Apply (pkg/sat/constraints.go:54-204) and produces...
+ *
+ *   2. Lowered records (one int32 record per problem, layout below) — the
+ *      format the GPU consumes.  A caller that lowers on its own side (the
+ *      survey's Go-side lowering) can hand records straight to...
+ *
+ *   3. dp_solve / dp_upload+dp_run+dp_download — batched resolution on one or
+ *      more MI355X devices.  One wavefront solves one problem.
+ *
+ * Result statuses map onto the reference's return values:
+ *   DP_SAT        -> ([]Variable in input order, nil)          solve.go:105-110, lit_mapping.go:176-184
+ *   DP_UNSAT      -> (nil, NotSatisfiable{...})                solve.go:114-115, lit_mapping.go:198-207
+ *   DP_INCOMPLETE -> (nil, ErrIncomplete)                       solve.go:14, 118
+ *   DP_ERROR      -> (nil, <error>)                              solve.go:54-61, 113
+ */
+#ifndef DEPPY_HIP_H
+#define DEPPY_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DP_ABI_VERSION 1
+
+/* ------------------------------------------------------------------------ */
+/* 1. Wire format                                                            */
+/* ------------------------------------------------------------------------ */
+
+/* Constraint kinds: pkg/sat/constraints.go:74 (Mandatory), :100 (Prohibited),
+ * :138 (Dependency), :163 (Conflict), :199 (AtMost). */
+enum dp_kind {
+  DP_MANDATORY = 1,
+  DP_PROHIBITED = 2,
+  DP_DEPENDENCY = 3, /* args = candidate identifiers in preference order */
+  DP_CONFLICT = 4,   /* args = exactly one identifier                    */
+  DP_ATMOST = 5      /* args = identifiers; n = bound                     */
+};
+
+/* A batch of independent problems.  Every problem is the []Variable handed to
+ * sat.WithInput (solve.go:133).  Identifiers are byte strings in a shared
+ * string table; they are compared by bytes within one problem. */
+typedef struct dp_wire {
+  int32_t n_problems;
+  const int64_t* prob_var_off; /* [n_problems+1] -> variables          */
+  const int64_t* var_id;       /* [n_vars]   string index of Identifier  */
+  const int64_t* var_con_off;  /* [n_vars+1] -> constraints             */
+  const int32_t* con_kind;     /* [n_cons]   enum dp_kind               */
+  const int32_t* con_n;        /* [n_cons]   AtMost bound (else ignored) */
+  const int64_t* con_arg_off;  /* [n_cons+1] -> con_arg                  */
+  const int64_t* con_arg;      /* [n_args]   string index               */
+  const int64_t* str_off;      /* [n_strs+1] -> str_bytes               */
+  const char* str_bytes;
+  int32_t interned; /* 1: equal bytes <=> equal string index (fast path) */
+} dp_wire;
+
+/* Per-problem lowering outcome (dp_lowered_error). */
+enum dp_lower_err {
+  DP_LOWER_OK = 0,
+  DP_LOWER_DUPLICATE = 1, /* NewSolver error: DuplicateIdentifier, lit_mapping.go:12-16,52-54 */
+  DP_LOWER_LOOKUP = 2     /* Solve error: "%d errors encountered: %s", lit_mapping.go:86,119-128 */
+};
+
+/* ------------------------------------------------------------------------ */
+/* 2. Lowered record (one per problem, int32 words, problem-local indices)   */
+/* ------------------------------------------------------------------------ */
+/*
+ *  Literal encoding: lit = 2*v + neg  (v = variable index in INPUT ORDER,
+ *  neg = 1 for the negated literal).  Card / choice / anchor entries are
+ *  plain variable indices.
+ *
+ *  Rows: clause rows 0..nc-1 then card rows nc..nc+nk-1 (one "row id" space).
+ *  Every row carries an identity id in 0..nid-1.  An identity is one assumed
+ *  constraint literal of the reference (constraints[m], lit_mapping.go:69-72):
+ *  constraints whose gate literal coincides share one identity and one set of
+ *  rows; NotSatisfiable reports identities.
+ *
+ *  header[DP_H_SIZE], then, in this order:
+ *    clause_off[nc+1]      offsets into clause_lits (relative)
+ *    clause_lits[ncl]
+ *    clause_id[nc]
+ *    card_off[nk+1]        offsets into card_lits (relative)
+ *    card_lits[nkl]        variable indices, duplicates kept (multiplicity)
+ *    card_bound[nk]        at most card_bound[k] of the positions are true
+ *    card_id[nk]
+ *    var_choice_off[nv+1]  choice rows of variable v: [var_choice_off[v], var_choice_off[v+1])
+ *    choice_off[nch+1]     offsets into choice_lits (relative)
+ *    choice_lits[nchl]     candidate variables in preference order (constraint.Order(), search.go:60-69)
+ *    anchors[na]           variables with a Mandatory constraint, input order (lit_mapping.go:163-174)
+ */
+#define DP_REC_MAGIC 0x31525044 /* "DPR1" little-endian */
+enum dp_rec_header {
+  DP_H_MAGIC = 0,
+  DP_H_NV = 1,
+  DP_H_NC = 2,
+  DP_H_NK = 3,
+  DP_H_NCH = 4,
+  DP_H_NA = 5,
+  DP_H_NID = 6,
+  DP_H_NCL = 7,
+  DP_H_NKL = 8,
+  DP_H_NCHL = 9,
+  DP_H_WORDS = 10, /* total record length in int32 words, header included */
+  DP_H_SIZE = 16
+};
+
+/* Offsets (in int32 words from the record start) of each array. */
+typedef struct dp_rec_layout {
+  int32_t clause_off, clause_lits, clause_id;
+  int32_t card_off, card_lits, card_bound, card_id;
+  int32_t var_choice_off, choice_off, choice_lits, anchors;
+  int32_t words;
+} dp_rec_layout;
+
+static inline dp_rec_layout dp_rec_layout_of(const int32_t* h) {
+  dp_rec_layout L;
+  int32_t o = DP_H_SIZE;
+  L.clause_off = o;     o += h[DP_H_NC] + 1;
+  L.clause_lits = o;    o += h[DP_H_NCL];
+  L.clause_id = o;      o += h[DP_H_NC];
+  L.card_off = o;       o += h[DP_H_NK] + 1;
+  L.card_lits = o;      o += h[DP_H_NKL];
+  L.card_bound = o;     o += h[DP_H_NK];
+  L.card_id = o;        o += h[DP_H_NK];
+  L.var_choice_off = o; o += h[DP_H_NV] + 1;
+  L.choice_off = o;     o += h[DP_H_NCH] + 1;
+  L.choice_lits = o;    o += h[DP_H_NCHL];
+  L.anchors = o;        o += h[DP_H_NA];
+  L.words = o;
+  return L;
+}
+
+/* Validate one record (bounds of every index).  Returns 0 if well formed. */
+int dp_rec_validate(const int32_t* rec, int64_t words);
+
+/* ------------------------------------------------------------------------ */
+/* Lowering: wire -> records                                                  */
+/* ------------------------------------------------------------------------ */
+
+typedef struct dp_lowered dp_lowered; /* host-owned, opaque */
+
+/* Lower a wire batch (restates newLitMapping, lit_mapping.go:40-77).  Never
+ * fails per problem: DuplicateIdentifier / lookup errors are recorded per
+ * problem (dp_lowered_error) and such problems get an empty record.
+ * Returns 0, or -1 on malformed input (text in dp_last_global_error()). */
+int dp_lower(const dp_wire* wire, dp_lowered** out);
+void dp_lowered_free(dp_lowered* lw);
+int32_t dp_lowered_num_problems(const dp_lowered* lw);
+const int64_t* dp_lowered_rec_off(const dp_lowered* lw); /* [P+1] */
+const int32_t* dp_lowered_rec(const dp_lowered* lw);
+/* Identity -> reported AppliedConstraint (last writer, lit_mapping.go:69-72):
+ * ident_var[ident_off[p] + i] = variable index, ident_con[...] = index of the
+ * constraint in that variable's Constraints(). */
+const int64_t* dp_lowered_ident_off(const dp_lowered* lw); /* [P+1] */
+const int32_t* dp_lowered_ident_var(const dp_lowered* lw);
+const int32_t* dp_lowered_ident_con(const dp_lowered* lw);
+/* enum dp_lower_err; *msg (may be NULL) receives the reference's error text. */
+int32_t dp_lowered_error(const dp_lowered* lw, int32_t p, const char** msg);
+
+/* ------------------------------------------------------------------------ */
+/* 3. Solving                                                                 */
+/* ------------------------------------------------------------------------ */
+
+enum dp_status { DP_SAT = 1, DP_UNSAT = -1, DP_INCOMPLETE = 0, DP_ERROR = -2 };
+
+/* Per-problem flag bits (class mix). */
+enum dp_flag {
+  DP_F_SEARCH_SKIPPED = 1 << 0, /* base Test returned 1 (solve.go:80)                  */
+  DP_F_CLASS_B = 1 << 1,        /* an exhausted choice was guessed (A.6.3): gini-unpinned */
+  DP_F_SOLVE_UNSAT = 1 << 2,    /* search Solve() returned -1 at least once              */
+  DP_F_EPILOGUE = 1 << 3,       /* SAT epilogue had extras to minimise (solve.go:86-110) */
+  DP_F_BASE_UNSAT = 1 << 4,     /* base Test returned -1                                 */
+  DP_F_CORE_BUDGET = 1 << 5,    /* core not fully minimised within the step budget        */
+  DP_F_BUDGET = 1 << 6,         /* step budget exhausted -> DP_INCOMPLETE                 */
+  DP_F_TOO_LARGE = 1 << 7       /* record does not fit the device path                    */
+};
+
+typedef struct dp_opts {
+  int32_t first_device; /* HIP device ordinal of the first device used     */
+  int32_t n_devices;    /* 0 = every visible device from first_device       */
+  int64_t step_budget;  /* per-problem budget (BCP invocations); 0 = default */
+  int32_t flags;        /* reserved, 0                                      */
+} dp_opts;
+
+typedef struct dp_ctx dp_ctx;
+
+/* Host-side batch of lowered records (caller memory, not retained). */
+typedef struct dp_batch {
+  int32_t n_problems;
+  const int64_t* rec_off; /* [n_problems+1] word offsets into rec */
+  const int32_t* rec;
+} dp_batch;
+
+/* Caller-allocated results.  Sizes come from dp_result_layout(). */
+typedef struct dp_result {
+  int8_t* status;            /* [P] enum dp_status                                  */
+  int32_t* flags;            /* [P] enum dp_flag bits                               */
+  uint32_t* installed;       /* bitmap, ceil(nv/32) words per problem (input order) */
+  const int64_t* inst_off;   /* [P+1] word offsets into installed                   */
+  int32_t* core;             /* identities of the NotSatisfiable explanation        */
+  const int64_t* core_off;   /* [P+1] capacity offsets (nid per problem)            */
+  int32_t* core_len;         /* [P]                                                 */
+  int64_t* steps;            /* [P] BCP invocations used (may be NULL)              */
+} dp_result;
+
+/* Fill inst_off[P+1] and core_off[P+1] for a batch.  Returns 0 or -1. */
+int dp_result_layout(const dp_batch* b, int64_t* inst_off, int64_t* core_off);
+
+/* Create a context bound to MI355X device(s).  Returns NULL when no usable
+ * gfx950 device exists (text in dp_last_global_error()); there is no CPU path. */
+dp_ctx* dp_create(const dp_opts* opts);
+void dp_destroy(dp_ctx* ctx);
+const char* dp_last_error(const dp_ctx* ctx);
+const char* dp_last_global_error(void);
+int32_t dp_num_devices(const dp_ctx* ctx);
+
+/* Synchronous batch solve: H2D, kernel(s), D2H.  Returns 0, or a negative
+ * whole-batch error (text in dp_last_error); per-problem outcomes in res. */
+int dp_solve(dp_ctx* ctx, const dp_batch* b, dp_result* res);
+
+/* Device-resident form (benchmarks, pipelines): the batch is partitioned over
+ * the context's devices and copied once; dp_run solves it in place. */
+typedef struct dp_resident dp_resident;
+int dp_upload(dp_ctx* ctx, const dp_batch* b, dp_resident** out);
+int dp_run(dp_ctx* ctx, dp_resident* r);           /* launch + wait; results stay in HBM */
+int dp_download(dp_ctx* ctx, dp_resident* r, dp_result* res);
+void dp_resident_free(dp_ctx* ctx, dp_resident* r);
+/* Device time of the solve kernel(s) of the last dp_run/dp_solve, measured with
+ * HIP events on the launch stream (max over devices). */
+int dp_last_kernel_ms(const dp_ctx* ctx, double* ms);
+
+/* ------------------------------------------------------------------------ */
+/* Synthetic catalogs (SURVEY.md §8(d) generator; bench/test tooling)         */
+/* ------------------------------------------------------------------------ */
+
+/* Configurations of BASELINE.json: 2 = ~200-entity catalogs, 3 = small
+ * (P~U{4..12}), 5 = mixed-size UNSAT-heavy.  seed_i = base_seed + i. */
+typedef struct dp_gen dp_gen; /* owns a dp_wire and its arrays */
+dp_gen* dp_gen_catalogs(int32_t config, int32_t n_problems, uint64_t base_seed);
+const dp_wire* dp_gen_wire(const dp_gen* g);
+void dp_gen_free(dp_gen* g);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DEPPY_HIP_H */

@@ -1,0 +1,829 @@
+/*
+ * sat_oracle.c — CPU restatement of deppy's pkg/sat solve path.
+ *
+ * TEST INFRASTRUCTURE (see sat_oracle.h).  Plain C, single problem per call,
+ * sequential.  The HIP kernel (deppy_amd/csrc/solve_kernel.hip) computes the
+ * same function with one wavefront per problem; tests require bit-identical
+ * status / installed set / core / steps.
+ *
+ * Semantics:
+ *
+ *  Unit propagation ("BCP", gini Test) is run in synchronous rounds: every row
+ *  watched by a literal assigned in round t is evaluated against the
+ *  assignment as it stood at the start of round t+1; implications are
+ *  committed together.  The reason of a variable is the lowest row id that
+ *  implied it; the reported conflict of a round is the lowest conflicting row,
+ *  else the lowest variable implied both ways.  The fixpoint / conflict verdict
+ *  equals any other unit-propagation schedule; fixing the schedule makes
+ *  reasons (and therefore cores) deterministic.
+ *
+ *  AtMost rows propagate by counting (generalised arc consistency, the
+ *  propagation strength of the sorting network gini.CardSort builds,
+ *  constraints.go:180-186); a variable listed m times counts m.
+ *
+ *  Test(m)   = assume m, propagate; -1 conflict, 1 all variables assigned, else 0.
+ *  Untest()  = truncate the trail to the scope mark; result of the restored scope.
+ *  Solve()   = complete search under the open scopes (dpll below).
+ */
+#include "sat_oracle.h"
+
+#include "../include/deppy_hip.h"
+
+#include <limits.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define INF INT32_MAX
+#define R_DECISION (-1) /* assumption / guess / decision: no reason row */
+#define R_EXTRA (-2)    /* epilogue cardinality bound over the extras    */
+
+enum { CK_NONE = 0, CK_ROW, CK_VAR, CK_ASSUME, CK_EXTRA };
+
+typedef struct {
+  int nv, nc, nk, nch, na, nid, nrows;
+  const int32_t *clause_off, *clause_lits, *clause_id;
+  const int32_t *card_off, *card_lits, *card_bound, *card_id;
+  const int32_t *var_choice_off, *choice_off, *choice_lits, *anchors;
+} prob_t;
+
+typedef struct search_s search_t;
+
+typedef struct {
+  prob_t p;
+  /* watch lists: rows to evaluate when literal l becomes TRUE */
+  int32_t *w_off, *w;
+  /* assignment */
+  int8_t* val; /* 0 unassigned, 1 true, -1 false */
+  int32_t *reason, *rnd, *trail;
+  int32_t tlen, qhead, round;
+  /* per-round implication scratch */
+  int32_t *imp_pos, *imp_neg, *touched;
+  int32_t ntouched;
+  /* row filter (core refutations) */
+  const uint8_t* enabled;
+  /* epilogue cardinality bound over extras */
+  int extra_mode, extra_w;
+  uint8_t* is_extra;
+  /* last conflict */
+  int ck, c_row, c_var, c_rp, c_rn;
+  /* budget */
+  int64_t steps, budget;
+  int budget_hit;
+  /* conflict analysis */
+  uint8_t *seen, *used;
+  int32_t* work;
+  int32_t nwork;
+  int collect;
+  /* search */
+  uint8_t* inS;
+  uint32_t* model;
+  int model_valid;
+  /* dpll decision stack */
+  int32_t *d_lit, *d_mark;
+  uint8_t* d_flip;
+} st_t;
+
+/* ------------------------------------------------------------------ */
+/* record parsing + watch lists                                        */
+/* ------------------------------------------------------------------ */
+
+static void parse(prob_t* p, const int32_t* rec) {
+  dp_rec_layout L = dp_rec_layout_of(rec);
+  p->nv = rec[DP_H_NV];
+  p->nc = rec[DP_H_NC];
+  p->nk = rec[DP_H_NK];
+  p->nch = rec[DP_H_NCH];
+  p->na = rec[DP_H_NA];
+  p->nid = rec[DP_H_NID];
+  p->nrows = p->nc + p->nk;
+  p->clause_off = rec + L.clause_off;
+  p->clause_lits = rec + L.clause_lits;
+  p->clause_id = rec + L.clause_id;
+  p->card_off = rec + L.card_off;
+  p->card_lits = rec + L.card_lits;
+  p->card_bound = rec + L.card_bound;
+  p->card_id = rec + L.card_id;
+  p->var_choice_off = rec + L.var_choice_off;
+  p->choice_off = rec + L.choice_off;
+  p->choice_lits = rec + L.choice_lits;
+  p->anchors = rec + L.anchors;
+}
+
+static int row_ident(const prob_t* p, int r) {
+  return r < p->nc ? p->clause_id[r] : p->card_id[r - p->nc];
+}
+
+static void* xcalloc(size_t n, size_t sz) { return calloc(n ? n : 1, sz); }
+
+static int st_init(st_t* s, const int32_t* rec) {
+  memset(s, 0, sizeof(*s));
+  parse(&s->p, rec);
+  const prob_t* p = &s->p;
+  int nl = 2 * p->nv;
+  s->w_off = xcalloc((size_t)nl + 1, sizeof(int32_t));
+  /* count: clause literal x in row r -> watched by ~x; card var v -> by +v */
+  for (int r = 0; r < p->nc; ++r)
+    for (int j = p->clause_off[r]; j < p->clause_off[r + 1]; ++j) s->w_off[(p->clause_lits[j] ^ 1) + 1]++;
+  for (int k = 0; k < p->nk; ++k)
+    for (int j = p->card_off[k]; j < p->card_off[k + 1]; ++j) s->w_off[2 * p->card_lits[j] + 1]++;
+  for (int l = 0; l < nl; ++l) s->w_off[l + 1] += s->w_off[l];
+  s->w = xcalloc((size_t)s->w_off[nl], sizeof(int32_t));
+  int32_t* cur = xcalloc((size_t)nl, sizeof(int32_t));
+  for (int l = 0; l < nl; ++l) cur[l] = s->w_off[l];
+  for (int r = 0; r < p->nc; ++r)
+    for (int j = p->clause_off[r]; j < p->clause_off[r + 1]; ++j) s->w[cur[p->clause_lits[j] ^ 1]++] = r;
+  for (int k = 0; k < p->nk; ++k)
+    for (int j = p->card_off[k]; j < p->card_off[k + 1]; ++j) s->w[cur[2 * p->card_lits[j]]++] = p->nc + k;
+  free(cur);
+  int nv = p->nv;
+  s->val = xcalloc((size_t)nv, 1);
+  s->reason = xcalloc((size_t)nv, sizeof(int32_t));
+  s->rnd = xcalloc((size_t)nv, sizeof(int32_t));
+  s->trail = xcalloc((size_t)nv, sizeof(int32_t));
+  s->imp_pos = xcalloc((size_t)nv, sizeof(int32_t));
+  s->imp_neg = xcalloc((size_t)nv, sizeof(int32_t));
+  s->touched = xcalloc((size_t)nv, sizeof(int32_t));
+  for (int v = 0; v < nv; ++v) s->imp_pos[v] = s->imp_neg[v] = INF;
+  s->is_extra = xcalloc((size_t)nv, 1);
+  s->seen = xcalloc((size_t)nv, 1);
+  s->used = xcalloc((size_t)p->nid, 1);
+  s->work = xcalloc((size_t)nv, sizeof(int32_t));
+  s->inS = xcalloc((size_t)nv, 1);
+  s->model = xcalloc((size_t)(nv + 31) / 32, sizeof(uint32_t));
+  s->d_lit = xcalloc((size_t)nv, sizeof(int32_t));
+  s->d_mark = xcalloc((size_t)nv, sizeof(int32_t));
+  s->d_flip = xcalloc((size_t)nv, 1);
+  return 0;
+}
+
+static void st_free(st_t* s) {
+  free(s->w_off); free(s->w); free(s->val); free(s->reason); free(s->rnd); free(s->trail);
+  free(s->imp_pos); free(s->imp_neg); free(s->touched); free(s->is_extra); free(s->seen);
+  free(s->used); free(s->work); free(s->inS); free(s->model); free(s->d_lit); free(s->d_mark);
+  free(s->d_flip);
+}
+
+/* ------------------------------------------------------------------ */
+/* unit propagation                                                    */
+/* ------------------------------------------------------------------ */
+
+static inline int row_on(const st_t* s, int r) {
+  return !s->enabled || s->enabled[row_ident(&s->p, r)];
+}
+
+static inline int lit_val(const st_t* s, int l) {
+  int x = s->val[l >> 1];
+  return (l & 1) ? -x : x;
+}
+
+static inline void note(st_t* s, int l, int r) {
+  int v = l >> 1;
+  if (s->imp_pos[v] == INF && s->imp_neg[v] == INF) s->touched[s->ntouched++] = v;
+  if (l & 1) {
+    if (r < s->imp_neg[v]) s->imp_neg[v] = r;
+  } else {
+    if (r < s->imp_pos[v]) s->imp_pos[v] = r;
+  }
+}
+
+/* Evaluate one row against the current assignment (start-of-round snapshot:
+ * nothing is committed while a round is being evaluated). */
+static void eval_row(st_t* s, int r, int* crow) {
+  const prob_t* p = &s->p;
+  if (r < p->nc) {
+    int a = p->clause_off[r], b = p->clause_off[r + 1], nun = 0, ul = -1;
+    for (int j = a; j < b; ++j) {
+      int x = lit_val(s, p->clause_lits[j]);
+      if (x > 0) return; /* satisfied */
+      if (x == 0) { ++nun; ul = p->clause_lits[j]; }
+    }
+    if (nun == 0) { if (r < *crow) *crow = r; }
+    else if (nun == 1) note(s, ul, r);
+  } else {
+    int k = r - p->nc, a = p->card_off[k], b = p->card_off[k + 1], cnt = 0, nun = 0;
+    for (int j = a; j < b; ++j) {
+      int x = s->val[p->card_lits[j]];
+      cnt += (x > 0);
+      nun += (x == 0);
+    }
+    int bound = p->card_bound[k];
+    if (cnt > bound) { if (r < *crow) *crow = r; }
+    else if (nun > 0) {
+      /* a variable repeated m times is a run of m equal positions; it is
+       * forced false once cnt + m exceeds the bound */
+      for (int j = a; j < b;) {
+        int v = p->card_lits[j], e = j + 1;
+        while (e < b && p->card_lits[e] == v) ++e;
+        if (s->val[v] == 0 && cnt + (e - j) > bound) note(s, 2 * v + 1, r);
+        j = e;
+      }
+    }
+  }
+}
+
+static inline void assign(st_t* s, int l, int reason, int rd) {
+  int v = l >> 1;
+  s->val[v] = (l & 1) ? -1 : 1;
+  s->reason[v] = reason;
+  s->rnd[v] = rd;
+  s->trail[s->tlen++] = l;
+}
+
+static void clear_touched(st_t* s) {
+  for (int i = 0; i < s->ntouched; ++i) s->imp_pos[s->touched[i]] = s->imp_neg[s->touched[i]] = INF;
+  s->ntouched = 0;
+}
+
+/* Commit the implications of round rd, or report its conflict. */
+static int finish_round(st_t* s, int rd, int crow) {
+  if (crow != INF) {
+    clear_touched(s);
+    s->ck = CK_ROW; s->c_row = crow;
+    return -1;
+  }
+  int cvar = INF;
+  for (int i = 0; i < s->ntouched; ++i) {
+    int v = s->touched[i];
+    if (s->imp_pos[v] != INF && s->imp_neg[v] != INF && v < cvar) cvar = v;
+  }
+  if (cvar != INF) {
+    s->ck = CK_VAR; s->c_var = cvar; s->c_rp = s->imp_pos[cvar]; s->c_rn = s->imp_neg[cvar];
+    s->c_row = rd; /* round of the conflict, bounds card antecedents */
+    clear_touched(s);
+    return -1;
+  }
+  for (int i = 0; i < s->ntouched; ++i) {
+    int v = s->touched[i];
+    if (s->imp_pos[v] != INF) assign(s, 2 * v, s->imp_pos[v], rd);
+    else assign(s, 2 * v + 1, s->imp_neg[v], rd);
+  }
+  clear_touched(s);
+  return 0;
+}
+
+/* Epilogue bound "at most extra_w of the extras are true" (the Leq(w)
+ * assumption over CardinalityConstrainer, solve.go:105-107). */
+static int extra_check(st_t* s) {
+  int cnt = 0, nun = 0;
+  for (int v = 0; v < s->p.nv; ++v)
+    if (s->is_extra[v]) { cnt += (s->val[v] > 0); nun += (s->val[v] == 0); }
+  if (cnt > s->extra_w) { s->ck = CK_EXTRA; return -1; }
+  if (cnt == s->extra_w && nun > 0) {
+    int rd = ++s->round;
+    for (int v = 0; v < s->p.nv; ++v)
+      if (s->is_extra[v] && s->val[v] == 0) assign(s, 2 * v + 1, R_EXTRA, rd);
+    return 1;
+  }
+  return 0;
+}
+
+static int propagate(st_t* s) {
+  for (;;) {
+    if (s->qhead == s->tlen) {
+      if (s->extra_mode) {
+        int r = extra_check(s);
+        if (r < 0) return -1;
+        if (r > 0) continue;
+      }
+      return s->tlen == s->p.nv ? 1 : 0;
+    }
+    int lo = s->qhead, hi = s->tlen, rd = ++s->round, crow = INF;
+    s->qhead = hi;
+    for (int i = lo; i < hi; ++i) {
+      int l = s->trail[i];
+      for (int k = s->w_off[l]; k < s->w_off[l + 1]; ++k)
+        if (row_on(s, s->w[k])) eval_row(s, s->w[k], &crow);
+    }
+    if (finish_round(s, rd, crow) < 0) return -1;
+  }
+}
+
+/* The base scope (solve.go:63-79): every constraint row is hard and every
+ * anchor is assumed; one round evaluates every (enabled) row. */
+static int base_propagate(st_t* s) {
+  int rd = ++s->round, crow = INF;
+  for (int r = 0; r < s->p.nrows; ++r)
+    if (row_on(s, r)) eval_row(s, r, &crow);
+  if (finish_round(s, rd, crow) < 0) return -1;
+  return propagate(s);
+}
+
+static void truncate_to(st_t* s, int mark) {
+  while (s->tlen > mark) s->val[s->trail[--s->tlen] >> 1] = 0;
+  s->qhead = s->tlen;
+}
+
+/* gini Assume(m) + Test(): one scope, one BCP. */
+static int test_assume(st_t* s, int l) {
+  s->steps++;
+  int x = lit_val(s, l);
+  if (x > 0) return propagate(s);
+  if (x < 0) { s->ck = CK_ASSUME; s->c_var = l >> 1; return -1; }
+  assign(s, l, R_DECISION, ++s->round);
+  return propagate(s);
+}
+
+/* ------------------------------------------------------------------ */
+/* conflict analysis: identities of the rows a conflict depends on     */
+/* ------------------------------------------------------------------ */
+
+static void push_ante(st_t* s, int r, int u, int bound_rd) {
+  const prob_t* p = &s->p;
+  if (r < 0) return;
+  s->used[row_ident(p, r)] = 1;
+  if (r < p->nc) {
+    for (int j = p->clause_off[r]; j < p->clause_off[r + 1]; ++j) {
+      int v = p->clause_lits[j] >> 1;
+      if (v != u && !s->seen[v]) { s->seen[v] = 1; s->work[s->nwork++] = v; }
+    }
+  } else {
+    int k = r - p->nc;
+    for (int j = p->card_off[k]; j < p->card_off[k + 1]; ++j) {
+      int v = p->card_lits[j];
+      if (v != u && s->val[v] > 0 && s->rnd[v] < bound_rd && !s->seen[v]) {
+        s->seen[v] = 1; s->work[s->nwork++] = v;
+      }
+    }
+  }
+}
+
+static void analyze(st_t* s) {
+  s->nwork = 0;
+  if (s->ck == CK_ROW) push_ante(s, s->c_row, -1, INF);
+  else if (s->ck == CK_VAR) {
+    push_ante(s, s->c_rp, s->c_var, s->c_row);
+    push_ante(s, s->c_rn, s->c_var, s->c_row);
+  } else return;
+  for (int i = 0; i < s->nwork; ++i) {
+    int u = s->work[i];
+    int r = s->reason[u];
+    if (r >= 0) push_ante(s, r, u, s->rnd[u]);
+  }
+  for (int i = 0; i < s->nwork; ++i) s->seen[s->work[i]] = 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* Solve(): complete search under the open scopes                      */
+/* ------------------------------------------------------------------ */
+
+/* Decision literal: the first positive, unassigned literal of the lowest
+ * clause row that the all-false completion of the current assignment
+ * violates; -1 if that completion is a model. */
+static int first_violated(const st_t* s) {
+  const prob_t* p = &s->p;
+  for (int c = 0; c < p->nc; ++c) {
+    if (!row_on(s, c)) continue;
+    int viol = 1, fu = -1;
+    for (int j = p->clause_off[c]; j < p->clause_off[c + 1]; ++j) {
+      int l = p->clause_lits[j], x = s->val[l >> 1];
+      if (l & 1) { if (x != 1) { viol = 0; break; } }
+      else {
+        if (x == 1) { viol = 0; break; }
+        if (x == 0 && fu < 0) fu = l;
+      }
+    }
+    if (viol) return fu;
+  }
+  return -1;
+}
+
+static void save_model(st_t* s) {
+  int nw = (s->p.nv + 31) / 32;
+  memset(s->model, 0, (size_t)nw * 4);
+  for (int v = 0; v < s->p.nv; ++v)
+    if (s->val[v] > 0) s->model[v >> 5] |= 1u << (v & 31);
+  s->model_valid = 1;
+}
+
+enum { R_SAT = 1, R_UNSAT = -1, R_BUDGET = 2 };
+
+/* DPLL from a consistent fixpoint: decide the preferred candidate of the first
+ * violated dependency row true, then false; chronological backtracking.  On
+ * SAT the model is saved and the trail restored to `root`. */
+static int dpll(st_t* s) {
+  int root = s->tlen, nd = 0;
+  for (;;) {
+    int l = first_violated(s);
+    if (l < 0) {
+      save_model(s);
+      truncate_to(s, root);
+      return R_SAT;
+    }
+    if (++s->steps > s->budget) { s->budget_hit = 1; truncate_to(s, root); return R_BUDGET; }
+    s->d_lit[nd] = l; s->d_mark[nd] = s->tlen; s->d_flip[nd] = 0; ++nd;
+    assign(s, l, R_DECISION, ++s->round);
+    int res = propagate(s);
+    while (res < 0) {
+      if (s->collect) analyze(s);
+      while (nd > 0 && s->d_flip[nd - 1]) --nd;
+      if (nd == 0) { truncate_to(s, root); return R_UNSAT; }
+      truncate_to(s, s->d_mark[nd - 1]);
+      s->d_flip[nd - 1] = 1;
+      if (++s->steps > s->budget) { s->budget_hit = 1; truncate_to(s, root); return R_BUDGET; }
+      assign(s, s->d_lit[nd - 1] ^ 1, R_DECISION, ++s->round);
+      res = propagate(s);
+    }
+  }
+}
+
+/* ------------------------------------------------------------------ */
+/* search.Do (pkg/sat/search.go:158-203) over a pluggable inter.S       */
+/* ------------------------------------------------------------------ */
+
+typedef struct {
+  int (*test)(void* u, st_t* s, int lit); /* Assume(lit) + Test() */
+  int (*untest)(void* u, st_t* s, int mark);
+  int (*solve)(void* u, st_t* s);
+  void* u;
+} backend_t;
+
+typedef struct { int32_t list, idx; } choice_t; /* list>=0: choice row; <0: anchor ~list */
+typedef struct { int32_t list, idx, m, children, mark; } guess_t;
+
+struct search_s {
+  choice_t* dq;
+  int cap, head, n;
+  guess_t* g;
+  int ng;
+  int result;
+  int class_b, solve_unsat, last_solve;
+};
+
+static inline int list_len(const prob_t* p, int list) {
+  return list < 0 ? 1 : p->choice_off[list + 1] - p->choice_off[list];
+}
+static inline int list_at(const prob_t* p, int list, int i) {
+  return list < 0 ? ~list : p->choice_lits[p->choice_off[list] + i];
+}
+
+static void dq_push_back(search_t* h, choice_t c) { h->dq[(h->head + h->n++) % h->cap] = c; }
+static void dq_push_front(search_t* h, choice_t c) {
+  h->head = (h->head + h->cap - 1) % h->cap;
+  h->dq[h->head] = c;
+  h->n++;
+}
+static choice_t dq_pop_front(search_t* h) {
+  choice_t c = h->dq[h->head];
+  h->head = (h->head + 1) % h->cap;
+  h->n--;
+  return c;
+}
+static void dq_pop_back(search_t* h) { h->n--; }
+
+/* PushGuess, search.go:34-77 */
+static void push_guess(search_t* h, st_t* s, const backend_t* be) {
+  const prob_t* p = &s->p;
+  choice_t c = dq_pop_front(h);
+  int len = list_len(p, c.list);
+  guess_t g = {c.list, c.idx, -1, 0, s->tlen};
+  if (c.idx < len) g.m = list_at(p, c.list, c.idx);
+  int any = 0;
+  for (int i = 0; i < len; ++i)
+    if (s->inS[list_at(p, c.list, i)]) { any = 1; break; }
+  if (any) g.m = -1;
+  else if (c.idx >= len) h->class_b = 1; /* exhausted choice, SURVEY.md A.6.3 */
+  h->g[h->ng++] = g;
+  if (g.m < 0) return;
+  for (int r = p->var_choice_off[g.m]; r < p->var_choice_off[g.m + 1]; ++r) {
+    h->g[h->ng - 1].children++;
+    dq_push_back(h, (choice_t){r, 0});
+  }
+  s->inS[g.m] = 1;
+  h->result = be->test(be->u, s, 2 * g.m);
+  h->last_solve = 0;
+}
+
+/* PopGuess, search.go:79-98 */
+static void pop_guess(search_t* h, st_t* s, const backend_t* be) {
+  guess_t g = h->g[--h->ng];
+  if (g.m >= 0) {
+    s->inS[g.m] = 0;
+    h->result = be->untest(be->u, s, g.mark);
+    h->last_solve = 0;
+  }
+  for (int i = 0; i < g.children; ++i) dq_pop_back(h);
+  dq_push_front(h, (choice_t){g.list, g.idx + (g.m >= 0)});
+}
+
+/* Do, search.go:158-203.  Returns the result; leaves the guessed variables of
+ * the final stack (search.Lits()) in lits[0..*nlits) and pops every guess. */
+static int search_do(search_t* h, st_t* s, const backend_t* be, int32_t* lits, int32_t* nlits) {
+  const prob_t* p = &s->p;
+  h->cap = p->na + p->nch + 2;
+  h->dq = xcalloc((size_t)h->cap, sizeof(choice_t));
+  h->g = xcalloc((size_t)h->cap, sizeof(guess_t));
+  h->head = h->n = h->ng = 0;
+  h->result = 0;
+  for (int i = 0; i < p->na; ++i) dq_push_back(h, (choice_t){~p->anchors[i], 0});
+  for (;;) {
+    if (h->n == 0 && h->result == 0) {
+      h->result = be->solve(be->u, s);
+      h->last_solve = (h->result == 1);
+      if (h->result == R_BUDGET) break;
+      if (h->result < 0) h->solve_unsat = 1;
+    }
+    if (h->result < 0) {
+      /* tracer.Trace(h) would run here (search.go:173) */
+      if (h->ng == 0) break;
+      pop_guess(h, s, be);
+      continue;
+    }
+    if (h->n == 0) break;
+    push_guess(h, s, be);
+    if (s->budget_hit) { h->result = R_BUDGET; break; }
+  }
+  /* Value() after a Test()==1 ending reads the full assignment of that scope */
+  if (h->result == 1 && !h->last_solve) save_model(s);
+  int k = 0;
+  for (int i = 0; i < h->ng; ++i)
+    if (h->g[i].m >= 0) lits[k++] = h->g[i].m;
+  *nlits = k;
+  int result = h->result;
+  if (result != R_BUDGET)
+    while (h->ng > 0) pop_guess(h, s, be);
+  free(h->dq);
+  free(h->g);
+  return result;
+}
+
+/* the real backend: our BCP */
+static int be_test(void* u, st_t* s, int lit) {
+  (void)u;
+  if (s->steps + 1 > s->budget) { s->budget_hit = 1; return 0; }
+  return test_assume(s, lit);
+}
+static int be_untest(void* u, st_t* s, int mark) {
+  (void)u;
+  truncate_to(s, mark);
+  return s->tlen == s->p.nv ? 1 : 0;
+}
+static int be_solve(void* u, st_t* s) {
+  (void)u;
+  int r = dpll(s);
+  if (r == R_SAT) return 1;
+  if (r == R_UNSAT) return -1;
+  return R_BUDGET;
+}
+
+/* ------------------------------------------------------------------ */
+/* NotSatisfiable: deletion-minimal core over identities               */
+/* ------------------------------------------------------------------ */
+
+static void reset_all(st_t* s) {
+  truncate_to(s, 0);
+  s->tlen = s->qhead = 0;
+}
+
+/* Complete refutation of the enabled identities; on UNSAT s->used holds the
+ * identities of every conflict the refutation met. */
+static int refute(st_t* s, const uint8_t* en) {
+  reset_all(s);
+  s->enabled = en;
+  memset(s->used, 0, (size_t)s->p.nid);
+  s->collect = 1;
+  int r;
+  if (base_propagate(s) < 0) { analyze(s); r = R_UNSAT; }
+  else r = dpll(s);
+  s->collect = 0;
+  reset_all(s);
+  s->enabled = NULL;
+  return r;
+}
+
+static int core_extract(st_t* s, int32_t* core, int32_t* flags) {
+  int nid = s->p.nid, len = 0;
+  uint8_t* K = xcalloc((size_t)nid, 1);
+  uint8_t* K2 = xcalloc((size_t)nid, 1);
+  memset(K, 1, (size_t)nid);
+  int64_t saved_steps = s->steps;
+  s->steps = 0; /* the explanation has its own budget */
+  int r = refute(s, K);
+  if (r == R_UNSAT) {
+    memcpy(K, s->used, (size_t)nid);
+    for (int id = 0; id < nid; ++id) {
+      if (!K[id]) continue;
+      memcpy(K2, K, (size_t)nid);
+      K2[id] = 0;
+      r = refute(s, K2);
+      if (r == R_UNSAT) memcpy(K, s->used, (size_t)nid);
+      else if (r == R_BUDGET) { *flags |= DP_F_CORE_BUDGET; break; }
+    }
+    for (int id = 0; id < nid; ++id)
+      if (K[id]) core[len++] = id;
+  } else {
+    *flags |= DP_F_CORE_BUDGET; /* verdict stands; explanation empty */
+  }
+  s->budget_hit = 0;
+  s->steps += saved_steps;
+  free(K);
+  free(K2);
+  return len;
+}
+
+/* ------------------------------------------------------------------ */
+/* SAT epilogue, solve.go:86-110                                        */
+/* ------------------------------------------------------------------ */
+
+static int epilogue(st_t* s, int32_t* flags, uint32_t* installed) {
+  const prob_t* p = &s->p;
+  int nv = p->nv, ne = 0;
+  int nw = (nv + 31) / 32;
+  for (int v = 0; v < nv; ++v) {
+    int mv = (s->model[v >> 5] >> (v & 31)) & 1;
+    s->is_extra[v] = (uint8_t)(!s->inS[v] && mv);
+    ne += s->is_extra[v];
+  }
+  if (ne == 0) {
+    memset(installed, 0, (size_t)nw * 4);
+    for (int v = 0; v < nv; ++v)
+      if (s->inS[v]) installed[v >> 5] |= 1u << (v & 31);
+    return DP_SAT;
+  }
+  *flags |= DP_F_EPILOGUE;
+  /* Untest the base, re-assume constraints + aset + excluded (solve.go:99-104) */
+  reset_all(s);
+  if (base_propagate(s) < 0) return DP_ERROR;
+  int rd = ++s->round;
+  for (int v = 0; v < nv; ++v) {
+    if (s->is_extra[v]) continue;
+    int want = s->inS[v] ? 1 : -1;
+    if (s->val[v] == -want) return DP_ERROR;
+    if (s->val[v] == 0) assign(s, 2 * v + (want < 0), R_DECISION, rd);
+  }
+  if (propagate(s) < 0) return DP_ERROR;
+  int mark = s->tlen, f = 0;
+  for (int v = 0; v < nv; ++v) f += s->is_extra[v] && s->val[v] > 0;
+  s->extra_mode = 1;
+  for (int w = f; w <= ne; ++w) {
+    truncate_to(s, mark);
+    s->extra_w = w;
+    if (propagate(s) < 0) continue;
+    int r = dpll(s);
+    if (r == R_SAT) {
+      s->extra_mode = 0;
+      memcpy(installed, s->model, (size_t)nw * 4);
+      return DP_SAT;
+    }
+    if (r == R_BUDGET) { s->extra_mode = 0; return DP_INCOMPLETE; }
+  }
+  s->extra_mode = 0;
+  return DP_ERROR; /* "unexpected internal error", solve.go:113 */
+}
+
+/* ------------------------------------------------------------------ */
+/* solver.Solve, solve.go:53-119                                        */
+/* ------------------------------------------------------------------ */
+
+int oracle_solve(const int32_t* rec, int64_t budget, int32_t* flags, uint32_t* installed,
+                 int32_t* core, int32_t* core_len, int64_t* steps) {
+  st_t s;
+  st_init(&s, rec);
+  s.budget = budget > 0 ? budget : (1 << 16);
+  int nv = s.p.nv, nw = (nv + 31) / 32;
+  *flags = 0;
+  *core_len = 0;
+  memset(installed, 0, (size_t)nw * 4);
+  int status;
+  int base = base_propagate(&s);
+  if (base < 0) {
+    *flags |= DP_F_BASE_UNSAT;
+    status = DP_UNSAT;
+  } else if (base == 1) {
+    *flags |= DP_F_SEARCH_SKIPPED;
+    save_model(&s);
+    status = epilogue(&s, flags, installed);
+  } else {
+    search_t h;
+    memset(&h, 0, sizeof(h));
+    backend_t be = {be_test, be_untest, be_solve, NULL};
+    int32_t* lits = xcalloc((size_t)nv, sizeof(int32_t));
+    int32_t nl = 0;
+    int r = search_do(&h, &s, &be, lits, &nl);
+    if (h.class_b) *flags |= DP_F_CLASS_B;
+    if (h.solve_unsat) *flags |= DP_F_SOLVE_UNSAT;
+    if (r == R_BUDGET) {
+      *flags |= DP_F_BUDGET;
+      status = DP_INCOMPLETE;
+    } else if (r < 0) {
+      status = DP_UNSAT;
+    } else {
+      memset(s.inS, 0, (size_t)nv);
+      for (int i = 0; i < nl; ++i) s.inS[lits[i]] = 1;
+      status = epilogue(&s, flags, installed);
+      if (status == DP_INCOMPLETE) *flags |= DP_F_BUDGET;
+    }
+    free(lits);
+  }
+  if (status == DP_UNSAT) *core_len = core_extract(&s, core, flags);
+  if (steps) *steps = s.steps;
+  st_free(&s);
+  return status;
+}
+
+int oracle_refute(const int32_t* rec, const uint8_t* enabled, int64_t budget) {
+  st_t s;
+  st_init(&s, rec);
+  s.budget = budget > 0 ? budget : (1 << 20);
+  int r = refute(&s, enabled);
+  st_free(&s);
+  return r == R_UNSAT ? -1 : (r == R_SAT ? 1 : 0);
+}
+
+/* ------------------------------------------------------------------ */
+/* scripted backend (FakeS)                                            */
+/* ------------------------------------------------------------------ */
+
+typedef struct {
+  const int32_t *tr, *ur;
+  int nt, nu, it, iu, depth;
+} script_t;
+
+static int sc_test(void* u, st_t* s, int lit) {
+  (void)s; (void)lit;
+  script_t* c = u;
+  c->depth++;
+  int r = c->it < c->nt ? c->tr[c->it] : 0;
+  c->it++;
+  return r;
+}
+static int sc_untest(void* u, st_t* s, int mark) {
+  (void)s; (void)mark;
+  script_t* c = u;
+  c->depth--;
+  int r = c->iu < c->nu ? c->ur[c->iu] : 0;
+  c->iu++;
+  return r;
+}
+static int sc_solve(void* u, st_t* s) { (void)u; (void)s; return 0; }
+
+int oracle_search_scripted(const int32_t* rec, const int32_t* test_ret, int32_t n_test,
+                           const int32_t* untest_ret, int32_t n_untest, int32_t* out_result,
+                           int32_t* out_lits, int32_t* out_nlits, int32_t* out_depth) {
+  st_t s;
+  st_init(&s, rec);
+  s.budget = 1 << 20;
+  script_t sc = {test_ret, untest_ret, n_test, n_untest, 0, 0, 0};
+  backend_t be = {sc_test, sc_untest, sc_solve, &sc};
+  search_t h;
+  memset(&h, 0, sizeof(h));
+  *out_result = search_do(&h, &s, &be, out_lits, out_nlits);
+  *out_depth = sc.depth;
+  st_free(&s);
+  return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* batch (CPU baseline)                                                 */
+/* ------------------------------------------------------------------ */
+
+typedef struct {
+  int32_t n;
+  const int64_t* rec_off;
+  const int32_t* rec;
+  int64_t budget;
+  int8_t* status;
+  int32_t* flags;
+  uint32_t* installed;
+  const int64_t* inst_off;
+  int32_t* core;
+  const int64_t* core_off;
+  int32_t* core_len;
+  int64_t* steps;
+  int32_t next; /* shared work counter */
+  pthread_mutex_t mu;
+} batch_t;
+
+static void* batch_worker(void* arg) {
+  batch_t* b = arg;
+  for (;;) {
+    pthread_mutex_lock(&b->mu);
+    int i0 = b->next;
+    b->next += 16;
+    pthread_mutex_unlock(&b->mu);
+    if (i0 >= b->n) break;
+    int i1 = i0 + 16 < b->n ? i0 + 16 : b->n;
+    for (int i = i0; i < i1; ++i) {
+      int64_t st = 0;
+      b->status[i] = (int8_t)oracle_solve(b->rec + b->rec_off[i], b->budget, &b->flags[i],
+                                          b->installed + b->inst_off[i], b->core + b->core_off[i],
+                                          &b->core_len[i], &st);
+      if (b->steps) b->steps[i] = st;
+    }
+  }
+  return NULL;
+}
+
+int oracle_solve_batch(int32_t n, const int64_t* rec_off, const int32_t* rec, int64_t budget,
+                       int32_t nthreads, int8_t* status, int32_t* flags, uint32_t* installed,
+                       const int64_t* inst_off, int32_t* core, const int64_t* core_off,
+                       int32_t* core_len, int64_t* steps) {
+  batch_t b = {n, rec_off, rec, budget, status, flags, installed, inst_off, core, core_off,
+               core_len, steps, 0, PTHREAD_MUTEX_INITIALIZER};
+  if (nthreads < 1) nthreads = 1;
+  pthread_t* th = xcalloc((size_t)nthreads, sizeof(pthread_t));
+  for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, batch_worker, &b);
+  for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+  free(th);
+  return 0;
+}
