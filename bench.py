@@ -1,0 +1,188 @@
+"""Benchmark: batched pkg/sat resolution on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+One step = one pass of the solve kernel over one batch of BASELINE config 2:
+10,000 synthetic operator catalogs (~200 bundle entities, Dependency +
+Conflict + AtMost; SURVEY.md §8(d) generator), resident in HBM when the timed
+region starts.  With N > 1 (torchrun, one process per GPU) every rank solves
+its own 10,000 catalogs (distinct seeds): weak scaling, no collective on the
+data path (torch.distributed is used only for the barrier and the max-over-
+ranks of the timing).
+
+Rank 0 prints one JSON line.  `value` = resolutions/s over all ranks.
+`roofline.achieved` = compulsory bytes of the batch (input records + outputs,
+DESIGN.md §Measurement) / the solve kernel's mean device time (HIP events on
+its stream).  `cpu_baseline` = the CPU restatement (oracle/, "port") on the
+host, on the same batch repeated for a bounded time.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from deppy_amd import _lib  # noqa: E402
+
+METRIC = "resolutions/sec (node) on synthetic catalogs at 1/2/4/8 GPUs; BCP HBM GB/s"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def lowered_config(config, n, seed):
+    w = _lib.generate(config, n, seed)
+    wa = _lib.WireArrays(**{k: w[k] for k in (
+        "prob_var_off", "var_id", "var_con_off", "con_kind", "con_n", "con_arg_off", "con_arg",
+        "str_off")}, str_bytes=w["str_bytes"].tobytes())
+    t0 = time.perf_counter()
+    lw = _lib.Lowered(wa)
+    t_lower = time.perf_counter() - t0
+    return lw, t_lower
+
+
+def compulsory_bytes(lw, res) -> int:
+    """Input record words + every output word the kernel writes."""
+    rec_bytes = 4 * int(lw.rec_off[-1])
+    n = lw.n
+    out = n * (1 + 4 + 4 + 8)  # status, flags, core_len, steps
+    out += 4 * int(res["inst_off"][-1])  # installed bitmaps
+    out += 4 * int(res["core_len"].sum())  # cores
+    return rec_bytes + out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--problems", type=int, default=10000)
+    ap.add_argument("--seed", type=int, default=1000)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--pmc-json", default=None,
+                    help="per-dispatch HBM bytes measured by a separate rocprofv3 --pmc pass")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl")
+        dist = tdist
+
+    def barrier_max(x: float) -> float:
+        if dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    lw, t_lower = lowered_config(args.config, args.problems, args.seed + rank * args.problems)
+    ctx = _lib.Context(local, 1)
+
+    # PCIe-inclusive single pass (host records -> host results), reported only
+    t0 = time.perf_counter()
+    ctx.solve(lw.rec_off, lw.rec)
+    t_pcie = time.perf_counter() - t0
+
+    r = ctx.upload(lw.rec_off, lw.rec)
+    for _ in range(args.warmup):
+        r.run()
+    if dist is not None:
+        dist.barrier()
+    kms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        r.run()  # launch(es) + hipStreamSynchronize
+        kms.append(ctx.last_kernel_ms())
+    t1 = time.perf_counter()
+    if dist is not None:
+        dist.barrier()
+    elapsed = barrier_max(t1 - t0)
+    res = r.download()
+    r.free()
+
+    total = world * args.problems * args.steps
+    value = total / elapsed
+    st = res["status"]
+    kernel_ms = float(np.mean(kms))
+    nbytes = compulsory_bytes(lw, res)
+    achieved = nbytes / (kernel_ms * 1e-3) / 1e9
+
+    traffic = None
+    if args.pmc_json and os.path.exists(args.pmc_json):
+        with open(args.pmc_json) as f:
+            traffic = json.load(f).get("hbm_bytes_per_dispatch")
+
+    line = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "resolutions/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic",
+        "config": {"workload": "config2: %d synthetic operator catalogs per GPU (P=40 packages,"
+                               " ~240 variables; Dependency+Conflict+AtMost), one wavefront per"
+                               " catalog" % args.problems if args.config == 2 else
+                               "config%d: %d catalogs per GPU" % (args.config, args.problems),
+                   "catalogs_per_gpu": args.problems, "parallelism": "dp%d (host partition)" % world,
+                   "seed": args.seed},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
+                     "traffic": traffic, "kernel_ms": round(kernel_ms, 4),
+                     "algorithmic_bytes_per_launch": nbytes},
+        "classes": {"sat": int((st == 1).sum()), "unsat": int((st == -1).sum()),
+                    "incomplete": int((st == 0).sum()), "error": int((st == -2).sum()),
+                    "class_b": int(((res["flags"] & 2) != 0).sum())},
+        "pcie_inclusive_res_per_s": round(args.problems / t_pcie, 1),
+        "host_lowering_res_per_s": round(args.problems / t_lower, 1),
+    }
+
+    if rank == 0 and not args.no_cpu:
+        from oracle import oracle  # CPU baseline + checker only
+        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        o = oracle.solve_batch(lw.rec_off, lw.rec, 0, threads)  # also the parity check
+        ok = (np.array_equal(o["status"], st) and np.array_equal(o["flags"], res["flags"])
+              and np.array_equal(o["installed"], res["installed"])
+              and np.array_equal(o["core_len"], res["core_len"])
+              and np.array_equal(o["steps"], res["steps"]))
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            oracle.solve_batch(lw.rec_off, lw.rec, 0, threads)
+            reps += 1
+            if time.perf_counter() - t0 >= args.cpu_seconds:
+                break
+        cpu_t = time.perf_counter() - t0
+        line["cpu_baseline"] = {"value": round(reps * args.problems / cpu_t, 1),
+                                "unit": "resolutions/s", "cores": threads, "kind": "port",
+                                "sample": "the timed batch (%d catalogs) solved %d times by "
+                                          "oracle/sat_oracle.c on %d host threads (%.1f s)"
+                                          % (args.problems, reps, threads, cpu_t)}
+        line["verified_bit_exact_vs_oracle"] = bool(ok)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,331 @@
+"""ctypes binding of libdeppy_hip.so (include/deppy_hip.h).
+
+This is the same C-ABI a Go caller binds through cgo.  The
+library is built in-tree by deppy_amd/build.py; importing this module never
+falls back to anything else: a missing library or a missing MI355X is an error.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libdeppy_hip.so")
+
+c_i32p = ctypes.POINTER(ctypes.c_int32)
+c_i64p = ctypes.POINTER(ctypes.c_int64)
+c_u32p = ctypes.POINTER(ctypes.c_uint32)
+c_i8p = ctypes.POINTER(ctypes.c_int8)
+
+# every entry point declared in include/deppy_hip.h
+EXPORTS = [
+    "dp_rec_validate", "dp_lower", "dp_lowered_free", "dp_lowered_num_problems",
+    "dp_lowered_rec_off", "dp_lowered_rec", "dp_lowered_ident_off", "dp_lowered_ident_var",
+    "dp_lowered_ident_con", "dp_lowered_error", "dp_result_layout", "dp_create", "dp_destroy",
+    "dp_last_error", "dp_last_global_error", "dp_num_devices", "dp_solve", "dp_upload", "dp_run",
+    "dp_download", "dp_resident_free", "dp_last_kernel_ms", "dp_gen_catalogs", "dp_gen_wire",
+    "dp_gen_free",
+]
+
+
+class Wire(ctypes.Structure):
+    _fields_ = [
+        ("n_problems", ctypes.c_int32),
+        ("prob_var_off", c_i64p),
+        ("var_id", c_i64p),
+        ("var_con_off", c_i64p),
+        ("con_kind", c_i32p),
+        ("con_n", c_i32p),
+        ("con_arg_off", c_i64p),
+        ("con_arg", c_i64p),
+        ("n_strs", ctypes.c_int64),
+        ("str_off", c_i64p),
+        ("str_bytes", ctypes.c_char_p),
+        ("interned", ctypes.c_int32),
+    ]
+
+
+class Opts(ctypes.Structure):
+    _fields_ = [("first_device", ctypes.c_int32), ("n_devices", ctypes.c_int32),
+                ("step_budget", ctypes.c_int64), ("flags", ctypes.c_int32)]
+
+
+class Batch(ctypes.Structure):
+    _fields_ = [("n_problems", ctypes.c_int32), ("rec_off", c_i64p), ("rec", c_i32p)]
+
+
+class Result(ctypes.Structure):
+    _fields_ = [("status", c_i8p), ("flags", c_i32p), ("installed", c_u32p),
+                ("inst_off", c_i64p), ("core", c_i32p), ("core_off", c_i64p),
+                ("core_len", c_i32p), ("steps", c_i64p)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("deppy_amd: %s is missing; run __graft_entry__.build() "
+                           "(python deppy_amd/build.py)" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    vp = ctypes.c_void_p
+    L.dp_rec_validate.argtypes = [c_i32p, ctypes.c_int64]
+    L.dp_lower.argtypes = [ctypes.POINTER(Wire), ctypes.POINTER(vp)]
+    L.dp_lowered_free.argtypes = [vp]
+    L.dp_lowered_num_problems.argtypes = [vp]
+    for f in ("dp_lowered_rec_off", "dp_lowered_ident_off"):
+        getattr(L, f).argtypes = [vp]
+        getattr(L, f).restype = c_i64p
+    for f in ("dp_lowered_rec", "dp_lowered_ident_var", "dp_lowered_ident_con"):
+        getattr(L, f).argtypes = [vp]
+        getattr(L, f).restype = c_i32p
+    L.dp_lowered_error.argtypes = [vp, ctypes.c_int32, ctypes.POINTER(ctypes.c_char_p)]
+    L.dp_result_layout.argtypes = [ctypes.POINTER(Batch), c_i64p, c_i64p]
+    L.dp_create.argtypes = [ctypes.POINTER(Opts)]
+    L.dp_create.restype = vp
+    L.dp_destroy.argtypes = [vp]
+    L.dp_last_error.argtypes = [vp]
+    L.dp_last_error.restype = ctypes.c_char_p
+    L.dp_last_global_error.restype = ctypes.c_char_p
+    L.dp_num_devices.argtypes = [vp]
+    L.dp_solve.argtypes = [vp, ctypes.POINTER(Batch), ctypes.POINTER(Result)]
+    L.dp_upload.argtypes = [vp, ctypes.POINTER(Batch), ctypes.POINTER(vp)]
+    L.dp_run.argtypes = [vp, vp]
+    L.dp_download.argtypes = [vp, vp, ctypes.POINTER(Result)]
+    L.dp_resident_free.argtypes = [vp, vp]
+    L.dp_last_kernel_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
+    L.dp_gen_catalogs.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64]
+    L.dp_gen_catalogs.restype = vp
+    L.dp_gen_wire.argtypes = [vp]
+    L.dp_gen_wire.restype = ctypes.POINTER(Wire)
+    L.dp_gen_free.argtypes = [vp]
+    _lib = L
+    return L
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+# ---------------------------------------------------------------------------
+# wire batches
+# ---------------------------------------------------------------------------
+class WireArrays:
+    """numpy-backed dp_wire (keeps the arrays alive while C reads them)."""
+
+    def __init__(self, prob_var_off, var_id, var_con_off, con_kind, con_n, con_arg_off, con_arg,
+                 str_off, str_bytes, interned=True):
+        self.a = dict(prob_var_off=np.ascontiguousarray(prob_var_off, np.int64),
+                      var_id=np.ascontiguousarray(var_id, np.int64),
+                      var_con_off=np.ascontiguousarray(var_con_off, np.int64),
+                      con_kind=np.ascontiguousarray(con_kind, np.int32),
+                      con_n=np.ascontiguousarray(con_n, np.int32),
+                      con_arg_off=np.ascontiguousarray(con_arg_off, np.int64),
+                      con_arg=np.ascontiguousarray(con_arg, np.int64),
+                      str_off=np.ascontiguousarray(str_off, np.int64),
+                      str_bytes=np.frombuffer(bytes(str_bytes) + b"\0", np.uint8))
+        self.interned = interned
+
+    def struct(self) -> Wire:
+        a = self.a
+        # keep one extra element so empty arrays still have a valid pointer
+        for k in ("var_id", "con_kind", "con_n", "con_arg"):
+            if len(a[k]) == 0:
+                a[k] = np.zeros(1, a[k].dtype)
+        w = Wire()
+        w.n_problems = len(a["prob_var_off"]) - 1
+        w.prob_var_off = _p(a["prob_var_off"], c_i64p)
+        w.var_id = _p(a["var_id"], c_i64p)
+        w.var_con_off = _p(a["var_con_off"], c_i64p)
+        w.con_kind = _p(a["con_kind"], c_i32p)
+        w.con_n = _p(a["con_n"], c_i32p)
+        w.con_arg_off = _p(a["con_arg_off"], c_i64p)
+        w.con_arg = _p(a["con_arg"], c_i64p)
+        w.n_strs = len(a["str_off"]) - 1
+        w.str_off = _p(a["str_off"], c_i64p)
+        w.str_bytes = ctypes.cast(a["str_bytes"].ctypes.data, ctypes.c_char_p)
+        w.interned = 1 if self.interned else 0
+        return w
+
+
+def wire_to_numpy(w: Wire) -> dict:
+    """Copy a C-owned dp_wire (e.g. from dp_gen_wire) into numpy arrays."""
+    P = w.n_problems
+    pvo = np.ctypeslib.as_array(w.prob_var_off, (P + 1,)).copy()
+    nv = int(pvo[-1])
+    vco = np.ctypeslib.as_array(w.var_con_off, (nv + 1,)).copy() if nv else np.zeros(1, np.int64)
+    nc = int(vco[-1])
+    cao = np.ctypeslib.as_array(w.con_arg_off, (nc + 1,)).copy() if nc else np.zeros(1, np.int64)
+    na = int(cao[-1])
+    so = np.ctypeslib.as_array(w.str_off, (w.n_strs + 1,)).copy()
+    sb = ctypes.string_at(w.str_bytes, int(so[-1]))
+    return dict(prob_var_off=pvo,
+                var_id=np.ctypeslib.as_array(w.var_id, (nv,)).copy() if nv else np.zeros(0, np.int64),
+                var_con_off=vco,
+                con_kind=np.ctypeslib.as_array(w.con_kind, (nc,)).copy() if nc else np.zeros(0, np.int32),
+                con_n=np.ctypeslib.as_array(w.con_n, (nc,)).copy() if nc else np.zeros(0, np.int32),
+                con_arg_off=cao,
+                con_arg=np.ctypeslib.as_array(w.con_arg, (na,)).copy() if na else np.zeros(0, np.int64),
+                str_off=so, str_bytes=np.frombuffer(sb, np.uint8))
+
+
+class Lowered:
+    """Result of dp_lower, copied into numpy."""
+
+    def __init__(self, wire: WireArrays):
+        L = lib()
+        h = ctypes.c_void_p()
+        ws = wire.struct()
+        if L.dp_lower(ctypes.byref(ws), ctypes.byref(h)) != 0:
+            raise ValueError(L.dp_last_global_error().decode())
+        try:
+            P = L.dp_lowered_num_problems(h)
+            self.n = P
+            self.rec_off = np.ctypeslib.as_array(L.dp_lowered_rec_off(h), (P + 1,)).copy()
+            nw = int(self.rec_off[-1])
+            self.rec = np.ctypeslib.as_array(L.dp_lowered_rec(h), (max(nw, 1),))[:nw].copy()
+            self.ident_off = np.ctypeslib.as_array(L.dp_lowered_ident_off(h), (P + 1,)).copy()
+            ni = int(self.ident_off[-1])
+            if ni:
+                self.ident_var = np.ctypeslib.as_array(L.dp_lowered_ident_var(h), (ni,)).copy()
+                self.ident_con = np.ctypeslib.as_array(L.dp_lowered_ident_con(h), (ni,)).copy()
+            else:
+                self.ident_var = np.zeros(0, np.int32)
+                self.ident_con = np.zeros(0, np.int32)
+            self.err = np.zeros(P, np.int32)
+            self.msg = [None] * P
+            m = ctypes.c_char_p()
+            for p in range(P):
+                self.err[p] = L.dp_lowered_error(h, p, ctypes.byref(m))
+                if self.err[p]:
+                    self.msg[p] = m.value.decode("utf-8", "surrogateescape")
+        finally:
+            L.dp_lowered_free(h)
+
+    def record(self, p: int) -> np.ndarray:
+        return self.rec[self.rec_off[p]:self.rec_off[p + 1]]
+
+
+# ---------------------------------------------------------------------------
+# device context and batch solve
+# ---------------------------------------------------------------------------
+class Context:
+    def __init__(self, first_device: int = 0, n_devices: int = 1, step_budget: int = 0):
+        L = lib()
+        o = Opts(first_device, n_devices, step_budget, 0)
+        h = L.dp_create(ctypes.byref(o))
+        if not h:
+            raise RuntimeError("deppy_amd: no usable MI355X: " + L.dp_last_global_error().decode())
+        self.h = h
+
+    def close(self):
+        if self.h:
+            lib().dp_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def error(self) -> str:
+        return lib().dp_last_error(self.h).decode()
+
+    def upload(self, rec_off: np.ndarray, rec: np.ndarray) -> "Resident":
+        return Resident(self, rec_off, rec)
+
+    def solve(self, rec_off: np.ndarray, rec: np.ndarray) -> dict:
+        r = self.upload(rec_off, rec)
+        try:
+            r.run()
+            return r.download()
+        finally:
+            r.free()
+
+    def last_kernel_ms(self) -> float:
+        ms = ctypes.c_double()
+        lib().dp_last_kernel_ms(self.h, ctypes.byref(ms))
+        return ms.value
+
+
+def _batch(rec_off, rec):
+    b = Batch()
+    b.n_problems = len(rec_off) - 1
+    b.rec_off = _p(rec_off, c_i64p)
+    b.rec = _p(rec, c_i32p)
+    return b
+
+
+class Resident:
+    """A batch resident in HBM (dp_upload); run() solves it in place."""
+
+    def __init__(self, ctx: Context, rec_off, rec):
+        self.ctx = ctx
+        self.rec_off = np.ascontiguousarray(rec_off, np.int64)
+        self.rec = np.ascontiguousarray(rec if len(rec) else np.zeros(1, np.int32), np.int32)
+        n = len(self.rec_off) - 1
+        self.n = n
+        b = _batch(self.rec_off, self.rec)
+        self.inst_off = np.zeros(n + 1, np.int64)
+        self.core_off = np.zeros(n + 1, np.int64)
+        lib().dp_result_layout(ctypes.byref(b), _p(self.inst_off, c_i64p), _p(self.core_off, c_i64p))
+        h = ctypes.c_void_p()
+        if lib().dp_upload(ctx.h, ctypes.byref(b), ctypes.byref(h)) != 0:
+            raise RuntimeError("dp_upload: " + ctx.error())
+        self.h = h
+
+    def run(self):
+        if lib().dp_run(self.ctx.h, self.h) != 0:
+            raise RuntimeError("dp_run: " + self.ctx.error())
+
+    def download(self) -> dict:
+        n = self.n
+        out = dict(status=np.zeros(max(n, 1), np.int8), flags=np.zeros(max(n, 1), np.int32),
+                   installed=np.zeros(max(1, int(self.inst_off[-1])), np.uint32),
+                   inst_off=self.inst_off,
+                   core=np.zeros(max(1, int(self.core_off[-1])), np.int32), core_off=self.core_off,
+                   core_len=np.zeros(max(n, 1), np.int32), steps=np.zeros(max(n, 1), np.int64))
+        r = Result(_p(out["status"], c_i8p), _p(out["flags"], c_i32p),
+                   _p(out["installed"], c_u32p), _p(self.inst_off, c_i64p),
+                   _p(out["core"], c_i32p), _p(self.core_off, c_i64p),
+                   _p(out["core_len"], c_i32p), _p(out["steps"], c_i64p))
+        if lib().dp_download(self.ctx.h, self.h, ctypes.byref(r)) != 0:
+            raise RuntimeError("dp_download: " + self.ctx.error())
+        for k in ("status", "flags", "core_len", "steps"):
+            out[k] = out[k][:n]
+        return out
+
+    def free(self):
+        if self.h:
+            lib().dp_resident_free(self.ctx.h, self.h)
+            self.h = None
+
+
+def generate(config: int, n: int, seed: int) -> dict:
+    """Synthetic catalogs (dp_gen_catalogs) as numpy wire arrays."""
+    L = lib()
+    g = L.dp_gen_catalogs(config, n, seed)
+    if not g:
+        raise ValueError(L.dp_last_global_error().decode())
+    try:
+        return wire_to_numpy(L.dp_gen_wire(g).contents)
+    finally:
+        L.dp_gen_free(g)
+
+
+def installed_list(res: dict, p: int, nv: int) -> list[int]:
+    base = int(res["inst_off"][p])
+    words = res["installed"][base:base + (nv + 31) // 32]
+    bits = np.unpackbits(words.view(np.uint8), bitorder="little")[:nv]
+    return [int(i) for i in np.flatnonzero(bits)]
+
+
+def core_list(res: dict, p: int) -> list[int]:
+    base = int(res["core_off"][p])
+    return [int(x) for x in res["core"][base:base + int(res["core_len"][p])]]

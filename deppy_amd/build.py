@@ -1,0 +1,52 @@
+"""Builds libdeppy_hip.so in-tree with hipcc for gfx950 (no JIT cache, so the
+.so travels with the repo snapshot to the GPU box)."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libdeppy_hip.so")
+OBJ = os.path.join(HERE, "_obj")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+SOURCES = ["solve_kernel.hip", "runtime.cpp", "lower.cpp", "gen.cpp"]
+FLAGS = ["-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function",
+         "--offload-arch=" + ARCH, "-I" + os.path.join(HERE, "..", "include")]
+
+
+def _needs(target: str, deps: list[str]) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(verbose: bool = False, extra: list[str] | None = None) -> str:
+    os.makedirs(OBJ, exist_ok=True)
+    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h"))]
+    headers.append(os.path.join(HERE, "..", "include", "deppy_hip.h"))
+    jobs = []
+    for src in SOURCES:
+        s = os.path.join(CSRC, src)
+        o = os.path.join(OBJ, src + ".o")
+        if _needs(o, [s] + headers) or extra:
+            lang = ["-x", "hip"] if src.endswith(".hip") else ["-x", "hip"] if src == "runtime.cpp" else []
+            jobs.append([HIPCC] + FLAGS + (extra or []) + lang + ["-c", s, "-o", o])
+    def run(cmd):
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    with ThreadPoolExecutor(max_workers=4) as ex:
+        list(ex.map(run, jobs))
+    objs = [os.path.join(OBJ, s + ".o") for s in SOURCES]
+    if _needs(LIB, objs) or jobs:
+        run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs + ["-lpthread"])
+    return LIB
+
+
+if __name__ == "__main__":
+    build(verbose=True, extra=sys.argv[1:] or None)

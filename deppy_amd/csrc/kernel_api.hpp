@@ -1,0 +1,33 @@
+// Host <-> kernel interface of the solve kernel (solve_kernel.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace dp {
+
+struct KernelArgs {
+  const int32_t* rec;      // records, each 16-byte aligned
+  const int64_t* rec_off;  // [n] word offset of each record
+  const int32_t* order;    // [grid] problem index of each workgroup
+  int8_t* status;
+  int32_t* flags;
+  uint32_t* installed;
+  const int64_t* inst_off;
+  int32_t* core;
+  const int64_t* core_off;
+  int32_t* core_len;
+  int64_t* steps;
+  int64_t budget;
+  // HBM-resident working sets (problems over the LDS limit): when non-null,
+  // workgroup b works in scratch + scratch_off[b] instead of LDS
+  int32_t* scratch;
+  const int64_t* scratch_off;
+};
+
+// Launch one wavefront per problem of order[0..n_blocks) with lds_bytes of LDS.
+hipError_t launch_solve(const KernelArgs& a, int n_blocks, int lds_bytes, hipStream_t stream);
+// Raise the kernel's dynamic-LDS limit to the device maximum.
+hipError_t configure_solve_kernel(int max_lds_bytes);
+
+}  // namespace dp

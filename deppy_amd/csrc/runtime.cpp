@@ -1,0 +1,397 @@
+// Host runtime of libdeppy_hip: device discovery, batch partitioning across
+// MI355X devices, HBM residency, launch and result download.
+//
+// Problems are independent: a batch is cut into contiguous,
+// cost-balanced slices, one per device, with no inter-device traffic.  On each
+// device, problems are bucketed by working-set footprint so every launch
+// requests only the dynamic LDS its largest problem needs (occupancy follows
+// the footprint); problems beyond the 160 KiB LDS of a CU run with their
+// working set in an HBM scratch region (one more launch).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "common.hpp"
+#include "kernel_api.hpp"
+#include "layout.hpp"
+
+namespace {
+
+constexpr int kMaxLdsBytes = 160 * 1024;          // LDS per CU on gfx950
+constexpr int64_t kDefaultBudget = 1 << 16;        // BCP invocations per problem
+// LDS bucket ceilings (bytes); one launch per non-empty bucket
+constexpr int kBuckets[] = {8 << 10, 16 << 10, 24 << 10, 32 << 10, 48 << 10, 64 << 10,
+                            96 << 10, 160 << 10};
+constexpr int kNBuckets = (int)(sizeof(kBuckets) / sizeof(kBuckets[0]));
+
+#define HIP_OK(expr)                                                         \
+  do {                                                                       \
+    hipError_t e_ = (expr);                                                  \
+    if (e_ != hipSuccess) {                                                  \
+      fail(std::string(#expr) + ": " + hipGetErrorString(e_));               \
+      return -1;                                                             \
+    }                                                                        \
+  } while (0)
+
+}  // namespace
+
+struct DevSlice {
+  int device = 0;
+  int32_t p0 = 0, p1 = 0;  // global problem range
+  int64_t inst0 = 0, core0 = 0;
+  // device buffers
+  int32_t* rec = nullptr;
+  int64_t* rec_off = nullptr;
+  int32_t* order = nullptr;
+  int8_t* status = nullptr;
+  int32_t* flags = nullptr;
+  uint32_t* installed = nullptr;
+  int64_t* inst_off = nullptr;
+  int32_t* core = nullptr;
+  int64_t* core_off = nullptr;
+  int32_t* core_len = nullptr;
+  int64_t* steps = nullptr;
+  int64_t n_inst = 0, n_core = 0;
+  // launches: [bucket] -> (first order index, count, lds bytes)
+  std::vector<int> b_first, b_count, b_lds;
+  std::vector<int32_t> too_large;             // local indices (-> DP_ERROR)
+  // HBM-resident working sets for problems over the LDS limit
+  int hbm_first = 0, hbm_count = 0;
+  int32_t* scratch = nullptr;
+  int64_t* scratch_off = nullptr;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+struct dp_resident {
+  int32_t n = 0;
+  std::vector<DevSlice> slices;
+};
+
+struct dp_ctx {
+  std::vector<int> devices;
+  int64_t budget = kDefaultBudget;
+  std::string err;
+  double last_ms = 0.0;
+  std::mutex mu;
+};
+
+namespace {
+
+thread_local dp_ctx* t_ctx = nullptr;
+void fail(const std::string& s) {
+  if (t_ctx) t_ctx->err = s;
+  else dp::set_global_error(s);
+}
+
+void free_slice(DevSlice& s) {
+  if (s.stream) (void)hipSetDevice(s.device);
+  void* ptrs[] = {s.rec, s.rec_off, s.order, s.status, s.flags, s.installed,
+                  s.inst_off, s.core, s.core_off, s.core_len, s.steps, s.scratch, s.scratch_off};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  if (s.ev0) (void)hipEventDestroy(s.ev0);
+  if (s.ev1) (void)hipEventDestroy(s.ev1);
+  if (s.stream) (void)hipStreamDestroy(s.stream);
+  s = DevSlice{};
+}
+
+template <class T>
+int upload_vec(T** dst, const T* src, size_t n, hipStream_t st) {
+  HIP_OK(hipMalloc(reinterpret_cast<void**>(dst), std::max<size_t>(n, 1) * sizeof(T)));
+  if (n) HIP_OK(hipMemcpyAsync(*dst, src, n * sizeof(T), hipMemcpyHostToDevice, st));
+  return 0;
+}
+
+// Build one device's slice: aligned records, bucketed launch order, outputs.
+int build_slice(DevSlice& s, const dp_batch* b, const int64_t* inst_off, const int64_t* core_off) {
+  HIP_OK(hipSetDevice(s.device));
+  HIP_OK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+  HIP_OK(hipEventCreate(&s.ev0));
+  HIP_OK(hipEventCreate(&s.ev1));
+  const int32_t n = s.p1 - s.p0;
+  std::vector<int64_t> roff((size_t)n + 1, 0);
+  for (int32_t i = 0; i < n; ++i) {
+    const int32_t* r = b->rec + b->rec_off[s.p0 + i];
+    roff[(size_t)i + 1] = roff[(size_t)i] + ((dp::words_of(r) + 3) & ~3LL);
+  }
+  std::vector<int32_t> rec((size_t)roff[(size_t)n], 0);
+  std::vector<std::vector<int32_t>> bucket(kNBuckets);
+  std::vector<int32_t> hbm;
+  std::vector<int64_t> soff(1, 0);
+  for (int32_t i = 0; i < n; ++i) {
+    const int32_t* r = b->rec + b->rec_off[s.p0 + i];
+    std::memcpy(&rec[(size_t)roff[(size_t)i]], r, (size_t)dp::words_of(r) * 4);
+    const int64_t words = dp::lds_layout(r).words;
+    const int64_t lds = words * 4;
+    int k = 0;
+    while (k < kNBuckets && lds > kBuckets[k]) ++k;
+    if (k < kNBuckets) bucket[(size_t)k].push_back(i);
+    else if (words < (int64_t)1 << 31) { hbm.push_back(i); soff.push_back(soff.back() + words); }
+    else s.too_large.push_back(i);
+  }
+  std::vector<int32_t> order;
+  for (int k = 0; k < kNBuckets; ++k) {
+    if (bucket[(size_t)k].empty()) continue;
+    s.b_first.push_back((int)order.size());
+    s.b_count.push_back((int)bucket[(size_t)k].size());
+    int mx = 0;
+    for (int32_t i : bucket[(size_t)k])
+      mx = std::max(mx, dp::lds_layout(b->rec + b->rec_off[s.p0 + i]).words * 4);
+    s.b_lds.push_back(mx);
+    order.insert(order.end(), bucket[(size_t)k].begin(), bucket[(size_t)k].end());
+  }
+  s.hbm_first = (int)order.size();
+  s.hbm_count = (int)hbm.size();
+  order.insert(order.end(), hbm.begin(), hbm.end());
+  s.inst0 = inst_off[s.p0];
+  s.core0 = core_off[s.p0];
+  s.n_inst = inst_off[s.p1] - s.inst0;
+  s.n_core = core_off[s.p1] - s.core0;
+  std::vector<int64_t> li((size_t)n + 1), lc((size_t)n + 1);
+  for (int32_t i = 0; i <= n; ++i) {
+    li[(size_t)i] = inst_off[s.p0 + i] - s.inst0;
+    lc[(size_t)i] = core_off[s.p0 + i] - s.core0;
+  }
+  if (upload_vec(&s.rec, rec.data(), rec.size(), s.stream)) return -1;
+  if (upload_vec(&s.rec_off, roff.data(), (size_t)n, s.stream)) return -1;
+  if (upload_vec(&s.order, order.data(), order.size(), s.stream)) return -1;
+  if (upload_vec(&s.inst_off, li.data(), (size_t)n + 1, s.stream)) return -1;
+  if (upload_vec(&s.core_off, lc.data(), (size_t)n + 1, s.stream)) return -1;
+  if (s.hbm_count) {
+    if (upload_vec(&s.scratch_off, soff.data(), (size_t)s.hbm_count, s.stream)) return -1;
+    HIP_OK(hipMalloc(&s.scratch, (size_t)soff.back() * 4));
+  }
+  HIP_OK(hipMalloc(&s.status, std::max<size_t>((size_t)n, 1)));
+  HIP_OK(hipMalloc(&s.flags, std::max<size_t>((size_t)n, 1) * 4));
+  HIP_OK(hipMalloc(&s.core_len, std::max<size_t>((size_t)n, 1) * 4));
+  HIP_OK(hipMalloc(&s.steps, std::max<size_t>((size_t)n, 1) * 8));
+  HIP_OK(hipMalloc(&s.installed, (size_t)std::max<int64_t>(s.n_inst, 1) * 4));
+  HIP_OK(hipMalloc(&s.core, (size_t)std::max<int64_t>(s.n_core, 1) * 4));
+  // problems that fit no bucket are reported DP_ERROR | DP_F_TOO_LARGE
+  HIP_OK(hipMemsetAsync(s.status, 0, std::max<size_t>((size_t)n, 1), s.stream));
+  HIP_OK(hipMemsetAsync(s.flags, 0, std::max<size_t>((size_t)n, 1) * 4, s.stream));
+  HIP_OK(hipMemsetAsync(s.core_len, 0, std::max<size_t>((size_t)n, 1) * 4, s.stream));
+  HIP_OK(hipMemsetAsync(s.steps, 0, std::max<size_t>((size_t)n, 1) * 8, s.stream));
+  HIP_OK(hipMemsetAsync(s.installed, 0, (size_t)std::max<int64_t>(s.n_inst, 1) * 4, s.stream));
+  HIP_OK(hipStreamSynchronize(s.stream));
+  return 0;
+}
+
+int run_slice(DevSlice& s, int64_t budget) {
+  HIP_OK(hipSetDevice(s.device));
+  dp::KernelArgs a;
+  a.rec = s.rec;
+  a.rec_off = s.rec_off;
+  a.status = s.status;
+  a.flags = s.flags;
+  a.installed = s.installed;
+  a.inst_off = s.inst_off;
+  a.core = s.core;
+  a.core_off = s.core_off;
+  a.core_len = s.core_len;
+  a.steps = s.steps;
+  a.budget = budget;
+  a.scratch = nullptr;
+  a.scratch_off = nullptr;
+  HIP_OK(hipEventRecord(s.ev0, s.stream));
+  for (size_t k = 0; k < s.b_first.size(); ++k) {
+    a.order = s.order + s.b_first[k];
+    HIP_OK(dp::launch_solve(a, s.b_count[k], s.b_lds[k], s.stream));
+  }
+  if (s.hbm_count) {
+    a.order = s.order + s.hbm_first;
+    a.scratch = s.scratch;
+    a.scratch_off = s.scratch_off;
+    HIP_OK(dp::launch_solve(a, s.hbm_count, 0, s.stream));
+  }
+  HIP_OK(hipEventRecord(s.ev1, s.stream));
+  HIP_OK(hipStreamSynchronize(s.stream));
+  return 0;
+}
+
+int download_slice(DevSlice& s, dp_result* res) {
+  HIP_OK(hipSetDevice(s.device));
+  const int32_t n = s.p1 - s.p0;
+  if (n == 0) return 0;
+  HIP_OK(hipMemcpyAsync(res->status + s.p0, s.status, (size_t)n, hipMemcpyDeviceToHost, s.stream));
+  HIP_OK(hipMemcpyAsync(res->flags + s.p0, s.flags, (size_t)n * 4, hipMemcpyDeviceToHost, s.stream));
+  HIP_OK(hipMemcpyAsync(res->core_len + s.p0, s.core_len, (size_t)n * 4, hipMemcpyDeviceToHost, s.stream));
+  if (res->steps)
+    HIP_OK(hipMemcpyAsync(res->steps + s.p0, s.steps, (size_t)n * 8, hipMemcpyDeviceToHost, s.stream));
+  if (s.n_inst)
+    HIP_OK(hipMemcpyAsync(res->installed + s.inst0, s.installed, (size_t)s.n_inst * 4,
+                          hipMemcpyDeviceToHost, s.stream));
+  if (s.n_core)
+    HIP_OK(hipMemcpyAsync(res->core + s.core0, s.core, (size_t)s.n_core * 4, hipMemcpyDeviceToHost,
+                          s.stream));
+  HIP_OK(hipStreamSynchronize(s.stream));
+  for (int32_t i : s.too_large) {
+    res->status[s.p0 + i] = DP_ERROR;
+    res->flags[s.p0 + i] = DP_F_TOO_LARGE;
+    res->core_len[s.p0 + i] = 0;
+  }
+  return 0;
+}
+
+// Run fn(slice) on every slice, one host thread per device.
+template <class F>
+int for_slices(dp_ctx* ctx, dp_resident* r, F fn) {
+  if (r->slices.size() == 1) return fn(r->slices[0]);
+  std::vector<int> rc(r->slices.size(), 0);
+  std::vector<std::thread> th;
+  for (size_t i = 0; i < r->slices.size(); ++i)
+    th.emplace_back([&, i]() {
+      t_ctx = ctx;
+      rc[i] = fn(r->slices[i]);
+    });
+  for (auto& t : th) t.join();
+  for (int x : rc)
+    if (x) return x;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+dp_ctx* dp_create(const dp_opts* opts) {
+  t_ctx = nullptr;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0) {
+    dp::set_global_error(std::string("dp_create: no HIP device (") + hipGetErrorString(e) + ")");
+    return nullptr;
+  }
+  int first = opts ? opts->first_device : 0;
+  int cnt = opts && opts->n_devices > 0 ? opts->n_devices : n - first;
+  if (first < 0 || cnt <= 0 || first + cnt > n) {
+    dp::set_global_error("dp_create: device range out of bounds");
+    return nullptr;
+  }
+  auto* ctx = new dp_ctx;
+  for (int d = first; d < first + cnt; ++d) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, d) != hipSuccess ||
+        std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+      dp::set_global_error(std::string("dp_create: device ") + std::to_string(d) +
+                           " is not gfx950 (" + prop.gcnArchName + ")");
+      delete ctx;
+      return nullptr;
+    }
+    if (hipSetDevice(d) != hipSuccess || dp::configure_solve_kernel(kMaxLdsBytes) != hipSuccess) {
+      dp::set_global_error("dp_create: cannot configure the solve kernel");
+      delete ctx;
+      return nullptr;
+    }
+    ctx->devices.push_back(d);
+  }
+  if (opts && opts->step_budget > 0) ctx->budget = opts->step_budget;
+  return ctx;
+}
+
+void dp_destroy(dp_ctx* ctx) { delete ctx; }
+const char* dp_last_error(const dp_ctx* ctx) { return ctx ? ctx->err.c_str() : dp_last_global_error(); }
+int32_t dp_num_devices(const dp_ctx* ctx) { return ctx ? (int32_t)ctx->devices.size() : 0; }
+
+int dp_result_layout(const dp_batch* b, int64_t* inst_off, int64_t* core_off) {
+  if (!b || !inst_off || !core_off || b->n_problems < 0) return -1;
+  inst_off[0] = core_off[0] = 0;
+  for (int32_t i = 0; i < b->n_problems; ++i) {
+    const int32_t* r = b->rec + b->rec_off[i];
+    inst_off[i + 1] = inst_off[i] + dp::bits_words(r[DP_H_NV]);
+    core_off[i + 1] = core_off[i] + r[DP_H_NID];
+  }
+  return 0;
+}
+
+int dp_upload(dp_ctx* ctx, const dp_batch* b, dp_resident** out) {
+  if (!ctx || !b || !out) return -1;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  t_ctx = ctx;
+  const int32_t P = b->n_problems;
+  for (int32_t i = 0; i < P; ++i) {
+    int64_t words = b->rec_off[i + 1] - b->rec_off[i];
+    int rc = dp_rec_validate(b->rec + b->rec_off[i], words);
+    if (rc) {
+      fail("dp_upload: record " + std::to_string(i) + " malformed (" + std::to_string(rc) + ")");
+      return -1;
+    }
+  }
+  std::vector<int64_t> inst_off((size_t)P + 1), core_off((size_t)P + 1);
+  dp_result_layout(b, inst_off.data(), core_off.data());
+  auto* r = new dp_resident;
+  r->n = P;
+  // contiguous slices balanced by record words (a proxy of solve cost)
+  const int nd = (int)ctx->devices.size();
+  const int64_t total = P ? b->rec_off[P] - b->rec_off[0] : 0;
+  int32_t p = 0;
+  for (int d = 0; d < nd; ++d) {
+    DevSlice s;
+    s.device = ctx->devices[(size_t)d];
+    s.p0 = p;
+    const int64_t target = b->rec_off[0] + total * (d + 1) / nd;
+    while (p < P && (d == nd - 1 || b->rec_off[p + 1] <= target)) ++p;
+    s.p1 = p;
+    r->slices.push_back(s);
+  }
+  int rc = for_slices(ctx, r, [&](DevSlice& s) { return build_slice(s, b, inst_off.data(), core_off.data()); });
+  if (rc) {
+    dp_resident_free(ctx, r);
+    return -1;
+  }
+  *out = r;
+  return 0;
+}
+
+int dp_run(dp_ctx* ctx, dp_resident* r) {
+  if (!ctx || !r) return -1;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  t_ctx = ctx;
+  const int64_t budget = ctx->budget;
+  int rc = for_slices(ctx, r, [&](DevSlice& s) { return run_slice(s, budget); });
+  if (rc) return -1;
+  double mx = 0.0;
+  for (auto& s : r->slices) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, s.ev0, s.ev1) == hipSuccess) mx = std::max(mx, (double)ms);
+  }
+  ctx->last_ms = mx;
+  return 0;
+}
+
+int dp_download(dp_ctx* ctx, dp_resident* r, dp_result* res) {
+  if (!ctx || !r || !res) return -1;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  t_ctx = ctx;
+  return for_slices(ctx, r, [&](DevSlice& s) { return download_slice(s, res); });
+}
+
+void dp_resident_free(dp_ctx* ctx, dp_resident* r) {
+  (void)ctx;
+  if (!r) return;
+  for (auto& s : r->slices) free_slice(s);
+  delete r;
+}
+
+int dp_solve(dp_ctx* ctx, const dp_batch* b, dp_result* res) {
+  dp_resident* r = nullptr;
+  if (dp_upload(ctx, b, &r)) return -1;
+  int rc = dp_run(ctx, r);
+  if (!rc) rc = dp_download(ctx, r, res);
+  dp_resident_free(ctx, r);
+  return rc;
+}
+
+int dp_last_kernel_ms(const dp_ctx* ctx, double* ms) {
+  if (!ctx || !ms) return -1;
+  *ms = ctx->last_ms;
+  return 0;
+}
+
+}  // extern "C"

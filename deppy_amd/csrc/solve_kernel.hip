@@ -1,0 +1,908 @@
+// Batched pkg/sat resolution on MI355X (gfx950): one wavefront per problem.
+//
+// Each workgroup is one 64-lane wavefront that owns one problem.  The problem's
+// lowered record is copied into LDS, watch lists are built in LDS, and the whole
+// solve runs out of LDS:
+//
+//   base scope + BCP        pkg/sat/solve.go:63-79           (base_propagate)
+//   preference search       pkg/sat/search.go:34-203         (search)
+//   Solve() under scopes    search.go:167-169, gini contract (dpll)
+//   SAT epilogue            solve.go:86-110                  (epilogue)
+//   NotSatisfiable          solve.go:114-115                 (core)
+//
+// Control flow is wave-uniform (every lane runs the same scalar logic on
+// broadcast LDS reads); the data-parallel parts are row evaluation (lanes over
+// the rows watched by a round's frontier, flattened with a wave prefix sum),
+// the all-false-completion check (lanes over clause rows), candidate
+// membership tests (ballot), AtMost counting and conflict analysis.
+//
+// Semantics are exactly those of oracle/sat_oracle.c (the test oracle): in
+// particular a round's implications are resolved to the lowest implying row
+// with LDS atomicMin, so reasons, cores and step counts are bit-identical.
+#include <hip/hip_runtime.h>
+
+#include "kernel_api.hpp"
+#include "layout.hpp"
+
+namespace dp {
+
+namespace {
+
+constexpr int32_t INF = 0x7fffffff;
+constexpr int32_t R_DEC = -1;    // decision / assumption / guess
+constexpr int32_t R_EXTRA = -2;  // epilogue bound over the extras
+enum { CK_NONE = 0, CK_ROW, CK_VAR, CK_ASSUME, CK_EXTRA };
+enum { RS_SAT = 1, RS_UNSAT = -1, RS_BUDGET = 2 };
+
+// Lanes of the wave hand values to each other through the working set (LDS,
+// or HBM for oversized problems): complete every access before the next phase.
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ uint64_t lanemask_lt() {
+  return (1ull << lane_id()) - 1ull;
+}
+
+__device__ __forceinline__ int wave_incl_scan(int x) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    int y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
+
+__device__ __forceinline__ bool getb(const uint32_t* b, int i) { return (b[i >> 5] >> (i & 31)) & 1u; }
+
+struct Wave {
+  // ---- record views (LDS) ----
+  int nv, nc, nk, nid, nrows, nbv, nbi, na;
+  const int32_t *clause_off, *clause_lits, *clause_id;
+  const int32_t *card_off, *card_lits, *card_bound, *card_id;
+  const int32_t *var_choice_off, *choice_off, *choice_lits, *anchors;
+  // ---- working set (LDS) ----
+  int32_t *w_off, *w;
+  int8_t* val;
+  int32_t *reason, *rnd, *trail, *imp_pos, *imp_neg, *impflag, *touched, *d_lit, *d_mark, *dix;
+  uint32_t *d_flip, *inS, *extra, *seen, *model, *used, *en, *en2, *dset, *fg;
+  int32_t *l_off, *l_lits;
+  int32_t *dq, *stk, *pre, *preA, *scal;
+  int cap, lcap;
+  int lane;
+  // ---- wave-uniform state (registers) ----
+  int tlen, qhead, round;
+  int64_t steps, budget;
+  bool budget_hit;
+  int ck, c_row, c_var, c_rp, c_rn;
+  bool collect_guess, learn_on;
+  int nl;
+  const uint32_t* enabled;  // nullptr: every row
+  bool extra_mode;
+  int extra_w;
+
+  // ------------------------------------------------------------------
+  // set-up (oracle: st_init)
+  // ------------------------------------------------------------------
+  __device__ void init(int32_t* lds, const int32_t* __restrict__ grec) {
+    lane = lane_id();
+    // copy the record (16-byte aligned in HBM and LDS) with dwordx4 loads
+    const int words = grec[DP_H_WORDS];
+    const int q = (words + 3) >> 2;
+    const int4* src = reinterpret_cast<const int4*>(grec);
+    int4* dst = reinterpret_cast<int4*>(lds);
+    for (int i = lane; i < q; i += 64) dst[i] = src[i];
+    wsync();
+    const int32_t* h = lds;
+    LdsLayout L = lds_layout(h);
+    dp_rec_layout R = rec_layout(h);
+    nv = h[DP_H_NV]; nc = h[DP_H_NC]; nk = h[DP_H_NK]; nid = h[DP_H_NID]; na = h[DP_H_NA];
+    nrows = nc + nk;
+    nbv = bits_words(nv); nbi = bits_words(nid);
+    clause_off = h + R.clause_off; clause_lits = h + R.clause_lits; clause_id = h + R.clause_id;
+    card_off = h + R.card_off; card_lits = h + R.card_lits; card_bound = h + R.card_bound;
+    card_id = h + R.card_id; var_choice_off = h + R.var_choice_off; choice_off = h + R.choice_off;
+    choice_lits = h + R.choice_lits; anchors = h + R.anchors;
+    w_off = lds + L.w_off; w = lds + L.w;
+    val = reinterpret_cast<int8_t*>(lds + L.val);
+    reason = lds + L.reason; rnd = lds + L.rnd; trail = lds + L.trail;
+    imp_pos = lds + L.imp_pos; imp_neg = lds + L.imp_neg; impflag = lds + L.impflag;
+    touched = lds + L.touched; d_lit = lds + L.d_lit; d_mark = lds + L.d_mark; dix = lds + L.dix;
+    d_flip = reinterpret_cast<uint32_t*>(lds + L.d_flip);
+    inS = reinterpret_cast<uint32_t*>(lds + L.inS);
+    extra = reinterpret_cast<uint32_t*>(lds + L.extra);
+    seen = reinterpret_cast<uint32_t*>(lds + L.seen);
+    model = reinterpret_cast<uint32_t*>(lds + L.model);
+    used = reinterpret_cast<uint32_t*>(lds + L.used);
+    en = reinterpret_cast<uint32_t*>(lds + L.en);
+    en2 = reinterpret_cast<uint32_t*>(lds + L.en2);
+    dset = reinterpret_cast<uint32_t*>(lds + L.dset);
+    fg = reinterpret_cast<uint32_t*>(lds + L.fg);
+    l_off = lds + L.l_off; l_lits = lds + L.l_lits;
+    dq = lds + L.dq; stk = lds + L.stk; pre = lds + L.pre; preA = lds + L.preA; scal = lds + L.scal;
+    cap = L.cap; lcap = L.lcap;
+    tlen = qhead = round = 0;
+    steps = 0;
+    budget_hit = false;
+    ck = CK_NONE; c_row = c_var = c_rp = c_rn = 0;
+    collect_guess = false;
+    learn_on = true;
+    nl = 0;
+    enabled = nullptr;
+    extra_mode = false;
+    extra_w = 0;
+
+    for (int v = lane; v < nv; v += 64) {
+      val[v] = 0; impflag[v] = 0;
+    }
+    for (int i = lane; i < nbv; i += 64) {
+      d_flip[i] = 0; inS[i] = 0; extra[i] = 0; seen[i] = 0; model[i] = 0; dset[i] = 0; fg[i] = 0;
+    }
+    if (lane == 0) l_off[0] = 0;
+    // watch lists: a clause literal x of row r is watched by ~x; a card
+    // position v of row k by +v
+    const int nl2 = 2 * nv;
+    for (int l = lane; l <= nl2; l += 64) w_off[l] = 0;
+    wsync();
+    for (int j = lane; j < h[DP_H_NCL]; j += 64) atomicAdd(&w_off[(clause_lits[j] ^ 1) + 1], 1);
+    for (int j = lane; j < h[DP_H_NKL]; j += 64) atomicAdd(&w_off[2 * card_lits[j] + 1], 1);
+    wsync();
+    int carry = 0;
+    for (int base = 0; base < nl2; base += 64) {
+      const int i = base + 1 + lane;
+      const int x = i <= nl2 ? w_off[i] : 0;
+      const int inc = wave_incl_scan(x) + carry;
+      if (i <= nl2) w_off[i] = inc;
+      carry = __shfl(inc, 63);
+    }
+    wsync();
+    int32_t* cursor = imp_pos;  // imp_pos|imp_neg hold >= 2nv words
+    for (int l = lane; l < nl2; l += 64) cursor[l] = w_off[l];
+    wsync();
+    for (int r = lane; r < nc; r += 64)
+      for (int j = clause_off[r]; j < clause_off[r + 1]; ++j) w[atomicAdd(&cursor[clause_lits[j] ^ 1], 1)] = r;
+    for (int k = lane; k < nk; k += 64)
+      for (int j = card_off[k]; j < card_off[k + 1]; ++j) w[atomicAdd(&cursor[2 * card_lits[j]], 1)] = nc + k;
+    wsync();
+    for (int v = lane; v < nv; v += 64) { imp_pos[v] = INF; imp_neg[v] = INF; }
+    wsync();
+  }
+
+  // ------------------------------------------------------------------
+  // unit propagation (oracle: eval_row / finish_round / propagate)
+  // ------------------------------------------------------------------
+  __device__ __forceinline__ int row_ident(int r) const {
+    return r < nc ? clause_id[r] : r < nrows ? card_id[r - nc] : -1;
+  }
+  __device__ __forceinline__ bool row_on(int r) const { return !enabled || getb(enabled, row_ident(r)); }
+  __device__ __forceinline__ int lit_val(int l) const {
+    const int x = val[l >> 1];
+    return (l & 1) ? -x : x;
+  }
+
+  __device__ __forceinline__ void note(int l, int r) {
+    const int v = l >> 1;
+    const int old = atomicOr(&impflag[v], (l & 1) ? 2 : 1);
+    if (old == 0) touched[atomicAdd(&scal[S_NTOUCHED], 1)] = v;
+    atomicMin((l & 1) ? &imp_neg[v] : &imp_pos[v], r);
+  }
+
+  __device__ __forceinline__ void eval_clause(int r, const int32_t* lits, int a, int b) {
+    int nun = 0, ul = -1;
+    for (int j = a; j < b; ++j) {
+      const int l = lits[j];
+      const int x = lit_val(l);
+      if (x > 0) return;
+      if (x == 0) { ++nun; ul = l; }
+    }
+    if (nun == 0) atomicMin(&scal[S_CROW], r);
+    else if (nun == 1) note(ul, r);
+  }
+
+  __device__ void eval_row(int r) {
+    if (r < nc) {
+      eval_clause(r, clause_lits, clause_off[r], clause_off[r + 1]);
+    } else if (r >= nrows) {
+      const int j = r - nrows;
+      eval_clause(r, l_lits, l_off[j], l_off[j + 1]);
+    } else {
+      const int k = r - nc, a = card_off[k], b = card_off[k + 1];
+      int cnt = 0, nun = 0;
+      for (int j = a; j < b; ++j) {
+        const int x = val[card_lits[j]];
+        cnt += (x > 0);
+        nun += (x == 0);
+      }
+      const int bound = card_bound[k];
+      if (cnt > bound) atomicMin(&scal[S_CROW], r);
+      else if (nun > 0) {
+        // a variable repeated m times is a run of m positions
+        for (int j = a; j < b;) {
+          const int v = card_lits[j];
+          int e = j + 1;
+          while (e < b && card_lits[e] == v) ++e;
+          if (val[v] == 0 && cnt + (e - j) > bound) note(2 * v + 1, r);
+          j = e;
+        }
+      }
+    }
+  }
+
+  // learned rows are evaluated in every round (lanes over rows)
+  __device__ __forceinline__ void eval_learned() {
+    if (!learn_on) return;
+    for (int j = lane; j < nl; j += 64) eval_row(nrows + j);
+  }
+
+  __device__ __forceinline__ void begin_round() {
+    scal[S_CROW] = INF;
+    scal[S_CVAR] = INF;
+    scal[S_NTOUCHED] = 0;
+    wsync();
+  }
+
+  __device__ void clear_touched(int nt) {
+    for (int i = lane; i < nt; i += 64) {
+      const int v = touched[i];
+      impflag[v] = 0; imp_pos[v] = INF; imp_neg[v] = INF;
+    }
+    wsync();
+  }
+
+  __device__ int finish_round(int rd) {
+    wsync();
+    const int crow = scal[S_CROW];
+    const int nt = scal[S_NTOUCHED];
+    if (crow != INF) {
+      clear_touched(nt);
+      ck = CK_ROW; c_row = crow;
+      return -1;
+    }
+    for (int i = lane; i < nt; i += 64) {
+      const int v = touched[i];
+      if (impflag[v] == 3) atomicMin(&scal[S_CVAR], v);
+    }
+    wsync();
+    const int cvar = scal[S_CVAR];
+    if (cvar != INF) {
+      c_rp = imp_pos[cvar]; c_rn = imp_neg[cvar];
+      wsync();
+      ck = CK_VAR; c_var = cvar; c_row = rd;
+      clear_touched(nt);
+      return -1;
+    }
+    for (int i = lane; i < nt; i += 64) {
+      const int v = touched[i];
+      const int rp = imp_pos[v];
+      const bool pos = rp != INF;
+      val[v] = pos ? 1 : -1;
+      reason[v] = pos ? rp : imp_neg[v];
+      rnd[v] = rd;
+      dix[v] = -1;
+      trail[tlen + i] = 2 * v + (pos ? 0 : 1);
+      impflag[v] = 0; imp_pos[v] = INF; imp_neg[v] = INF;
+    }
+    tlen += nt;
+    wsync();
+    return 0;
+  }
+
+  __device__ int extra_check() {
+    int cnt = 0, nun = 0;
+    for (int base = 0; base < nv; base += 64) {
+      const int v = base + lane;
+      const bool ex = v < nv && getb(extra, v);
+      const int x = ex ? val[v] : 0;
+      cnt += __popcll(__ballot(ex && x > 0));
+      nun += __popcll(__ballot(ex && x == 0));
+    }
+    if (cnt > extra_w) { ck = CK_EXTRA; return -1; }
+    if (cnt == extra_w && nun > 0) {
+      const int rd = ++round;
+      for (int base = 0; base < nv; base += 64) {
+        const int v = base + lane;
+        const bool f = v < nv && getb(extra, v) && val[v] == 0;
+        const uint64_t m = __ballot(f);
+        if (f) {
+          val[v] = -1; reason[v] = R_EXTRA; rnd[v] = rd; dix[v] = -1;
+          trail[tlen + __popcll(m & lanemask_lt())] = 2 * v + 1;
+        }
+        tlen += __popcll(m);
+      }
+      wsync();
+      return 1;
+    }
+    return 0;
+  }
+
+  __device__ int propagate() {
+    for (;;) {
+      if (qhead == tlen) {
+        if (extra_mode) {
+          const int r = extra_check();
+          if (r < 0) return -1;
+          if (r > 0) continue;
+        }
+        return tlen == nv ? 1 : 0;
+      }
+      const int lo = qhead, hi = tlen, rd = ++round;
+      qhead = hi;
+      begin_round();
+      for (int base = lo; base < hi; base += 64) {
+        const int i = base + lane;
+        int cnt = 0, a = 0;
+        if (i < hi) {
+          const int l = trail[i];
+          a = w_off[l];
+          cnt = w_off[l + 1] - a;
+        }
+        const int incl = wave_incl_scan(cnt);
+        const int total = __shfl(incl, 63);
+        pre[lane] = incl - cnt;
+        preA[lane] = a;
+        wsync();
+        for (int t = lane; t < total; t += 64) {
+          int lo2 = 0, hi2 = 63;  // last frontier entry whose range starts at or before t
+          while (lo2 < hi2) {
+            const int mid = (lo2 + hi2 + 1) >> 1;
+            if (pre[mid] <= t) lo2 = mid; else hi2 = mid - 1;
+          }
+          const int r = w[preA[lo2] + (t - pre[lo2])];
+          if (row_on(r)) eval_row(r);
+        }
+        wsync();
+      }
+      eval_learned();
+      if (finish_round(rd) < 0) return -1;
+    }
+  }
+
+  __device__ int base_propagate() {
+    const int rd = ++round;
+    begin_round();
+    for (int r = lane; r < nrows; r += 64)
+      if (row_on(r)) eval_row(r);
+    eval_learned();
+    if (finish_round(rd) < 0) return -1;
+    return propagate();
+  }
+
+  __device__ void truncate_to(int mark) {
+    for (int i = mark + lane; i < tlen; i += 64) val[trail[i] >> 1] = 0;
+    tlen = qhead = mark;
+    wsync();
+  }
+
+  // gini Untest() (search.go:84): the learned rows decide the restored scope
+  __device__ int untest_to(int mark) {
+    truncate_to(mark);
+    if (learn_on && nl > 0) {
+      const int rd = ++round;
+      begin_round();
+      eval_learned();
+      if (finish_round(rd) < 0) return -1;
+      return propagate();
+    }
+    return tlen == nv ? 1 : 0;
+  }
+
+  __device__ void assign_one(int l, int why, int rd, int decision) {
+    if (lane == 0) {
+      const int v = l >> 1;
+      val[v] = (l & 1) ? -1 : 1; reason[v] = why; rnd[v] = rd; dix[v] = decision; trail[tlen] = l;
+    }
+    ++tlen;
+    wsync();
+  }
+
+  // gini Assume(m) + Test() (search.go:75-76)
+  __device__ int test_assume(int l) {
+    ++steps;
+    const int x = lit_val(l);
+    if (x > 0) return propagate();
+    if (x < 0) { ck = CK_ASSUME; c_var = l >> 1; return -1; }
+    assign_one(l, R_DEC, ++round, -1);
+    return propagate();
+  }
+
+  // ------------------------------------------------------------------
+  // conflict analysis (oracle: analyze)
+  // ------------------------------------------------------------------
+  __device__ __forceinline__ void mark_push(int v) {
+    const uint32_t bit = 1u << (v & 31);
+    const uint32_t old = atomicOr(&seen[v >> 5], bit);
+    if (!(old & bit)) touched[atomicAdd(&scal[S_NWORK], 1)] = v;
+  }
+  __device__ __forceinline__ void set_bit_atomic(uint32_t* b, int i) { atomicOr(&b[i >> 5], 1u << (i & 31)); }
+
+  // antecedents of row r for variable u (assigned in round bound_rd); serial
+  // in the calling lane
+  __device__ void ante_serial(int r, int u, int bound_rd) {
+    if (r < nc || r >= nrows) {
+      const int32_t* lits = clause_lits;
+      int a, b;
+      if (r < nc) { a = clause_off[r]; b = clause_off[r + 1]; set_bit_atomic(used, clause_id[r]); }
+      else { lits = l_lits; a = l_off[r - nrows]; b = l_off[r - nrows + 1]; }
+      for (int j = a; j < b; ++j) {
+        const int v = lits[j] >> 1;
+        if (v != u) mark_push(v);
+      }
+    } else {
+      const int k = r - nc;
+      set_bit_atomic(used, card_id[k]);
+      for (int j = card_off[k]; j < card_off[k + 1]; ++j) {
+        const int v = card_lits[j];
+        if (v != u && val[v] > 0 && rnd[v] < bound_rd) mark_push(v);
+      }
+    }
+  }
+  __device__ void extra_serial(int u, int bound_rd) {
+    for (int v = 0; v < nv; ++v)
+      if (v != u && getb(extra, v) && val[v] > 0 && rnd[v] < bound_rd) mark_push(v);
+  }
+
+  __device__ void analyze() {
+    scal[S_NWORK] = 0;
+    wsync();
+    if (lane == 0) {
+      if (ck == CK_ROW) ante_serial(c_row, -1, INF);
+      else if (ck == CK_VAR) { ante_serial(c_rp, c_var, c_row); ante_serial(c_rn, c_var, c_row); }
+      else if (ck == CK_EXTRA) extra_serial(-1, INF);
+    }
+    wsync();
+    int head = 0;
+    for (;;) {
+      const int nw = scal[S_NWORK];
+      if (head >= nw) break;
+      for (int i = head + lane; i < nw; i += 64) {
+        const int u = touched[i];
+        const int r = reason[u];
+        if (r >= 0) ante_serial(r, u, rnd[u]);
+        else if (r == R_EXTRA) extra_serial(u, rnd[u]);
+        else if (dix[u] >= 0) set_bit_atomic(dset, dix[u]);
+        else if (collect_guess && getb(inS, u)) set_bit_atomic(fg, u);
+      }
+      head = nw;
+      wsync();
+    }
+    const int nw = scal[S_NWORK];
+    for (int i = lane; i < nw; i += 64) {
+      const int v = touched[i];
+      atomicAnd(&seen[v >> 5], ~(1u << (v & 31)));
+    }
+    wsync();
+  }
+
+  // ------------------------------------------------------------------
+  // Solve(): CDCL from a consistent fixpoint (oracle: first_violated / dpll)
+  // ------------------------------------------------------------------
+  __device__ int first_violated() {
+    for (int base = 0; base < nc; base += 64) {
+      const int c = base + lane;
+      bool viol = false;
+      int fu = -1;
+      if (c < nc && row_on(c)) {
+        viol = true;
+        for (int j = clause_off[c]; j < clause_off[c + 1]; ++j) {
+          const int l = clause_lits[j];
+          const int x = val[l >> 1];
+          if (l & 1) {
+            if (x != 1) { viol = false; break; }
+          } else {
+            if (x == 1) { viol = false; break; }
+            if (x == 0 && fu < 0) fu = l;
+          }
+        }
+      }
+      const uint64_t m = __ballot(viol);
+      if (m) return __shfl(fu, __ffsll((unsigned long long)m) - 1);
+    }
+    return -1;
+  }
+
+  __device__ void save_model() {
+    for (int base = 0; base < nv; base += 64) {
+      const int v = base + lane;
+      const uint64_t m = __ballot(v < nv && val[v] > 0);
+      if (lane == 0) {
+        model[base >> 5] = (uint32_t)m;
+        if ((base >> 5) + 1 < nbv) model[(base >> 5) + 1] = (uint32_t)(m >> 32);
+      }
+    }
+    wsync();
+  }
+
+  __device__ void clear_bits(uint32_t* b, int n) {
+    for (int i = lane; i < bits_words(n); i += 64) b[i] = 0;
+    wsync();
+  }
+
+  __device__ int dpll() {
+    const int root = tlen, nl0 = nl;
+    int nd = 0, r;
+    for (;;) {
+      const int l = first_violated();
+      if (l < 0) { save_model(); r = RS_SAT; break; }
+      if (++steps > budget) { budget_hit = true; r = RS_BUDGET; break; }
+      if (lane == 0) {
+        d_lit[nd] = l; d_mark[nd] = tlen;
+        d_flip[nd >> 5] &= ~(1u << (nd & 31));
+      }
+      assign_one(l, R_DEC, ++round, nd);
+      ++nd;
+      int res = propagate();
+      bool unsat = false;
+      while (res < 0) {
+        clear_bits(dset, nd);
+        analyze();
+        // h = highest decision reached, b = the next one below (or -1)
+        int h = -1, b = -1, n = 0;
+        for (int wi = bits_words(nd) - 1; wi >= 0 && b < 0; --wi) {
+          uint32_t x = dset[wi];
+          while (x && b < 0) {
+            const int i = wi * 32 + 31 - __clz(x);
+            x &= ~(1u << (i & 31));
+            if (h < 0) h = i; else b = i;
+          }
+        }
+        for (int wi = 0; wi < bits_words(nd); ++wi) n += __popc(dset[wi]);
+        if (h < 0) { unsat = true; break; }
+        if (++steps > budget) { budget_hit = true; r = RS_BUDGET; goto done; }
+        const int lat = l_off[nl];
+        if (nl < L_MAX && lat + n <= lcap) {
+          // learned row: negated decisions, ascending decision index
+          int at = lat;
+          for (int base = 0; base < nd; base += 64) {
+            const int i = base + lane;
+            const bool in = i < nd && getb(dset, i);
+            const uint64_t m = __ballot(in);
+            if (in) l_lits[at + __popcll(m & lanemask_lt())] = d_lit[i] ^ 1;
+            at += __popcll(m);
+          }
+          if (lane == 0) l_off[nl + 1] = at;
+          ++nl;
+          wsync();
+          nd = b + 1;
+          truncate_to(d_mark[nd]);
+          assign_one(d_lit[h] ^ 1, nrows + nl - 1, ++round, -1);
+        } else {
+          while (nd > 0 && getb(d_flip, nd - 1)) --nd;
+          if (nd == 0) { unsat = true; break; }
+          truncate_to(d_mark[nd - 1]);
+          if (lane == 0) d_flip[(nd - 1) >> 5] |= 1u << ((nd - 1) & 31);
+          wsync();
+          assign_one(d_lit[nd - 1] ^ 1, R_DEC, ++round, nd - 1);
+        }
+        res = propagate();
+      }
+      if (unsat) { r = RS_UNSAT; break; }
+    }
+  done:
+    truncate_to(root);
+    nl = nl0;
+    return r;
+  }
+
+  // ------------------------------------------------------------------
+  // search.Do (search.go:158-203)
+  // ------------------------------------------------------------------
+  int dq_head, dq_n, ng, result;
+  bool class_b, solve_unsat, last_solve;
+
+  __device__ __forceinline__ int list_len(int list) const {
+    return list < 0 ? 1 : choice_off[list + 1] - choice_off[list];
+  }
+  __device__ __forceinline__ int list_at(int list, int i) const {
+    return list < 0 ? ~list : choice_lits[choice_off[list] + i];
+  }
+  __device__ __forceinline__ void dq_push_back(int list, int idx) {
+    const int at = (dq_head + dq_n) % cap;
+    if (lane == 0) { dq[2 * at] = list; dq[2 * at + 1] = idx; }
+    ++dq_n;
+  }
+  __device__ __forceinline__ void dq_push_front(int list, int idx) {
+    dq_head = (dq_head + cap - 1) % cap;
+    if (lane == 0) { dq[2 * dq_head] = list; dq[2 * dq_head + 1] = idx; }
+    ++dq_n;
+  }
+
+  // PushGuess, search.go:34-77
+  __device__ void push_guess() {
+    wsync();
+    const int list = dq[2 * dq_head], idx = dq[2 * dq_head + 1];
+    dq_head = (dq_head + 1) % cap;
+    --dq_n;
+    const int len = list_len(list);
+    int m = idx < len ? list_at(list, idx) : -1;
+    bool any = false;
+    for (int i = lane; i < len; i += 64) any |= getb(inS, list_at(list, i));
+    if (__ballot(any)) m = -1;
+    else if (idx >= len) class_b = true;  // exhausted choice
+    int children = 0;
+    if (m >= 0)
+      for (int r = var_choice_off[m]; r < var_choice_off[m + 1]; ++r) {
+        dq_push_back(r, 0);
+        ++children;
+      }
+    if (lane == 0) {
+      int32_t* g = stk + 5 * ng;
+      g[0] = list; g[1] = idx; g[2] = m; g[3] = children; g[4] = tlen;
+    }
+    ++ng;
+    wsync();
+    if (m < 0) return;
+    if (lane == 0) inS[m >> 5] |= 1u << (m & 31);
+    wsync();
+    if (steps >= budget) { budget_hit = true; result = 0; return; }
+    result = test_assume(2 * m);
+    last_solve = false;
+  }
+
+  // PopGuess, search.go:79-98
+  __device__ void pop_guess() {
+    wsync();
+    --ng;
+    const int32_t* g = stk + 5 * ng;
+    const int list = g[0], idx = g[1], m = g[2], children = g[3], mark = g[4];
+    wsync();
+    if (m >= 0) {
+      if (lane == 0) inS[m >> 5] &= ~(1u << (m & 31));
+      wsync();
+      result = untest_to(mark);
+      last_solve = false;
+    }
+    dq_n -= children;
+    dq_push_front(list, idx + (m >= 0 ? 1 : 0));
+    wsync();
+  }
+
+  // Solve() within the search: a failure learns the nogood of the guesses its
+  // refutation reached (oracle: be_solve / learn)
+  __device__ int search_solve() {
+    clear_bits(fg, nv);
+    collect_guess = true;
+    const int r = dpll();
+    collect_guess = false;
+    if (r == RS_UNSAT) {
+      int n = 0;
+      for (int wi = 0; wi < nbv; ++wi) n += __popc(fg[wi]);
+      const int lat = l_off[nl];
+      if (nl < L_MAX && lat + n <= lcap) {
+        int at = lat;
+        for (int base = 0; base < nv; base += 64) {
+          const int v = base + lane;
+          const bool in = v < nv && getb(fg, v);
+          const uint64_t m = __ballot(in);
+          if (in) l_lits[at + __popcll(m & lanemask_lt())] = 2 * v + 1;
+          at += __popcll(m);
+        }
+        if (lane == 0) l_off[nl + 1] = at;
+        ++nl;
+        wsync();
+      }
+    }
+    return r;
+  }
+
+  // Returns the search result; leaves the final guess set in inS.
+  __device__ int search() {
+    dq_head = dq_n = ng = 0;
+    result = 0;
+    class_b = solve_unsat = last_solve = false;
+    for (int i = 0; i < na; ++i) dq_push_back(~anchors[i], 0);
+    wsync();
+    for (;;) {
+      if (dq_n == 0 && result == 0) {
+        const int r = search_solve();
+        if (r == RS_BUDGET) { result = RS_BUDGET; break; }
+        result = r;
+        last_solve = (r == RS_SAT);
+        if (r == RS_UNSAT) solve_unsat = true;
+      }
+      if (result < 0) {
+        if (ng == 0) break;
+        pop_guess();
+        continue;
+      }
+      if (dq_n == 0) break;
+      push_guess();
+      if (budget_hit) { result = RS_BUDGET; break; }
+    }
+    // Value() after an ending on Test()==1 reads that scope's full assignment
+    if (result == 1 && !last_solve) save_model();
+    return result;
+  }
+
+  // ------------------------------------------------------------------
+  // NotSatisfiable (oracle: refute / core_extract)
+  // ------------------------------------------------------------------
+  __device__ void reset_all() { truncate_to(0); }
+
+  __device__ void fill_bits(uint32_t* b, int n, bool ones) {
+    const int nw = bits_words(n);
+    for (int i = lane; i < nw; i += 64) {
+      uint32_t x = 0;
+      if (ones) x = (i == nw - 1 && (n & 31)) ? ((1u << (n & 31)) - 1u) : 0xffffffffu;
+      b[i] = x;
+    }
+    wsync();
+  }
+  __device__ void copy_bits(uint32_t* dst, const uint32_t* src, int n) {
+    for (int i = lane; i < bits_words(n); i += 64) dst[i] = src[i];
+    wsync();
+  }
+
+  __device__ int refute(const uint32_t* K) {
+    reset_all();
+    learn_on = false;
+    enabled = K;
+    fill_bits(used, nid, false);
+    int r;
+    if (base_propagate() < 0) { analyze(); r = RS_UNSAT; }
+    else r = dpll();
+    reset_all();
+    enabled = nullptr;
+    learn_on = true;
+    return r;
+  }
+
+  __device__ int core(int32_t* out, int32_t& flags) {
+    const int64_t saved = steps;
+    steps = 0;
+    int len = 0;
+    fill_bits(en, nid, true);
+    int r = refute(en);
+    if (r == RS_UNSAT) {
+      copy_bits(en, used, nid);
+      for (int id = 0; id < nid; ++id) {
+        if (!getb(en, id)) continue;
+        copy_bits(en2, en, nid);
+        if (lane == 0) en2[id >> 5] &= ~(1u << (id & 31));
+        wsync();
+        r = refute(en2);
+        if (r == RS_UNSAT) copy_bits(en, used, nid);
+        else if (r == RS_BUDGET) { flags |= DP_F_CORE_BUDGET; break; }
+      }
+      for (int base = 0; base < nid; base += 64) {  // ascending identity ids
+        const int id = base + lane;
+        const bool in = id < nid && getb(en, id);
+        const uint64_t m = __ballot(in);
+        if (in) out[len + __popcll(m & lanemask_lt())] = id;
+        len += __popcll(m);
+      }
+    } else {
+      flags |= DP_F_CORE_BUDGET;
+    }
+    budget_hit = false;
+    steps += saved;
+    return len;
+  }
+
+  // ------------------------------------------------------------------
+  // SAT epilogue, solve.go:86-110 (oracle: epilogue)
+  // ------------------------------------------------------------------
+  __device__ int epilogue(int32_t& flags, uint32_t* __restrict__ out) {
+    for (int i = lane; i < nbv; i += 64) extra[i] = model[i] & ~inS[i];
+    wsync();
+    int ne = 0;
+    for (int i = 0; i < nbv; ++i) ne += __popc(extra[i]);
+    if (ne == 0) {
+      for (int i = lane; i < nbv; i += 64) out[i] = inS[i];
+      return DP_SAT;
+    }
+    flags |= DP_F_EPILOGUE;
+    reset_all();
+    if (base_propagate() < 0) return DP_ERROR;
+    const int rd = ++round;
+    bool bad = false;
+    for (int base = 0; base < nv; base += 64) {
+      const int v = base + lane;
+      bool f = false;
+      int l = 0;
+      if (v < nv && !getb(extra, v)) {
+        const int want = getb(inS, v) ? 1 : -1;
+        if (val[v] == -want) bad = true;
+        if (val[v] == 0) { f = true; l = 2 * v + (want < 0 ? 1 : 0); }
+      }
+      const uint64_t m = __ballot(f);
+      if (f) {
+        val[v] = (l & 1) ? -1 : 1; reason[v] = R_DEC; rnd[v] = rd; dix[v] = -1;
+        trail[tlen + __popcll(m & lanemask_lt())] = l;
+      }
+      tlen += __popcll(m);
+    }
+    wsync();
+    if (__ballot(bad)) return DP_ERROR;
+    if (propagate() < 0) return DP_ERROR;
+    const int mark = tlen;
+    int f = 0;
+    for (int base = 0; base < nv; base += 64) {
+      const int v = base + lane;
+      f += __popcll(__ballot(v < nv && getb(extra, v) && val[v] > 0));
+    }
+    extra_mode = true;
+    for (int wv = f; wv <= ne; ++wv) {
+      truncate_to(mark);
+      extra_w = wv;
+      if (propagate() < 0) continue;
+      const int r = dpll();
+      if (r == RS_SAT) {
+        extra_mode = false;
+        for (int i = lane; i < nbv; i += 64) out[i] = model[i];
+        return DP_SAT;
+      }
+      if (r == RS_BUDGET) { extra_mode = false; return DP_INCOMPLETE; }
+    }
+    extra_mode = false;
+    return DP_ERROR;
+  }
+};
+
+}  // namespace
+
+// One wavefront per problem; blockIdx.x indexes `order` (problems bucketed by
+// working-set footprint; the largest bucket works in HBM scratch).  Outputs: status / flags / installed / core (oracle_solve).
+__global__ void __launch_bounds__(64) solve_kernel(KernelArgs a) {
+  extern __shared__ int32_t lds[];
+  const int pid = a.order[blockIdx.x];
+  const int32_t* grec = a.rec + a.rec_off[pid];
+  int32_t* ws = a.scratch ? a.scratch + a.scratch_off[blockIdx.x] : lds;
+  Wave W;
+  W.init(ws, grec);
+  W.budget = a.budget;
+  uint32_t* inst = a.installed + a.inst_off[pid];
+  int32_t flags = 0;
+  int status;
+  for (int i = W.lane; i < W.nbv; i += 64) inst[i] = 0;
+  const int base = W.base_propagate();
+  if (base < 0) {
+    flags |= DP_F_BASE_UNSAT;
+    status = DP_UNSAT;
+  } else if (base == 1) {
+    flags |= DP_F_SEARCH_SKIPPED;
+    W.save_model();
+    status = W.epilogue(flags, inst);
+  } else {
+    const int r = W.search();
+    if (W.class_b) flags |= DP_F_CLASS_B;
+    if (W.solve_unsat) flags |= DP_F_SOLVE_UNSAT;
+    if (r == RS_BUDGET) {
+      flags |= DP_F_BUDGET;
+      status = DP_INCOMPLETE;
+    } else if (r < 0) {
+      status = DP_UNSAT;
+    } else {
+      status = W.epilogue(flags, inst);
+      if (status == DP_INCOMPLETE) flags |= DP_F_BUDGET;
+    }
+  }
+  int clen = 0;
+  if (status == DP_UNSAT) clen = W.core(a.core + a.core_off[pid], flags);
+  if (W.lane == 0) {
+    a.status[pid] = (int8_t)status;
+    a.flags[pid] = flags;
+    a.core_len[pid] = clen;
+    a.steps[pid] = W.steps;
+  }
+}
+
+}  // namespace dp
+
+namespace dp {
+
+hipError_t launch_solve(const KernelArgs& a, int n_blocks, int lds_bytes, hipStream_t stream) {
+  if (n_blocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(solve_kernel, dim3((unsigned)n_blocks), dim3(64), (size_t)lds_bytes, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t configure_solve_kernel(int max_lds_bytes) {
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(&solve_kernel),
+                             hipFuncAttributeMaxDynamicSharedMemorySize, max_lds_bytes);
+}
+
+}  // namespace dp

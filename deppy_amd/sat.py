@@ -1,0 +1,463 @@
+"""The deppy `pkg/sat` API, backed by the MI355X engine.
+
+Mirrors /root/reference/pkg/sat so callers (pkg/solver, entitysource users) and
+tests read the same as the reference's:
+
+    s, err = NewSolver(WithInput(variables), WithTracer(t))     # solve.go:121-146
+    installed, err = s.Solve(ctx)                                 # solve.go:53-119
+
+Errors are returned as values, as in Go: DuplicateIdentifier from NewSolver
+(lit_mapping.go:52-54); NotSatisfiable (solve.go:18-30), ErrIncomplete
+(solve.go:14) or a lookup error ("%d errors encountered: ...",
+lit_mapping.go:119-128) from Solve.  Installed variables come back in input
+order and are the caller's own Variable objects (lit_mapping.go:176-184).
+
+Solve() lowers the input (C++ dp_lower), solves it on the GPU (dp_solve) and
+maps the result back.  There is no CPU path: without the HIP library or an
+MI355X, Solve raises RuntimeError.  SolveBatch() solves many inputs in one
+launch — the data-parallel form this engine exists for.
+"""
+from __future__ import annotations
+
+import io
+import threading
+from dataclasses import dataclass, field
+from typing import Iterable, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+
+MANDATORY, PROHIBITED, DEPENDENCY, CONFLICT, ATMOST = 1, 2, 3, 4, 5
+SAT, UNSAT, INCOMPLETE, ERROR = 1, -1, 0, -2
+
+
+# ---------------------------------------------------------------------------
+# variable.go
+# ---------------------------------------------------------------------------
+class Identifier(str):
+    """variable.go:5-16"""
+
+    def String(self) -> str:
+        return str(self)
+
+
+def IdentifierFromString(s: str) -> Identifier:
+    return Identifier(s)
+
+
+class Variable:
+    """variable.go:19-27: anything with Identifier() and Constraints()."""
+
+    def Identifier(self) -> Identifier:  # pragma: no cover - interface
+        raise NotImplementedError
+
+    def Constraints(self) -> list:  # pragma: no cover - interface
+        raise NotImplementedError
+
+
+class zeroVariable(Variable):
+    def Identifier(self):
+        return Identifier("")
+
+    def Constraints(self):
+        return []
+
+
+# ---------------------------------------------------------------------------
+# constraints.go
+# ---------------------------------------------------------------------------
+def _ids(ids) -> tuple:
+    return tuple(Identifier(i) for i in ids)
+
+
+@dataclass(frozen=True)
+class Constraint:
+    """constraints.go:13-18.  Apply(c, lm, subject) is replaced by the C++
+    lowering (deppy_amd/csrc/lower.cpp); String/Order/Anchor are as in Go."""
+    kind: int
+    ids: tuple = ()
+    n: int = 0
+
+    def String(self, subject) -> str:
+        s = str(subject)
+        if self.kind == MANDATORY:
+            return "%s is mandatory" % s  # constraints.go:57
+        if self.kind == PROHIBITED:
+            return "%s is prohibited" % s  # :81
+        if self.kind == DEPENDENCY:
+            if not self.ids:
+                return "%s has a dependency without any candidates to satisfy it" % s  # :108
+            return "%s requires at least one of %s" % (s, ", ".join(self.ids))  # :110-114
+        if self.kind == CONFLICT:
+            return "%s conflicts with %s" % (s, self.ids[0])  # :145
+        if self.kind == ATMOST:
+            return "%s permits at most %d of %s" % (s, self.n, ", ".join(self.ids))  # :173-177
+        return ""
+
+    def Order(self) -> Optional[list]:
+        """constraints.go:125-127; nil for every other kind."""
+        if self.kind == DEPENDENCY:
+            return list(self.ids)
+        return None
+
+    def Anchor(self) -> bool:
+        return self.kind == MANDATORY  # constraints.go:68-70
+
+    def __repr__(self):
+        names = {MANDATORY: "Mandatory", PROHIBITED: "Prohibited", DEPENDENCY: "Dependency",
+                 CONFLICT: "Conflict", ATMOST: "AtMost"}
+        args = ([str(self.n)] if self.kind == ATMOST else []) + [repr(str(i)) for i in self.ids]
+        return "%s(%s)" % (names.get(self.kind, "?"), ", ".join(args))
+
+
+def Mandatory() -> Constraint:
+    return Constraint(MANDATORY)
+
+
+def Prohibited() -> Constraint:
+    return Constraint(PROHIBITED)
+
+
+def Dependency(*ids) -> Constraint:
+    return Constraint(DEPENDENCY, _ids(ids))
+
+
+def Conflict(id) -> Constraint:
+    return Constraint(CONFLICT, (Identifier(id),))
+
+
+def AtMost(n: int, *ids) -> Constraint:
+    return Constraint(ATMOST, _ids(ids), int(n))
+
+
+class zeroConstraint(Constraint):
+    def __init__(self):
+        super().__init__(0)
+
+
+@dataclass(eq=False)
+class AppliedConstraint:
+    """constraints.go:43-52"""
+    Variable: Variable
+    Constraint: Constraint
+
+    def String(self) -> str:
+        return self.Constraint.String(self.Variable.Identifier())
+
+    def __str__(self):
+        return self.String()
+
+    def __eq__(self, other):
+        return (isinstance(other, AppliedConstraint) and _var_eq(self.Variable, other.Variable)
+                and self.Constraint == other.Constraint)
+
+    def __repr__(self):
+        return "AppliedConstraint(%r, %r)" % (str(self.Variable.Identifier()), self.Constraint)
+
+
+def _var_eq(a, b) -> bool:
+    return (a is b) or (a.Identifier() == b.Identifier() and
+                        list(a.Constraints()) == list(b.Constraints()))
+
+
+# ---------------------------------------------------------------------------
+# errors (solve.go:14-30, lit_mapping.go:12-16, 119-128)
+# ---------------------------------------------------------------------------
+class SatError(Exception):
+    def Error(self) -> str:
+        return str(self)
+
+
+class NotSatisfiable(SatError):
+    """A (deletion-minimal, verified) set of applied constraints that cannot
+    hold together (solve.go:16-30)."""
+
+    def __init__(self, applied: Iterable[AppliedConstraint] = ()):
+        self.applied = list(applied)
+        super().__init__(self.Error())
+
+    def Error(self) -> str:
+        msg = "constraints not satisfiable"
+        if not self.applied:
+            return msg
+        return msg + ": " + ", ".join(a.String() for a in self.applied)
+
+    def __str__(self):
+        return self.Error()
+
+    def __iter__(self):
+        return iter(self.applied)
+
+    def __len__(self):
+        return len(self.applied)
+
+    def __getitem__(self, i):
+        return self.applied[i]
+
+    def __eq__(self, other):
+        if isinstance(other, NotSatisfiable):
+            return self.applied == other.applied
+        return NotImplemented
+
+    def __hash__(self):
+        return id(self)
+
+
+class DuplicateIdentifier(SatError):
+    def __init__(self, ident, msg: Optional[str] = None):
+        self.identifier = Identifier(ident)
+        super().__init__(msg or 'duplicate identifier "%s" in input' % ident)
+
+    def __eq__(self, other):
+        return isinstance(other, DuplicateIdentifier) and self.identifier == other.identifier
+
+    def __hash__(self):
+        return hash(self.identifier)
+
+
+class _Incomplete(SatError):
+    pass
+
+
+ErrIncomplete = _Incomplete("cancelled before a solution could be found")
+
+
+class LookupErrors(SatError):
+    """The aggregate returned by LitMapping.Error() (lit_mapping.go:119-128)."""
+
+
+class InternalError(SatError):
+    pass
+
+
+# ---------------------------------------------------------------------------
+# tracer.go
+# ---------------------------------------------------------------------------
+class SearchPosition:
+    def Variables(self) -> list:  # pragma: no cover - interface
+        raise NotImplementedError
+
+    def Conflicts(self) -> list:  # pragma: no cover - interface
+        raise NotImplementedError
+
+
+class Tracer:
+    def Trace(self, p: SearchPosition) -> None:  # pragma: no cover - interface
+        raise NotImplementedError
+
+
+class DefaultTracer(Tracer):
+    def Trace(self, p):
+        pass
+
+
+class LoggingTracer(Tracer):
+    """tracer.go:22-35"""
+
+    def __init__(self, Writer: io.TextIOBase):
+        self.Writer = Writer
+
+    def Trace(self, p):
+        self.Writer.write("---\nAssumptions:\n")
+        for v in p.Variables():
+            self.Writer.write("- %s\n" % v.Identifier())
+        self.Writer.write("Conflicts:\n")
+        for a in p.Conflicts():
+            self.Writer.write("- %s\n" % a)
+
+
+# ---------------------------------------------------------------------------
+# solver (solve.go:32-163)
+# ---------------------------------------------------------------------------
+_ctx_lock = threading.Lock()
+_ctx: Optional[_lib.Context] = None
+
+
+def device_context() -> _lib.Context:
+    """The process-wide device context (device 0 of HIP_VISIBLE_DEVICES unless
+    set_device() chose another)."""
+    global _ctx
+    with _ctx_lock:
+        if _ctx is None:
+            _ctx = _lib.Context(_device[0], 1)
+        return _ctx
+
+
+_device = [0]
+
+
+def set_device(ordinal: int, step_budget: int = 0) -> None:
+    """Bind this process to one MI355X (one process per GPU)."""
+    global _ctx
+    with _ctx_lock:
+        if _ctx is not None:
+            _ctx.close()
+        _device[0] = ordinal
+        _ctx = _lib.Context(ordinal, 1, step_budget)
+
+
+class _Input:
+    __slots__ = ("variables", "err")
+
+    def __init__(self, variables):
+        self.variables = list(variables) if variables is not None else []
+        self.err = None
+
+
+def encode_inputs(inputs: Sequence[Sequence[Variable]]) -> _lib.WireArrays:
+    """[]Variable per problem -> wire arrays (identifiers interned per batch)."""
+    strs: dict = {}
+    str_bytes = bytearray()
+    str_off = [0]
+
+    def sid(x) -> int:
+        b = str(x).encode("utf-8", "surrogateescape")
+        i = strs.get(b)
+        if i is None:
+            i = len(str_off) - 1
+            strs[b] = i
+            str_bytes.extend(b)
+            str_off.append(len(str_bytes))
+        return i
+
+    pvo, vid, vco, ck, cn, cao, ca = [0], [], [0], [], [], [0], []
+    for variables in inputs:
+        for v in variables:
+            vid.append(sid(v.Identifier()))
+            cons = v.Constraints() or []
+            for c in cons:
+                ck.append(c.kind)
+                cn.append(c.n)
+                for a in c.ids:
+                    ca.append(sid(a))
+                cao.append(len(ca))
+            vco.append(vco[-1] + len(cons))
+        pvo.append(len(vid))
+    return _lib.WireArrays(pvo, vid, vco, ck, cn, cao, ca, str_off, bytes(str_bytes), True)
+
+
+class Solver:
+    """solve.go:32-34"""
+
+    def Solve(self, ctx=None):  # pragma: no cover - interface
+        raise NotImplementedError
+
+
+class _solver(Solver):
+    def __init__(self):
+        self.input: Optional[_Input] = None
+        self.tracer: Optional[Tracer] = None
+
+    def Solve(self, ctx=None):
+        """Returns (installed []Variable in input order | None, error | None).
+        ctx is accepted for signature parity; like the reference (solve.go:83)
+        a single solve is not interruptible."""
+        return SolveBatch([self.input.variables], tracer=self.tracer)[0]
+
+
+def NewSolver(*options):
+    """solve.go:121-129: options first, then defaults."""
+    s = _solver()
+    for opt in list(options) + _defaults:
+        err = opt(s)
+        if err is not None:
+            return None, err
+    return s, None
+
+
+def WithInput(input: Sequence[Variable]):
+    def opt(s: _solver):
+        s.input = _Input(input)
+        err = _duplicate(s.input.variables)
+        return err
+    return opt
+
+
+def WithTracer(t: Tracer):
+    def opt(s: _solver):
+        s.tracer = t
+        return None
+    return opt
+
+
+def _default_input(s: _solver):
+    if s.input is None:
+        s.input = _Input([])
+    return None
+
+
+def _default_tracer(s: _solver):
+    if s.tracer is None:
+        s.tracer = DefaultTracer()
+    return None
+
+
+_defaults = [_default_input, _default_tracer]
+
+
+def _duplicate(variables) -> Optional[DuplicateIdentifier]:
+    seen = set()
+    for v in variables:
+        i = v.Identifier()
+        if i in seen:
+            lw = _lib.Lowered(encode_inputs([variables]))  # the library formats %q
+            return DuplicateIdentifier(i, lw.msg[0])
+        seen.add(i)
+    return None
+
+
+def SolveBatch(inputs: Sequence[Sequence[Variable]], tracer: Optional[Tracer] = None,
+               context: Optional[_lib.Context] = None) -> list:
+    """Solve many independent problems in one GPU launch.
+
+    Returns [(installed | None, error | None)] in input order."""
+    inputs = [list(v) for v in inputs]
+    lw = _lib.Lowered(encode_inputs(inputs))
+    out: list = [None] * len(inputs)
+    ok = [p for p in range(len(inputs)) if lw.err[p] == 0]
+    for p in range(len(inputs)):
+        if lw.err[p] == 1:
+            vid = _dup_id(inputs[p])
+            out[p] = (None, DuplicateIdentifier(vid, lw.msg[p]))
+        elif lw.err[p] == 2:
+            out[p] = (None, LookupErrors(lw.msg[p]))
+    if ok:
+        offs = [0]
+        parts = []
+        for p in ok:
+            r = lw.record(p)
+            parts.append(r)
+            offs.append(offs[-1] + len(r))
+        rec = np.concatenate(parts).astype(np.int32)
+        ctx = context or device_context()
+        res = ctx.solve(np.array(offs, np.int64), rec)
+        for j, p in enumerate(ok):
+            variables = inputs[p]
+            st = int(res["status"][j])
+            if st == SAT:
+                inst = _lib.installed_list(res, j, len(variables))
+                out[p] = ([variables[v] for v in inst] or None, None)
+            elif st == UNSAT:
+                i0 = int(lw.ident_off[p])
+                applied = []
+                for ident in _lib.core_list(res, j):
+                    vi = int(lw.ident_var[i0 + ident])
+                    ci = int(lw.ident_con[i0 + ident])
+                    var = variables[vi]
+                    applied.append(AppliedConstraint(var, var.Constraints()[ci]))
+                out[p] = (None, NotSatisfiable(applied))
+            elif st == INCOMPLETE:
+                out[p] = (None, ErrIncomplete)
+            else:
+                out[p] = (None, InternalError("unexpected internal error"))
+    return out
+
+
+def _dup_id(variables):
+    seen = set()
+    for v in variables:
+        if v.Identifier() in seen:
+            return v.Identifier()
+        seen.add(v.Identifier())
+    return Identifier("")

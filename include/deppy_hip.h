@@ -68,6 +68,7 @@ typedef struct dp_wire {
   const int32_t* con_n;        /* [n_cons]   AtMost bound (else ignored) */
   const int64_t* con_arg_off;  /* [n_cons+1] -> con_arg                  */
   const int64_t* con_arg;      /* [n_args]   string index               */
+  int64_t n_strs;
   const int64_t* str_off;      /* [n_strs+1] -> str_bytes               */
   const char* str_bytes;
   int32_t interned; /* 1: equal bytes <=> equal string index (fast path) */

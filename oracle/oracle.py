@@ -46,6 +46,8 @@ def lib():
                                              ctypes.POINTER(ctypes.c_int32)]
         L.oracle_refute.argtypes = [_i32p, ctypes.c_void_p, ctypes.c_int64]
         L.oracle_refute.restype = ctypes.c_int
+        L.oracle_check_model.argtypes = [_i32p, _u32p]
+        L.oracle_check_model.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -111,3 +113,12 @@ def refute(rec, enabled_idents, budget: int = 0) -> int:
     for i in enabled_idents:
         en[i] = 1
     return lib().oracle_refute(rec, en.ctypes.data_as(ctypes.c_void_p), budget)
+
+
+def check_model(rec, installed_words) -> int:
+    """-1 if the installed bitmap satisfies every row of rec, else a violated row."""
+    rec = np.ascontiguousarray(rec, dtype=np.int32)
+    w = np.ascontiguousarray(installed_words, dtype=np.uint32)
+    if len(w) == 0:
+        w = np.zeros(1, np.uint32)
+    return lib().oracle_check_model(rec, w)

@@ -22,8 +22,11 @@
  *  constraints.go:180-186); a variable listed m times counts m.
  *
  *  Test(m)   = assume m, propagate; -1 conflict, 1 all variables assigned, else 0.
- *  Untest()  = truncate the trail to the scope mark; result of the restored scope.
- *  Solve()   = complete search under the open scopes (dpll below).
+ *  Untest()  = truncate the trail to the scope mark; unit propagation of the
+ *              learned rows decides the restored scope's result.
+ *  Solve()   = complete search under the open scopes (dpll below); when it
+ *              fails, the nogood of the guesses its refutation used is learned
+ *              (gini keeps the clauses Solve learns).
  */
 #include "sat_oracle.h"
 
@@ -82,7 +85,16 @@ typedef struct {
   /* dpll decision stack */
   int32_t *d_lit, *d_mark;
   uint8_t* d_flip;
+  /* learned nogoods of failed Solve() calls: rows nrows.. (see learn()) */
+  int32_t *l_off, *l_lits;
+  int32_t nl, lcap, learn_on, collect_guess;
+  uint8_t* fg; /* guesses met by the refutation of the current Solve() */
+  int32_t* dix;    /* decision index of a Solve() decision variable, else -1 */
+  uint8_t* dset;   /* decisions met by the last conflict analysis */
 } st_t;
+
+/* learned-row store: at most L_MAX rows and 2*nv+64 literals */
+#define L_MAX 64
 
 /* ------------------------------------------------------------------ */
 /* record parsing + watch lists                                        */
@@ -111,7 +123,7 @@ static void parse(prob_t* p, const int32_t* rec) {
 }
 
 static int row_ident(const prob_t* p, int r) {
-  return r < p->nc ? p->clause_id[r] : p->card_id[r - p->nc];
+  return r < p->nc ? p->clause_id[r] : r < p->nrows ? p->card_id[r - p->nc] : -1;
 }
 
 static void* xcalloc(size_t n, size_t sz) { return calloc(n ? n : 1, sz); }
@@ -154,6 +166,13 @@ static int st_init(st_t* s, const int32_t* rec) {
   s->d_lit = xcalloc((size_t)nv, sizeof(int32_t));
   s->d_mark = xcalloc((size_t)nv, sizeof(int32_t));
   s->d_flip = xcalloc((size_t)nv, 1);
+  s->lcap = 4 * nv + 256;
+  s->l_off = xcalloc(L_MAX + 1, sizeof(int32_t));
+  s->l_lits = xcalloc((size_t)s->lcap, sizeof(int32_t));
+  s->fg = xcalloc((size_t)nv, 1);
+  s->dix = xcalloc((size_t)nv, sizeof(int32_t));
+  s->dset = xcalloc((size_t)nv + 1, 1);
+  s->learn_on = 1;
   return 0;
 }
 
@@ -161,7 +180,7 @@ static void st_free(st_t* s) {
   free(s->w_off); free(s->w); free(s->val); free(s->reason); free(s->rnd); free(s->trail);
   free(s->imp_pos); free(s->imp_neg); free(s->touched); free(s->is_extra); free(s->seen);
   free(s->used); free(s->work); free(s->inS); free(s->model); free(s->d_lit); free(s->d_mark);
-  free(s->d_flip);
+  free(s->d_flip); free(s->l_off); free(s->l_lits); free(s->fg); free(s->dix); free(s->dset);
 }
 
 /* ------------------------------------------------------------------ */
@@ -189,17 +208,24 @@ static inline void note(st_t* s, int l, int r) {
 
 /* Evaluate one row against the current assignment (start-of-round snapshot:
  * nothing is committed while a round is being evaluated). */
+static void eval_clause(st_t* s, int r, const int32_t* lits, int a, int b, int* crow) {
+  int nun = 0, ul = -1;
+  for (int j = a; j < b; ++j) {
+    int x = lit_val(s, lits[j]);
+    if (x > 0) return; /* satisfied */
+    if (x == 0) { ++nun; ul = lits[j]; }
+  }
+  if (nun == 0) { if (r < *crow) *crow = r; }
+  else if (nun == 1) note(s, ul, r);
+}
+
 static void eval_row(st_t* s, int r, int* crow) {
   const prob_t* p = &s->p;
   if (r < p->nc) {
-    int a = p->clause_off[r], b = p->clause_off[r + 1], nun = 0, ul = -1;
-    for (int j = a; j < b; ++j) {
-      int x = lit_val(s, p->clause_lits[j]);
-      if (x > 0) return; /* satisfied */
-      if (x == 0) { ++nun; ul = p->clause_lits[j]; }
-    }
-    if (nun == 0) { if (r < *crow) *crow = r; }
-    else if (nun == 1) note(s, ul, r);
+    eval_clause(s, r, p->clause_lits, p->clause_off[r], p->clause_off[r + 1], crow);
+  } else if (r >= p->nrows) {
+    int j = r - p->nrows;
+    eval_clause(s, r, s->l_lits, s->l_off[j], s->l_off[j + 1], crow);
   } else {
     int k = r - p->nc, a = p->card_off[k], b = p->card_off[k + 1], cnt = 0, nun = 0;
     for (int j = a; j < b; ++j) {
@@ -227,6 +253,7 @@ static inline void assign(st_t* s, int l, int reason, int rd) {
   s->val[v] = (l & 1) ? -1 : 1;
   s->reason[v] = reason;
   s->rnd[v] = rd;
+  s->dix[v] = -1;
   s->trail[s->tlen++] = l;
 }
 
@@ -278,6 +305,12 @@ static int extra_check(st_t* s) {
   return 0;
 }
 
+/* Learned rows are evaluated in every round (they are few). */
+static void eval_learned(st_t* s, int* crow) {
+  if (!s->learn_on) return;
+  for (int j = 0; j < s->nl; ++j) eval_row(s, s->p.nrows + j, crow);
+}
+
 static int propagate(st_t* s) {
   for (;;) {
     if (s->qhead == s->tlen) {
@@ -295,6 +328,7 @@ static int propagate(st_t* s) {
       for (int k = s->w_off[l]; k < s->w_off[l + 1]; ++k)
         if (row_on(s, s->w[k])) eval_row(s, s->w[k], &crow);
     }
+    eval_learned(s, &crow);
     if (finish_round(s, rd, crow) < 0) return -1;
   }
 }
@@ -305,6 +339,7 @@ static int base_propagate(st_t* s) {
   int rd = ++s->round, crow = INF;
   for (int r = 0; r < s->p.nrows; ++r)
     if (row_on(s, r)) eval_row(s, r, &crow);
+  eval_learned(s, &crow);
   if (finish_round(s, rd, crow) < 0) return -1;
   return propagate(s);
 }
@@ -312,6 +347,19 @@ static int base_propagate(st_t* s) {
 static void truncate_to(st_t* s, int mark) {
   while (s->tlen > mark) s->val[s->trail[--s->tlen] >> 1] = 0;
   s->qhead = s->tlen;
+}
+
+/* gini Untest(): close the scope and report the restored scope's consistency
+ * under unit propagation, learned rows included (search.go:84). */
+static int untest_to(st_t* s, int mark) {
+  truncate_to(s, mark);
+  if (s->learn_on && s->nl > 0) {
+    int rd = ++s->round, crow = INF;
+    eval_learned(s, &crow);
+    if (finish_round(s, rd, crow) < 0) return -1;
+    return propagate(s);
+  }
+  return s->tlen == s->p.nv ? 1 : 0;
 }
 
 /* gini Assume(m) + Test(): one scope, one BCP. */
@@ -331,13 +379,17 @@ static int test_assume(st_t* s, int l) {
 static void push_ante(st_t* s, int r, int u, int bound_rd) {
   const prob_t* p = &s->p;
   if (r < 0) return;
-  s->used[row_ident(p, r)] = 1;
-  if (r < p->nc) {
-    for (int j = p->clause_off[r]; j < p->clause_off[r + 1]; ++j) {
-      int v = p->clause_lits[j] >> 1;
+  if (r < p->nc || r >= p->nrows) {
+    const int32_t* lits = p->clause_lits;
+    int a, b;
+    if (r < p->nc) { a = p->clause_off[r]; b = p->clause_off[r + 1]; s->used[p->clause_id[r]] = 1; }
+    else { lits = s->l_lits; a = s->l_off[r - p->nrows]; b = s->l_off[r - p->nrows + 1]; }
+    for (int j = a; j < b; ++j) {
+      int v = lits[j] >> 1;
       if (v != u && !s->seen[v]) { s->seen[v] = 1; s->work[s->nwork++] = v; }
     }
   } else {
+    s->used[p->card_id[r - p->nc]] = 1;
     int k = r - p->nc;
     for (int j = p->card_off[k]; j < p->card_off[k + 1]; ++j) {
       int v = p->card_lits[j];
@@ -348,17 +400,32 @@ static void push_ante(st_t* s, int r, int u, int bound_rd) {
   }
 }
 
+/* antecedents of the epilogue bound: the extras already true */
+static void push_extra(st_t* s, int u, int bound_rd) {
+  for (int v = 0; v < s->p.nv; ++v)
+    if (v != u && s->is_extra[v] && s->val[v] > 0 && s->rnd[v] < bound_rd && !s->seen[v]) {
+      s->seen[v] = 1; s->work[s->nwork++] = v;
+    }
+}
+
+/* Walk the implication graph back from the last conflict.  Marks the
+ * identities of every row used (used[]), the Solve() decisions reached
+ * (dset[] by decision index) and, when collecting, the guesses reached (fg[]). */
 static void analyze(st_t* s) {
   s->nwork = 0;
   if (s->ck == CK_ROW) push_ante(s, s->c_row, -1, INF);
   else if (s->ck == CK_VAR) {
     push_ante(s, s->c_rp, s->c_var, s->c_row);
     push_ante(s, s->c_rn, s->c_var, s->c_row);
-  } else return;
+  } else if (s->ck == CK_EXTRA) push_extra(s, -1, INF);
+  else return;
   for (int i = 0; i < s->nwork; ++i) {
     int u = s->work[i];
     int r = s->reason[u];
     if (r >= 0) push_ante(s, r, u, s->rnd[u]);
+    else if (r == R_EXTRA) push_extra(s, u, s->rnd[u]);
+    else if (s->dix[u] >= 0) s->dset[s->dix[u]] = 1;
+    else if (s->collect_guess && s->inS[u]) s->fg[u] = 1;
   }
   for (int i = 0; i < s->nwork; ++i) s->seen[s->work[i]] = 0;
 }
@@ -398,33 +465,56 @@ static void save_model(st_t* s) {
 
 enum { R_SAT = 1, R_UNSAT = -1, R_BUDGET = 2 };
 
-/* DPLL from a consistent fixpoint: decide the preferred candidate of the first
- * violated dependency row true, then false; chronological backtracking.  On
- * SAT the model is saved and the trail restored to `root`. */
+/* Solve(): CDCL from a consistent fixpoint.  Decision: the preferred
+ * (first unassigned) candidate of the first dependency row the all-false
+ * completion violates, set true.  A conflict learns the nogood of the
+ * decisions its analysis reaches (ascending decision order), backjumps to the
+ * second-highest of them and asserts the negation of the highest.  Learned
+ * rows live until this call returns; when their store is full the conflict is
+ * resolved by flipping the last unflipped decision instead (plain DPLL).
+ * On SAT the model is saved; the trail is restored to `root` either way. */
 static int dpll(st_t* s) {
-  int root = s->tlen, nd = 0;
+  const int root = s->tlen, nl0 = s->nl;
+  int nd = 0, r;
   for (;;) {
     int l = first_violated(s);
-    if (l < 0) {
-      save_model(s);
-      truncate_to(s, root);
-      return R_SAT;
-    }
-    if (++s->steps > s->budget) { s->budget_hit = 1; truncate_to(s, root); return R_BUDGET; }
-    s->d_lit[nd] = l; s->d_mark[nd] = s->tlen; s->d_flip[nd] = 0; ++nd;
+    if (l < 0) { save_model(s); r = R_SAT; break; }
+    if (++s->steps > s->budget) { s->budget_hit = 1; r = R_BUDGET; break; }
+    s->d_lit[nd] = l; s->d_mark[nd] = s->tlen; s->d_flip[nd] = 0;
     assign(s, l, R_DECISION, ++s->round);
+    s->dix[l >> 1] = nd++;
     int res = propagate(s);
     while (res < 0) {
-      if (s->collect) analyze(s);
-      while (nd > 0 && s->d_flip[nd - 1]) --nd;
-      if (nd == 0) { truncate_to(s, root); return R_UNSAT; }
-      truncate_to(s, s->d_mark[nd - 1]);
-      s->d_flip[nd - 1] = 1;
-      if (++s->steps > s->budget) { s->budget_hit = 1; truncate_to(s, root); return R_BUDGET; }
-      assign(s, s->d_lit[nd - 1] ^ 1, R_DECISION, ++s->round);
+      memset(s->dset, 0, (size_t)nd);
+      analyze(s);
+      int h = -1, b = -1, n = 0;
+      for (int i = 0; i < nd; ++i)
+        if (s->dset[i]) { b = h; h = i; ++n; }
+      if (h < 0) { r = R_UNSAT; goto done; }
+      if (++s->steps > s->budget) { s->budget_hit = 1; r = R_BUDGET; goto done; }
+      if (s->nl < L_MAX && s->l_off[s->nl] + n <= s->lcap) {
+        int at = s->l_off[s->nl];
+        for (int i = 0; i < nd; ++i)
+          if (s->dset[i]) s->l_lits[at++] = s->d_lit[i] ^ 1;
+        s->l_off[++s->nl] = at;
+        nd = b + 1;
+        truncate_to(s, s->d_mark[nd]);
+        assign(s, s->d_lit[h] ^ 1, s->p.nrows + s->nl - 1, ++s->round);
+      } else {
+        while (nd > 0 && s->d_flip[nd - 1]) --nd;
+        if (nd == 0) { r = R_UNSAT; goto done; }
+        truncate_to(s, s->d_mark[nd - 1]);
+        s->d_flip[nd - 1] = 1;
+        assign(s, s->d_lit[nd - 1] ^ 1, R_DECISION, ++s->round);
+        s->dix[s->d_lit[nd - 1] >> 1] = nd - 1;
+      }
       res = propagate(s);
     }
   }
+done:
+  truncate_to(s, root);
+  s->nl = nl0;
+  return r;
 }
 
 /* ------------------------------------------------------------------ */
@@ -555,14 +645,34 @@ static int be_test(void* u, st_t* s, int lit) {
 }
 static int be_untest(void* u, st_t* s, int mark) {
   (void)u;
-  truncate_to(s, mark);
-  return s->tlen == s->p.nv ? 1 : 0;
+  return untest_to(s, mark);
 }
+
+/* A failed Solve() leaves gini with learned clauses that make every scope
+ * still holding the refuted guesses inconsistent (search_test.go:50 scripts
+ * such Untest() == -1 returns).  Restated: the refutation's conflict analyses
+ * collect the guesses they reach; their nogood becomes a learned row. */
+static void learn(st_t* s) {
+  int n = 0;
+  for (int v = 0; v < s->p.nv; ++v) n += s->fg[v];
+  if (s->nl >= L_MAX || s->l_off[s->nl] + n > s->lcap) return;
+  int at = s->l_off[s->nl];
+  for (int v = 0; v < s->p.nv; ++v)
+    if (s->fg[v]) s->l_lits[at++] = 2 * v + 1;
+  s->l_off[++s->nl] = at;
+}
+
 static int be_solve(void* u, st_t* s) {
   (void)u;
+  memset(s->fg, 0, (size_t)s->p.nv);
+  s->collect_guess = 1;
   int r = dpll(s);
+  s->collect_guess = 0;
   if (r == R_SAT) return 1;
-  if (r == R_UNSAT) return -1;
+  if (r == R_UNSAT) {
+    learn(s);
+    return -1;
+  }
   return R_BUDGET;
 }
 
@@ -579,6 +689,7 @@ static void reset_all(st_t* s) {
  * identities of every conflict the refutation met. */
 static int refute(st_t* s, const uint8_t* en) {
   reset_all(s);
+  s->learn_on = 0;
   s->enabled = en;
   memset(s->used, 0, (size_t)s->p.nid);
   s->collect = 1;
@@ -588,6 +699,7 @@ static int refute(st_t* s, const uint8_t* en) {
   s->collect = 0;
   reset_all(s);
   s->enabled = NULL;
+  s->learn_on = 1;
   return r;
 }
 
@@ -826,4 +938,29 @@ int oracle_solve_batch(int32_t n, const int64_t* rec_off, const int32_t* rec, in
   for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
   free(th);
   return 0;
+}
+
+/* Model check: every clause and card row satisfied by the installed set
+ * (variables not installed are false).  Returns the first violated row, or -1. */
+int oracle_check_model(const int32_t* rec, const uint32_t* installed) {
+  prob_t p;
+  parse(&p, rec);
+  for (int r = 0; r < p.nc; ++r) {
+    int sat = 0;
+    for (int j = p.clause_off[r]; j < p.clause_off[r + 1]; ++j) {
+      int l = p.clause_lits[j], v = l >> 1;
+      int x = (installed[v >> 5] >> (v & 31)) & 1;
+      if (x != (l & 1)) { sat = 1; break; }
+    }
+    if (!sat) return r;
+  }
+  for (int k = 0; k < p.nk; ++k) {
+    int cnt = 0;
+    for (int j = p.card_off[k]; j < p.card_off[k + 1]; ++j) {
+      int v = p.card_lits[j];
+      cnt += (installed[v >> 5] >> (v & 31)) & 1;
+    }
+    if (cnt > p.card_bound[k]) return p.nc + k;
+  }
+  return -1;
 }

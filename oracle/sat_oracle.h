@@ -47,6 +47,9 @@ int oracle_search_scripted(const int32_t* rec, const int32_t* test_ret, int32_t 
  * conflict, else 0/1; used to verify cores (re-solve the core alone). */
 int oracle_refute(const int32_t* rec, const uint8_t* enabled, int64_t budget);
 
+/* -1 if the installed set satisfies every row, else the first violated row. */
+int oracle_check_model(const int32_t* rec, const uint32_t* installed);
+
 #ifdef __cplusplus
 }
 #endif

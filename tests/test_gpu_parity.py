@@ -1,0 +1,156 @@
+"""Parity of the HIP path (libdeppy_hip.so on an MI355X) with the CPU
+restatement (oracle/) and with the reference's own test vectors.
+
+Run on the GPU box:  python -m pytest tests -m gpu
+"""
+import io
+import sys
+
+import numpy as np
+import pytest
+
+from deppy_amd import _lib, sat
+from oracle import oracle
+from tests import fixtures
+from tests.gpu_common import compare_results, lowered_config
+from tests.test_lowering import V, sat_var
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = _lib.Context(0, 1)
+    yield c
+    c.close()
+
+
+def test_native_library_is_loaded(ctx):
+    # the product path is the in-tree HIP library, nothing else
+    maps = open("/proc/self/maps").read()
+    assert _lib.LIB_PATH in maps
+
+
+# ---------------------------------------------------------------------------
+# the reference's own tests, through the full product path
+# ---------------------------------------------------------------------------
+SOLVE = fixtures.load("testsolve")["cases"] + fixtures.load("readme")["cases"]
+
+
+@pytest.mark.parametrize("case", SOLVE, ids=[c["name"] for c in SOLVE])
+def test_solve_golden(case):
+    """pkg/sat/solve_test.go TestSolve, verbatim semantics (:299-355)."""
+    variables = [sat_var(v) for v in case["variables"]]
+    traces = io.StringIO()
+    s, err = sat.NewSolver(sat.WithInput(variables), sat.WithTracer(sat.LoggingTracer(traces)))
+    assert err is None
+    installed, err = s.Solve(None)
+    ids = sorted(str(v.Identifier()) for v in (installed or [])) or None
+    assert ids == case["installed"]
+    if case["error"] is None:
+        assert err is None
+    else:
+        assert isinstance(err, sat.NotSatisfiable)
+        got = sorted(err, key=lambda a: (str(a.Variable.Identifier()).encode(),
+                                         a.Variable.Constraints().index(a.Constraint)))
+        expect = []
+        by = {str(v.Identifier()): v for v in variables}
+        for a in case["error"]["applied"]:
+            var = by[a["var"]]
+            expect.append(sat.AppliedConstraint(var, var.Constraints()[a["constraint"]]))
+        assert got == expect
+        assert sat.NotSatisfiable(got).Error() == case["error"]["string"]
+
+
+def test_duplicate_identifier():
+    _, err = sat.NewSolver(sat.WithInput([V("a"), V("a")]))
+    assert err == sat.DuplicateIdentifier("a")
+    assert err.Error() == 'duplicate identifier "a" in input'
+
+
+def test_lookup_error_surface():
+    s, err = sat.NewSolver(sat.WithInput([V("a", sat.Mandatory(), sat.Dependency("x"))]))
+    assert err is None
+    installed, err = s.Solve(None)
+    assert installed is None
+    assert err.Error() == '1 errors encountered: variable "x" referenced but not provided'
+
+
+def test_batch_mixed_with_errors():
+    inputs = [[V("a", sat.Mandatory())], [V("a"), V("a")], [],
+              [V("a", sat.Mandatory(), sat.Prohibited())]]
+    out = sat.SolveBatch(inputs)
+    assert [v.Identifier() for v in out[0][0]] == ["a"] and out[0][1] is None
+    assert isinstance(out[1][1], sat.DuplicateIdentifier)
+    assert out[2] == (None, None)
+    assert isinstance(out[3][1], sat.NotSatisfiable) and len(out[3][1]) == 2
+
+
+def test_golden_records_bit_exact(ctx):
+    lw = _lib.Lowered(sat.encode_inputs([[sat_var(v) for v in c["variables"]] for c in SOLVE]))
+    g = ctx.solve(lw.rec_off, lw.rec)
+    o = oracle.solve_batch(lw.rec_off, lw.rec)
+    assert compare_results(g, o, lw.n) == []
+
+
+# ---------------------------------------------------------------------------
+# seeded synthetic batches: bit-exact against the oracle
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("config,n,seed", [(2, 3000, 11), (3, 8000, 12), (5, 300, 13)])
+def test_generated_bit_exact(ctx, config, n, seed):
+    lw = lowered_config(config, n, seed)
+    g = ctx.solve(lw.rec_off, lw.rec)
+    o = oracle.solve_batch(lw.rec_off, lw.rec, 0, 16)
+    bad = compare_results(g, o, n)
+    assert bad == [], bad[:10]
+    st = g["status"]
+    print("config", config, "SAT", int((st == 1).sum()), "UNSAT", int((st == -1).sum()),
+          "INCOMPLETE", int((st == 0).sum()), "ERROR", int((st == -2).sum()),
+          "class B", int(((g["flags"] & 2) != 0).sum()), file=sys.stderr)
+
+
+@pytest.mark.parametrize("config,n,seed", [(2, 400, 21), (5, 60, 22)])
+def test_models_and_cores_verified(ctx, config, n, seed):
+    """Every SAT answer satisfies every row; every core is UNSAT on its own and
+    deletion-minimal (north_star: 'a verified conflicting constraint subset')."""
+    lw = lowered_config(config, n, seed)
+    g = ctx.solve(lw.rec_off, lw.rec)
+    for p in range(n):
+        rec = lw.record(p)
+        if g["status"][p] == 1:
+            a0, a1 = g["inst_off"][p], g["inst_off"][p + 1]
+            assert oracle.check_model(rec, g["installed"][a0:a1]) == -1
+        elif g["status"][p] == -1 and not g["flags"][p] & 32:
+            core = _lib.core_list(g, p)
+            assert oracle.refute(rec, core) == -1
+            for drop in core:
+                assert oracle.refute(rec, [i for i in core if i != drop]) == 1
+
+
+def test_full_size_properties(ctx):
+    """BASELINE config 2 at full size (10k catalogs): deterministic, models
+    check out, verdicts agree with the oracle on a sample."""
+    lw = lowered_config(2, 10000, 2024)
+    r = ctx.upload(lw.rec_off, lw.rec)
+    try:
+        r.run()
+        a = r.download()
+        r.run()
+        b = r.download()
+    finally:
+        r.free()
+    for k in ("status", "flags", "installed", "core", "core_len", "steps"):
+        np.testing.assert_array_equal(a[k], b[k])
+    assert (a["status"] != 0).all() and (a["status"] != -2).all()
+    rng = np.random.default_rng(0)
+    sample = rng.choice(10000, 500, replace=False)
+    for p in sample:
+        st, fl, inst, core, steps = oracle.solve(lw.record(p))
+        assert st == a["status"][p] and fl == a["flags"][p]
+        assert inst == _lib.installed_list(a, p, int(lw.record(p)[1]))
+        assert core == _lib.core_list(a, p)
+
+
+def test_empty_batch(ctx):
+    g = ctx.solve(np.zeros(1, np.int64), np.zeros(0, np.int32))
+    assert len(g["status"]) == 0

@@ -1,0 +1,140 @@
+"""Host logic on CPU: the product's C++ lowering (dp_lower) equals the
+restatement in oracle/lower_ref.py record-for-record, and the library exports
+every symbol include/deppy_hip.h declares."""
+import ctypes
+import re
+
+import numpy as np
+import pytest
+
+from deppy_amd import _lib, sat
+from oracle import lower_ref
+from tests import fixtures
+
+ROOT = fixtures.GOLDEN.rsplit("/tests/", 1)[0]
+
+
+def test_exports_match_header():
+    hdr = open(ROOT + "/include/deppy_hip.h").read()
+    declared = set(re.findall(r"\b(dp_[a-z_0-9]+)\s*\(", hdr)) - {"dp_rec_layout_of"}
+    assert declared == set(_lib.EXPORTS)
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    for name in declared:
+        assert hasattr(L, name), name
+
+
+def variables_of(fixture_vars):
+    return [sat_var(v) for v in fixture_vars]
+
+
+class V(sat.Variable):
+    def __init__(self, ident, *cons):
+        self.ident = sat.Identifier(ident)
+        self.cons = list(cons)
+
+    def Identifier(self):
+        return self.ident
+
+    def Constraints(self):
+        return self.cons
+
+
+def sat_var(v):
+    cons = []
+    for c in v["constraints"]:
+        k = c["kind"]
+        if k == "mandatory":
+            cons.append(sat.Mandatory())
+        elif k == "prohibited":
+            cons.append(sat.Prohibited())
+        elif k == "dependency":
+            cons.append(sat.Dependency(*c["ids"]))
+        elif k == "conflict":
+            cons.append(sat.Conflict(c["ids"][0]))
+        else:
+            cons.append(sat.AtMost(c["n"], *c["ids"]))
+    return V(v["id"], *cons)
+
+
+def all_golden_variable_sets():
+    out = []
+    for name in ("testsolve", "readme", "testsearch"):
+        out += [c["variables"] for c in fixtures.load(name)["cases"]]
+    return out
+
+
+def compare(lw_product, p, ref):
+    assert lw_product.err[p] == ref.error, (lw_product.msg[p], ref.msg)
+    if ref.error:
+        assert lw_product.msg[p] == ref.msg
+        return
+    np.testing.assert_array_equal(lw_product.record(p), ref.rec)
+    i0, i1 = lw_product.ident_off[p], lw_product.ident_off[p + 1]
+    assert list(lw_product.ident_var[i0:i1]) == list(ref.ident_var)
+    assert list(lw_product.ident_con[i0:i1]) == list(ref.ident_con)
+
+
+def test_golden_records_match_restatement():
+    sets = all_golden_variable_sets()
+    lw = _lib.Lowered(sat.encode_inputs([variables_of(vs) for vs in sets]))
+    for p, vs in enumerate(sets):
+        compare(lw, p, lower_ref.lower_problem(fixtures.to_problem(vs)))
+        assert _lib.lib().dp_rec_validate(
+            lw.record(p).ctypes.data_as(_lib.c_i32p), len(lw.record(p))) == 0
+
+
+EDGE = [
+    # identities that collide (lit_mapping.go:69-72): last writer is reported
+    [V("a", sat.Conflict("b")), V("b", sat.Conflict("a"), sat.AtMost(1, "a", "b"))],
+    [V("a", sat.Prohibited(), sat.Dependency(), sat.Conflict("a"), sat.AtMost(0, "a"))],
+    [V("a", sat.Mandatory(), sat.Mandatory()), V("b", sat.AtMost(1, "b", "b"))],
+    # tautologies and constants
+    [V("a", sat.Dependency("a", "b")), V("b", sat.Dependency("c", "b")), V("c"),
+     V("d", sat.AtMost(-1, "a")), V("e", sat.AtMost(3, "a", "b"))],
+    # duplicates inside rows, multiplicity in AtMost
+    [V("a", sat.Mandatory(), sat.Dependency("b", "b", "c")), V("b"), V("c"),
+     V("u", sat.AtMost(2, "b", "c", "b", "a", "c"))],
+    # empty problem, empty constraint lists
+    [],
+    [V("x"), V("y", sat.AtMost(0))],
+    # errors: lookups accumulate in Apply order, %q quoting
+    [V("a", sat.Dependency("nope", "b"), sat.AtMost(1, "zz")), V("b", sat.Conflict('q"\\\n\x01é '))],
+    [V("a"), V("b"), V("a")],
+]
+
+
+def test_edge_records_match_restatement():
+    lw = _lib.Lowered(sat.encode_inputs(EDGE))
+    for p, vs in enumerate(EDGE):
+        ref = lower_ref.lower_problem([
+            (v.Identifier().encode(), [(c.kind, c.n, [i.encode() for i in c.ids]) for c in v.Constraints()])
+            for v in vs])
+        compare(lw, p, ref)
+
+
+@pytest.mark.parametrize("config", [2, 3, 5])
+def test_generated_records_match_restatement(config):
+    w = _lib.generate(config, 40, 1234)
+    lw = _lib.Lowered(_lib.WireArrays(**{k: w[k] for k in (
+        "prob_var_off", "var_id", "var_con_off", "con_kind", "con_n", "con_arg_off", "con_arg",
+        "str_off")}, str_bytes=w["str_bytes"].tobytes()))
+    probs = lower_ref.problems_from_wire(w)
+    for p, prob in enumerate(probs):
+        compare(lw, p, lower_ref.lower_problem(prob))
+
+
+def test_generator_is_deterministic():
+    a = _lib.generate(2, 5, 77)
+    b = _lib.generate(2, 5, 77)
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k])
+    c = _lib.generate(2, 5, 78)
+    assert not np.array_equal(a["con_arg"][:50], c["con_arg"][:50]) or len(a["con_arg"]) != len(c["con_arg"])
+
+
+def test_no_gpu_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(RuntimeError):
+        _lib.Context(0, 1)
