@@ -1,6 +1,14 @@
-// LDS layout of one problem's working set (one wavefront per problem).
+// Working-set layout of one problem (one wavefront per problem).
 // Shared by the host runtime (to size dynamic LDS and bucket launches) and the
-// kernel (to carve the allocation).  All sizes in 32-bit words.
+// kernel (to carve the allocation).  Offsets and sizes are in BYTES.
+//
+// Two images of the same layout exist:
+//   IX = uint16_t : the LDS image.  Record arrays are narrowed to 16 bits on
+//                   load (every index of an eligible problem is < 65000), so a
+//                   ~240-variable catalog needs ~18 KiB and 8-9 problems fit
+//                   in one CU's 160 KiB of LDS.
+//   IX = int32_t  : the HBM image for problems too large for LDS (or with
+//                   larger indices); same code, working set in HBM scratch.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -10,57 +18,12 @@
 
 namespace dp {
 
-struct LdsLayout {
-  // static problem image
-  int32_t rec;       // record copy (header + arrays), DP_H_WORDS words, rounded to 4
-  int32_t w_off;     // [2nv+1] watch offsets per literal
-  int32_t w;         // [ncl+nkl] rows to evaluate when a literal becomes true
-  // per-variable state
-  int32_t val;       // int8[nv]: 0 unassigned, 1 true, -1 false
-  int32_t reason;    // [nv] implying row, -1 decision/assumption, -2 extras bound
-  int32_t rnd;       // [nv] propagation round of the assignment
-  int32_t trail;     // [nv] true literals in assignment order
-  int32_t imp_pos;   // [nv] lowest row implying +v this round   (also: watch-build cursor, 2nv)
-  int32_t imp_neg;   // [nv] lowest row implying -v this round
-  int32_t impflag;   // [nv] bit0 +v implied, bit1 -v implied this round
-  int32_t touched;   // [nv] variables implied this round (also: analysis work list)
-  int32_t d_lit;     // [nv] Solve() decision literals
-  int32_t d_mark;    // [nv] trail length before each decision
-  int32_t d_flip;    // bits[nv] decision already flipped
-  int32_t inS;       // bits[nv] guessed set (search.assumptions)
-  int32_t extra;     // bits[nv] SAT-epilogue extras
-  int32_t seen;      // bits[nv] conflict analysis
-  int32_t model;     // bits[nv] last model (Value)
-  int32_t used;      // bits[nid] identities met by a refutation
-  int32_t en;        // bits[nid] identities enabled (core search)
-  int32_t en2;       // bits[nid]
-  int32_t dix;       // [nv] Solve() decision index of a variable, -1 otherwise
-  int32_t dset;      // bits[nv] decisions met by the last conflict analysis
-  int32_t fg;        // bits[nv] guesses met by the refutation of a Solve()
-  int32_t l_off;     // [L_MAX+1] learned rows (rows nrows..)
-  int32_t l_lits;    // [lcap] learned literals
-  int32_t lcap;
-  int32_t dq;        // [2*cap] deque of choices (list, idx)
-  int32_t stk;       // [5*cap] guess stack (list, idx, m, children, mark)
-  int32_t pre;       // [64] exclusive prefix of watch-list lengths
-  int32_t preA;      // [64] watch-list starts
-  int32_t scal;      // [16] wave-shared scalars
-  int32_t words;     // total
-  int32_t cap;       // deque / stack capacity
-};
-
-enum Scalar {  // indices into the scal block
-  S_CROW = 0,     // lowest conflicting row of the round
-  S_CVAR = 1,     // lowest variable implied both ways
-  S_NTOUCHED = 2, // implied variables this round
-  S_NWORK = 3,    // analysis work list length
-  S_TMP = 4
-};
-
 __host__ __device__ inline int32_t bits_words(int32_t n) { return (n + 31) >> 5; }
 
-// learned-row store (oracle L_MAX, lcap = 4*nv + 256)
+// learned-row store (oracle: L_MAX rows, lcap = 4*nv + 256 literals)
 constexpr int32_t L_MAX = 64;
+// work list of one propagation chunk (rows watched by <= 64 frontier literals)
+constexpr int32_t WBUF = 256;
 
 // dp_rec_layout_of (include/deppy_hip.h) for host and device code.
 __host__ __device__ inline dp_rec_layout rec_layout(const int32_t* h) {
@@ -81,55 +44,96 @@ __host__ __device__ inline dp_rec_layout rec_layout(const int32_t* h) {
   return L;
 }
 
-__host__ __device__ inline LdsLayout lds_layout(const int32_t* h) {
-  LdsLayout L;
+struct Layout {
+  int32_t body;      // record arrays (header dropped), one IX per record word
+  int32_t w_off;     // IX[2nv+1] watch offsets per literal
+  int32_t w;         // IX[ncl+nkl] rows to evaluate when a literal becomes true
+  int32_t val;       // int8[nv]: 0 unassigned, 1 true, -1 false
+  int32_t reason;    // IX[nv] implying row; R_DEC / R_EXTRA
+  int32_t rs;        // IX[nv] trail position where the assigning round started
+  int32_t trail;     // IX[nv] true literals in assignment order
+  int32_t touched;   // IX[nv] variables implied this round; analysis work list
+  int32_t d_lit;     // IX[nv] Solve() decision literals
+  int32_t d_mark;    // IX[nv] trail length before each decision
+  int32_t dix;       // IX[nv] decision index of a variable (NONE otherwise)
+  int32_t imp;       // u32[2nv] lowest implying row of +v | -v this round; watch-build cursor
+  int32_t impflag;   // bits[2nv] +v / -v implied this round
+  int32_t d_flip;    // bits[nv] decision already flipped
+  int32_t inS;       // bits[nv] guessed set (search.assumptions)
+  int32_t extra;     // bits[nv] SAT-epilogue extras
+  int32_t seen;      // bits[nv] conflict analysis
+  int32_t model;     // bits[nv] last model (Value)
+  int32_t dset;      // bits[nv] decisions met by the last conflict analysis
+  int32_t fg;        // bits[nv] guesses met by the refutation of a Solve()
+  int32_t used;      // bits[nid] identities met by a refutation
+  int32_t en;        // bits[nid] identities enabled (core search)
+  int32_t en2;       // bits[nid]
+  int32_t l_off;     // IX[L_MAX+1] learned rows (rows nrows..)
+  int32_t l_lits;    // IX[lcap]
+  int32_t dq;        // IX[2*cap] deque of choices (list, idx)
+  int32_t stk;       // IX[5*cap] guess stack (list, idx, m, children, mark)
+  int32_t wbuf;      // i32[WBUF] flattened work list
+  int32_t scal;      // i32[16] wave-shared scalars
+  int32_t bytes;     // total
+  int32_t cap, lcap;
+};
+
+enum Scalar { S_NTOUCHED = 0, S_NWORK = 1 };
+
+template <class IX>
+__host__ __device__ inline Layout layout(const int32_t* h) {
+  Layout L;
   const int32_t nv = h[DP_H_NV], nid = h[DP_H_NID];
   const int32_t nbv = bits_words(nv), nbi = bits_words(nid);
+  const int32_t ix = (int32_t)sizeof(IX);
   int32_t o = 0;
-  auto take = [&](int32_t n) {
+  auto take = [&](int32_t nbytes) {
     int32_t at = o;
-    o += (n + 3) & ~3;  // keep every array 16-byte aligned
+    o += (nbytes + 15) & ~15;  // every array 16-byte aligned
     return at;
   };
   L.cap = h[DP_H_NA] + h[DP_H_NCH] + 2;
-  L.rec = take(h[DP_H_WORDS]);
-  L.w_off = take(2 * nv + 1);
-  L.w = take(h[DP_H_NCL] + h[DP_H_NKL]);
-  L.val = take((nv + 3) >> 2);
-  L.reason = take(nv);
-  L.rnd = take(nv);
-  L.trail = take(nv);
-  L.imp_pos = take(nv);
-  L.imp_neg = take(nv);
-  L.impflag = take(nv);
-  L.touched = take(nv);
-  L.d_lit = take(nv);
-  L.d_mark = take(nv);
-  L.d_flip = take(nbv);
-  L.inS = take(nbv);
-  L.extra = take(nbv);
-  L.seen = take(nbv);
-  L.model = take(nbv);
-  L.used = take(nbi);
-  L.en = take(nbi);
-  L.en2 = take(nbi);
-  L.dix = take(nv);
-  L.dset = take(nbv);
-  L.fg = take(nbv);
-  L.l_off = take(L_MAX + 1);
   L.lcap = 4 * nv + 256;
-  L.l_lits = take(L.lcap);
-  L.dq = take(2 * L.cap);
-  L.stk = take(5 * L.cap);
-  L.pre = take(64);
-  L.preA = take(64);
-  L.scal = take(16);
-  L.words = o;
+  L.body = take((h[DP_H_WORDS] - DP_H_SIZE + 4) * ix);  // +4: dwordx4 copy slack
+  L.w_off = take((2 * nv + 1) * ix);
+  L.w = take((h[DP_H_NCL] + h[DP_H_NKL]) * ix);
+  L.val = take(nv);
+  L.reason = take(nv * ix);
+  L.rs = take(nv * ix);
+  L.trail = take(nv * ix);
+  L.touched = take(nv * ix);
+  L.d_lit = take(nv * ix);
+  L.d_mark = take(nv * ix);
+  L.dix = take(nv * ix);
+  L.imp = take(2 * nv * 4);
+  L.impflag = take(bits_words(2 * nv) * 4);
+  L.d_flip = take(nbv * 4);
+  L.inS = take(nbv * 4);
+  L.extra = take(nbv * 4);
+  L.seen = take(nbv * 4);
+  L.model = take(nbv * 4);
+  L.dset = take(nbv * 4);
+  L.fg = take(nbv * 4);
+  L.used = take(nbi * 4);
+  L.en = take(nbi * 4);
+  L.en2 = take(nbi * 4);
+  L.l_off = take((L_MAX + 1) * ix);
+  L.l_lits = take(L.lcap * ix);
+  L.dq = take(2 * L.cap * ix);
+  L.stk = take(5 * L.cap * ix);
+  L.wbuf = take(WBUF * 4);
+  L.scal = take(16 * 4);
+  L.bytes = o;
   return L;
 }
 
-// imp_pos and imp_neg are adjacent (2nv words) so they double as the per-literal
-// cursor while watch lists are built.
-static_assert(sizeof(int32_t) == 4, "");
+// Can the record run on the 16-bit LDS image?  Every index it holds, and every
+// value the solve stores per variable / row, must stay below 0xfffe (0xffff and
+// 0xfffe encode the no-row reasons).
+__host__ __device__ inline bool fits16(const int32_t* h) {
+  const int32_t nv = h[DP_H_NV];
+  return h[DP_H_WORDS] < 65000 && nv < 16000 && h[DP_H_NID] < 65000 &&
+         h[DP_H_NC] + h[DP_H_NK] + L_MAX < 65000 && h[DP_H_NA] + h[DP_H_NCH] < 65000;
+}
 
 }  // namespace dp

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -66,6 +67,9 @@ struct DevSlice {
   int64_t* scratch_off = nullptr;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // bucket launches run concurrently on side streams joined back by events
+  hipStream_t side[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t done[3] = {nullptr, nullptr, nullptr};
 };
 
 struct dp_resident {
@@ -97,6 +101,10 @@ void free_slice(DevSlice& s) {
     if (p) (void)hipFree(p);
   if (s.ev0) (void)hipEventDestroy(s.ev0);
   if (s.ev1) (void)hipEventDestroy(s.ev1);
+  for (int i = 0; i < 3; ++i) {
+    if (s.side[i]) (void)hipStreamDestroy(s.side[i]);
+    if (s.done[i]) (void)hipEventDestroy(s.done[i]);
+  }
   if (s.stream) (void)hipStreamDestroy(s.stream);
   s = DevSlice{};
 }
@@ -114,6 +122,10 @@ int build_slice(DevSlice& s, const dp_batch* b, const int64_t* inst_off, const i
   HIP_OK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
   HIP_OK(hipEventCreate(&s.ev0));
   HIP_OK(hipEventCreate(&s.ev1));
+  for (int i = 0; i < 3; ++i) {
+    HIP_OK(hipStreamCreateWithFlags(&s.side[i], hipStreamNonBlocking));
+    HIP_OK(hipEventCreateWithFlags(&s.done[i], hipEventDisableTiming));
+  }
   const int32_t n = s.p1 - s.p0;
   std::vector<int64_t> roff((size_t)n + 1, 0);
   for (int32_t i = 0; i < n; ++i) {
@@ -127,13 +139,16 @@ int build_slice(DevSlice& s, const dp_batch* b, const int64_t* inst_off, const i
   for (int32_t i = 0; i < n; ++i) {
     const int32_t* r = b->rec + b->rec_off[s.p0 + i];
     std::memcpy(&rec[(size_t)roff[(size_t)i]], r, (size_t)dp::words_of(r) * 4);
-    const int64_t words = dp::lds_layout(r).words;
-    const int64_t lds = words * 4;
+    const int64_t lds = dp::fits16(r) ? (int64_t)dp::layout<uint16_t>(r).bytes : INT64_MAX;
     int k = 0;
     while (k < kNBuckets && lds > kBuckets[k]) ++k;
-    if (k < kNBuckets) bucket[(size_t)k].push_back(i);
-    else if (words < (int64_t)1 << 31) { hbm.push_back(i); soff.push_back(soff.back() + words); }
-    else s.too_large.push_back(i);
+    if (k < kNBuckets) {
+      bucket[(size_t)k].push_back(i);
+    } else {
+      const int64_t bytes = (int64_t)dp::layout<int32_t>(r).bytes;
+      if (bytes < ((int64_t)1 << 31)) { hbm.push_back(i); soff.push_back(soff.back() + bytes / 4); }
+      else s.too_large.push_back(i);
+    }
   }
   std::vector<int32_t> order;
   for (int k = 0; k < kNBuckets; ++k) {
@@ -142,7 +157,7 @@ int build_slice(DevSlice& s, const dp_batch* b, const int64_t* inst_off, const i
     s.b_count.push_back((int)bucket[(size_t)k].size());
     int mx = 0;
     for (int32_t i : bucket[(size_t)k])
-      mx = std::max(mx, dp::lds_layout(b->rec + b->rec_off[s.p0 + i]).words * 4);
+      mx = std::max(mx, dp::layout<uint16_t>(b->rec + b->rec_off[s.p0 + i]).bytes);
     s.b_lds.push_back(mx);
     order.insert(order.end(), bucket[(size_t)k].begin(), bucket[(size_t)k].end());
   }
@@ -199,16 +214,34 @@ int run_slice(DevSlice& s, int64_t budget) {
   a.budget = budget;
   a.scratch = nullptr;
   a.scratch_off = nullptr;
+  // launch i goes to stream i % 4 (the main stream, then three side streams);
+  // the largest buckets come first so they start earliest
+  std::vector<int> launch_order;
+  for (size_t k = 0; k < s.b_first.size(); ++k) launch_order.push_back((int)k);
+  std::sort(launch_order.begin(), launch_order.end(),
+            [&](int x, int y) { return s.b_count[(size_t)x] > s.b_count[(size_t)y]; });
+  if (s.hbm_count) launch_order.insert(launch_order.begin(), -1);
+  const int nside = std::min<int>(3, (int)launch_order.size() - 1);
   HIP_OK(hipEventRecord(s.ev0, s.stream));
-  for (size_t k = 0; k < s.b_first.size(); ++k) {
-    a.order = s.order + s.b_first[k];
-    HIP_OK(dp::launch_solve(a, s.b_count[k], s.b_lds[k], s.stream));
+  for (int i = 0; i < nside; ++i) HIP_OK(hipStreamWaitEvent(s.side[i], s.ev0, 0));
+  for (size_t i = 0; i < launch_order.size(); ++i) {
+    hipStream_t st = (i % 4 == 0) ? s.stream : s.side[i % 4 - 1];
+    const int k = launch_order[i];
+    if (k < 0) {
+      a.order = s.order + s.hbm_first;
+      a.scratch = s.scratch;
+      a.scratch_off = s.scratch_off;
+      HIP_OK(dp::launch_solve(a, s.hbm_count, 0, st));
+      a.scratch = nullptr;
+      a.scratch_off = nullptr;
+    } else {
+      a.order = s.order + s.b_first[(size_t)k];
+      HIP_OK(dp::launch_solve(a, s.b_count[(size_t)k], s.b_lds[(size_t)k], st));
+    }
   }
-  if (s.hbm_count) {
-    a.order = s.order + s.hbm_first;
-    a.scratch = s.scratch;
-    a.scratch_off = s.scratch_off;
-    HIP_OK(dp::launch_solve(a, s.hbm_count, 0, s.stream));
+  for (int i = 0; i < nside; ++i) {
+    HIP_OK(hipEventRecord(s.done[i], s.side[i]));
+    HIP_OK(hipStreamWaitEvent(s.stream, s.done[i], 0));
   }
   HIP_OK(hipEventRecord(s.ev1, s.stream));
   HIP_OK(hipStreamSynchronize(s.stream));

@@ -1,8 +1,8 @@
 // Batched pkg/sat resolution on MI355X (gfx950): one wavefront per problem.
 //
 // Each workgroup is one 64-lane wavefront that owns one problem.  The problem's
-// lowered record is copied into LDS, watch lists are built in LDS, and the whole
-// solve runs out of LDS:
+// lowered record is narrowed to 16 bits into LDS, watch lists are built in LDS,
+// and the whole solve runs out of LDS:
 //
 //   base scope + BCP        pkg/sat/solve.go:63-79           (base_propagate)
 //   preference search       pkg/sat/search.go:34-203         (search)
@@ -12,14 +12,21 @@
 //
 // Control flow is wave-uniform (every lane runs the same scalar logic on
 // broadcast LDS reads); the data-parallel parts are row evaluation (lanes over
-// the rows watched by a round's frontier, flattened with a wave prefix sum),
+// the rows watched by a round's frontier, flattened through an LDS work list),
 // the all-false-completion check (lanes over clause rows), candidate
 // membership tests (ballot), AtMost counting and conflict analysis.
 //
-// Semantics are exactly those of oracle/sat_oracle.c (the test oracle): in
-// particular a round's implications are resolved to the lowest implying row
-// with LDS atomicMin, so reasons, cores and step counts are bit-identical.
+// Semantics are exactly those of oracle/sat_oracle.c (the test oracle): a
+// round's implications are resolved to the lowest implying row with LDS
+// atomicMin, so reasons, cores and step counts are bit-identical.  (The oracle
+// orders assignments by round number, this kernel by the trail position where
+// the round started; the two orders agree on every pair of assigned variables.)
+//
+// Problems too large for LDS run the same code (HBM = true) on an int32 image
+// in an HBM scratch region.
 #include <hip/hip_runtime.h>
+
+#include <type_traits>
 
 #include "kernel_api.hpp"
 #include "layout.hpp"
@@ -42,40 +49,53 @@ __device__ __forceinline__ void wsync() {
 }
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
-
-__device__ __forceinline__ uint64_t lanemask_lt() {
-  return (1ull << lane_id()) - 1ull;
-}
+__device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
 
 __device__ __forceinline__ int wave_incl_scan(int x) {
   const int lane = lane_id();
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
-    int y = __shfl_up(x, d);
+    const int y = __shfl_up(x, d);
     if (lane >= d) x += y;
   }
   return x;
 }
 
+__device__ __forceinline__ int wave_min(int x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x = min(x, __shfl_xor(x, d));
+  return x;
+}
+
 __device__ __forceinline__ bool getb(const uint32_t* b, int i) { return (b[i >> 5] >> (i & 31)) & 1u; }
 
+template <bool HBM>
 struct Wave {
-  // ---- record views (LDS) ----
-  int nv, nc, nk, nid, nrows, nbv, nbi, na;
-  const int32_t *clause_off, *clause_lits, *clause_id;
-  const int32_t *card_off, *card_lits, *card_bound, *card_id;
-  const int32_t *var_choice_off, *choice_off, *choice_lits, *anchors;
-  // ---- working set (LDS) ----
-  int32_t *w_off, *w;
+  using IX = typename std::conditional<HBM, int32_t, uint16_t>::type;
+
+  // IX <-> int for the signed values (reasons R_DEC / R_EXTRA, "none" = -1)
+  __device__ __forceinline__ static int dec(IX x) {
+    if constexpr (HBM) return x;
+    else return x >= 0xfffe ? (int)x - 0x10000 : (int)x;
+  }
+  __device__ __forceinline__ static IX enc(int x) { return (IX)x; }
+
+  // ---- record views ----
+  int nv, nc, nk, nid, nrows, nbv, nbi, na, nch;
+  const IX *clause_off, *clause_lits, *clause_id;
+  const IX *card_off, *card_lits, *card_bound, *card_id;
+  const IX *var_choice_off, *choice_off, *choice_lits, *anchors;
+  // ---- working set ----
+  IX *w_off, *w;
   int8_t* val;
-  int32_t *reason, *rnd, *trail, *imp_pos, *imp_neg, *impflag, *touched, *d_lit, *d_mark, *dix;
-  uint32_t *d_flip, *inS, *extra, *seen, *model, *used, *en, *en2, *dset, *fg;
-  int32_t *l_off, *l_lits;
-  int32_t *dq, *stk, *pre, *preA, *scal;
+  IX *reason, *rs, *trail, *touched, *d_lit, *d_mark, *dix, *l_off, *l_lits, *dq, *stk;
+  uint32_t* imp;  // imp[2v] = lowest row implying +v, imp[2v+1] = -v
+  uint32_t *impflag, *d_flip, *inS, *extra, *seen, *model, *used, *en, *en2, *dset, *fg;
+  int32_t *wbuf, *scal;
   int cap, lcap;
   int lane;
   // ---- wave-uniform state (registers) ----
-  int tlen, qhead, round;
+  int tlen, qhead;
   int64_t steps, budget;
   bool budget_hit;
   int ck, c_row, c_var, c_rp, c_rn;
@@ -88,44 +108,70 @@ struct Wave {
   // ------------------------------------------------------------------
   // set-up (oracle: st_init)
   // ------------------------------------------------------------------
-  __device__ void init(int32_t* lds, const int32_t* __restrict__ grec) {
+  __device__ __forceinline__ void init(char* base, const int32_t* __restrict__ grec) {
     lane = lane_id();
-    // copy the record (16-byte aligned in HBM and LDS) with dwordx4 loads
-    const int words = grec[DP_H_WORDS];
-    const int q = (words + 3) >> 2;
-    const int4* src = reinterpret_cast<const int4*>(grec);
-    int4* dst = reinterpret_cast<int4*>(lds);
-    for (int i = lane; i < q; i += 64) dst[i] = src[i];
-    wsync();
-    const int32_t* h = lds;
-    LdsLayout L = lds_layout(h);
-    dp_rec_layout R = rec_layout(h);
+    int32_t h[DP_H_SIZE];
+#pragma unroll
+    for (int i = 0; i < DP_H_SIZE; ++i) h[i] = grec[i];
+    const Layout L = layout<IX>(h);
+    const dp_rec_layout R = rec_layout(h);
     nv = h[DP_H_NV]; nc = h[DP_H_NC]; nk = h[DP_H_NK]; nid = h[DP_H_NID]; na = h[DP_H_NA];
+    nch = h[DP_H_NCH];
     nrows = nc + nk;
     nbv = bits_words(nv); nbi = bits_words(nid);
-    clause_off = h + R.clause_off; clause_lits = h + R.clause_lits; clause_id = h + R.clause_id;
-    card_off = h + R.card_off; card_lits = h + R.card_lits; card_bound = h + R.card_bound;
-    card_id = h + R.card_id; var_choice_off = h + R.var_choice_off; choice_off = h + R.choice_off;
-    choice_lits = h + R.choice_lits; anchors = h + R.anchors;
-    w_off = lds + L.w_off; w = lds + L.w;
-    val = reinterpret_cast<int8_t*>(lds + L.val);
-    reason = lds + L.reason; rnd = lds + L.rnd; trail = lds + L.trail;
-    imp_pos = lds + L.imp_pos; imp_neg = lds + L.imp_neg; impflag = lds + L.impflag;
-    touched = lds + L.touched; d_lit = lds + L.d_lit; d_mark = lds + L.d_mark; dix = lds + L.dix;
-    d_flip = reinterpret_cast<uint32_t*>(lds + L.d_flip);
-    inS = reinterpret_cast<uint32_t*>(lds + L.inS);
-    extra = reinterpret_cast<uint32_t*>(lds + L.extra);
-    seen = reinterpret_cast<uint32_t*>(lds + L.seen);
-    model = reinterpret_cast<uint32_t*>(lds + L.model);
-    used = reinterpret_cast<uint32_t*>(lds + L.used);
-    en = reinterpret_cast<uint32_t*>(lds + L.en);
-    en2 = reinterpret_cast<uint32_t*>(lds + L.en2);
-    dset = reinterpret_cast<uint32_t*>(lds + L.dset);
-    fg = reinterpret_cast<uint32_t*>(lds + L.fg);
-    l_off = lds + L.l_off; l_lits = lds + L.l_lits;
-    dq = lds + L.dq; stk = lds + L.stk; pre = lds + L.pre; preA = lds + L.preA; scal = lds + L.scal;
+    // record body: HBM int32 -> working-set IX (dwordx4 loads; records are
+    // 16-byte aligned and padded to 4 words)
+    IX* body = reinterpret_cast<IX*>(base + L.body);
+    {
+      const int groups = (h[DP_H_WORDS] - DP_H_SIZE + 3) >> 2;
+      const int4* src = reinterpret_cast<const int4*>(grec + DP_H_SIZE);
+      for (int i = lane; i < groups; i += 64) {
+        const int4 x = src[i];
+        if constexpr (HBM) {
+          reinterpret_cast<int4*>(body)[i] = x;
+        } else {
+          uint2 y;
+          y.x = (uint32_t)(x.x & 0xffff) | ((uint32_t)x.y << 16);
+          y.y = (uint32_t)(x.z & 0xffff) | ((uint32_t)x.w << 16);
+          reinterpret_cast<uint2*>(body)[i] = y;
+        }
+      }
+    }
+    auto rv = [&](int32_t word_off) { return body + (word_off - DP_H_SIZE); };
+    clause_off = rv(R.clause_off); clause_lits = rv(R.clause_lits); clause_id = rv(R.clause_id);
+    card_off = rv(R.card_off); card_lits = rv(R.card_lits); card_bound = rv(R.card_bound);
+    card_id = rv(R.card_id); var_choice_off = rv(R.var_choice_off); choice_off = rv(R.choice_off);
+    choice_lits = rv(R.choice_lits); anchors = rv(R.anchors);
+    w_off = reinterpret_cast<IX*>(base + L.w_off);
+    w = reinterpret_cast<IX*>(base + L.w);
+    val = reinterpret_cast<int8_t*>(base + L.val);
+    reason = reinterpret_cast<IX*>(base + L.reason);
+    rs = reinterpret_cast<IX*>(base + L.rs);
+    trail = reinterpret_cast<IX*>(base + L.trail);
+    touched = reinterpret_cast<IX*>(base + L.touched);
+    d_lit = reinterpret_cast<IX*>(base + L.d_lit);
+    d_mark = reinterpret_cast<IX*>(base + L.d_mark);
+    dix = reinterpret_cast<IX*>(base + L.dix);
+    imp = reinterpret_cast<uint32_t*>(base + L.imp);
+    impflag = reinterpret_cast<uint32_t*>(base + L.impflag);
+    d_flip = reinterpret_cast<uint32_t*>(base + L.d_flip);
+    inS = reinterpret_cast<uint32_t*>(base + L.inS);
+    extra = reinterpret_cast<uint32_t*>(base + L.extra);
+    seen = reinterpret_cast<uint32_t*>(base + L.seen);
+    model = reinterpret_cast<uint32_t*>(base + L.model);
+    dset = reinterpret_cast<uint32_t*>(base + L.dset);
+    fg = reinterpret_cast<uint32_t*>(base + L.fg);
+    used = reinterpret_cast<uint32_t*>(base + L.used);
+    en = reinterpret_cast<uint32_t*>(base + L.en);
+    en2 = reinterpret_cast<uint32_t*>(base + L.en2);
+    l_off = reinterpret_cast<IX*>(base + L.l_off);
+    l_lits = reinterpret_cast<IX*>(base + L.l_lits);
+    dq = reinterpret_cast<IX*>(base + L.dq);
+    stk = reinterpret_cast<IX*>(base + L.stk);
+    wbuf = reinterpret_cast<int32_t*>(base + L.wbuf);
+    scal = reinterpret_cast<int32_t*>(base + L.scal);
     cap = L.cap; lcap = L.lcap;
-    tlen = qhead = round = 0;
+    tlen = qhead = 0;
     steps = 0;
     budget_hit = false;
     ck = CK_NONE; c_row = c_var = c_rp = c_rn = 0;
@@ -136,39 +182,40 @@ struct Wave {
     extra_mode = false;
     extra_w = 0;
 
-    for (int v = lane; v < nv; v += 64) {
-      val[v] = 0; impflag[v] = 0;
-    }
+    for (int v = lane; v < nv; v += 64) val[v] = 0;
+    for (int i = lane; i < bits_words(2 * nv); i += 64) impflag[i] = 0;
     for (int i = lane; i < nbv; i += 64) {
       d_flip[i] = 0; inS[i] = 0; extra[i] = 0; seen[i] = 0; model[i] = 0; dset[i] = 0; fg[i] = 0;
     }
-    if (lane == 0) l_off[0] = 0;
+    if (lane == 0) { l_off[0] = 0; scal[S_NTOUCHED] = 0; }
     // watch lists: a clause literal x of row r is watched by ~x; a card
-    // position v of row k by +v
+    // position v of row k by +v (oracle st_init); counts go through the
+    // 32-bit imp[] (2nv words) so LDS atomics can build them
     const int nl2 = 2 * nv;
-    for (int l = lane; l <= nl2; l += 64) w_off[l] = 0;
+    uint32_t* cnt = imp;
+    for (int l = lane; l < nl2; l += 64) cnt[l] = 0;
     wsync();
-    for (int j = lane; j < h[DP_H_NCL]; j += 64) atomicAdd(&w_off[(clause_lits[j] ^ 1) + 1], 1);
-    for (int j = lane; j < h[DP_H_NKL]; j += 64) atomicAdd(&w_off[2 * card_lits[j] + 1], 1);
+    for (int j = lane; j < h[DP_H_NCL]; j += 64) atomicAdd(&cnt[clause_lits[j] ^ 1], 1u);
+    for (int j = lane; j < h[DP_H_NKL]; j += 64) atomicAdd(&cnt[2 * (int)card_lits[j]], 1u);
     wsync();
     int carry = 0;
-    for (int base = 0; base < nl2; base += 64) {
-      const int i = base + 1 + lane;
-      const int x = i <= nl2 ? w_off[i] : 0;
+    for (int b = 0; b < nl2; b += 64) {
+      const int l = b + lane;
+      const int x = l < nl2 ? (int)cnt[l] : 0;
       const int inc = wave_incl_scan(x) + carry;
-      if (i <= nl2) w_off[i] = inc;
+      if (l < nl2) { w_off[l + 1] = enc(inc); cnt[l] = (uint32_t)(inc - x); }  // cnt -> cursor
       carry = __shfl(inc, 63);
     }
-    wsync();
-    int32_t* cursor = imp_pos;  // imp_pos|imp_neg hold >= 2nv words
-    for (int l = lane; l < nl2; l += 64) cursor[l] = w_off[l];
+    if (lane == 0) w_off[0] = 0;
     wsync();
     for (int r = lane; r < nc; r += 64)
-      for (int j = clause_off[r]; j < clause_off[r + 1]; ++j) w[atomicAdd(&cursor[clause_lits[j] ^ 1], 1)] = r;
+      for (int j = clause_off[r]; j < clause_off[r + 1]; ++j)
+        w[atomicAdd(&cnt[clause_lits[j] ^ 1], 1u)] = enc(r);
     for (int k = lane; k < nk; k += 64)
-      for (int j = card_off[k]; j < card_off[k + 1]; ++j) w[atomicAdd(&cursor[2 * card_lits[j]], 1)] = nc + k;
+      for (int j = card_off[k]; j < card_off[k + 1]; ++j)
+        w[atomicAdd(&cnt[2 * (int)card_lits[j]], 1u)] = enc(nc + k);
     wsync();
-    for (int v = lane; v < nv; v += 64) { imp_pos[v] = INF; imp_neg[v] = INF; }
+    for (int l = lane; l < nl2; l += 64) imp[l] = (uint32_t)INF;
     wsync();
   }
 
@@ -176,7 +223,7 @@ struct Wave {
   // unit propagation (oracle: eval_row / finish_round / propagate)
   // ------------------------------------------------------------------
   __device__ __forceinline__ int row_ident(int r) const {
-    return r < nc ? clause_id[r] : r < nrows ? card_id[r - nc] : -1;
+    return r < nc ? (int)clause_id[r] : r < nrows ? (int)card_id[r - nc] : -1;
   }
   __device__ __forceinline__ bool row_on(int r) const { return !enabled || getb(enabled, row_ident(r)); }
   __device__ __forceinline__ int lit_val(int l) const {
@@ -184,31 +231,41 @@ struct Wave {
     return (l & 1) ? -x : x;
   }
 
+  // record "row r implies literal l" (lowest row wins, oracle: note)
   __device__ __forceinline__ void note(int l, int r) {
     const int v = l >> 1;
-    const int old = atomicOr(&impflag[v], (l & 1) ? 2 : 1);
-    if (old == 0) touched[atomicAdd(&scal[S_NTOUCHED], 1)] = v;
-    atomicMin((l & 1) ? &imp_neg[v] : &imp_pos[v], r);
+    const uint32_t sh = (uint32_t)(2 * v) & 31u;
+    const uint32_t old = atomicOr(&impflag[(2 * v) >> 5], 1u << (sh + (l & 1)));
+    if (((old >> sh) & 3u) == 0) touched[atomicAdd(&scal[S_NTOUCHED], 1)] = enc(v);
+    atomicMin(&imp[l], (uint32_t)r);
   }
 
-  __device__ __forceinline__ void eval_clause(int r, const int32_t* lits, int a, int b) {
+  // clause row evaluation; the literal loads are issued four at a time
+  __device__ __forceinline__ void eval_clause(int r, const IX* lits, int a, int b, int& crow) {
     int nun = 0, ul = -1;
-    for (int j = a; j < b; ++j) {
-      const int l = lits[j];
-      const int x = lit_val(l);
-      if (x > 0) return;
-      if (x == 0) { ++nun; ul = l; }
+    for (int j = a; j < b; j += 4) {
+      int l[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) l[k] = j + k < b ? (int)lits[j + k] : -1;
+      int x[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) x[k] = l[k] >= 0 ? lit_val(l[k]) : -1;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (x[k] > 0) return;  // satisfied
+        if (x[k] == 0) { ++nun; ul = l[k]; }
+      }
     }
-    if (nun == 0) atomicMin(&scal[S_CROW], r);
+    if (nun == 0) crow = min(crow, r);
     else if (nun == 1) note(ul, r);
   }
 
-  __device__ void eval_row(int r) {
+  __device__ __forceinline__ void eval_row(int r, int& crow) {
     if (r < nc) {
-      eval_clause(r, clause_lits, clause_off[r], clause_off[r + 1]);
+      eval_clause(r, clause_lits, clause_off[r], clause_off[r + 1], crow);
     } else if (r >= nrows) {
       const int j = r - nrows;
-      eval_clause(r, l_lits, l_off[j], l_off[j + 1]);
+      eval_clause(r, l_lits, l_off[j], l_off[j + 1], crow);
     } else {
       const int k = r - nc, a = card_off[k], b = card_off[k + 1];
       int cnt = 0, nun = 0;
@@ -218,13 +275,13 @@ struct Wave {
         nun += (x == 0);
       }
       const int bound = card_bound[k];
-      if (cnt > bound) atomicMin(&scal[S_CROW], r);
+      if (cnt > bound) crow = min(crow, r);
       else if (nun > 0) {
         // a variable repeated m times is a run of m positions
         for (int j = a; j < b;) {
           const int v = card_lits[j];
           int e = j + 1;
-          while (e < b && card_lits[e] == v) ++e;
+          while (e < b && (int)card_lits[e] == v) ++e;
           if (val[v] == 0 && cnt + (e - j) > bound) note(2 * v + 1, r);
           j = e;
         }
@@ -233,68 +290,68 @@ struct Wave {
   }
 
   // learned rows are evaluated in every round (lanes over rows)
-  __device__ __forceinline__ void eval_learned() {
+  __device__ __forceinline__ void eval_learned(int& crow) {
     if (!learn_on) return;
-    for (int j = lane; j < nl; j += 64) eval_row(nrows + j);
+    for (int j = lane; j < nl; j += 64) eval_row(nrows + j, crow);
   }
 
-  __device__ __forceinline__ void begin_round() {
-    scal[S_CROW] = INF;
-    scal[S_CVAR] = INF;
-    scal[S_NTOUCHED] = 0;
-    wsync();
-  }
-
-  __device__ void clear_touched(int nt) {
+  __device__ __forceinline__ void clear_touched(int nt) {
     for (int i = lane; i < nt; i += 64) {
       const int v = touched[i];
-      impflag[v] = 0; imp_pos[v] = INF; imp_neg[v] = INF;
+      imp[2 * v] = (uint32_t)INF; imp[2 * v + 1] = (uint32_t)INF;
     }
+    for (int i = lane; i < bits_words(2 * nv); i += 64) impflag[i] = 0;
+    if (lane == 0) scal[S_NTOUCHED] = 0;
     wsync();
   }
 
-  __device__ int finish_round(int rd) {
+  // Commit the implications of the round, or report its conflict: the lowest
+  // conflicting row, else the lowest variable implied both ways.
+  __device__ __forceinline__ int finish_round(int crow) {
     wsync();
-    const int crow = scal[S_CROW];
     const int nt = scal[S_NTOUCHED];
-    if (crow != INF) {
+    if (__ballot(crow != INF)) {
+      c_row = wave_min(crow);
       clear_touched(nt);
-      ck = CK_ROW; c_row = crow;
+      ck = CK_ROW;
       return -1;
     }
+    int cv = INF;
     for (int i = lane; i < nt; i += 64) {
       const int v = touched[i];
-      if (impflag[v] == 3) atomicMin(&scal[S_CVAR], v);
+      const uint32_t f = (impflag[(2 * v) >> 5] >> ((2 * v) & 31)) & 3u;
+      if (f == 3u) cv = min(cv, v);
     }
-    wsync();
-    const int cvar = scal[S_CVAR];
-    if (cvar != INF) {
-      c_rp = imp_pos[cvar]; c_rn = imp_neg[cvar];
-      wsync();
-      ck = CK_VAR; c_var = cvar; c_row = rd;
+    if (__ballot(cv != INF)) {
+      cv = wave_min(cv);
+      c_rp = (int)imp[2 * cv]; c_rn = (int)imp[2 * cv + 1];
+      ck = CK_VAR; c_var = cv; c_row = tlen;  // bound: every variable assigned so far
       clear_touched(nt);
       return -1;
     }
+    const int start = tlen;
     for (int i = lane; i < nt; i += 64) {
       const int v = touched[i];
-      const int rp = imp_pos[v];
-      const bool pos = rp != INF;
+      const uint32_t rp = imp[2 * v];
+      const bool pos = rp != (uint32_t)INF;
       val[v] = pos ? 1 : -1;
-      reason[v] = pos ? rp : imp_neg[v];
-      rnd[v] = rd;
-      dix[v] = -1;
-      trail[tlen + i] = 2 * v + (pos ? 0 : 1);
-      impflag[v] = 0; imp_pos[v] = INF; imp_neg[v] = INF;
+      reason[v] = enc(pos ? (int)rp : (int)imp[2 * v + 1]);
+      rs[v] = enc(start);
+      dix[v] = enc(-1);
+      trail[start + i] = enc(2 * v + (pos ? 0 : 1));
+      imp[2 * v] = (uint32_t)INF; imp[2 * v + 1] = (uint32_t)INF;
     }
+    for (int i = lane; i < bits_words(2 * nv); i += 64) impflag[i] = 0;
+    if (lane == 0) scal[S_NTOUCHED] = 0;
     tlen += nt;
     wsync();
     return 0;
   }
 
-  __device__ int extra_check() {
+  __device__ __forceinline__ int extra_check() {
     int cnt = 0, nun = 0;
-    for (int base = 0; base < nv; base += 64) {
-      const int v = base + lane;
+    for (int b = 0; b < nv; b += 64) {
+      const int v = b + lane;
       const bool ex = v < nv && getb(extra, v);
       const int x = ex ? val[v] : 0;
       cnt += __popcll(__ballot(ex && x > 0));
@@ -302,14 +359,14 @@ struct Wave {
     }
     if (cnt > extra_w) { ck = CK_EXTRA; return -1; }
     if (cnt == extra_w && nun > 0) {
-      const int rd = ++round;
-      for (int base = 0; base < nv; base += 64) {
-        const int v = base + lane;
+      const int start = tlen;
+      for (int b = 0; b < nv; b += 64) {
+        const int v = b + lane;
         const bool f = v < nv && getb(extra, v) && val[v] == 0;
         const uint64_t m = __ballot(f);
         if (f) {
-          val[v] = -1; reason[v] = R_EXTRA; rnd[v] = rd; dix[v] = -1;
-          trail[tlen + __popcll(m & lanemask_lt())] = 2 * v + 1;
+          val[v] = -1; reason[v] = enc(R_EXTRA); rs[v] = enc(start); dix[v] = enc(-1);
+          trail[tlen + __popcll(m & lanemask_lt())] = enc(2 * v + 1);
         }
         tlen += __popcll(m);
       }
@@ -319,7 +376,7 @@ struct Wave {
     return 0;
   }
 
-  __device__ int propagate() {
+  __device__ __forceinline__ int propagate() {
     for (;;) {
       if (qhead == tlen) {
         if (extra_mode) {
@@ -329,83 +386,90 @@ struct Wave {
         }
         return tlen == nv ? 1 : 0;
       }
-      const int lo = qhead, hi = tlen, rd = ++round;
+      const int lo = qhead, hi = tlen;
       qhead = hi;
-      begin_round();
-      for (int base = lo; base < hi; base += 64) {
-        const int i = base + lane;
+      int crow = INF;
+      for (int b = lo; b < hi; b += 64) {
+        const int i = b + lane;
         int cnt = 0, a = 0;
         if (i < hi) {
           const int l = trail[i];
           a = w_off[l];
-          cnt = w_off[l + 1] - a;
+          cnt = (int)w_off[l + 1] - a;
         }
         const int incl = wave_incl_scan(cnt);
         const int total = __shfl(incl, 63);
-        pre[lane] = incl - cnt;
-        preA[lane] = a;
-        wsync();
-        for (int t = lane; t < total; t += 64) {
-          int lo2 = 0, hi2 = 63;  // last frontier entry whose range starts at or before t
-          while (lo2 < hi2) {
-            const int mid = (lo2 + hi2 + 1) >> 1;
-            if (pre[mid] <= t) lo2 = mid; else hi2 = mid - 1;
+        if (total <= WBUF) {
+          // flatten: every frontier literal writes its watch range into the list
+          for (int k = 0, at = incl - cnt; k < cnt; ++k) wbuf[at + k] = a + k;
+          wsync();
+          for (int t = lane; t < total; t += 64) {
+            const int r = w[wbuf[t]];
+            if (row_on(r)) eval_row(r, crow);
           }
-          const int r = w[preA[lo2] + (t - pre[lo2])];
-          if (row_on(r)) eval_row(r);
+          wsync();
+        } else {
+          // a very large chunk: one frontier literal at a time
+          const int n = min(64, hi - b);
+          for (int e = 0; e < n; ++e) {
+            const int l = trail[b + e];
+            for (int k = (int)w_off[l] + lane; k < (int)w_off[l + 1]; k += 64) {
+              const int r = w[k];
+              if (row_on(r)) eval_row(r, crow);
+            }
+          }
         }
-        wsync();
       }
-      eval_learned();
-      if (finish_round(rd) < 0) return -1;
+      eval_learned(crow);
+      if (finish_round(crow) < 0) return -1;
     }
   }
 
-  __device__ int base_propagate() {
-    const int rd = ++round;
-    begin_round();
+  // The base scope (solve.go:63-79): one round evaluates every (enabled) row.
+  __device__ __forceinline__ int base_propagate() {
+    int crow = INF;
     for (int r = lane; r < nrows; r += 64)
-      if (row_on(r)) eval_row(r);
-    eval_learned();
-    if (finish_round(rd) < 0) return -1;
+      if (row_on(r)) eval_row(r, crow);
+    eval_learned(crow);
+    if (finish_round(crow) < 0) return -1;
     return propagate();
   }
 
-  __device__ void truncate_to(int mark) {
-    for (int i = mark + lane; i < tlen; i += 64) val[trail[i] >> 1] = 0;
+  __device__ __forceinline__ void truncate_to(int mark) {
+    for (int i = mark + lane; i < tlen; i += 64) val[(int)trail[i] >> 1] = 0;
     tlen = qhead = mark;
     wsync();
   }
 
   // gini Untest() (search.go:84): the learned rows decide the restored scope
-  __device__ int untest_to(int mark) {
+  __device__ __forceinline__ int untest_to(int mark) {
     truncate_to(mark);
     if (learn_on && nl > 0) {
-      const int rd = ++round;
-      begin_round();
-      eval_learned();
-      if (finish_round(rd) < 0) return -1;
+      int crow = INF;
+      eval_learned(crow);
+      if (finish_round(crow) < 0) return -1;
       return propagate();
     }
     return tlen == nv ? 1 : 0;
   }
 
-  __device__ void assign_one(int l, int why, int rd, int decision) {
+  __device__ __forceinline__ void assign_one(int l, int why, int decision) {
     if (lane == 0) {
       const int v = l >> 1;
-      val[v] = (l & 1) ? -1 : 1; reason[v] = why; rnd[v] = rd; dix[v] = decision; trail[tlen] = l;
+      val[v] = (l & 1) ? -1 : 1; reason[v] = enc(why); rs[v] = enc(tlen);
+      dix[v] = enc(decision); trail[tlen] = enc(l);
     }
     ++tlen;
     wsync();
   }
 
   // gini Assume(m) + Test() (search.go:75-76)
-  __device__ int test_assume(int l) {
+  __device__ __forceinline__ int test_assume(int l) {
     ++steps;
     const int x = lit_val(l);
     if (x > 0) return propagate();
     if (x < 0) { ck = CK_ASSUME; c_var = l >> 1; return -1; }
-    assign_one(l, R_DEC, ++round, -1);
+    assign_one(l, R_DEC, -1);
     return propagate();
   }
 
@@ -415,20 +479,20 @@ struct Wave {
   __device__ __forceinline__ void mark_push(int v) {
     const uint32_t bit = 1u << (v & 31);
     const uint32_t old = atomicOr(&seen[v >> 5], bit);
-    if (!(old & bit)) touched[atomicAdd(&scal[S_NWORK], 1)] = v;
+    if (!(old & bit)) touched[atomicAdd(&scal[S_NWORK], 1)] = enc(v);
   }
   __device__ __forceinline__ void set_bit_atomic(uint32_t* b, int i) { atomicOr(&b[i >> 5], 1u << (i & 31)); }
 
-  // antecedents of row r for variable u (assigned in round bound_rd); serial
-  // in the calling lane
-  __device__ void ante_serial(int r, int u, int bound_rd) {
+  // antecedents of row r for variable u, whose round started at trail
+  // position bound (serial in the calling lane)
+  __device__ __forceinline__ void ante_serial(int r, int u, int bound) {
     if (r < nc || r >= nrows) {
-      const int32_t* lits = clause_lits;
+      const IX* lits = clause_lits;
       int a, b;
       if (r < nc) { a = clause_off[r]; b = clause_off[r + 1]; set_bit_atomic(used, clause_id[r]); }
       else { lits = l_lits; a = l_off[r - nrows]; b = l_off[r - nrows + 1]; }
       for (int j = a; j < b; ++j) {
-        const int v = lits[j] >> 1;
+        const int v = (int)lits[j] >> 1;
         if (v != u) mark_push(v);
       }
     } else {
@@ -436,17 +500,17 @@ struct Wave {
       set_bit_atomic(used, card_id[k]);
       for (int j = card_off[k]; j < card_off[k + 1]; ++j) {
         const int v = card_lits[j];
-        if (v != u && val[v] > 0 && rnd[v] < bound_rd) mark_push(v);
+        if (v != u && val[v] > 0 && (int)rs[v] < bound) mark_push(v);
       }
     }
   }
-  __device__ void extra_serial(int u, int bound_rd) {
+  __device__ __forceinline__ void extra_serial(int u, int bound) {
     for (int v = 0; v < nv; ++v)
-      if (v != u && getb(extra, v) && val[v] > 0 && rnd[v] < bound_rd) mark_push(v);
+      if (v != u && getb(extra, v) && val[v] > 0 && (int)rs[v] < bound) mark_push(v);
   }
 
-  __device__ void analyze() {
-    scal[S_NWORK] = 0;
+  __device__ __forceinline__ void analyze() {
+    if (lane == 0) scal[S_NWORK] = 0;
     wsync();
     if (lane == 0) {
       if (ck == CK_ROW) ante_serial(c_row, -1, INF);
@@ -460,10 +524,10 @@ struct Wave {
       if (head >= nw) break;
       for (int i = head + lane; i < nw; i += 64) {
         const int u = touched[i];
-        const int r = reason[u];
-        if (r >= 0) ante_serial(r, u, rnd[u]);
-        else if (r == R_EXTRA) extra_serial(u, rnd[u]);
-        else if (dix[u] >= 0) set_bit_atomic(dset, dix[u]);
+        const int r = dec(reason[u]);
+        if (r >= 0) ante_serial(r, u, rs[u]);
+        else if (r == R_EXTRA) extra_serial(u, rs[u]);
+        else if (dec(dix[u]) >= 0) set_bit_atomic(dset, dix[u]);
         else if (collect_guess && getb(inS, u)) set_bit_atomic(fg, u);
       }
       head = nw;
@@ -480,9 +544,9 @@ struct Wave {
   // ------------------------------------------------------------------
   // Solve(): CDCL from a consistent fixpoint (oracle: first_violated / dpll)
   // ------------------------------------------------------------------
-  __device__ int first_violated() {
-    for (int base = 0; base < nc; base += 64) {
-      const int c = base + lane;
+  __device__ __forceinline__ int first_violated() {
+    for (int b = 0; b < nc; b += 64) {
+      const int c = b + lane;
       bool viol = false;
       int fu = -1;
       if (c < nc && row_on(c)) {
@@ -504,24 +568,24 @@ struct Wave {
     return -1;
   }
 
-  __device__ void save_model() {
-    for (int base = 0; base < nv; base += 64) {
-      const int v = base + lane;
+  __device__ __forceinline__ void save_model() {
+    for (int b = 0; b < nv; b += 64) {
+      const int v = b + lane;
       const uint64_t m = __ballot(v < nv && val[v] > 0);
       if (lane == 0) {
-        model[base >> 5] = (uint32_t)m;
-        if ((base >> 5) + 1 < nbv) model[(base >> 5) + 1] = (uint32_t)(m >> 32);
+        model[b >> 5] = (uint32_t)m;
+        if ((b >> 5) + 1 < nbv) model[(b >> 5) + 1] = (uint32_t)(m >> 32);
       }
     }
     wsync();
   }
 
-  __device__ void clear_bits(uint32_t* b, int n) {
-    for (int i = lane; i < bits_words(n); i += 64) b[i] = 0;
+  __device__ __forceinline__ void clear_bits(uint32_t* bs, int n) {
+    for (int i = lane; i < bits_words(n); i += 64) bs[i] = 0;
     wsync();
   }
 
-  __device__ int dpll() {
+  __device__ __forceinline__ int dpll() {
     const int root = tlen, nl0 = nl;
     int nd = 0, r;
     for (;;) {
@@ -529,10 +593,10 @@ struct Wave {
       if (l < 0) { save_model(); r = RS_SAT; break; }
       if (++steps > budget) { budget_hit = true; r = RS_BUDGET; break; }
       if (lane == 0) {
-        d_lit[nd] = l; d_mark[nd] = tlen;
+        d_lit[nd] = enc(l); d_mark[nd] = enc(tlen);
         d_flip[nd >> 5] &= ~(1u << (nd & 31));
       }
-      assign_one(l, R_DEC, ++round, nd);
+      assign_one(l, R_DEC, nd);
       ++nd;
       int res = propagate();
       bool unsat = false;
@@ -560,22 +624,22 @@ struct Wave {
             const int i = base + lane;
             const bool in = i < nd && getb(dset, i);
             const uint64_t m = __ballot(in);
-            if (in) l_lits[at + __popcll(m & lanemask_lt())] = d_lit[i] ^ 1;
+            if (in) l_lits[at + __popcll(m & lanemask_lt())] = enc((int)d_lit[i] ^ 1);
             at += __popcll(m);
           }
-          if (lane == 0) l_off[nl + 1] = at;
+          if (lane == 0) l_off[nl + 1] = enc(at);
           ++nl;
           wsync();
           nd = b + 1;
           truncate_to(d_mark[nd]);
-          assign_one(d_lit[h] ^ 1, nrows + nl - 1, ++round, -1);
+          assign_one((int)d_lit[h] ^ 1, nrows + nl - 1, -1);
         } else {
           while (nd > 0 && getb(d_flip, nd - 1)) --nd;
           if (nd == 0) { unsat = true; break; }
           truncate_to(d_mark[nd - 1]);
           if (lane == 0) d_flip[(nd - 1) >> 5] |= 1u << ((nd - 1) & 31);
           wsync();
-          assign_one(d_lit[nd - 1] ^ 1, R_DEC, ++round, nd - 1);
+          assign_one((int)d_lit[nd - 1] ^ 1, R_DEC, nd - 1);
         }
         res = propagate();
       }
@@ -593,25 +657,26 @@ struct Wave {
   int dq_head, dq_n, ng, result;
   bool class_b, solve_unsat, last_solve;
 
+  // choice lists: rows 0..nch-1; the singleton list of anchor v is nch + v
   __device__ __forceinline__ int list_len(int list) const {
-    return list < 0 ? 1 : choice_off[list + 1] - choice_off[list];
+    return list >= nch ? 1 : (int)choice_off[list + 1] - (int)choice_off[list];
   }
   __device__ __forceinline__ int list_at(int list, int i) const {
-    return list < 0 ? ~list : choice_lits[choice_off[list] + i];
+    return list >= nch ? list - nch : (int)choice_lits[(int)choice_off[list] + i];
   }
   __device__ __forceinline__ void dq_push_back(int list, int idx) {
     const int at = (dq_head + dq_n) % cap;
-    if (lane == 0) { dq[2 * at] = list; dq[2 * at + 1] = idx; }
+    if (lane == 0) { dq[2 * at] = enc(list); dq[2 * at + 1] = enc(idx); }
     ++dq_n;
   }
   __device__ __forceinline__ void dq_push_front(int list, int idx) {
     dq_head = (dq_head + cap - 1) % cap;
-    if (lane == 0) { dq[2 * dq_head] = list; dq[2 * dq_head + 1] = idx; }
+    if (lane == 0) { dq[2 * dq_head] = enc(list); dq[2 * dq_head + 1] = enc(idx); }
     ++dq_n;
   }
 
   // PushGuess, search.go:34-77
-  __device__ void push_guess() {
+  __device__ __forceinline__ void push_guess() {
     wsync();
     const int list = dq[2 * dq_head], idx = dq[2 * dq_head + 1];
     dq_head = (dq_head + 1) % cap;
@@ -624,30 +689,29 @@ struct Wave {
     else if (idx >= len) class_b = true;  // exhausted choice
     int children = 0;
     if (m >= 0)
-      for (int r = var_choice_off[m]; r < var_choice_off[m + 1]; ++r) {
+      for (int r = var_choice_off[m]; r < (int)var_choice_off[m + 1]; ++r) {
         dq_push_back(r, 0);
         ++children;
       }
     if (lane == 0) {
-      int32_t* g = stk + 5 * ng;
-      g[0] = list; g[1] = idx; g[2] = m; g[3] = children; g[4] = tlen;
+      IX* g = stk + 5 * ng;
+      g[0] = enc(list); g[1] = enc(idx); g[2] = enc(m); g[3] = enc(children); g[4] = enc(tlen);
+      if (m >= 0) inS[m >> 5] |= 1u << (m & 31);
     }
     ++ng;
     wsync();
     if (m < 0) return;
-    if (lane == 0) inS[m >> 5] |= 1u << (m & 31);
-    wsync();
     if (steps >= budget) { budget_hit = true; result = 0; return; }
     result = test_assume(2 * m);
     last_solve = false;
   }
 
   // PopGuess, search.go:79-98
-  __device__ void pop_guess() {
+  __device__ __forceinline__ void pop_guess() {
     wsync();
     --ng;
-    const int32_t* g = stk + 5 * ng;
-    const int list = g[0], idx = g[1], m = g[2], children = g[3], mark = g[4];
+    const IX* g = stk + 5 * ng;
+    const int list = g[0], idx = g[1], m = dec(g[2]), children = g[3], mark = g[4];
     wsync();
     if (m >= 0) {
       if (lane == 0) inS[m >> 5] &= ~(1u << (m & 31));
@@ -662,7 +726,7 @@ struct Wave {
 
   // Solve() within the search: a failure learns the nogood of the guesses its
   // refutation reached (oracle: be_solve / learn)
-  __device__ int search_solve() {
+  __device__ __forceinline__ int search_solve() {
     clear_bits(fg, nv);
     collect_guess = true;
     const int r = dpll();
@@ -673,14 +737,14 @@ struct Wave {
       const int lat = l_off[nl];
       if (nl < L_MAX && lat + n <= lcap) {
         int at = lat;
-        for (int base = 0; base < nv; base += 64) {
-          const int v = base + lane;
+        for (int b = 0; b < nv; b += 64) {
+          const int v = b + lane;
           const bool in = v < nv && getb(fg, v);
           const uint64_t m = __ballot(in);
-          if (in) l_lits[at + __popcll(m & lanemask_lt())] = 2 * v + 1;
+          if (in) l_lits[at + __popcll(m & lanemask_lt())] = enc(2 * v + 1);
           at += __popcll(m);
         }
-        if (lane == 0) l_off[nl + 1] = at;
+        if (lane == 0) l_off[nl + 1] = enc(at);
         ++nl;
         wsync();
       }
@@ -689,11 +753,11 @@ struct Wave {
   }
 
   // Returns the search result; leaves the final guess set in inS.
-  __device__ int search() {
+  __device__ __forceinline__ int search() {
     dq_head = dq_n = ng = 0;
     result = 0;
     class_b = solve_unsat = last_solve = false;
-    for (int i = 0; i < na; ++i) dq_push_back(~anchors[i], 0);
+    for (int i = 0; i < na; ++i) dq_push_back(nch + (int)anchors[i], 0);
     wsync();
     for (;;) {
       if (dq_n == 0 && result == 0) {
@@ -720,23 +784,23 @@ struct Wave {
   // ------------------------------------------------------------------
   // NotSatisfiable (oracle: refute / core_extract)
   // ------------------------------------------------------------------
-  __device__ void reset_all() { truncate_to(0); }
+  __device__ __forceinline__ void reset_all() { truncate_to(0); }
 
-  __device__ void fill_bits(uint32_t* b, int n, bool ones) {
+  __device__ __forceinline__ void fill_bits(uint32_t* bs, int n, bool ones) {
     const int nw = bits_words(n);
     for (int i = lane; i < nw; i += 64) {
       uint32_t x = 0;
       if (ones) x = (i == nw - 1 && (n & 31)) ? ((1u << (n & 31)) - 1u) : 0xffffffffu;
-      b[i] = x;
+      bs[i] = x;
     }
     wsync();
   }
-  __device__ void copy_bits(uint32_t* dst, const uint32_t* src, int n) {
+  __device__ __forceinline__ void copy_bits(uint32_t* dst, const uint32_t* src, int n) {
     for (int i = lane; i < bits_words(n); i += 64) dst[i] = src[i];
     wsync();
   }
 
-  __device__ int refute(const uint32_t* K) {
+  __device__ __forceinline__ int refute(const uint32_t* K) {
     reset_all();
     learn_on = false;
     enabled = K;
@@ -750,7 +814,7 @@ struct Wave {
     return r;
   }
 
-  __device__ int core(int32_t* out, int32_t& flags) {
+  __device__ __forceinline__ int core(int32_t* out, int32_t& flags) {
     const int64_t saved = steps;
     steps = 0;
     int len = 0;
@@ -767,8 +831,8 @@ struct Wave {
         if (r == RS_UNSAT) copy_bits(en, used, nid);
         else if (r == RS_BUDGET) { flags |= DP_F_CORE_BUDGET; break; }
       }
-      for (int base = 0; base < nid; base += 64) {  // ascending identity ids
-        const int id = base + lane;
+      for (int b = 0; b < nid; b += 64) {  // ascending identity ids
+        const int id = b + lane;
         const bool in = id < nid && getb(en, id);
         const uint64_t m = __ballot(in);
         if (in) out[len + __popcll(m & lanemask_lt())] = id;
@@ -785,7 +849,7 @@ struct Wave {
   // ------------------------------------------------------------------
   // SAT epilogue, solve.go:86-110 (oracle: epilogue)
   // ------------------------------------------------------------------
-  __device__ int epilogue(int32_t& flags, uint32_t* __restrict__ out) {
+  __device__ __forceinline__ int epilogue(int32_t& flags, uint32_t* __restrict__ out) {
     for (int i = lane; i < nbv; i += 64) extra[i] = model[i] & ~inS[i];
     wsync();
     int ne = 0;
@@ -797,10 +861,10 @@ struct Wave {
     flags |= DP_F_EPILOGUE;
     reset_all();
     if (base_propagate() < 0) return DP_ERROR;
-    const int rd = ++round;
+    const int start = tlen;
     bool bad = false;
-    for (int base = 0; base < nv; base += 64) {
-      const int v = base + lane;
+    for (int b = 0; b < nv; b += 64) {
+      const int v = b + lane;
       bool f = false;
       int l = 0;
       if (v < nv && !getb(extra, v)) {
@@ -810,8 +874,8 @@ struct Wave {
       }
       const uint64_t m = __ballot(f);
       if (f) {
-        val[v] = (l & 1) ? -1 : 1; reason[v] = R_DEC; rnd[v] = rd; dix[v] = -1;
-        trail[tlen + __popcll(m & lanemask_lt())] = l;
+        val[v] = (l & 1) ? -1 : 1; reason[v] = enc(R_DEC); rs[v] = enc(start); dix[v] = enc(-1);
+        trail[tlen + __popcll(m & lanemask_lt())] = enc(l);
       }
       tlen += __popcll(m);
     }
@@ -820,8 +884,8 @@ struct Wave {
     if (propagate() < 0) return DP_ERROR;
     const int mark = tlen;
     int f = 0;
-    for (int base = 0; base < nv; base += 64) {
-      const int v = base + lane;
+    for (int b = 0; b < nv; b += 64) {
+      const int v = b + lane;
       f += __popcll(__ballot(v < nv && getb(extra, v) && val[v] > 0));
     }
     extra_mode = true;
@@ -845,14 +909,16 @@ struct Wave {
 }  // namespace
 
 // One wavefront per problem; blockIdx.x indexes `order` (problems bucketed by
-// working-set footprint; the largest bucket works in HBM scratch).  Outputs: status / flags / installed / core (oracle_solve).
+// working-set footprint; the HBM instantiation works in HBM scratch).
+// Outputs: status / flags / installed / core / steps (oracle_solve).
+template <bool HBM>
 __global__ void __launch_bounds__(64) solve_kernel(KernelArgs a) {
-  extern __shared__ int32_t lds[];
+  extern __shared__ int4 lds4[];
   const int pid = a.order[blockIdx.x];
   const int32_t* grec = a.rec + a.rec_off[pid];
-  int32_t* ws = a.scratch ? a.scratch + a.scratch_off[blockIdx.x] : lds;
-  Wave W;
-  W.init(ws, grec);
+  Wave<HBM> W;
+  if constexpr (HBM) W.init(reinterpret_cast<char*>(a.scratch + a.scratch_off[blockIdx.x]), grec);
+  else W.init(reinterpret_cast<char*>(lds4), grec);
   W.budget = a.budget;
   uint32_t* inst = a.installed + a.inst_off[pid];
   int32_t flags = 0;
@@ -890,18 +956,18 @@ __global__ void __launch_bounds__(64) solve_kernel(KernelArgs a) {
   }
 }
 
-}  // namespace dp
-
-namespace dp {
-
 hipError_t launch_solve(const KernelArgs& a, int n_blocks, int lds_bytes, hipStream_t stream) {
   if (n_blocks <= 0) return hipSuccess;
-  hipLaunchKernelGGL(solve_kernel, dim3((unsigned)n_blocks), dim3(64), (size_t)lds_bytes, stream, a);
+  if (a.scratch)
+    hipLaunchKernelGGL(solve_kernel<true>, dim3((unsigned)n_blocks), dim3(64), 0, stream, a);
+  else
+    hipLaunchKernelGGL(solve_kernel<false>, dim3((unsigned)n_blocks), dim3(64), (size_t)lds_bytes,
+                       stream, a);
   return hipGetLastError();
 }
 
 hipError_t configure_solve_kernel(int max_lds_bytes) {
-  return hipFuncSetAttribute(reinterpret_cast<const void*>(&solve_kernel),
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(&solve_kernel<false>),
                              hipFuncAttributeMaxDynamicSharedMemorySize, max_lds_bytes);
 }
 
