@@ -13,6 +13,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libdeppy_hip.so")
+if os.environ.get("DEPPY_STAMPS") == "1":  # diagnostic phase-stamp build (scripts/ only)
+    LIB_PATH = os.path.join(HERE, "libdeppy_hip_stamps.so")
 
 c_i32p = ctypes.POINTER(ctypes.c_int32)
 c_i64p = ctypes.POINTER(ctypes.c_int64)

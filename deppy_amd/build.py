@@ -11,6 +11,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libdeppy_hip.so")
 OBJ = os.path.join(HERE, "_obj")
+# diagnostic variant (phase stamps); never loaded by the product path
+STAMPS_LIB = os.path.join(HERE, "libdeppy_hip_stamps.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 SOURCES = ["solve_kernel.hip", "runtime.cpp", "lower.cpp", "gen.cpp"]
@@ -25,7 +27,17 @@ def _needs(target: str, deps: list[str]) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(verbose: bool = False, extra: list[str] | None = None) -> str:
+def build(verbose: bool = False, extra: list[str] | None = None, stamps: bool = False) -> str:
+    global OBJ, LIB
+    if stamps:
+        extra = (extra or []) + ["-DDP_STAMPS"]
+        obj, lib = OBJ + "_stamps", STAMPS_LIB
+    else:
+        obj, lib = OBJ, LIB
+    return _build(verbose, extra, obj, lib)
+
+
+def _build(verbose, extra, OBJ, LIB) -> str:
     os.makedirs(OBJ, exist_ok=True)
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h"))]
     headers.append(os.path.join(HERE, "..", "include", "deppy_hip.h"))
@@ -49,4 +61,7 @@ def build(verbose: bool = False, extra: list[str] | None = None) -> str:
 
 
 if __name__ == "__main__":
-    build(verbose=True, extra=sys.argv[1:] or None)
+    args = sys.argv[1:]
+    stamps = "--stamps" in args
+    args = [a for a in args if a != "--stamps"]
+    build(verbose=True, extra=args or None, stamps=stamps)

@@ -23,6 +23,8 @@ struct KernelArgs {
   // workgroup b works in scratch + scratch_off[b] instead of LDS
   int32_t* scratch;
   const int64_t* scratch_off;
+  // diagnostic builds only (-DDP_STAMPS): per-problem phase cycle counts
+  int64_t* stamps;
 };
 
 // Launch one wavefront per problem of order[0..n_blocks) with lds_bytes of LDS.

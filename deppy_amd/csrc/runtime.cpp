@@ -65,6 +65,7 @@ struct DevSlice {
   int hbm_first = 0, hbm_count = 0;
   int32_t* scratch = nullptr;
   int64_t* scratch_off = nullptr;
+  int64_t* stamps = nullptr;  // diagnostic builds only
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // bucket launches run concurrently on side streams joined back by events
@@ -96,7 +97,8 @@ void fail(const std::string& s) {
 void free_slice(DevSlice& s) {
   if (s.stream) (void)hipSetDevice(s.device);
   void* ptrs[] = {s.rec, s.rec_off, s.order, s.status, s.flags, s.installed,
-                  s.inst_off, s.core, s.core_off, s.core_len, s.steps, s.scratch, s.scratch_off};
+                  s.inst_off, s.core, s.core_off, s.core_len, s.steps, s.scratch, s.scratch_off,
+                  s.stamps};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s.ev0) (void)hipEventDestroy(s.ev0);
@@ -116,7 +118,59 @@ int upload_vec(T** dst, const T* src, size_t n, hipStream_t st) {
   return 0;
 }
 
-// Build one device's slice: aligned records, bucketed launch order, outputs.
+// Device image of one record (layout.hpp img_layout): the record, then its
+// watch lists and base rows.  Returns the image length.
+int64_t build_image(const int32_t* rec, std::vector<int32_t>& out) {
+  const dp_rec_layout R = dp::rec_layout(rec);
+  const int32_t nv = rec[DP_H_NV], nc = rec[DP_H_NC], nk = rec[DP_H_NK];
+  const int32_t* clause_off = rec + R.clause_off;
+  const int32_t* clause_lits = rec + R.clause_lits;
+  const int32_t* card_off = rec + R.card_off;
+  const int32_t* card_lits = rec + R.card_lits;
+  const int32_t* card_bound = rec + R.card_bound;
+  const size_t at = out.size();
+  out.insert(out.end(), rec, rec + rec[DP_H_WORDS]);
+  // watch lists, rows in ascending order; one entry per distinct AtMost variable
+  std::vector<int32_t> cnt((size_t)2 * nv + 1, 0);
+  for (int32_t r = 0; r < nc; ++r)
+    for (int32_t j = clause_off[r]; j < clause_off[r + 1]; ++j) cnt[(size_t)(clause_lits[j] ^ 1) + 1]++;
+  for (int32_t k = 0; k < nk; ++k)
+    for (int32_t j = card_off[k]; j < card_off[k + 1]; ++j)
+      if (j == card_off[k] || card_lits[j] != card_lits[j - 1]) cnt[(size_t)2 * card_lits[j] + 1]++;
+  for (int32_t l = 0; l < 2 * nv; ++l) cnt[(size_t)l + 1] += cnt[(size_t)l];
+  const size_t woff = out.size();
+  out.insert(out.end(), cnt.begin(), cnt.end());
+  const size_t wat = out.size();
+  out.resize(wat + (size_t)cnt[(size_t)2 * nv], 0);
+  for (int32_t r = 0; r < nc; ++r)
+    for (int32_t j = clause_off[r]; j < clause_off[r + 1]; ++j) out[wat + (size_t)cnt[(size_t)(clause_lits[j] ^ 1)]++] = r;
+  for (int32_t k = 0; k < nk; ++k)
+    for (int32_t j = card_off[k]; j < card_off[k + 1]; ++j)
+      if (j == card_off[k] || card_lits[j] != card_lits[j - 1])
+        out[wat + (size_t)cnt[(size_t)2 * card_lits[j]]++] = nc + k;
+  (void)woff;
+  // rows that can fire on the empty assignment
+  int32_t nbase = 0;
+  for (int32_t r = 0; r < nc; ++r)
+    if (clause_off[r + 1] - clause_off[r] <= 1) { out.push_back(r); ++nbase; }
+  for (int32_t k = 0; k < nk; ++k) {
+    bool fires = false;
+    for (int32_t j = card_off[k]; j < card_off[k + 1] && !fires;) {
+      int32_t e = j + 1;
+      while (e < card_off[k + 1] && card_lits[e] == card_lits[j]) ++e;
+      fires = (e - j) > card_bound[k];
+      j = e;
+    }
+    if (fires) { out.push_back(nc + k); ++nbase; }
+  }
+  const int64_t words = (int64_t)(out.size() - at);
+  out[at + dp::DP_H_NBASE] = nbase;
+  out[at + dp::DP_H_IMG] = (int32_t)words;
+  out.resize(at + (size_t)((words + 3) & ~3LL), 0);  // 16-byte aligned images
+  return words;
+}
+
+// Build one device's slice: device images, bucketed launch order, outputs.
 int build_slice(DevSlice& s, const dp_batch* b, const int64_t* inst_off, const int64_t* core_off) {
   HIP_OK(hipSetDevice(s.device));
   HIP_OK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
@@ -128,17 +182,16 @@ int build_slice(DevSlice& s, const dp_batch* b, const int64_t* inst_off, const i
   }
   const int32_t n = s.p1 - s.p0;
   std::vector<int64_t> roff((size_t)n + 1, 0);
+  std::vector<int32_t> rec;
   for (int32_t i = 0; i < n; ++i) {
-    const int32_t* r = b->rec + b->rec_off[s.p0 + i];
-    roff[(size_t)i + 1] = roff[(size_t)i] + ((dp::words_of(r) + 3) & ~3LL);
+    build_image(b->rec + b->rec_off[s.p0 + i], rec);
+    roff[(size_t)i + 1] = (int64_t)rec.size();
   }
-  std::vector<int32_t> rec((size_t)roff[(size_t)n], 0);
   std::vector<std::vector<int32_t>> bucket(kNBuckets);
   std::vector<int32_t> hbm;
   std::vector<int64_t> soff(1, 0);
   for (int32_t i = 0; i < n; ++i) {
-    const int32_t* r = b->rec + b->rec_off[s.p0 + i];
-    std::memcpy(&rec[(size_t)roff[(size_t)i]], r, (size_t)dp::words_of(r) * 4);
+    const int32_t* r = rec.data() + roff[(size_t)i];
     const int64_t lds = dp::fits16(r) ? (int64_t)dp::layout<uint16_t>(r).bytes : INT64_MAX;
     int k = 0;
     while (k < kNBuckets && lds > kBuckets[k]) ++k;
@@ -157,7 +210,7 @@ int build_slice(DevSlice& s, const dp_batch* b, const int64_t* inst_off, const i
     s.b_count.push_back((int)bucket[(size_t)k].size());
     int mx = 0;
     for (int32_t i : bucket[(size_t)k])
-      mx = std::max(mx, dp::layout<uint16_t>(b->rec + b->rec_off[s.p0 + i]).bytes);
+      mx = std::max(mx, dp::layout<uint16_t>(rec.data() + roff[(size_t)i]).bytes);
     s.b_lds.push_back(mx);
     order.insert(order.end(), bucket[(size_t)k].begin(), bucket[(size_t)k].end());
   }
@@ -186,6 +239,10 @@ int build_slice(DevSlice& s, const dp_batch* b, const int64_t* inst_off, const i
   HIP_OK(hipMalloc(&s.flags, std::max<size_t>((size_t)n, 1) * 4));
   HIP_OK(hipMalloc(&s.core_len, std::max<size_t>((size_t)n, 1) * 4));
   HIP_OK(hipMalloc(&s.steps, std::max<size_t>((size_t)n, 1) * 8));
+#ifdef DP_STAMPS
+  HIP_OK(hipMalloc(&s.stamps, std::max<size_t>((size_t)n, 1) * 10 * 8));
+  HIP_OK(hipMemsetAsync(s.stamps, 0, std::max<size_t>((size_t)n, 1) * 10 * 8, s.stream));
+#endif
   HIP_OK(hipMalloc(&s.installed, (size_t)std::max<int64_t>(s.n_inst, 1) * 4));
   HIP_OK(hipMalloc(&s.core, (size_t)std::max<int64_t>(s.n_core, 1) * 4));
   // problems that fit no bucket are reported DP_ERROR | DP_F_TOO_LARGE
@@ -214,6 +271,7 @@ int run_slice(DevSlice& s, int64_t budget) {
   a.budget = budget;
   a.scratch = nullptr;
   a.scratch_off = nullptr;
+  a.stamps = s.stamps;
   // launch i goes to stream i % 4 (the main stream, then three side streams);
   // the largest buckets come first so they start earliest
   std::vector<int> launch_order;
@@ -420,6 +478,20 @@ int dp_solve(dp_ctx* ctx, const dp_batch* b, dp_result* res) {
   dp_resident_free(ctx, r);
   return rc;
 }
+
+#ifdef DP_STAMPS
+// Diagnostic builds only: per-problem phase cycles [init, base, search,
+// epilogue, core] of the last run (not part of include/deppy_hip.h).
+int dp_debug_stamps(dp_ctx* ctx, dp_resident* r, int64_t* out) {
+  t_ctx = ctx;
+  for (auto& s : r->slices) {
+    HIP_OK(hipSetDevice(s.device));
+    HIP_OK(hipMemcpy(out + 10 * (size_t)s.p0, s.stamps, (size_t)(s.p1 - s.p0) * 10 * 8,
+                     hipMemcpyDeviceToHost));
+  }
+  return 0;
+}
+#endif
 
 int dp_last_kernel_ms(const dp_ctx* ctx, double* ms) {
   if (!ctx || !ms) return -1;

@@ -51,14 +51,18 @@ __device__ __forceinline__ void wsync() {
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 __device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
 
+// Inclusive prefix sum over the 64 lanes with DPP row shifts and row
+// broadcasts (no LDS round trips).
 __device__ __forceinline__ int wave_incl_scan(int x) {
-  const int lane = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int y = __shfl_up(x, d);
-    if (lane >= d) x += y;
-  }
-  return x;
+  int y = x;
+  y += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);   // row_shr:1
+  y += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);   // row_shr:2
+  y += __builtin_amdgcn_update_dpp(0, x, 0x113, 0xf, 0xf, true);   // row_shr:3
+  y += __builtin_amdgcn_update_dpp(0, y, 0x114, 0xf, 0xe, false);  // row_shr:4, banks 1-3
+  y += __builtin_amdgcn_update_dpp(0, y, 0x118, 0xf, 0xc, false);  // row_shr:8, banks 2-3
+  y += __builtin_amdgcn_update_dpp(0, y, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  y += __builtin_amdgcn_update_dpp(0, y, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return y;
 }
 
 __device__ __forceinline__ int wave_min(int x) {
@@ -68,6 +72,23 @@ __device__ __forceinline__ int wave_min(int x) {
 }
 
 __device__ __forceinline__ bool getb(const uint32_t* b, int i) { return (b[i >> 5] >> (i & 31)) & 1u; }
+
+}  // namespace
+// Diagnostic builds (-DDP_STAMPS, never the shipped library) record the
+// shader-clock cycles of each phase; the release build compiles them away.
+#ifdef DP_STAMPS
+__device__ __forceinline__ int64_t stamp() {
+  int64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define DP_STAMP(i) t[i] = stamp()
+#else
+#define DP_STAMP(i) (void)0
+#endif
+namespace {
 
 template <bool HBM>
 struct Wave {
@@ -85,13 +106,15 @@ struct Wave {
   const IX *clause_off, *clause_lits, *clause_id;
   const IX *card_off, *card_lits, *card_bound, *card_id;
   const IX *var_choice_off, *choice_off, *choice_lits, *anchors;
+  const IX *w_off, *w, *base_rows;
+  int nbase;
   // ---- working set ----
-  IX *w_off, *w;
   int8_t* val;
   IX *reason, *rs, *trail, *touched, *d_lit, *d_mark, *dix, *l_off, *l_lits, *dq, *stk;
-  uint32_t* imp;  // imp[2v] = lowest row implying +v, imp[2v+1] = -v
-  uint32_t *impflag, *d_flip, *inS, *extra, *seen, *model, *used, *en, *en2, *dset, *fg;
-  int32_t *wbuf, *scal;
+  uint32_t* imp;  // imp[l] = lowest row implying literal l this round
+  uint32_t *d_flip, *inS, *extra, *seen, *model, *used, *en, *en2, *dset, *fg;
+  IX* wbuf;
+  int32_t *cardq, *scal;
   int cap, lcap;
   int lane;
   // ---- wave-uniform state (registers) ----
@@ -104,6 +127,12 @@ struct Wave {
   const uint32_t* enabled;  // nullptr: every row
   bool extra_mode;
   int extra_w;
+#ifdef DP_STAMPS
+  int64_t acc[5];  // round eval cycles, round finish cycles, rounds, 1-literal rounds, push+pop cycles
+#define DP_ACC(i, x) acc[i] += (x)
+#else
+#define DP_ACC(i, x) (void)0
+#endif
 
   // ------------------------------------------------------------------
   // set-up (oracle: st_init)
@@ -115,15 +144,17 @@ struct Wave {
     for (int i = 0; i < DP_H_SIZE; ++i) h[i] = grec[i];
     const Layout L = layout<IX>(h);
     const dp_rec_layout R = rec_layout(h);
+    const ImgLayout X = img_layout(h);
     nv = h[DP_H_NV]; nc = h[DP_H_NC]; nk = h[DP_H_NK]; nid = h[DP_H_NID]; na = h[DP_H_NA];
     nch = h[DP_H_NCH];
     nrows = nc + nk;
     nbv = bits_words(nv); nbi = bits_words(nid);
-    // record body: HBM int32 -> working-set IX (dwordx4 loads; records are
-    // 16-byte aligned and padded to 4 words)
+    // device image (record + host-built watch lists and base rows):
+    // HBM int32 -> working-set IX with dwordx4 loads (images are 16-byte
+    // aligned and padded to 4 words)
     IX* body = reinterpret_cast<IX*>(base + L.body);
     {
-      const int groups = (h[DP_H_WORDS] - DP_H_SIZE + 3) >> 2;
+      const int groups = (h[DP_H_IMG] - DP_H_SIZE + 3) >> 2;
       const int4* src = reinterpret_cast<const int4*>(grec + DP_H_SIZE);
       for (int i = lane; i < groups; i += 64) {
         const int4 x = src[i];
@@ -142,8 +173,8 @@ struct Wave {
     card_off = rv(R.card_off); card_lits = rv(R.card_lits); card_bound = rv(R.card_bound);
     card_id = rv(R.card_id); var_choice_off = rv(R.var_choice_off); choice_off = rv(R.choice_off);
     choice_lits = rv(R.choice_lits); anchors = rv(R.anchors);
-    w_off = reinterpret_cast<IX*>(base + L.w_off);
-    w = reinterpret_cast<IX*>(base + L.w);
+    w_off = rv(X.w_off); w = rv(X.w); base_rows = rv(X.base);
+    nbase = h[DP_H_NBASE];
     val = reinterpret_cast<int8_t*>(base + L.val);
     reason = reinterpret_cast<IX*>(base + L.reason);
     rs = reinterpret_cast<IX*>(base + L.rs);
@@ -153,7 +184,6 @@ struct Wave {
     d_mark = reinterpret_cast<IX*>(base + L.d_mark);
     dix = reinterpret_cast<IX*>(base + L.dix);
     imp = reinterpret_cast<uint32_t*>(base + L.imp);
-    impflag = reinterpret_cast<uint32_t*>(base + L.impflag);
     d_flip = reinterpret_cast<uint32_t*>(base + L.d_flip);
     inS = reinterpret_cast<uint32_t*>(base + L.inS);
     extra = reinterpret_cast<uint32_t*>(base + L.extra);
@@ -168,7 +198,8 @@ struct Wave {
     l_lits = reinterpret_cast<IX*>(base + L.l_lits);
     dq = reinterpret_cast<IX*>(base + L.dq);
     stk = reinterpret_cast<IX*>(base + L.stk);
-    wbuf = reinterpret_cast<int32_t*>(base + L.wbuf);
+    wbuf = reinterpret_cast<IX*>(base + L.wbuf);
+    cardq = reinterpret_cast<int32_t*>(base + L.cardq);
     scal = reinterpret_cast<int32_t*>(base + L.scal);
     cap = L.cap; lcap = L.lcap;
     tlen = qhead = 0;
@@ -181,41 +212,16 @@ struct Wave {
     enabled = nullptr;
     extra_mode = false;
     extra_w = 0;
+#ifdef DP_STAMPS
+    for (int i = 0; i < 5; ++i) acc[i] = 0;
+#endif
 
     for (int v = lane; v < nv; v += 64) val[v] = 0;
-    for (int i = lane; i < bits_words(2 * nv); i += 64) impflag[i] = 0;
+    for (int l = lane; l < 2 * nv; l += 64) imp[l] = (uint32_t)INF;
     for (int i = lane; i < nbv; i += 64) {
       d_flip[i] = 0; inS[i] = 0; extra[i] = 0; seen[i] = 0; model[i] = 0; dset[i] = 0; fg[i] = 0;
     }
     if (lane == 0) { l_off[0] = 0; scal[S_NTOUCHED] = 0; }
-    // watch lists: a clause literal x of row r is watched by ~x; a card
-    // position v of row k by +v (oracle st_init); counts go through the
-    // 32-bit imp[] (2nv words) so LDS atomics can build them
-    const int nl2 = 2 * nv;
-    uint32_t* cnt = imp;
-    for (int l = lane; l < nl2; l += 64) cnt[l] = 0;
-    wsync();
-    for (int j = lane; j < h[DP_H_NCL]; j += 64) atomicAdd(&cnt[clause_lits[j] ^ 1], 1u);
-    for (int j = lane; j < h[DP_H_NKL]; j += 64) atomicAdd(&cnt[2 * (int)card_lits[j]], 1u);
-    wsync();
-    int carry = 0;
-    for (int b = 0; b < nl2; b += 64) {
-      const int l = b + lane;
-      const int x = l < nl2 ? (int)cnt[l] : 0;
-      const int inc = wave_incl_scan(x) + carry;
-      if (l < nl2) { w_off[l + 1] = enc(inc); cnt[l] = (uint32_t)(inc - x); }  // cnt -> cursor
-      carry = __shfl(inc, 63);
-    }
-    if (lane == 0) w_off[0] = 0;
-    wsync();
-    for (int r = lane; r < nc; r += 64)
-      for (int j = clause_off[r]; j < clause_off[r + 1]; ++j)
-        w[atomicAdd(&cnt[clause_lits[j] ^ 1], 1u)] = enc(r);
-    for (int k = lane; k < nk; k += 64)
-      for (int j = card_off[k]; j < card_off[k + 1]; ++j)
-        w[atomicAdd(&cnt[2 * (int)card_lits[j]], 1u)] = enc(nc + k);
-    wsync();
-    for (int l = lane; l < nl2; l += 64) imp[l] = (uint32_t)INF;
     wsync();
   }
 
@@ -231,13 +237,11 @@ struct Wave {
     return (l & 1) ? -x : x;
   }
 
-  // record "row r implies literal l" (lowest row wins, oracle: note)
+  // record "row r implies literal l" (lowest row wins, oracle: note); the
+  // first implication of a literal in the round lists it
   __device__ __forceinline__ void note(int l, int r) {
-    const int v = l >> 1;
-    const uint32_t sh = (uint32_t)(2 * v) & 31u;
-    const uint32_t old = atomicOr(&impflag[(2 * v) >> 5], 1u << (sh + (l & 1)));
-    if (((old >> sh) & 3u) == 0) touched[atomicAdd(&scal[S_NTOUCHED], 1)] = enc(v);
-    atomicMin(&imp[l], (uint32_t)r);
+    if (atomicMin(&imp[l], (uint32_t)r) == (uint32_t)INF)
+      touched[atomicAdd(&scal[S_NTOUCHED], 1)] = enc(l);
   }
 
   // clause row evaluation; the literal loads are issued four at a time
@@ -289,6 +293,46 @@ struct Wave {
     }
   }
 
+  // A watched row reached in a round: clause rows are evaluated by the lane
+  // that reached them; AtMost rows are queued (ballot compaction) and later
+  // evaluated by the whole wave, one row at a time (flush_cards).  Call from
+  // converged code: every active lane passes its row (or -1).
+  __device__ __forceinline__ void visit(int r, int& crow, int& ncq) {
+    const bool ok = r >= 0 && row_on(r);
+    const bool card = ok && r >= nc && r < nrows;
+    uint64_t m = __ballot(card);
+    if (ncq + __popcll(m) > CQ) m = 0;  // queue full: evaluate in-lane
+    if ((m >> lane) & 1ull) cardq[ncq + __popcll(m & lanemask_lt())] = r;
+    else if (ok) eval_row(r, crow);
+    ncq += __popcll(m);
+  }
+
+  // AtMost rows, one at a time, lanes over positions (oracle: eval_row):
+  // counts by ballot; a variable listed m times is a run of m positions,
+  // forced false when the count plus m exceeds the bound.
+  __device__ __forceinline__ void flush_cards(int& crow, int ncq) {
+    if (ncq == 0) return;
+    wsync();
+    for (int q = 0; q < ncq; ++q) {
+      const int r = cardq[q], k = r - nc;
+      const int a = card_off[k], len = (int)card_off[k + 1] - a, bound = card_bound[k];
+      if (len > 64) {  // long rows: one lane
+        if (lane == 0) eval_row(r, crow);
+        continue;
+      }
+      const int v = lane < len ? (int)card_lits[a + lane] : -1;
+      const int x = v >= 0 ? val[v] : 0;
+      const int cnt = __popcll(__ballot(v >= 0 && x > 0));
+      if (cnt > bound) { crow = min(crow, r); continue; }
+      if (!__ballot(v >= 0 && x == 0)) continue;
+      const bool start = v >= 0 && (lane == 0 || (int)card_lits[a + lane - 1] != v);
+      const uint64_t ms = __ballot(start);
+      const uint64_t after = lane < 63 ? ms >> (lane + 1) : 0ull;
+      const int run = (after ? lane + 1 + __ffsll((unsigned long long)after) - 1 : len) - lane;
+      if (start && x == 0 && cnt + run > bound) note(2 * v + 1, r);
+    }
+  }
+
   // learned rows are evaluated in every round (lanes over rows)
   __device__ __forceinline__ void eval_learned(int& crow) {
     if (!learn_on) return;
@@ -296,13 +340,19 @@ struct Wave {
   }
 
   __device__ __forceinline__ void clear_touched(int nt) {
-    for (int i = lane; i < nt; i += 64) {
-      const int v = touched[i];
-      imp[2 * v] = (uint32_t)INF; imp[2 * v + 1] = (uint32_t)INF;
-    }
-    for (int i = lane; i < bits_words(2 * nv); i += 64) impflag[i] = 0;
+    for (int i = lane; i < nt; i += 64) imp[(int)touched[i]] = (uint32_t)INF;
     if (lane == 0) scal[S_NTOUCHED] = 0;
     wsync();
+  }
+
+  __device__ __forceinline__ void commit(int l, int r, int start, int i) {
+    const int v = l >> 1;
+    val[v] = (l & 1) ? -1 : 1;
+    reason[v] = enc(r);
+    rs[v] = enc(start);
+    dix[v] = enc(-1);
+    trail[start + i] = enc(l);
+    imp[l] = (uint32_t)INF;
   }
 
   // Commit the implications of the round, or report its conflict: the lowest
@@ -316,32 +366,37 @@ struct Wave {
       ck = CK_ROW;
       return -1;
     }
-    int cv = INF;
-    for (int i = lane; i < nt; i += 64) {
-      const int v = touched[i];
-      const uint32_t f = (impflag[(2 * v) >> 5] >> ((2 * v) & 31)) & 3u;
-      if (f == 3u) cv = min(cv, v);
-    }
-    if (__ballot(cv != INF)) {
-      cv = wave_min(cv);
-      c_rp = (int)imp[2 * cv]; c_rn = (int)imp[2 * cv + 1];
-      ck = CK_VAR; c_var = cv; c_row = tlen;  // bound: every variable assigned so far
-      clear_touched(nt);
-      return -1;
-    }
     const int start = tlen;
-    for (int i = lane; i < nt; i += 64) {
-      const int v = touched[i];
-      const uint32_t rp = imp[2 * v];
-      const bool pos = rp != (uint32_t)INF;
-      val[v] = pos ? 1 : -1;
-      reason[v] = enc(pos ? (int)rp : (int)imp[2 * v + 1]);
-      rs[v] = enc(start);
-      dix[v] = enc(-1);
-      trail[start + i] = enc(2 * v + (pos ? 0 : 1));
-      imp[2 * v] = (uint32_t)INF; imp[2 * v + 1] = (uint32_t)INF;
+    if (nt <= 64) {  // one literal per lane: a single pass
+      const int l = lane < nt ? (int)touched[lane] : 0;
+      const uint32_t r = lane < nt ? imp[l] : 0u, rn = lane < nt ? imp[l ^ 1] : (uint32_t)INF;
+      const int cv = rn != (uint32_t)INF ? (l >> 1) : INF;
+      if (__ballot(cv != INF)) {
+        c_var = wave_min(cv);
+        c_rp = (int)imp[2 * c_var]; c_rn = (int)imp[2 * c_var + 1];
+        ck = CK_VAR; c_row = tlen;  // bound: every variable assigned so far
+        clear_touched(nt);
+        return -1;
+      }
+      if (lane < nt) commit(l, (int)r, start, lane);
+    } else {
+      int cv = INF;
+      for (int i = lane; i < nt; i += 64) {
+        const int l = touched[i];
+        if (imp[l ^ 1] != (uint32_t)INF) cv = min(cv, l >> 1);
+      }
+      if (__ballot(cv != INF)) {
+        c_var = wave_min(cv);
+        c_rp = (int)imp[2 * c_var]; c_rn = (int)imp[2 * c_var + 1];
+        ck = CK_VAR; c_row = tlen;
+        clear_touched(nt);
+        return -1;
+      }
+      for (int i = lane; i < nt; i += 64) {
+        const int l = touched[i];
+        commit(l, (int)imp[l], start, i);
+      }
     }
-    for (int i = lane; i < bits_words(2 * nv); i += 64) impflag[i] = 0;
     if (lane == 0) scal[S_NTOUCHED] = 0;
     tlen += nt;
     wsync();
@@ -389,6 +444,17 @@ struct Wave {
       const int lo = qhead, hi = tlen;
       qhead = hi;
       int crow = INF;
+#ifdef DP_STAMPS
+      const int64_t t0 = stamp();
+      DP_ACC(2, 1);
+      DP_ACC(3, hi - lo == 1);
+#endif
+      int ncq = 0;
+      if (hi - lo == 1) {  // one new literal: lanes over its watch list
+        const int l = trail[lo];
+        const int a = w_off[l], e = w_off[l + 1];
+        for (int k0 = a; k0 < e; k0 += 64) visit(k0 + lane < e ? (int)w[k0 + lane] : -1, crow, ncq);
+      } else
       for (int b = lo; b < hi; b += 64) {
         const int i = b + lane;
         int cnt = 0, a = 0;
@@ -398,38 +464,46 @@ struct Wave {
           cnt = (int)w_off[l + 1] - a;
         }
         const int incl = wave_incl_scan(cnt);
-        const int total = __shfl(incl, 63);
+        const int total = __builtin_amdgcn_readlane(incl, 63);
         if (total <= WBUF) {
           // flatten: every frontier literal writes its watch range into the list
-          for (int k = 0, at = incl - cnt; k < cnt; ++k) wbuf[at + k] = a + k;
+          for (int k = 0, at = incl - cnt; k < cnt; ++k) wbuf[at + k] = enc(a + k);
           wsync();
-          for (int t = lane; t < total; t += 64) {
-            const int r = w[wbuf[t]];
-            if (row_on(r)) eval_row(r, crow);
-          }
+          for (int t0 = 0; t0 < total; t0 += 64)
+            visit(t0 + lane < total ? (int)w[wbuf[t0 + lane]] : -1, crow, ncq);
           wsync();
         } else {
           // a very large chunk: one frontier literal at a time
           const int n = min(64, hi - b);
           for (int e = 0; e < n; ++e) {
             const int l = trail[b + e];
-            for (int k = (int)w_off[l] + lane; k < (int)w_off[l + 1]; k += 64) {
-              const int r = w[k];
-              if (row_on(r)) eval_row(r, crow);
-            }
+            const int a2 = w_off[l], e2 = w_off[l + 1];
+            for (int k0 = a2; k0 < e2; k0 += 64)
+              visit(k0 + lane < e2 ? (int)w[k0 + lane] : -1, crow, ncq);
           }
         }
       }
+      flush_cards(crow, ncq);
       eval_learned(crow);
+#ifdef DP_STAMPS
+      const int64_t t1 = stamp();
+      const int fr = finish_round(crow);
+      const int64_t t2 = stamp();
+      DP_ACC(0, t1 - t0);
+      DP_ACC(1, t2 - t1);
+      if (fr < 0) return -1;
+#else
       if (finish_round(crow) < 0) return -1;
+#endif
     }
   }
 
-  // The base scope (solve.go:63-79): one round evaluates every (enabled) row.
+  // The base scope (solve.go:63-79): one round evaluates every (enabled) row;
+  // on the empty assignment only the rows of the base list can fire.
   __device__ __forceinline__ int base_propagate() {
-    int crow = INF;
-    for (int r = lane; r < nrows; r += 64)
-      if (row_on(r)) eval_row(r, crow);
+    int crow = INF, ncq = 0;
+    for (int i0 = 0; i0 < nbase; i0 += 64) visit(i0 + lane < nbase ? (int)base_rows[i0 + lane] : -1, crow, ncq);
+    flush_cards(crow, ncq);
     eval_learned(crow);
     if (finish_round(crow) < 0) return -1;
     return propagate();
@@ -544,28 +618,46 @@ struct Wave {
   // ------------------------------------------------------------------
   // Solve(): CDCL from a consistent fixpoint (oracle: first_violated / dpll)
   // ------------------------------------------------------------------
-  __device__ __forceinline__ int first_violated() {
-    for (int b = 0; b < nc; b += 64) {
-      const int c = b + lane;
-      bool viol = false;
-      int fu = -1;
-      if (c < nc && row_on(c)) {
-        viol = true;
-        for (int j = clause_off[c]; j < clause_off[c + 1]; ++j) {
-          const int l = clause_lits[j];
-          const int x = val[l >> 1];
-          if (l & 1) {
-            if (x != 1) { viol = false; break; }
-          } else {
-            if (x == 1) { viol = false; break; }
-            if (x == 0 && fu < 0) fu = l;
-          }
-        }
+  // Is clause row c violated by the all-false completion of the current
+  // assignment?  (oracle: first_violated)  fu = its first unassigned
+  // positive literal.
+  __device__ __forceinline__ bool violated(int c, int& fu) const {
+    fu = -1;
+    for (int j = clause_off[c]; j < clause_off[c + 1]; ++j) {
+      const int l = clause_lits[j];
+      const int x = val[l >> 1];
+      if (l & 1) {
+        if (x != 1) return false;
+      } else {
+        if (x == 1) return false;
+        if (x == 0 && fu < 0) fu = l;
       }
-      const uint64_t m = __ballot(viol);
-      if (m) return __shfl(fu, __ffsll((unsigned long long)m) - 1);
     }
-    return -1;
+    return true;
+  }
+
+  // The lowest clause row the all-false completion violates -> its first
+  // unassigned positive literal (the decision), or -1.  Such a row has a
+  // positive literal but no true one, and every negative literal on a true
+  // variable, so it is in the watch list of some true positive literal:
+  // lanes scan the watch lists of the variables assigned true instead of
+  // every clause row (same answer as the oracle's full scan).
+  __device__ __forceinline__ int first_violated() {
+    int best = INF;
+    for (int i = lane; i < tlen; i += 64) {
+      const int l = trail[i];
+      if (l & 1) continue;  // only variables assigned true own violations
+      for (int k = w_off[l]; k < (int)w_off[l + 1]; ++k) {
+        const int c = w[k];
+        int fu;
+        if (c < nc && c < best && row_on(c) && violated(c, fu)) best = c;
+      }
+    }
+    if (!__ballot(best != INF)) return -1;
+    best = wave_min(best);
+    int fu;
+    violated(best, fu);
+    return fu;
   }
 
   __device__ __forceinline__ void save_model() {
@@ -588,64 +680,63 @@ struct Wave {
   __device__ __forceinline__ int dpll() {
     const int root = tlen, nl0 = nl;
     int nd = 0, r;
+    bool decide = true;
     for (;;) {
-      const int l = first_violated();
-      if (l < 0) { save_model(); r = RS_SAT; break; }
+      if (decide) {
+        const int l = first_violated();
+        if (l < 0) { save_model(); r = RS_SAT; break; }
+        if (++steps > budget) { budget_hit = true; r = RS_BUDGET; break; }
+        if (lane == 0) {
+          d_lit[nd] = enc(l); d_mark[nd] = enc(tlen);
+          d_flip[nd >> 5] &= ~(1u << (nd & 31));
+        }
+        assign_one(l, R_DEC, nd);
+        ++nd;
+      }
+      // the one propagation site of Solve(): after a decision or an assertion
+      if (propagate() >= 0) { decide = true; continue; }
+      decide = false;
+      clear_bits(dset, nd);
+      analyze();
+      // h = highest decision reached, b = the next one below (or -1)
+      int h = -1, b = -1, n = 0;
+      for (int wi = bits_words(nd) - 1; wi >= 0 && b < 0; --wi) {
+        uint32_t x = dset[wi];
+        while (x && b < 0) {
+          const int i = wi * 32 + 31 - __clz(x);
+          x &= ~(1u << (i & 31));
+          if (h < 0) h = i; else b = i;
+        }
+      }
+      for (int wi = 0; wi < bits_words(nd); ++wi) n += __popc(dset[wi]);
+      if (h < 0) { r = RS_UNSAT; break; }
       if (++steps > budget) { budget_hit = true; r = RS_BUDGET; break; }
-      if (lane == 0) {
-        d_lit[nd] = enc(l); d_mark[nd] = enc(tlen);
-        d_flip[nd >> 5] &= ~(1u << (nd & 31));
-      }
-      assign_one(l, R_DEC, nd);
-      ++nd;
-      int res = propagate();
-      bool unsat = false;
-      while (res < 0) {
-        clear_bits(dset, nd);
-        analyze();
-        // h = highest decision reached, b = the next one below (or -1)
-        int h = -1, b = -1, n = 0;
-        for (int wi = bits_words(nd) - 1; wi >= 0 && b < 0; --wi) {
-          uint32_t x = dset[wi];
-          while (x && b < 0) {
-            const int i = wi * 32 + 31 - __clz(x);
-            x &= ~(1u << (i & 31));
-            if (h < 0) h = i; else b = i;
-          }
+      const int lat = l_off[nl];
+      if (nl < L_MAX && lat + n <= lcap) {
+        // learned row: negated decisions, ascending decision index
+        int at = lat;
+        for (int base = 0; base < nd; base += 64) {
+          const int i = base + lane;
+          const bool in = i < nd && getb(dset, i);
+          const uint64_t m = __ballot(in);
+          if (in) l_lits[at + __popcll(m & lanemask_lt())] = enc((int)d_lit[i] ^ 1);
+          at += __popcll(m);
         }
-        for (int wi = 0; wi < bits_words(nd); ++wi) n += __popc(dset[wi]);
-        if (h < 0) { unsat = true; break; }
-        if (++steps > budget) { budget_hit = true; r = RS_BUDGET; goto done; }
-        const int lat = l_off[nl];
-        if (nl < L_MAX && lat + n <= lcap) {
-          // learned row: negated decisions, ascending decision index
-          int at = lat;
-          for (int base = 0; base < nd; base += 64) {
-            const int i = base + lane;
-            const bool in = i < nd && getb(dset, i);
-            const uint64_t m = __ballot(in);
-            if (in) l_lits[at + __popcll(m & lanemask_lt())] = enc((int)d_lit[i] ^ 1);
-            at += __popcll(m);
-          }
-          if (lane == 0) l_off[nl + 1] = enc(at);
-          ++nl;
-          wsync();
-          nd = b + 1;
-          truncate_to(d_mark[nd]);
-          assign_one((int)d_lit[h] ^ 1, nrows + nl - 1, -1);
-        } else {
-          while (nd > 0 && getb(d_flip, nd - 1)) --nd;
-          if (nd == 0) { unsat = true; break; }
-          truncate_to(d_mark[nd - 1]);
-          if (lane == 0) d_flip[(nd - 1) >> 5] |= 1u << ((nd - 1) & 31);
-          wsync();
-          assign_one((int)d_lit[nd - 1] ^ 1, R_DEC, nd - 1);
-        }
-        res = propagate();
+        if (lane == 0) l_off[nl + 1] = enc(at);
+        ++nl;
+        wsync();
+        nd = b + 1;
+        truncate_to(d_mark[nd]);
+        assign_one((int)d_lit[h] ^ 1, nrows + nl - 1, -1);
+      } else {
+        while (nd > 0 && getb(d_flip, nd - 1)) --nd;
+        if (nd == 0) { r = RS_UNSAT; break; }
+        truncate_to(d_mark[nd - 1]);
+        if (lane == 0) d_flip[(nd - 1) >> 5] |= 1u << ((nd - 1) & 31);
+        wsync();
+        assign_one((int)d_lit[nd - 1] ^ 1, R_DEC, nd - 1);
       }
-      if (unsat) { r = RS_UNSAT; break; }
     }
-  done:
     truncate_to(root);
     nl = nl0;
     return r;
@@ -773,7 +864,13 @@ struct Wave {
         continue;
       }
       if (dq_n == 0) break;
+#ifdef DP_STAMPS
+      const int64_t tp = stamp();
       push_guess();
+      DP_ACC(4, stamp() - tp);
+#else
+      push_guess();
+#endif
       if (budget_hit) { result = RS_BUDGET; break; }
     }
     // Value() after an ending on Test()==1 reads that scope's full assignment
@@ -911,9 +1008,14 @@ struct Wave {
 // One wavefront per problem; blockIdx.x indexes `order` (problems bucketed by
 // working-set footprint; the HBM instantiation works in HBM scratch).
 // Outputs: status / flags / installed / core / steps (oracle_solve).
+
 template <bool HBM>
 __global__ void __launch_bounds__(64) solve_kernel(KernelArgs a) {
   extern __shared__ int4 lds4[];
+#ifdef DP_STAMPS
+  int64_t t[6];
+#endif
+  DP_STAMP(0);
   const int pid = a.order[blockIdx.x];
   const int32_t* grec = a.rec + a.rec_off[pid];
   Wave<HBM> W;
@@ -924,7 +1026,10 @@ __global__ void __launch_bounds__(64) solve_kernel(KernelArgs a) {
   int32_t flags = 0;
   int status;
   for (int i = W.lane; i < W.nbv; i += 64) inst[i] = 0;
+  DP_STAMP(1);
   const int base = W.base_propagate();
+  DP_STAMP(2);
+  DP_STAMP(3);
   if (base < 0) {
     flags |= DP_F_BASE_UNSAT;
     status = DP_UNSAT;
@@ -934,6 +1039,7 @@ __global__ void __launch_bounds__(64) solve_kernel(KernelArgs a) {
     status = W.epilogue(flags, inst);
   } else {
     const int r = W.search();
+    DP_STAMP(3);
     if (W.class_b) flags |= DP_F_CLASS_B;
     if (W.solve_unsat) flags |= DP_F_SOLVE_UNSAT;
     if (r == RS_BUDGET) {
@@ -946,8 +1052,16 @@ __global__ void __launch_bounds__(64) solve_kernel(KernelArgs a) {
       if (status == DP_INCOMPLETE) flags |= DP_F_BUDGET;
     }
   }
+  DP_STAMP(4);
   int clen = 0;
   if (status == DP_UNSAT) clen = W.core(a.core + a.core_off[pid], flags);
+  DP_STAMP(5);
+#ifdef DP_STAMPS
+  if (W.lane == 0 && a.stamps) {
+    for (int i = 0; i < 5; ++i) a.stamps[10 * pid + i] = t[i + 1] - t[i];
+    for (int i = 0; i < 5; ++i) a.stamps[10 * pid + 5 + i] = W.acc[i];
+  }
+#endif
   if (W.lane == 0) {
     a.status[pid] = (int8_t)status;
     a.flags[pid] = flags;
