@@ -29,7 +29,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from deppy_amd import _lib  # noqa: E402
+from deppy_amd import _lib, shard  # noqa: E402
 
 METRIC = "resolutions/sec (node) on synthetic catalogs at 1/2/4/8 GPUs; BCP HBM GB/s"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -71,26 +71,10 @@ def main():
                     help="per-dispatch HBM bytes measured by a separate rocprofv3 --pmc pass")
     args = ap.parse_args()
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as tdist
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl")
-        dist = tdist
+    g = shard.init_from_env("nccl")
+    rank, world, local = g.rank, g.world, g.local
 
-    def barrier_max(x: float) -> float:
-        if dist is None:
-            return x
-        import torch
-        t = torch.tensor([x], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
-
-    lw, t_lower = lowered_config(args.config, args.problems, args.seed + rank * args.problems)
+    lw, t_lower = lowered_config(args.config, args.problems, shard.shard_seed(args.seed, rank, args.problems))
     ctx = _lib.Context(local, 1)
 
     # PCIe-inclusive single pass (host records -> host results), reported only
@@ -101,22 +85,19 @@ def main():
     r = ctx.upload(lw.rec_off, lw.rec)
     for _ in range(args.warmup):
         r.run()
-    if dist is not None:
-        dist.barrier()
+    g.barrier()
     kms = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         r.run()  # launch(es) + hipStreamSynchronize
         kms.append(ctx.last_kernel_ms())
     t1 = time.perf_counter()
-    if dist is not None:
-        dist.barrier()
-    elapsed = barrier_max(t1 - t0)
+    g.barrier()
+    elapsed = g.max(t1 - t0)
     res = r.download()
     r.free()
 
-    total = world * args.problems * args.steps
-    value = total / elapsed
+    value = shard.aggregate_rate(args.problems, world, args.steps, elapsed)
     st = res["status"]
     kernel_ms = float(np.mean(kms))
     nbytes = compulsory_bytes(lw, res)
@@ -180,8 +161,7 @@ def main():
         line["verified_bit_exact_vs_oracle"] = bool(ok)
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    g.close()
 
 
 if __name__ == "__main__":

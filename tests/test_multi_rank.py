@@ -1,0 +1,81 @@
+"""The N>1 path on CPU: world_size-2 gloo ranks, as bench.py runs them under
+torchrun (one process per GPU, RCCL) but with the oracle standing in for the
+device solve so the sharding + timing reduction are checked here.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from deppy_amd import _lib, shard
+
+N_PER_RANK = 40
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _lowered(config, n, seed):
+    w = _lib.generate(config, n, seed)
+    wa = _lib.WireArrays(**{k: w[k] for k in (
+        "prob_var_off", "var_id", "var_con_off", "con_kind", "con_n", "con_arg_off", "con_arg",
+        "str_off")}, str_bytes=w["str_bytes"].tobytes())
+    return _lib.Lowered(wa)
+
+
+def _rank(rank, world, port, outdir):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    from oracle import oracle
+    g = shard.init_from_env("gloo")
+    lw = _lowered(2, N_PER_RANK, shard.shard_seed(7, g.rank, N_PER_RANK))
+    res = oracle.solve_batch(lw.rec_off, lw.rec, 0, 1)
+    g.barrier()
+    fake_elapsed = 1.0 + g.rank  # rank 1 is the slowest
+    mx = g.max(fake_elapsed)
+    all_t = g.gather(fake_elapsed)
+    np.savez(os.path.join(outdir, "r%d.npz" % g.rank), rec_off=lw.rec_off, rec=lw.rec,
+             status=res["status"], steps=res["steps"], installed=res["installed"],
+             mx=mx, all_t=np.array(all_t))
+    g.close()
+
+
+def test_shard_seed_slices_one_global_sequence():
+    assert shard.shard_seed(1000, 0, 10000) == 1000
+    assert shard.shard_seed(1000, 3, 10000) == 31000
+    assert shard.aggregate_rate(10000, 8, 20, 2.0) == 8 * 10000 * 20 / 2.0
+
+
+def test_single_rank_group_is_local():
+    g = shard.Group()
+    g.barrier()
+    assert g.max(3.5) == 3.5 and g.gather(2.0) == [2.0]
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_gloo(tmp_path):
+    from oracle import oracle
+    port = _free_port()
+    mp.start_processes(_rank, args=(2, port, str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    r = [np.load(tmp_path / ("r%d.npz" % i)) for i in range(2)]
+    # timing reduction: every rank sees the max and the full gather
+    for x in r:
+        assert float(x["mx"]) == 2.0
+        assert list(x["all_t"]) == [1.0, 2.0]
+    # the two shards are the two halves of the single-process global batch
+    glob = _lowered(2, 2 * N_PER_RANK, 7)
+    gres = oracle.solve_batch(glob.rec_off, glob.rec, 0, 2)
+    ro = glob.rec_off
+    half = int(ro[N_PER_RANK])
+    assert np.array_equal(r[0]["rec"], glob.rec[:half])
+    assert np.array_equal(r[1]["rec"], glob.rec[half:])
+    assert np.array_equal(np.concatenate([r[0]["status"], r[1]["status"]]), gres["status"])
+    assert np.array_equal(np.concatenate([r[0]["steps"], r[1]["steps"]]), gres["steps"])
+    # no two ranks solved the same catalog
+    assert not np.array_equal(r[0]["rec"], r[1]["rec"])
