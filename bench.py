@@ -5,7 +5,12 @@
 One step = one pass of the solve kernel over one batch of BASELINE config 2:
 10,000 synthetic operator catalogs (~200 bundle entities, Dependency +
 Conflict + AtMost; SURVEY.md §8(d) generator), resident in HBM when the timed
-region starts.  With N > 1 (torchrun, one process per GPU) every rank solves
+region starts.  Steps are pipelined `--depth` deep (default 3) as a serving
+loop would run them: the batch is resident in `depth` slots, step i launches
+slot i % depth (dp_launch) after waiting for that slot's previous step
+(dp_wait), so one step's tail of hard catalogs overlaps the next step's bulk.
+Every step still resolves its whole batch; `serial_ms_per_step` reports the
+unpipelined launch+wait time beside it.  With N > 1 (torchrun, one process per GPU) every rank solves
 its own 10,000 catalogs (distinct seeds): weak scaling, no collective on the
 data path (torch.distributed is used only for the barrier and the max-over-
 ranks of the timing).
@@ -56,6 +61,10 @@ def compulsory_bytes(lw, res) -> int:
     return rec_bytes + out
 
 
+def _same(a, b) -> bool:
+    return all(np.array_equal(a[k], b[k]) for k in ("status", "flags", "installed", "core_len", "core", "steps"))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -67,6 +76,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--depth", type=int, default=3, help="steps in flight (1 = launch+wait per step)")
     ap.add_argument("--pmc-json", default=None,
                     help="per-dispatch HBM bytes measured by a separate rocprofv3 --pmc pass")
     args = ap.parse_args()
@@ -82,20 +92,39 @@ def main():
     ctx.solve(lw.rec_off, lw.rec)
     t_pcie = time.perf_counter() - t0
 
-    r = ctx.upload(lw.rec_off, lw.rec)
-    for _ in range(args.warmup):
-        r.run()
+    depth = max(1, args.depth)
+    slots = [ctx.upload(lw.rec_off, lw.rec) for _ in range(depth)]
+
+    def steps(n, kms):
+        for i in range(n):
+            r = slots[i % depth]
+            if i >= depth:
+                r.wait()
+                kms.append(ctx.last_kernel_ms())
+            r.launch()
+        for i in range(max(0, n - depth), n):
+            slots[i % depth].wait()
+            kms.append(ctx.last_kernel_ms())
+
+    # unpipelined reference figure (not the metric): launch + wait per step
+    serial = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        slots[0].run()
+        serial.append(time.perf_counter() - t0)
+
+    steps(args.warmup, [])
     g.barrier()
     kms = []
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        r.run()  # launch(es) + hipStreamSynchronize
-        kms.append(ctx.last_kernel_ms())
+    steps(args.steps, kms)
     t1 = time.perf_counter()
     g.barrier()
     elapsed = g.max(t1 - t0)
-    res = r.download()
-    r.free()
+    res = slots[0].download()
+    same = all(_same(res, x.download()) for x in slots[1:])
+    for x in slots:
+        x.free()
 
     value = shard.aggregate_rate(args.problems, world, args.steps, elapsed)
     st = res["status"]
@@ -130,7 +159,11 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                      "traffic": traffic, "kernel_ms": round(kernel_ms, 4),
-                     "algorithmic_bytes_per_launch": nbytes},
+                     "algorithmic_bytes_per_launch": nbytes,
+                     "effective_GBs_per_step": round(nbytes / (elapsed / args.steps) / 1e9, 3)},
+        "pipeline_depth": depth,
+        "serial_ms_per_step": round(float(np.median(serial)) * 1e3, 4),
+        "slots_identical": bool(same),
         "classes": {"sat": int((st == 1).sum()), "unsat": int((st == -1).sum()),
                     "incomplete": int((st == 0).sum()), "error": int((st == -2).sum()),
                     "class_b": int(((res["flags"] & 2) != 0).sum())},

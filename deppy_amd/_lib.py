@@ -27,7 +27,7 @@ EXPORTS = [
     "dp_lowered_rec_off", "dp_lowered_rec", "dp_lowered_ident_off", "dp_lowered_ident_var",
     "dp_lowered_ident_con", "dp_lowered_error", "dp_result_layout", "dp_create", "dp_destroy",
     "dp_last_error", "dp_last_global_error", "dp_num_devices", "dp_solve", "dp_upload", "dp_run",
-    "dp_download", "dp_resident_free", "dp_last_kernel_ms", "dp_gen_catalogs", "dp_gen_wire",
+    "dp_launch", "dp_wait", "dp_download", "dp_resident_free", "dp_last_kernel_ms", "dp_gen_catalogs", "dp_gen_wire",
     "dp_gen_free",
 ]
 
@@ -98,6 +98,8 @@ def lib():
     L.dp_solve.argtypes = [vp, ctypes.POINTER(Batch), ctypes.POINTER(Result)]
     L.dp_upload.argtypes = [vp, ctypes.POINTER(Batch), ctypes.POINTER(vp)]
     L.dp_run.argtypes = [vp, vp]
+    L.dp_launch.argtypes = [vp, vp]
+    L.dp_wait.argtypes = [vp, vp]
     L.dp_download.argtypes = [vp, vp, ctypes.POINTER(Result)]
     L.dp_resident_free.argtypes = [vp, vp]
     L.dp_last_kernel_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
@@ -285,6 +287,16 @@ class Resident:
     def run(self):
         if lib().dp_run(self.ctx.h, self.h) != 0:
             raise RuntimeError("dp_run: " + self.ctx.error())
+
+    def launch(self):
+        """Enqueue a solve of the batch and return (dp_launch)."""
+        if lib().dp_launch(self.ctx.h, self.h) != 0:
+            raise RuntimeError("dp_launch: " + self.ctx.error())
+
+    def wait(self):
+        """Block until the last launch finished (dp_wait)."""
+        if lib().dp_wait(self.ctx.h, self.h) != 0:
+            raise RuntimeError("dp_wait: " + self.ctx.error())
 
     def download(self) -> dict:
         n = self.n

@@ -6,6 +6,9 @@
 
 namespace dp {
 
+// diagnostic stamps per problem: 5 phase cycles, 5 counters, wall-clock start/end
+constexpr int DP_NSTAMP = 12;
+
 struct KernelArgs {
   const int32_t* rec;      // records, each 16-byte aligned
   const int64_t* rec_off;  // [n] word offset of each record

@@ -7,6 +7,13 @@
 // requests only the dynamic LDS its largest problem needs (occupancy follows
 // the footprint); problems beyond the 160 KiB LDS of a CU run with their
 // working set in an HBM scratch region (one more launch).
+//
+// Streams belong to the context: kLanes per device, one per hardware queue
+// (GPU_MAX_HW_QUEUES is 4), created first so each maps to its own queue.
+// Every dp_launch takes the next free lanes round-robin, one per bucket
+// launch, so back-to-back batches in flight (dp_launch ... dp_wait) run
+// concurrently and one batch's tail of hard problems overlaps the next
+// batch's bulk.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -29,6 +36,7 @@ constexpr int64_t kDefaultBudget = 1 << 16;        // BCP invocations per proble
 constexpr int kBuckets[] = {8 << 10, 16 << 10, 24 << 10, 32 << 10, 48 << 10, 64 << 10,
                             96 << 10, 160 << 10};
 constexpr int kNBuckets = (int)(sizeof(kBuckets) / sizeof(kBuckets[0]));
+constexpr int kLanes = 4;
 
 #define HIP_OK(expr)                                                         \
   do {                                                                       \
@@ -66,20 +74,26 @@ struct DevSlice {
   int32_t* scratch = nullptr;
   int64_t* scratch_off = nullptr;
   int64_t* stamps = nullptr;  // diagnostic builds only
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;  // lane of the last launch (context-owned)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  // bucket launches run concurrently on side streams joined back by events
-  hipStream_t side[3] = {nullptr, nullptr, nullptr};
-  hipEvent_t done[3] = {nullptr, nullptr, nullptr};
+  // bucket launches run concurrently on the other lanes, joined back by events
+  hipEvent_t done[kLanes - 1] = {};
 };
 
 struct dp_resident {
   int32_t n = 0;
+  bool inflight = false;
   std::vector<DevSlice> slices;
+};
+
+struct Lanes {
+  hipStream_t s[kLanes] = {};
+  int next = 0;
 };
 
 struct dp_ctx {
   std::vector<int> devices;
+  std::vector<Lanes> lanes;  // per device
   int64_t budget = kDefaultBudget;
   std::string err;
   double last_ms = 0.0;
@@ -94,8 +108,14 @@ void fail(const std::string& s) {
   else dp::set_global_error(s);
 }
 
+Lanes& lanes_of(dp_ctx* ctx, int device) {
+  for (size_t i = 0; i < ctx->devices.size(); ++i)
+    if (ctx->devices[i] == device) return ctx->lanes[i];
+  return ctx->lanes[0];
+}
+
 void free_slice(DevSlice& s) {
-  if (s.stream) (void)hipSetDevice(s.device);
+  (void)hipSetDevice(s.device);
   void* ptrs[] = {s.rec, s.rec_off, s.order, s.status, s.flags, s.installed,
                   s.inst_off, s.core, s.core_off, s.core_len, s.steps, s.scratch, s.scratch_off,
                   s.stamps};
@@ -103,11 +123,8 @@ void free_slice(DevSlice& s) {
     if (p) (void)hipFree(p);
   if (s.ev0) (void)hipEventDestroy(s.ev0);
   if (s.ev1) (void)hipEventDestroy(s.ev1);
-  for (int i = 0; i < 3; ++i) {
-    if (s.side[i]) (void)hipStreamDestroy(s.side[i]);
-    if (s.done[i]) (void)hipEventDestroy(s.done[i]);
-  }
-  if (s.stream) (void)hipStreamDestroy(s.stream);
+  for (auto& e : s.done)
+    if (e) (void)hipEventDestroy(e);
   s = DevSlice{};
 }
 
@@ -171,15 +188,13 @@ int64_t build_image(const int32_t* rec, std::vector<int32_t>& out) {
 }
 
 // Build one device's slice: device images, bucketed launch order, outputs.
-int build_slice(DevSlice& s, const dp_batch* b, const int64_t* inst_off, const int64_t* core_off) {
+int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_off,
+                const int64_t* core_off) {
   HIP_OK(hipSetDevice(s.device));
-  HIP_OK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+  s.stream = L.s[0];
   HIP_OK(hipEventCreate(&s.ev0));
   HIP_OK(hipEventCreate(&s.ev1));
-  for (int i = 0; i < 3; ++i) {
-    HIP_OK(hipStreamCreateWithFlags(&s.side[i], hipStreamNonBlocking));
-    HIP_OK(hipEventCreateWithFlags(&s.done[i], hipEventDisableTiming));
-  }
+  for (auto& e : s.done) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   const int32_t n = s.p1 - s.p0;
   std::vector<int64_t> roff((size_t)n + 1, 0);
   std::vector<int32_t> rec;
@@ -240,8 +255,8 @@ int build_slice(DevSlice& s, const dp_batch* b, const int64_t* inst_off, const i
   HIP_OK(hipMalloc(&s.core_len, std::max<size_t>((size_t)n, 1) * 4));
   HIP_OK(hipMalloc(&s.steps, std::max<size_t>((size_t)n, 1) * 8));
 #ifdef DP_STAMPS
-  HIP_OK(hipMalloc(&s.stamps, std::max<size_t>((size_t)n, 1) * 10 * 8));
-  HIP_OK(hipMemsetAsync(s.stamps, 0, std::max<size_t>((size_t)n, 1) * 10 * 8, s.stream));
+  HIP_OK(hipMalloc(&s.stamps, std::max<size_t>((size_t)n, 1) * dp::DP_NSTAMP * 8));
+  HIP_OK(hipMemsetAsync(s.stamps, 0, std::max<size_t>((size_t)n, 1) * dp::DP_NSTAMP * 8, s.stream));
 #endif
   HIP_OK(hipMalloc(&s.installed, (size_t)std::max<int64_t>(s.n_inst, 1) * 4));
   HIP_OK(hipMalloc(&s.core, (size_t)std::max<int64_t>(s.n_core, 1) * 4));
@@ -255,8 +270,16 @@ int build_slice(DevSlice& s, const dp_batch* b, const int64_t* inst_off, const i
   return 0;
 }
 
-int run_slice(DevSlice& s, int64_t budget) {
+// Enqueue the slice's launches (no wait).  A slice with m launches takes the
+// next m lanes (launch i on lane (base + i) % kLanes) and advances the cursor
+// past them, so the next batch in flight starts on lanes this one does not
+// use and the two overlap.
+int launch_slice(DevSlice& s, Lanes& L, int64_t budget) {
   HIP_OK(hipSetDevice(s.device));
+  const int nlaunch = (int)s.b_first.size() + (s.hbm_count ? 1 : 0);
+  const int base = L.next;
+  L.next = (L.next + std::max(1, std::min(nlaunch, kLanes))) % kLanes;
+  s.stream = L.s[base];
   dp::KernelArgs a;
   a.rec = s.rec;
   a.rec_off = s.rec_off;
@@ -272,18 +295,18 @@ int run_slice(DevSlice& s, int64_t budget) {
   a.scratch = nullptr;
   a.scratch_off = nullptr;
   a.stamps = s.stamps;
-  // launch i goes to stream i % 4 (the main stream, then three side streams);
   // the largest buckets come first so they start earliest
   std::vector<int> launch_order;
   for (size_t k = 0; k < s.b_first.size(); ++k) launch_order.push_back((int)k);
   std::sort(launch_order.begin(), launch_order.end(),
             [&](int x, int y) { return s.b_count[(size_t)x] > s.b_count[(size_t)y]; });
   if (s.hbm_count) launch_order.insert(launch_order.begin(), -1);
-  const int nside = std::min<int>(3, (int)launch_order.size() - 1);
+  const int nside = std::min<int>(kLanes - 1, (int)launch_order.size() - 1);
+  auto side = [&](int i) { return L.s[(base + 1 + i) % kLanes]; };
   HIP_OK(hipEventRecord(s.ev0, s.stream));
-  for (int i = 0; i < nside; ++i) HIP_OK(hipStreamWaitEvent(s.side[i], s.ev0, 0));
+  for (int i = 0; i < nside; ++i) HIP_OK(hipStreamWaitEvent(side(i), s.ev0, 0));
   for (size_t i = 0; i < launch_order.size(); ++i) {
-    hipStream_t st = (i % 4 == 0) ? s.stream : s.side[i % 4 - 1];
+    hipStream_t st = (i % kLanes == 0) ? s.stream : side((int)(i % kLanes) - 1);
     const int k = launch_order[i];
     if (k < 0) {
       a.order = s.order + s.hbm_first;
@@ -298,11 +321,16 @@ int run_slice(DevSlice& s, int64_t budget) {
     }
   }
   for (int i = 0; i < nside; ++i) {
-    HIP_OK(hipEventRecord(s.done[i], s.side[i]));
+    HIP_OK(hipEventRecord(s.done[i], side(i)));
     HIP_OK(hipStreamWaitEvent(s.stream, s.done[i], 0));
   }
   HIP_OK(hipEventRecord(s.ev1, s.stream));
-  HIP_OK(hipStreamSynchronize(s.stream));
+  return 0;
+}
+
+int wait_slice(DevSlice& s) {
+  HIP_OK(hipSetDevice(s.device));
+  HIP_OK(hipEventSynchronize(s.ev1));
   return 0;
 }
 
@@ -380,13 +408,30 @@ dp_ctx* dp_create(const dp_opts* opts) {
       delete ctx;
       return nullptr;
     }
+    Lanes L;
+    for (auto& st : L.s) {
+      if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+        dp::set_global_error("dp_create: cannot create streams");
+        dp_destroy(ctx);
+        return nullptr;
+      }
+    }
     ctx->devices.push_back(d);
+    ctx->lanes.push_back(L);
   }
   if (opts && opts->step_budget > 0) ctx->budget = opts->step_budget;
   return ctx;
 }
 
-void dp_destroy(dp_ctx* ctx) { delete ctx; }
+void dp_destroy(dp_ctx* ctx) {
+  if (!ctx) return;
+  for (size_t i = 0; i < ctx->lanes.size(); ++i) {
+    (void)hipSetDevice(ctx->devices.size() > i ? ctx->devices[i] : 0);
+    for (auto& st : ctx->lanes[i].s)
+      if (st) (void)hipStreamDestroy(st);
+  }
+  delete ctx;
+}
 const char* dp_last_error(const dp_ctx* ctx) { return ctx ? ctx->err.c_str() : dp_last_global_error(); }
 int32_t dp_num_devices(const dp_ctx* ctx) { return ctx ? (int32_t)ctx->devices.size() : 0; }
 
@@ -431,7 +476,9 @@ int dp_upload(dp_ctx* ctx, const dp_batch* b, dp_resident** out) {
     s.p1 = p;
     r->slices.push_back(s);
   }
-  int rc = for_slices(ctx, r, [&](DevSlice& s) { return build_slice(s, b, inst_off.data(), core_off.data()); });
+  int rc = for_slices(ctx, r, [&](DevSlice& s) {
+    return build_slice(s, lanes_of(ctx, s.device), b, inst_off.data(), core_off.data());
+  });
   if (rc) {
     dp_resident_free(ctx, r);
     return -1;
@@ -440,12 +487,11 @@ int dp_upload(dp_ctx* ctx, const dp_batch* b, dp_resident** out) {
   return 0;
 }
 
-int dp_run(dp_ctx* ctx, dp_resident* r) {
-  if (!ctx || !r) return -1;
-  std::lock_guard<std::mutex> lk(ctx->mu);
-  t_ctx = ctx;
-  const int64_t budget = ctx->budget;
-  int rc = for_slices(ctx, r, [&](DevSlice& s) { return run_slice(s, budget); });
+namespace {
+int wait_locked(dp_ctx* ctx, dp_resident* r) {
+  if (!r->inflight) return 0;
+  int rc = for_slices(ctx, r, [&](DevSlice& s) { return wait_slice(s); });
+  r->inflight = false;
   if (rc) return -1;
   double mx = 0.0;
   for (auto& s : r->slices) {
@@ -456,16 +502,55 @@ int dp_run(dp_ctx* ctx, dp_resident* r) {
   return 0;
 }
 
+int launch_locked(dp_ctx* ctx, dp_resident* r) {
+  if (r->inflight && wait_locked(ctx, r)) return -1;
+  const int64_t budget = ctx->budget;
+  int rc = 0;
+  // launches are asynchronous: one host thread issues every device's slice
+  for (auto& s : r->slices) rc = rc ? rc : launch_slice(s, lanes_of(ctx, s.device), budget);
+  if (rc) return -1;
+  r->inflight = true;
+  return 0;
+}
+}  // namespace
+
+int dp_launch(dp_ctx* ctx, dp_resident* r) {
+  if (!ctx || !r) return -1;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  t_ctx = ctx;
+  return launch_locked(ctx, r);
+}
+
+int dp_wait(dp_ctx* ctx, dp_resident* r) {
+  if (!ctx || !r) return -1;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  t_ctx = ctx;
+  return wait_locked(ctx, r);
+}
+
+int dp_run(dp_ctx* ctx, dp_resident* r) {
+  if (!ctx || !r) return -1;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  t_ctx = ctx;
+  if (launch_locked(ctx, r)) return -1;
+  return wait_locked(ctx, r);
+}
+
 int dp_download(dp_ctx* ctx, dp_resident* r, dp_result* res) {
   if (!ctx || !r || !res) return -1;
   std::lock_guard<std::mutex> lk(ctx->mu);
   t_ctx = ctx;
+  if (wait_locked(ctx, r)) return -1;
   return for_slices(ctx, r, [&](DevSlice& s) { return download_slice(s, res); });
 }
 
 void dp_resident_free(dp_ctx* ctx, dp_resident* r) {
-  (void)ctx;
   if (!r) return;
+  if (ctx && r->inflight) {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    t_ctx = ctx;
+    (void)wait_locked(ctx, r);
+  }
   for (auto& s : r->slices) free_slice(s);
   delete r;
 }
@@ -486,7 +571,7 @@ int dp_debug_stamps(dp_ctx* ctx, dp_resident* r, int64_t* out) {
   t_ctx = ctx;
   for (auto& s : r->slices) {
     HIP_OK(hipSetDevice(s.device));
-    HIP_OK(hipMemcpy(out + 10 * (size_t)s.p0, s.stamps, (size_t)(s.p1 - s.p0) * 10 * 8,
+    HIP_OK(hipMemcpy(out + dp::DP_NSTAMP * (size_t)s.p0, s.stamps, (size_t)(s.p1 - s.p0) * dp::DP_NSTAMP * 8,
                      hipMemcpyDeviceToHost));
   }
   return 0;

@@ -84,6 +84,11 @@ __device__ __forceinline__ int64_t stamp() {
   __builtin_amdgcn_sched_barrier(0);
   return t;
 }
+__device__ __forceinline__ int64_t wallclock() {
+  int64_t t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
 #define DP_STAMP(i) t[i] = stamp()
 #else
 #define DP_STAMP(i) (void)0
@@ -1015,6 +1020,9 @@ __global__ void __launch_bounds__(64) solve_kernel(KernelArgs a) {
 #ifdef DP_STAMPS
   int64_t t[6];
 #endif
+#ifdef DP_STAMPS
+  const int64_t wall0 = wallclock();
+#endif
   DP_STAMP(0);
   const int pid = a.order[blockIdx.x];
   const int32_t* grec = a.rec + a.rec_off[pid];
@@ -1058,8 +1066,11 @@ __global__ void __launch_bounds__(64) solve_kernel(KernelArgs a) {
   DP_STAMP(5);
 #ifdef DP_STAMPS
   if (W.lane == 0 && a.stamps) {
-    for (int i = 0; i < 5; ++i) a.stamps[10 * pid + i] = t[i + 1] - t[i];
-    for (int i = 0; i < 5; ++i) a.stamps[10 * pid + 5 + i] = W.acc[i];
+    int64_t* o = a.stamps + (int64_t)DP_NSTAMP * pid;
+    for (int i = 0; i < 5; ++i) o[i] = t[i + 1] - t[i];
+    for (int i = 0; i < 5; ++i) o[5 + i] = W.acc[i];
+    o[10] = wall0;
+    o[11] = wallclock();
   }
 #endif
   if (W.lane == 0) {

@@ -243,10 +243,17 @@ int dp_solve(dp_ctx* ctx, const dp_batch* b, dp_result* res);
 typedef struct dp_resident dp_resident;
 int dp_upload(dp_ctx* ctx, const dp_batch* b, dp_resident** out);
 int dp_run(dp_ctx* ctx, dp_resident* r);           /* launch + wait; results stay in HBM */
+/* Asynchronous form of dp_run for pipelines: dp_launch enqueues the solve and
+ * returns; dp_wait blocks until it finished.  Launches of different residents
+ * in flight run concurrently (each takes the next of four per-device streams,
+ * one per hardware queue).  dp_launch on a resident still in flight waits for
+ * it first; dp_download and dp_resident_free wait as well. */
+int dp_launch(dp_ctx* ctx, dp_resident* r);
+int dp_wait(dp_ctx* ctx, dp_resident* r);
 int dp_download(dp_ctx* ctx, dp_resident* r, dp_result* res);
 void dp_resident_free(dp_ctx* ctx, dp_resident* r);
-/* Device time of the solve kernel(s) of the last dp_run/dp_solve, measured with
- * HIP events on the launch stream (max over devices). */
+/* Device time of the solve kernel(s) of the last waited launch (dp_run,
+ * dp_wait, dp_solve), measured with HIP events on its stream (max over devices). */
 int dp_last_kernel_ms(const dp_ctx* ctx, double* ms);
 
 /* ------------------------------------------------------------------------ */

@@ -1,5 +1,7 @@
 """Per-phase shader cycles per problem from the diagnostic stamps build
-(DEPPY_STAMPS=1, libdeppy_hip_stamps.so): [init, base, search, epilogue, core]."""
+(DEPPY_STAMPS=1, libdeppy_hip_stamps.so): [init, base, search, epilogue, core],
+five counters, and the wall-clock (100 MHz) start/end of every wave, to see
+what the step's tail is made of."""
 import ctypes
 import json
 import os
@@ -12,27 +14,45 @@ import numpy as np  # noqa: E402
 from deppy_amd import _lib  # noqa: E402
 from tests.gpu_common import lowered_config  # noqa: E402
 
+NS = 12
+NAMES = ["init", "base", "search", "epilogue", "core", "round_eval", "round_finish", "rounds",
+         "rounds_1lit", "push_guess"]
 L = _lib.lib()
 L.dp_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _lib.c_i64p]
 config = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+sizes = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [64, 10000]
 ctx = _lib.Context(0, 1)
-for n in (64, 10000):
+for n in sizes:
     lw = lowered_config(config, n, 1000)
     r = ctx.upload(lw.rec_off, lw.rec)
     r.run()
     r.run()
     res = r.download()
-    st = np.zeros(10 * n, np.int64)
+    st = np.zeros(NS * n, np.int64)
     L.dp_debug_stamps(ctx.h, r.h, st.ctypes.data_as(_lib.c_i64p))
     r.free()
-    st = st.reshape(n, 10)
-    names = ["init", "base", "search", "epilogue", "core", "round_eval", "round_finish", "rounds", "rounds_1lit", "push_guess"]
+    st = st.reshape(n, NS)
     out = {"n": n, "kernel_ms": ctx.last_kernel_ms()}
+    cyc = st[:, :5].sum(1)
     for cls, mask in [("all", np.ones(n, bool)), ("sat_A", (res["status"] == 1) & ((res["flags"] & 2) == 0)),
                       ("sat_B", (res["status"] == 1) & ((res["flags"] & 2) != 0)), ("unsat", res["status"] == -1)]:
         if mask.sum() == 0:
             continue
         out[cls] = {"count": int(mask.sum()),
-                    **{nm: [int(np.mean(st[mask, i])), int(np.percentile(st[mask, i], 99))] for i, nm in enumerate(names)},
-                    "total_mean": int(st[mask, :5].sum(1).mean()), "total_max": int(st[mask, :5].sum(1).max())}
+                    **{nm: [int(np.mean(st[mask, i])), int(np.percentile(st[mask, i], 99))] for i, nm in enumerate(NAMES)},
+                    "total_mean": int(cyc[mask].mean()), "total_max": int(cyc[mask].max())}
+    # wall-clock timeline (us): when waves start / end relative to the first start
+    w0 = st[:, 10].min()
+    s_us = (st[:, 10] - w0) / 100.0
+    e_us = (st[:, 11] - w0) / 100.0
+    out["timeline_us"] = {"span": float(e_us.max()), "start_p50": float(np.median(s_us)),
+                          "start_max": float(s_us.max()),
+                          "end_p50": float(np.median(e_us)), "end_p90": float(np.percentile(e_us, 90)),
+                          "end_p99": float(np.percentile(e_us, 99)), "end_max": float(e_us.max()),
+                          "dur_mean": float((e_us - s_us).mean()), "dur_max": float((e_us - s_us).max())}
+    top = np.argsort(-(e_us - s_us))[:15]
+    out["slowest"] = [{"pid": int(p), "status": int(res["status"][p]), "flags": int(res["flags"][p]),
+                       "steps": int(res["steps"][p]), "start_us": round(float(s_us[p]), 1),
+                       "dur_us": round(float(e_us[p] - s_us[p]), 1),
+                       **{nm: int(st[p, i]) for i, nm in enumerate(NAMES)}} for p in top]
     print(json.dumps(out), flush=True)

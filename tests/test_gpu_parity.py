@@ -154,3 +154,24 @@ def test_full_size_properties(ctx):
 def test_empty_batch(ctx):
     g = ctx.solve(np.zeros(1, np.int64), np.zeros(0, np.int32))
     assert len(g["status"]) == 0
+
+
+def test_pipelined_launches_match_serial(ctx):
+    """dp_launch/dp_wait with several batches in flight on different streams
+    give the same results as dp_run, and a relaunch waits for the previous one."""
+    lw = lowered_config(5, 400, 31)
+    lw2 = lowered_config(2, 600, 32)
+    ref = ctx.solve(lw.rec_off, lw.rec)
+    ref2 = ctx.solve(lw2.rec_off, lw2.rec)
+    slots = [ctx.upload(lw.rec_off, lw.rec), ctx.upload(lw2.rec_off, lw2.rec), ctx.upload(lw.rec_off, lw.rec)]
+    try:
+        for _ in range(3):
+            for s in slots:
+                s.launch()
+        slots[1].launch()  # still in flight: waits, then relaunches
+        outs = [s.download() for s in slots]  # download waits
+    finally:
+        for s in slots:
+            s.free()
+    for out, want, n in ((outs[0], ref, 400), (outs[1], ref2, 600), (outs[2], ref, 400)):
+        assert compare_results(out, want, n) == []
