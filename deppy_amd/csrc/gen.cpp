@@ -14,7 +14,9 @@
 //     random package, newest first).
 // Input order: bundles, uniqueness variables, required variables.
 // config 2: P = 40;  config 3: P ~ U{4..12};  config 5: P ~ U{4..400} and half
-// the problems get an injected infeasibility (half BCP-level, half search-level).
+// the problems get an injected infeasibility (half BCP-level, half search-level);
+// config 4 (OLM-scale): P = 5000, n_q ~ U{5..15} (V ~ 55k), Dependency targets
+// only in packages (q, q+8] (deep chains), R = 50.
 #include <algorithm>
 #include <cstring>
 #include <string>
@@ -73,9 +75,10 @@ std::string bname(int q, int v) { return "p" + std::to_string(q) + "-v" + std::t
 
 void gen_problem(Builder& B, int config, uint64_t seed) {
   SplitMix64 r(seed);
-  int P = config == 2 ? 40 : config == 3 ? (int)r.uniform(4, 12) : (int)r.uniform(4, 400);
+  int P = config == 2 ? 40 : config == 3 ? (int)r.uniform(4, 12) : config == 4 ? 5000 : (int)r.uniform(4, 400);
+  const int vlo = config == 4 ? 5 : 1, vhi = config == 4 ? 15 : 9;
   std::vector<int> nver((size_t)P);
-  for (int q = 0; q < P; ++q) nver[(size_t)q] = (int)r.uniform(1, 9);
+  for (int q = 0; q < P; ++q) nver[(size_t)q] = (int)r.uniform(vlo, vhi);
   // injected infeasibility (config 5): 0 none, 1 BCP-level, 2 search-level
   int inject = 0, ia = -1, ic = -1;
   if (config == 5 && r.bernoulli(0.5)) {
@@ -108,7 +111,7 @@ void gen_problem(Builder& B, int config, uint64_t seed) {
         int nd = (int)r.uniform(1, 3);
         for (int d = 0; d < nd; ++d) {
           if (q == P - 1) break;
-          int t = (int)r.uniform(q + 1, P - 1);
+          int t = (int)r.uniform(q + 1, config == 4 ? std::min(q + 8, P - 1) : P - 1);
           int lo = (int)r.uniform(0, nver[(size_t)t] - 1);
           int hi = (int)r.uniform(lo, nver[(size_t)t] - 1);
           std::vector<std::string> ids;
@@ -129,7 +132,7 @@ void gen_problem(Builder& B, int config, uint64_t seed) {
     for (int v = nver[(size_t)q] - 1; v >= 0; --v) ids.push_back(bname(q, v));
     B.con(DP_ATMOST, 1, ids);
   }
-  int R = (int)r.uniform(1, 4);
+  int R = config == 4 ? 50 : (int)r.uniform(1, 4);
   for (int i = 0; i < R; ++i) {
     B.var("r" + std::to_string(i));
     B.con(DP_MANDATORY, 0, {});
@@ -172,8 +175,8 @@ struct dp_gen {
 extern "C" {
 
 dp_gen* dp_gen_catalogs(int32_t config, int32_t n_problems, uint64_t base_seed) {
-  if (config != 2 && config != 3 && config != 5) {
-    dp::set_global_error("dp_gen_catalogs: config must be 2, 3 or 5");
+  if (config < 2 || config > 5) {
+    dp::set_global_error("dp_gen_catalogs: config must be 2, 3, 4 or 5");
     return nullptr;
   }
   if (n_problems < 0) return nullptr;
