@@ -13,8 +13,11 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libdeppy_hip.so")
+# dp_opt_flag (include/deppy_hip.h): placement overrides
+OPT_FORCE_GROUP = 1 << 0
+OPT_FORCE_HBM = 1 << 1
 if os.environ.get("DEPPY_STAMPS") == "1":  # diagnostic phase-stamp build (scripts/ only)
-    LIB_PATH = os.path.join(HERE, "libdeppy_hip_stamps.so")
+    LIB_PATH = os.path.join(HERE, os.environ.get("DEPPY_STAMPS_LIB", "libdeppy_hip_stamps.so"))
 
 c_i32p = ctypes.POINTER(ctypes.c_int32)
 c_i64p = ctypes.POINTER(ctypes.c_int64)
@@ -219,9 +222,10 @@ class Lowered:
 # device context and batch solve
 # ---------------------------------------------------------------------------
 class Context:
-    def __init__(self, first_device: int = 0, n_devices: int = 1, step_budget: int = 0):
+    def __init__(self, first_device: int = 0, n_devices: int = 1, step_budget: int = 0,
+                 flags: int = 0):
         L = lib()
-        o = Opts(first_device, n_devices, step_budget, 0)
+        o = Opts(first_device, n_devices, step_budget, flags)
         h = L.dp_create(ctypes.byref(o))
         if not h:
             raise RuntimeError("deppy_amd: no usable MI355X: " + L.dp_last_global_error().decode())

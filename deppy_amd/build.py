@@ -15,7 +15,8 @@ OBJ = os.path.join(HERE, "_obj")
 STAMPS_LIB = os.path.join(HERE, "libdeppy_hip_stamps.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
-SOURCES = ["solve_kernel.hip", "runtime.cpp", "lower.cpp", "gen.cpp"]
+SOURCES = ["solve_lds.hip", "solve_split.hip", "solve_hbm.hip", "solve_launch.cpp", "runtime.cpp",
+           "lower.cpp", "gen.cpp"]
 FLAGS = ["-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function",
          "--offload-arch=" + ARCH, "-I" + os.path.join(HERE, "..", "include")]
 
@@ -27,11 +28,12 @@ def _needs(target: str, deps: list[str]) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(verbose: bool = False, extra: list[str] | None = None, stamps: bool = False) -> str:
+def build(verbose: bool = False, extra: list[str] | None = None, stamps: bool = False,
+          tag: str = "") -> str:
     global OBJ, LIB
     if stamps:
         extra = (extra or []) + ["-DDP_STAMPS"]
-        obj, lib = OBJ + "_stamps", STAMPS_LIB
+        obj, lib = OBJ + "_stamps" + tag, STAMPS_LIB.replace(".so", tag + ".so")
     else:
         obj, lib = OBJ, LIB
     return _build(verbose, extra, obj, lib)
@@ -46,13 +48,13 @@ def _build(verbose, extra, OBJ, LIB) -> str:
         s = os.path.join(CSRC, src)
         o = os.path.join(OBJ, src + ".o")
         if _needs(o, [s] + headers) or extra:
-            lang = ["-x", "hip"] if src.endswith(".hip") else ["-x", "hip"] if src == "runtime.cpp" else []
+            lang = ["-x", "hip"] if src.endswith(".hip") or src in ("runtime.cpp", "solve_launch.cpp") else []
             jobs.append([HIPCC] + FLAGS + (extra or []) + lang + ["-c", s, "-o", o])
     def run(cmd):
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
-    with ThreadPoolExecutor(max_workers=4) as ex:
+    with ThreadPoolExecutor(max_workers=8) as ex:
         list(ex.map(run, jobs))
     objs = [os.path.join(OBJ, s + ".o") for s in SOURCES]
     if _needs(LIB, objs) or jobs:
@@ -63,5 +65,6 @@ def _build(verbose, extra, OBJ, LIB) -> str:
 if __name__ == "__main__":
     args = sys.argv[1:]
     stamps = "--stamps" in args
-    args = [a for a in args if a != "--stamps"]
-    build(verbose=True, extra=args or None, stamps=stamps)
+    tag = next((a.split("=", 1)[1] for a in args if a.startswith("--tag=")), "")
+    args = [a for a in args if a != "--stamps" and not a.startswith("--tag=")]
+    build(verbose=True, extra=args or None, stamps=stamps, tag=tag)

@@ -1,4 +1,4 @@
-// Host <-> kernel interface of the solve kernel (solve_kernel.hip).
+// Host <-> kernel interface of the solve kernel (solve_kernel.hpp).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -6,8 +6,10 @@
 
 namespace dp {
 
-// diagnostic stamps per problem: 5 phase cycles, 5 counters, wall-clock start/end
-constexpr int DP_NSTAMP = 12;
+// diagnostic stamps per problem: 5 phase cycles, 5 counters, wall-clock
+// start/end, then the first failed index check (code, value, bound) and the
+// number of failed checks
+constexpr int DP_NSTAMP = 16;
 
 struct KernelArgs {
   const int32_t* rec;      // records, each 16-byte aligned
@@ -22,16 +24,17 @@ struct KernelArgs {
   int32_t* core_len;
   int64_t* steps;
   int64_t budget;
-  // HBM-resident working sets (problems over the LDS limit): when non-null,
-  // workgroup b works in scratch + scratch_off[b] instead of LDS
+  // HBM scratch of the multi-wave modes (M_SPLIT / M_HBM, problems over the
+  // LDS limit): workgroup b works in scratch + scratch_off[b] (and in LDS)
   int32_t* scratch;
   const int64_t* scratch_off;
   // diagnostic builds only (-DDP_STAMPS): per-problem phase cycle counts
   int64_t* stamps;
 };
 
-// Launch one wavefront per problem of order[0..n_blocks) with lds_bytes of LDS.
-hipError_t launch_solve(const KernelArgs& a, int n_blocks, int lds_bytes, hipStream_t stream);
+// Launch one workgroup per problem of order[0..n_blocks) with lds_bytes of
+// LDS: one wavefront (mode M_LDS) or BIG_WAVES wavefronts (M_SPLIT, M_HBM).
+hipError_t launch_solve(const KernelArgs& a, int mode, int n_blocks, int lds_bytes, hipStream_t stream);
 // Raise the kernel's dynamic-LDS limit to the device maximum.
 hipError_t configure_solve_kernel(int max_lds_bytes);
 

@@ -8,11 +8,13 @@
 //                   ~240-variable catalog needs ~18 KiB and 8-9 problems fit
 //                   in one CU's 160 KiB of LDS.
 //   IX = int32_t  : the HBM image for problems too large for LDS (or with
-//                   larger indices); same code, working set in HBM scratch.
+//                   larger indices), solved by one multi-wave workgroup
+//                   (M_SPLIT / M_HBM below).
 #pragma once
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "../../include/deppy_hip.h"
 
@@ -22,10 +24,30 @@ __host__ __device__ inline int32_t bits_words(int32_t n) { return (n + 31) >> 5;
 
 // learned-row store (oracle: L_MAX rows, lcap = 2*nv + 64 literals)
 constexpr int32_t L_MAX = 64;
-// work list of one propagation chunk (rows watched by <= 64 frontier literals)
-constexpr int32_t WBUF = 256;
+
+// Three placements of the same working set (one template instantiation each):
+//   M_LDS   one wavefront per problem, the whole image narrowed to 16 bits and
+//           the whole working set in LDS (the batched small-catalog path)
+//   M_SPLIT one workgroup of BIG_WAVES wavefronts per problem (large catalogs,
+//           e.g. config 4): the int32 image is read in place from HBM, the
+//           per-literal arrays live in an HBM scratch region, and the hot
+//           per-variable state (val, every bitset) plus the work lists live in
+//           LDS
+//   M_HBM   the same workgroup with everything but the work lists in HBM
+//           (catalogs whose per-variable state exceeds the LDS)
+enum Mode { M_LDS = 0, M_SPLIT = 1, M_HBM = 2 };
+#ifndef DP_BIG_WAVES
+#define DP_BIG_WAVES 8
+#endif
+constexpr int32_t BIG_WAVES = DP_BIG_WAVES;
+
+__host__ __device__ constexpr int32_t mode_waves(int mode) { return mode == M_LDS ? 1 : BIG_WAVES; }
+// work list of one propagation chunk (rows watched by <= 64*waves frontier literals)
+__host__ __device__ constexpr int32_t mode_wbuf(int mode) { return mode == M_LDS ? 256 : 4096; }
 // AtMost rows queued for wave-cooperative evaluation in one round
-constexpr int32_t CQ = 64;
+__host__ __device__ constexpr int32_t mode_cq(int mode) { return mode == M_LDS ? 64 : 512; }
+// wave-shared scalars (S_*), then per-wave reduction slots
+constexpr int32_t NSCAL = 64;
 
 // dp_rec_layout_of (include/deppy_hip.h) for host and device code.
 __host__ __device__ inline dp_rec_layout rec_layout(const int32_t* h) {
@@ -71,9 +93,12 @@ __host__ __device__ inline ImgLayout img_layout(const int32_t* h) {
   return X;
 }
 
+// Byte offsets of every working-set array.  An offset is into the LDS
+// allocation when the mode places that array in LDS (in_lds below), else into
+// the problem's HBM scratch region.
 struct Layout {
-  int32_t body;      // image arrays (header dropped), one IX per image word
-  int32_t val;       // int8[nv]: 0 unassigned, 1 true, -1 false
+  int32_t body;      // M_LDS only: image arrays (header dropped), one IX per image word
+  int32_t val;       // int8[nv]: 0 unassigned, 1 true, -1 false                  [LDS unless M_HBM]
   int32_t reason;    // IX[nv] implying row; R_DEC / R_EXTRA
   int32_t rs;        // IX[nv] trail position where the assigning round started
   int32_t trail;     // IX[nv] true literals in assignment order
@@ -82,71 +107,79 @@ struct Layout {
   int32_t d_mark;    // IX[nv] trail length before each decision
   int32_t dix;       // IX[nv] decision index of a variable (NONE otherwise)
   int32_t imp;       // u32[2nv] lowest row implying literal l this round (INF: none)
-  int32_t d_flip;    // bits[nv] decision already flipped
-  int32_t inS;       // bits[nv] guessed set (search.assumptions)
-  int32_t extra;     // bits[nv] SAT-epilogue extras
-  int32_t seen;      // bits[nv] conflict analysis
-  int32_t model;     // bits[nv] last model (Value)
-  int32_t dset;      // bits[nv] decisions met by the last conflict analysis
-  int32_t fg;        // bits[nv] guesses met by the refutation of a Solve()
-  int32_t used;      // bits[nid] identities met by a refutation
-  int32_t en;        // bits[nid] identities enabled (core search)
-  int32_t en2;       // bits[nid]
+  int32_t d_flip;    // bits[nv] decision already flipped                          [LDS unless M_HBM]
+  int32_t inS;       // bits[nv] guessed set (search.assumptions)                  [LDS unless M_HBM]
+  int32_t extra;     // bits[nv] SAT-epilogue extras                               [LDS unless M_HBM]
+  int32_t seen;      // bits[nv] conflict analysis                                 [LDS unless M_HBM]
+  int32_t model;     // bits[nv] last model (Value)                                [LDS unless M_HBM]
+  int32_t dset;      // bits[nv] decisions met by the last conflict analysis       [LDS unless M_HBM]
+  int32_t fg;        // bits[nv] guesses met by the refutation of a Solve()        [LDS unless M_HBM]
+  int32_t used;      // bits[nid] identities met by a refutation                   [LDS unless M_HBM]
+  int32_t en;        // bits[nid] identities enabled (core search)                 [LDS unless M_HBM]
+  int32_t en2;       // bits[nid]                                                  [LDS unless M_HBM]
   int32_t l_off;     // IX[L_MAX+1] learned rows (rows nrows..)
   int32_t l_lits;    // IX[lcap]
   int32_t dq;        // IX[2*cap] deque of choices (list, idx)
   int32_t stk;       // IX[5*cap] guess stack (list, idx, m, children, mark)
-  int32_t wbuf;      // IX[WBUF] flattened work list (watch-list positions)
-  int32_t cardq;     // i32[CQ] AtMost rows queued this round
-  int32_t scal;      // i32[16] wave-shared scalars
-  int32_t bytes;     // total
+  int32_t wbuf;      // IX[wbuf] flattened work list (watch-list positions)       [LDS]
+  int32_t cardq;     // i32[cq] AtMost rows queued this round                     [LDS]
+  int32_t scal;      // i32[NSCAL] wave-shared scalars and reduction slots        [LDS]
+  int32_t bytes;     // HBM scratch bytes (0 for M_LDS)
+  int32_t lds_bytes; // LDS bytes
   int32_t cap, lcap;
 };
 
-enum Scalar { S_NTOUCHED = 0, S_NWORK = 1, S_NK = 2 };
+enum Scalar { S_NTOUCHED = 0, S_NWORK = 1, S_NK = 2, S_APP = 3, S_SLOT = 32 };
 
-template <class IX>
+template <int MODE>
 __host__ __device__ inline Layout layout(const int32_t* h) {
+  using IX = typename std::conditional<MODE == M_LDS, uint16_t, int32_t>::type;
   Layout L;
   const int32_t nv = h[DP_H_NV], nid = h[DP_H_NID];
   const int32_t nbv = bits_words(nv), nbi = bits_words(nid);
   const int32_t ix = (int32_t)sizeof(IX);
-  int32_t o = 0;
-  auto take = [&](int32_t nbytes) {
-    int32_t at = o;
-    o += (nbytes + 15) & ~15;  // every array 16-byte aligned
+  int32_t og = 0, ol = 0;
+  // every array 16-byte aligned; `hot` arrays go to LDS unless M_HBM, the
+  // per-literal arrays to LDS only in M_LDS, the work lists always to LDS
+  auto take = [&](int32_t nbytes, int kind) {
+    const bool lds = MODE == M_LDS || kind == 2 || (kind == 1 && MODE == M_SPLIT);
+    int32_t& o = lds ? ol : og;
+    const int32_t at = o;
+    o += (nbytes + 15) & ~15;
     return at;
   };
+  enum { COLD = 0, HOT = 1, WORK = 2 };
   L.cap = h[DP_H_NA] + h[DP_H_NCH] + 2;
   L.lcap = 2 * nv + 64;
-  L.body = take((h[DP_H_IMG] - DP_H_SIZE + 4) * ix);  // +4: dwordx4 copy slack
-  L.val = take(nv);
-  L.reason = take(nv * ix);
-  L.rs = take(nv * ix);
-  L.trail = take(nv * ix);
-  L.touched = take(2 * nv * ix);
-  L.d_lit = take(nv * ix);
-  L.d_mark = take(nv * ix);
-  L.dix = take(nv * ix);
-  L.imp = take(2 * nv * 4);
-  L.d_flip = take(nbv * 4);
-  L.inS = take(nbv * 4);
-  L.extra = take(nbv * 4);
-  L.seen = take(nbv * 4);
-  L.model = take(nbv * 4);
-  L.dset = take(nbv * 4);
-  L.fg = take(nbv * 4);
-  L.used = take(nbi * 4);
-  L.en = take(nbi * 4);
-  L.en2 = take(nbi * 4);
-  L.l_off = take((L_MAX + 1) * ix);
-  L.l_lits = take(L.lcap * ix);
-  L.dq = take(2 * L.cap * ix);
-  L.stk = take(5 * L.cap * ix);
-  L.wbuf = take(WBUF * ix);
-  L.cardq = take(CQ * 4);
-  L.scal = take(16 * 4);
-  L.bytes = o;
+  L.body = MODE == M_LDS ? take((h[DP_H_IMG] - DP_H_SIZE + 4) * ix, COLD) : 0;  // +4: dwordx4 copy slack
+  L.scal = take(NSCAL * 4, WORK);
+  L.wbuf = take(mode_wbuf(MODE) * ix, WORK);
+  L.cardq = take(mode_cq(MODE) * 4, WORK);
+  L.val = take(nv, HOT);
+  L.d_flip = take(nbv * 4, HOT);
+  L.inS = take(nbv * 4, HOT);
+  L.extra = take(nbv * 4, HOT);
+  L.seen = take(nbv * 4, HOT);
+  L.model = take(nbv * 4, HOT);
+  L.dset = take(nbv * 4, HOT);
+  L.fg = take(nbv * 4, HOT);
+  L.used = take(nbi * 4, HOT);
+  L.en = take(nbi * 4, HOT);
+  L.en2 = take(nbi * 4, HOT);
+  L.reason = take(nv * ix, COLD);
+  L.rs = take(nv * ix, COLD);
+  L.trail = take(nv * ix, COLD);
+  L.touched = take(2 * nv * ix, COLD);
+  L.d_lit = take(nv * ix, COLD);
+  L.d_mark = take(nv * ix, COLD);
+  L.dix = take(nv * ix, COLD);
+  L.imp = take(2 * nv * 4, COLD);
+  L.l_off = take((L_MAX + 1) * ix, COLD);
+  L.l_lits = take(L.lcap * ix, COLD);
+  L.dq = take(2 * L.cap * ix, COLD);
+  L.stk = take(5 * L.cap * ix, COLD);
+  L.bytes = og;
+  L.lds_bytes = ol;
   return L;
 }
 

@@ -69,8 +69,11 @@ struct DevSlice {
   // launches: [bucket] -> (first order index, count, lds bytes)
   std::vector<int> b_first, b_count, b_lds;
   std::vector<int32_t> too_large;             // local indices (-> DP_ERROR)
-  // HBM-resident working sets for problems over the LDS limit
-  int hbm_first = 0, hbm_count = 0;
+  // multi-wave launches for problems over the LDS limit: [i] -> (first order
+  // index, count, mode, lds bytes); their scratch offsets are indexed from
+  // big_base (the first order index of the big problems)
+  std::vector<int> g_first, g_count, g_mode, g_lds;
+  int big_base = 0;
   int32_t* scratch = nullptr;
   int64_t* scratch_off = nullptr;
   int64_t* stamps = nullptr;  // diagnostic builds only
@@ -95,6 +98,7 @@ struct dp_ctx {
   std::vector<int> devices;
   std::vector<Lanes> lanes;  // per device
   int64_t budget = kDefaultBudget;
+  int32_t flags = 0;  // dp_opt_flag
   std::string err;
   double last_ms = 0.0;
   std::mutex mu;
@@ -189,7 +193,7 @@ int64_t build_image(const int32_t* rec, std::vector<int32_t>& out) {
 
 // Build one device's slice: device images, bucketed launch order, outputs.
 int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_off,
-                const int64_t* core_off) {
+                const int64_t* core_off, int32_t opt_flags) {
   HIP_OK(hipSetDevice(s.device));
   s.stream = L.s[0];
   HIP_OK(hipEventCreate(&s.ev0));
@@ -202,21 +206,23 @@ int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_of
     build_image(b->rec + b->rec_off[s.p0 + i], rec);
     roff[(size_t)i + 1] = (int64_t)rec.size();
   }
-  std::vector<std::vector<int32_t>> bucket(kNBuckets);
-  std::vector<int32_t> hbm;
-  std::vector<int64_t> soff(1, 0);
+  std::vector<std::vector<int32_t>> bucket(kNBuckets), big(3);
   for (int32_t i = 0; i < n; ++i) {
     const int32_t* r = rec.data() + roff[(size_t)i];
-    const int64_t lds = dp::fits16(r) ? (int64_t)dp::layout<uint16_t>(r).bytes : INT64_MAX;
+    const bool forced = opt_flags & (DP_OPT_FORCE_GROUP | DP_OPT_FORCE_HBM);
+    const int64_t lds = dp::fits16(r) && !forced ? (int64_t)dp::layout<dp::M_LDS>(r).lds_bytes : INT64_MAX;
     int k = 0;
     while (k < kNBuckets && lds > kBuckets[k]) ++k;
     if (k < kNBuckets) {
       bucket[(size_t)k].push_back(i);
-    } else {
-      const int64_t bytes = (int64_t)dp::layout<int32_t>(r).bytes;
-      if (bytes < ((int64_t)1 << 31)) { hbm.push_back(i); soff.push_back(soff.back() + bytes / 4); }
-      else s.too_large.push_back(i);
+      continue;
     }
+    const dp::Layout ls = dp::layout<dp::M_SPLIT>(r), lh = dp::layout<dp::M_HBM>(r);
+    // (layout arithmetic is int32: variables are capped well below its range)
+    const bool sized = r[DP_H_NV] < (1 << 24) && r[DP_H_NID] < (1 << 26);
+    if (sized && ls.lds_bytes <= kMaxLdsBytes && !(opt_flags & DP_OPT_FORCE_HBM)) big[dp::M_SPLIT].push_back(i);
+    else if (sized && lh.lds_bytes <= kMaxLdsBytes) big[dp::M_HBM].push_back(i);
+    else s.too_large.push_back(i);
   }
   std::vector<int32_t> order;
   for (int k = 0; k < kNBuckets; ++k) {
@@ -225,13 +231,27 @@ int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_of
     s.b_count.push_back((int)bucket[(size_t)k].size());
     int mx = 0;
     for (int32_t i : bucket[(size_t)k])
-      mx = std::max(mx, dp::layout<uint16_t>(rec.data() + roff[(size_t)i]).bytes);
+      mx = std::max(mx, dp::layout<dp::M_LDS>(rec.data() + roff[(size_t)i]).lds_bytes);
     s.b_lds.push_back(mx);
     order.insert(order.end(), bucket[(size_t)k].begin(), bucket[(size_t)k].end());
   }
-  s.hbm_first = (int)order.size();
-  s.hbm_count = (int)hbm.size();
-  order.insert(order.end(), hbm.begin(), hbm.end());
+  s.big_base = (int)order.size();
+  std::vector<int64_t> soff(1, 0);
+  for (int mode = dp::M_SPLIT; mode <= dp::M_HBM; ++mode) {
+    if (big[(size_t)mode].empty()) continue;
+    s.g_first.push_back((int)order.size());
+    s.g_count.push_back((int)big[(size_t)mode].size());
+    s.g_mode.push_back(mode);
+    int mx = 0;
+    for (int32_t i : big[(size_t)mode]) {
+      const int32_t* r = rec.data() + roff[(size_t)i];
+      const dp::Layout L = mode == dp::M_SPLIT ? dp::layout<dp::M_SPLIT>(r) : dp::layout<dp::M_HBM>(r);
+      mx = std::max(mx, L.lds_bytes);
+      soff.push_back(soff.back() + ((int64_t)L.bytes + 15) / 16 * 4);  // int32 words, 16-byte aligned
+    }
+    s.g_lds.push_back(mx);
+    order.insert(order.end(), big[(size_t)mode].begin(), big[(size_t)mode].end());
+  }
   s.inst0 = inst_off[s.p0];
   s.core0 = core_off[s.p0];
   s.n_inst = inst_off[s.p1] - s.inst0;
@@ -246,8 +266,8 @@ int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_of
   if (upload_vec(&s.order, order.data(), order.size(), s.stream)) return -1;
   if (upload_vec(&s.inst_off, li.data(), (size_t)n + 1, s.stream)) return -1;
   if (upload_vec(&s.core_off, lc.data(), (size_t)n + 1, s.stream)) return -1;
-  if (s.hbm_count) {
-    if (upload_vec(&s.scratch_off, soff.data(), (size_t)s.hbm_count, s.stream)) return -1;
+  if (soff.size() > 1) {
+    if (upload_vec(&s.scratch_off, soff.data(), soff.size() - 1, s.stream)) return -1;
     HIP_OK(hipMalloc(&s.scratch, (size_t)soff.back() * 4));
   }
   HIP_OK(hipMalloc(&s.status, std::max<size_t>((size_t)n, 1)));
@@ -276,7 +296,7 @@ int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_of
 // use and the two overlap.
 int launch_slice(DevSlice& s, Lanes& L, int64_t budget) {
   HIP_OK(hipSetDevice(s.device));
-  const int nlaunch = (int)s.b_first.size() + (s.hbm_count ? 1 : 0);
+  const int nlaunch = (int)s.b_first.size() + (int)s.g_first.size();
   const int base = L.next;
   L.next = (L.next + std::max(1, std::min(nlaunch, kLanes))) % kLanes;
   s.stream = L.s[base];
@@ -295,12 +315,13 @@ int launch_slice(DevSlice& s, Lanes& L, int64_t budget) {
   a.scratch = nullptr;
   a.scratch_off = nullptr;
   a.stamps = s.stamps;
-  // the largest buckets come first so they start earliest
+  // the multi-wave launches (long-running large catalogs) first, then the
+  // largest buckets, so they start earliest
   std::vector<int> launch_order;
   for (size_t k = 0; k < s.b_first.size(); ++k) launch_order.push_back((int)k);
   std::sort(launch_order.begin(), launch_order.end(),
             [&](int x, int y) { return s.b_count[(size_t)x] > s.b_count[(size_t)y]; });
-  if (s.hbm_count) launch_order.insert(launch_order.begin(), -1);
+  for (size_t g = 0; g < s.g_first.size(); ++g) launch_order.insert(launch_order.begin() + (long)g, -1 - (int)g);
   const int nside = std::min<int>(kLanes - 1, (int)launch_order.size() - 1);
   auto side = [&](int i) { return L.s[(base + 1 + i) % kLanes]; };
   HIP_OK(hipEventRecord(s.ev0, s.stream));
@@ -309,15 +330,16 @@ int launch_slice(DevSlice& s, Lanes& L, int64_t budget) {
     hipStream_t st = (i % kLanes == 0) ? s.stream : side((int)(i % kLanes) - 1);
     const int k = launch_order[i];
     if (k < 0) {
-      a.order = s.order + s.hbm_first;
+      const size_t g = (size_t)(-1 - k);
+      a.order = s.order + s.g_first[g];
       a.scratch = s.scratch;
-      a.scratch_off = s.scratch_off;
-      HIP_OK(dp::launch_solve(a, s.hbm_count, 0, st));
+      a.scratch_off = s.scratch_off + (s.g_first[g] - s.big_base);
+      HIP_OK(dp::launch_solve(a, s.g_mode[g], s.g_count[g], s.g_lds[g], st));
       a.scratch = nullptr;
       a.scratch_off = nullptr;
     } else {
       a.order = s.order + s.b_first[(size_t)k];
-      HIP_OK(dp::launch_solve(a, s.b_count[(size_t)k], s.b_lds[(size_t)k], st));
+      HIP_OK(dp::launch_solve(a, dp::M_LDS, s.b_count[(size_t)k], s.b_lds[(size_t)k], st));
     }
   }
   for (int i = 0; i < nside; ++i) {
@@ -420,6 +442,7 @@ dp_ctx* dp_create(const dp_opts* opts) {
     ctx->lanes.push_back(L);
   }
   if (opts && opts->step_budget > 0) ctx->budget = opts->step_budget;
+  if (opts) ctx->flags = opts->flags;
   return ctx;
 }
 
@@ -477,7 +500,7 @@ int dp_upload(dp_ctx* ctx, const dp_batch* b, dp_resident** out) {
     r->slices.push_back(s);
   }
   int rc = for_slices(ctx, r, [&](DevSlice& s) {
-    return build_slice(s, lanes_of(ctx, s.device), b, inst_off.data(), core_off.data());
+    return build_slice(s, lanes_of(ctx, s.device), b, inst_off.data(), core_off.data(), ctx->flags);
   });
   if (rc) {
     dp_resident_free(ctx, r);

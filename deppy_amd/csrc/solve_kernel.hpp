@@ -1,8 +1,11 @@
-// Batched pkg/sat resolution on MI355X (gfx950): one wavefront per problem.
+// Batched pkg/sat resolution on MI355X (gfx950).
 //
-// Each workgroup is one 64-lane wavefront that owns one problem.  The problem's
-// lowered record is narrowed to 16 bits into LDS, watch lists are built in LDS,
-// and the whole solve runs out of LDS:
+// Small catalogs (the batched hot path, M_LDS): one 64-lane wavefront owns one
+// problem.  The problem's device image is narrowed to 16 bits into LDS and the
+// whole solve runs out of LDS.  Large catalogs (config 4, M_SPLIT / M_HBM):
+// one workgroup of BIG_WAVES wavefronts owns one problem; the int32 image is
+// read in place from HBM, the hot per-variable state stays in LDS, and every
+// data-parallel loop is spread over the whole workgroup.
 //
 //   base scope + BCP        pkg/sat/solve.go:63-79           (base_propagate)
 //   preference search       pkg/sat/search.go:34-203         (search)
@@ -10,20 +13,20 @@
 //   SAT epilogue            solve.go:86-110                  (epilogue)
 //   NotSatisfiable          solve.go:114-115                 (core)
 //
-// Control flow is wave-uniform (every lane runs the same scalar logic on
-// broadcast LDS reads); the data-parallel parts are row evaluation (lanes over
-// the rows watched by a round's frontier, flattened through an LDS work list),
-// the all-false-completion check (lanes over clause rows), candidate
-// membership tests (ballot), AtMost counting and conflict analysis.
+// Control flow is group-uniform: every thread runs the same scalar logic on
+// broadcast LDS/HBM reads, and single-writer updates are made by thread 0.
+// The data-parallel parts are row evaluation (threads over the rows watched by
+// a round's frontier, flattened through an LDS work list), the
+// all-false-completion check, candidate membership tests, AtMost counting
+// (one wavefront per queued row), conflict analysis and every O(nv) sweep.
 //
 // Semantics are exactly those of oracle/sat_oracle.c (the test oracle): a
-// round's implications are resolved to the lowest implying row with LDS
-// atomicMin, so reasons, cores and step counts are bit-identical.  (The oracle
-// orders assignments by round number, this kernel by the trail position where
-// the round started; the two orders agree on every pair of assigned variables.)
-//
-// Problems too large for LDS run the same code (HBM = true) on an int32 image
-// in an HBM scratch region.
+// round's implications are resolved to the lowest implying row with atomicMin,
+// so reasons, cores and step counts are bit-identical.  (The oracle orders
+// assignments by round number, this kernel by the trail position where the
+// round started; the two orders agree on every pair of assigned variables, and
+// nothing depends on the order of assignments within one round.)
+#pragma once
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
@@ -32,6 +35,9 @@
 #include "layout.hpp"
 
 namespace dp {
+
+// Each mode's kernel is instantiated in its own translation unit
+// (solve_lds.hip, solve_split.hip, solve_hbm.hip) so they compile in parallel.
 
 namespace {
 
@@ -42,7 +48,7 @@ enum { CK_NONE = 0, CK_ROW, CK_VAR, CK_ASSUME, CK_EXTRA };
 enum { RS_SAT = 1, RS_UNSAT = -1, RS_BUDGET = 2 };
 
 // Lanes of the wave hand values to each other through the working set (LDS,
-// or HBM for oversized problems): complete every access before the next phase.
+// or HBM): complete every access before the next phase.
 __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   __builtin_amdgcn_wave_barrier();
@@ -70,6 +76,11 @@ __device__ __forceinline__ int wave_min(int x) {
   for (int d = 32; d >= 1; d >>= 1) x = min(x, __shfl_xor(x, d));
   return x;
 }
+__device__ __forceinline__ int wave_sum(int x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
+  return x;
+}
 
 __device__ __forceinline__ bool getb(const uint32_t* b, int i) { return (b[i >> 5] >> (i & 31)) & 1u; }
 
@@ -93,18 +104,43 @@ __device__ __forceinline__ int64_t wallclock() {
 #else
 #define DP_STAMP(i) (void)0
 #endif
+// Index checks of the diagnostic build: a data-derived index outside its
+// range is recorded (first failure per problem) and clamped to `lo`, so a
+// broken invariant shows up as a report instead of a memory fault.
+#ifdef DP_STAMPS
+#define DP_CHK(x, lo, hi, code) chk((x), (lo), (hi), (code))
+#else
+#define DP_CHK(x, lo, hi, code) (x)
+#endif
 namespace {
 
-template <bool HBM>
-struct Wave {
-  using IX = typename std::conditional<HBM, int32_t, uint16_t>::type;
+template <int MODE>
+struct Group {
+  using IX = typename std::conditional<MODE == M_LDS, uint16_t, int32_t>::type;
+  static constexpr int NW = mode_waves(MODE);  // wavefronts per problem
+  static constexpr int NT = 64 * NW;           // threads per problem
+  static constexpr int WBUF = mode_wbuf(MODE);
+  static constexpr int CQ = mode_cq(MODE);
 
   // IX <-> int for the signed values (reasons R_DEC / R_EXTRA, "none" = -1)
   __device__ __forceinline__ static int dec(IX x) {
-    if constexpr (HBM) return x;
+    if constexpr (MODE != M_LDS) return x;
     else return x >= 0xfffe ? (int)x - 0x10000 : (int)x;
   }
   __device__ __forceinline__ static IX enc(int x) { return (IX)x; }
+
+  // Words updated by global atomics (imp; in M_HBM also the used / dset / fg
+  // bitsets) are read from L2: the atomics are performed there and a plain
+  // load from another wavefront of the workgroup can hit a stale L1 line.
+  // LDS words need no such care.
+  __device__ __forceinline__ static uint32_t ld_imp(const uint32_t* p) {
+    if constexpr (MODE == M_LDS) return *p;
+    else return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __device__ __forceinline__ static uint32_t ld_bits(const uint32_t* p) {
+    if constexpr (MODE != M_HBM) return *p;
+    else return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 
   // ---- record views ----
   int nv, nc, nk, nid, nrows, nbv, nbi, na, nch;
@@ -112,7 +148,7 @@ struct Wave {
   const IX *card_off, *card_lits, *card_bound, *card_id;
   const IX *var_choice_off, *choice_off, *choice_lits, *anchors;
   const IX *w_off, *w, *base_rows;
-  int nbase;
+  int nbase, nwatch;
   // ---- working set ----
   int8_t* val;
   IX *reason, *rs, *trail, *touched, *d_lit, *d_mark, *dix, *l_off, *l_lits, *dq, *stk;
@@ -121,8 +157,8 @@ struct Wave {
   IX* wbuf;
   int32_t *cardq, *scal;
   int cap, lcap;
-  int lane;
-  // ---- wave-uniform state (registers) ----
+  int tid, lane, wid;
+  // ---- group-uniform state (registers, identical in every thread) ----
   int tlen, qhead;
   int64_t steps, budget;
   bool budget_hit;
@@ -134,44 +170,137 @@ struct Wave {
   int extra_w;
 #ifdef DP_STAMPS
   int64_t acc[5];  // round eval cycles, round finish cycles, rounds, 1-literal rounds, push+pop cycles
+  unsigned long long* dbg;  // [first code, value, bound, failures]
+  __device__ __noinline__ int chk_fail(int x, int hi, int code) {
+    if (dbg) {
+      if (atomicCAS(&dbg[0], 0ull, (unsigned long long)code) == 0ull) {
+        dbg[1] = (unsigned long long)(long long)x;
+        dbg[2] = (unsigned long long)(long long)hi;
+      }
+      atomicAdd(&dbg[3], 1ull);
+    }
+    return 0;
+  }
+  __device__ __forceinline__ int chk(int x, int lo, int hi, int code) {
+    return (x < lo || x >= hi) ? (chk_fail(x, hi, code), lo) : x;
+  }
 #define DP_ACC(i, x) acc[i] += (x)
 #else
 #define DP_ACC(i, x) (void)0
 #endif
 
   // ------------------------------------------------------------------
+  // group primitives (one wavefront: wave barrier and ballots; several:
+  // s_barrier and per-wave slots in LDS)
+  // ------------------------------------------------------------------
+  __device__ __forceinline__ void gsync() {
+    if constexpr (NW == 1) wsync();
+    else __syncthreads();
+  }
+  __device__ __forceinline__ bool g_any(bool b) {
+    const bool w = __ballot(b) != 0;
+    if constexpr (NW == 1) {
+      return w;
+    } else {
+      if (lane == 0) scal[S_SLOT + wid] = w;
+      __syncthreads();
+      int r = 0;
+#pragma unroll
+      for (int i = 0; i < NW; ++i) r |= scal[S_SLOT + i];
+      __syncthreads();
+      return r != 0;
+    }
+  }
+  __device__ __forceinline__ int g_min(int x) {
+    x = wave_min(x);
+    if constexpr (NW == 1) {
+      return x;
+    } else {
+      if (lane == 0) scal[S_SLOT + wid] = x;
+      __syncthreads();
+      int r = INF;
+#pragma unroll
+      for (int i = 0; i < NW; ++i) r = min(r, scal[S_SLOT + i]);
+      __syncthreads();
+      return r;
+    }
+  }
+  __device__ __forceinline__ int g_sum(int x) {
+    x = wave_sum(x);
+    if constexpr (NW == 1) {
+      return x;
+    } else {
+      if (lane == 0) scal[S_SLOT + wid] = x;
+      __syncthreads();
+      int r = 0;
+#pragma unroll
+      for (int i = 0; i < NW; ++i) r += scal[S_SLOT + i];
+      __syncthreads();
+      return r;
+    }
+  }
+  // Unordered append: position of a flagged thread in a list that grows by
+  // the flagged threads of every call.  One wavefront: ballot prefix on the
+  // register `run`.  Several: wave-aggregated LDS atomic on S_APP; the caller
+  // finishes with claim_end, which folds the appended count into `run`.
+  __device__ __forceinline__ int claim(bool f, int& run) {
+    const uint64_t m = __ballot(f);
+    if constexpr (NW == 1) {
+      const int at = run + __popcll(m & lanemask_lt());
+      run += __popcll(m);
+      return at;
+    } else {
+      int b = 0;
+      if (m && lane == 0) b = atomicAdd(&scal[S_APP], __popcll(m));
+      b = __shfl(b, 0);
+      return run + b + __popcll(m & lanemask_lt());
+    }
+  }
+  __device__ __forceinline__ void claim_end(int& run) {
+    if constexpr (NW > 1) {
+      __syncthreads();
+      run += scal[S_APP];
+      __syncthreads();
+      if (tid == 0) scal[S_APP] = 0;
+      __syncthreads();
+    }
+  }
+
+  // ------------------------------------------------------------------
   // set-up (oracle: st_init)
   // ------------------------------------------------------------------
-  __device__ __forceinline__ void init(char* base, const int32_t* __restrict__ grec) {
+  __device__ __forceinline__ void init(char* lds, char* hbm, const int32_t* __restrict__ grec) {
+    tid = (int)threadIdx.x;
     lane = lane_id();
+    wid = tid >> 6;
     int32_t h[DP_H_SIZE];
 #pragma unroll
     for (int i = 0; i < DP_H_SIZE; ++i) h[i] = grec[i];
-    const Layout L = layout<IX>(h);
+    const Layout L = layout<MODE>(h);
     const dp_rec_layout R = rec_layout(h);
     const ImgLayout X = img_layout(h);
     nv = h[DP_H_NV]; nc = h[DP_H_NC]; nk = h[DP_H_NK]; nid = h[DP_H_NID]; na = h[DP_H_NA];
     nch = h[DP_H_NCH];
     nrows = nc + nk;
     nbv = bits_words(nv); nbi = bits_words(nid);
-    // device image (record + host-built watch lists and base rows):
-    // HBM int32 -> working-set IX with dwordx4 loads (images are 16-byte
-    // aligned and padded to 4 words)
-    IX* body = reinterpret_cast<IX*>(base + L.body);
-    {
+    const IX* body;
+    if constexpr (MODE == M_LDS) {
+      // device image (record + host-built watch lists and base rows): HBM
+      // int32 -> LDS uint16 with dwordx4 loads (images are 16-byte aligned and
+      // padded to 4 words)
+      IX* b = reinterpret_cast<IX*>(lds + L.body);
       const int groups = (h[DP_H_IMG] - DP_H_SIZE + 3) >> 2;
       const int4* src = reinterpret_cast<const int4*>(grec + DP_H_SIZE);
-      for (int i = lane; i < groups; i += 64) {
+      for (int i = tid; i < groups; i += NT) {
         const int4 x = src[i];
-        if constexpr (HBM) {
-          reinterpret_cast<int4*>(body)[i] = x;
-        } else {
-          uint2 y;
-          y.x = (uint32_t)(x.x & 0xffff) | ((uint32_t)x.y << 16);
-          y.y = (uint32_t)(x.z & 0xffff) | ((uint32_t)x.w << 16);
-          reinterpret_cast<uint2*>(body)[i] = y;
-        }
+        uint2 y;
+        y.x = (uint32_t)(x.x & 0xffff) | ((uint32_t)x.y << 16);
+        y.y = (uint32_t)(x.z & 0xffff) | ((uint32_t)x.w << 16);
+        reinterpret_cast<uint2*>(b)[i] = y;
       }
+      body = b;
+    } else {
+      body = reinterpret_cast<const IX*>(grec + DP_H_SIZE);  // read in place (read-only)
     }
     auto rv = [&](int32_t word_off) { return body + (word_off - DP_H_SIZE); };
     clause_off = rv(R.clause_off); clause_lits = rv(R.clause_lits); clause_id = rv(R.clause_id);
@@ -180,32 +309,35 @@ struct Wave {
     choice_lits = rv(R.choice_lits); anchors = rv(R.anchors);
     w_off = rv(X.w_off); w = rv(X.w); base_rows = rv(X.base);
     nbase = h[DP_H_NBASE];
-    val = reinterpret_cast<int8_t*>(base + L.val);
-    reason = reinterpret_cast<IX*>(base + L.reason);
-    rs = reinterpret_cast<IX*>(base + L.rs);
-    trail = reinterpret_cast<IX*>(base + L.trail);
-    touched = reinterpret_cast<IX*>(base + L.touched);
-    d_lit = reinterpret_cast<IX*>(base + L.d_lit);
-    d_mark = reinterpret_cast<IX*>(base + L.d_mark);
-    dix = reinterpret_cast<IX*>(base + L.dix);
-    imp = reinterpret_cast<uint32_t*>(base + L.imp);
-    d_flip = reinterpret_cast<uint32_t*>(base + L.d_flip);
-    inS = reinterpret_cast<uint32_t*>(base + L.inS);
-    extra = reinterpret_cast<uint32_t*>(base + L.extra);
-    seen = reinterpret_cast<uint32_t*>(base + L.seen);
-    model = reinterpret_cast<uint32_t*>(base + L.model);
-    dset = reinterpret_cast<uint32_t*>(base + L.dset);
-    fg = reinterpret_cast<uint32_t*>(base + L.fg);
-    used = reinterpret_cast<uint32_t*>(base + L.used);
-    en = reinterpret_cast<uint32_t*>(base + L.en);
-    en2 = reinterpret_cast<uint32_t*>(base + L.en2);
-    l_off = reinterpret_cast<IX*>(base + L.l_off);
-    l_lits = reinterpret_cast<IX*>(base + L.l_lits);
-    dq = reinterpret_cast<IX*>(base + L.dq);
-    stk = reinterpret_cast<IX*>(base + L.stk);
-    wbuf = reinterpret_cast<IX*>(base + L.wbuf);
-    cardq = reinterpret_cast<int32_t*>(base + L.cardq);
-    scal = reinterpret_cast<int32_t*>(base + L.scal);
+    nwatch = h[DP_H_NCL] + h[DP_H_NKL];
+    char* hot = MODE == M_HBM ? hbm : lds;   // val and the bitsets
+    char* cold = MODE == M_LDS ? lds : hbm;  // per-literal arrays
+    val = reinterpret_cast<int8_t*>(hot + L.val);
+    reason = reinterpret_cast<IX*>(cold + L.reason);
+    rs = reinterpret_cast<IX*>(cold + L.rs);
+    trail = reinterpret_cast<IX*>(cold + L.trail);
+    touched = reinterpret_cast<IX*>(cold + L.touched);
+    d_lit = reinterpret_cast<IX*>(cold + L.d_lit);
+    d_mark = reinterpret_cast<IX*>(cold + L.d_mark);
+    dix = reinterpret_cast<IX*>(cold + L.dix);
+    imp = reinterpret_cast<uint32_t*>(cold + L.imp);
+    d_flip = reinterpret_cast<uint32_t*>(hot + L.d_flip);
+    inS = reinterpret_cast<uint32_t*>(hot + L.inS);
+    extra = reinterpret_cast<uint32_t*>(hot + L.extra);
+    seen = reinterpret_cast<uint32_t*>(hot + L.seen);
+    model = reinterpret_cast<uint32_t*>(hot + L.model);
+    dset = reinterpret_cast<uint32_t*>(hot + L.dset);
+    fg = reinterpret_cast<uint32_t*>(hot + L.fg);
+    used = reinterpret_cast<uint32_t*>(hot + L.used);
+    en = reinterpret_cast<uint32_t*>(hot + L.en);
+    en2 = reinterpret_cast<uint32_t*>(hot + L.en2);
+    l_off = reinterpret_cast<IX*>(cold + L.l_off);
+    l_lits = reinterpret_cast<IX*>(cold + L.l_lits);
+    dq = reinterpret_cast<IX*>(cold + L.dq);
+    stk = reinterpret_cast<IX*>(cold + L.stk);
+    wbuf = reinterpret_cast<IX*>(lds + L.wbuf);
+    cardq = reinterpret_cast<int32_t*>(lds + L.cardq);
+    scal = reinterpret_cast<int32_t*>(lds + L.scal);
     cap = L.cap; lcap = L.lcap;
     tlen = qhead = 0;
     steps = 0;
@@ -219,15 +351,21 @@ struct Wave {
     extra_w = 0;
 #ifdef DP_STAMPS
     for (int i = 0; i < 5; ++i) acc[i] = 0;
+    dbg = nullptr;
 #endif
 
-    for (int v = lane; v < nv; v += 64) val[v] = 0;
-    for (int l = lane; l < 2 * nv; l += 64) imp[l] = (uint32_t)INF;
-    for (int i = lane; i < nbv; i += 64) {
+    if constexpr (MODE == M_LDS) {
+      for (int v = tid; v < nv; v += NT) val[v] = 0;
+    } else {
+      for (int v = tid; v < (nv + 3) / 4; v += NT) reinterpret_cast<uint32_t*>(val)[v] = 0;
+    }
+    for (int l = tid; l < 2 * nv; l += NT) imp[l] = (uint32_t)INF;
+    for (int i = tid; i < nbv; i += NT) {
       d_flip[i] = 0; inS[i] = 0; extra[i] = 0; seen[i] = 0; model[i] = 0; dset[i] = 0; fg[i] = 0;
     }
-    if (lane == 0) { l_off[0] = 0; scal[S_NTOUCHED] = 0; }
-    wsync();
+    if (tid < NSCAL) scal[tid] = 0;
+    if (tid == 0) l_off[0] = 0;
+    gsync();
   }
 
   // ------------------------------------------------------------------
@@ -245,8 +383,9 @@ struct Wave {
   // record "row r implies literal l" (lowest row wins, oracle: note); the
   // first implication of a literal in the round lists it
   __device__ __forceinline__ void note(int l, int r) {
+    l = DP_CHK(l, 0, 2 * nv, 1);
     if (atomicMin(&imp[l], (uint32_t)r) == (uint32_t)INF)
-      touched[atomicAdd(&scal[S_NTOUCHED], 1)] = enc(l);
+      touched[DP_CHK(atomicAdd(&scal[S_NTOUCHED], 1), 0, 2 * nv, 2)] = enc(l);
   }
 
   // clause row evaluation; the literal loads are issued four at a time
@@ -274,7 +413,7 @@ struct Wave {
       eval_clause(r, clause_lits, clause_off[r], clause_off[r + 1], crow);
     } else if (r >= nrows) {
       const int j = r - nrows;
-      eval_clause(r, l_lits, l_off[j], l_off[j + 1], crow);
+      eval_clause(r, l_lits, DP_CHK((int)l_off[j], 0, lcap + 1, 33), DP_CHK((int)l_off[j + 1], 0, lcap + 1, 34), crow);
     } else {
       const int k = r - nc, a = card_off[k], b = card_off[k + 1];
       int cnt = 0, nun = 0;
@@ -298,28 +437,49 @@ struct Wave {
     }
   }
 
-  // A watched row reached in a round: clause rows are evaluated by the lane
+  // A watched row reached in a round: clause rows are evaluated by the thread
   // that reached them; AtMost rows are queued (ballot compaction) and later
-  // evaluated by the whole wave, one row at a time (flush_cards).  Call from
-  // converged code: every active lane passes its row (or -1).
+  // evaluated by a whole wavefront, one row at a time (flush_cards).  Call
+  // from wave-converged code: every active lane passes its row (or -1).
+  // ncq counts the queue in the one-wavefront mode (a register); with several
+  // wavefronts the queue length is the LDS counter S_NK.
   __device__ __forceinline__ void visit(int r, int& crow, int& ncq) {
     const bool ok = r >= 0 && row_on(r);
     const bool card = ok && r >= nc && r < nrows;
     uint64_t m = __ballot(card);
-    if (ncq + __popcll(m) > CQ) m = 0;  // queue full: evaluate in-lane
-    if ((m >> lane) & 1ull) cardq[ncq + __popcll(m & lanemask_lt())] = r;
-    else if (ok) eval_row(r, crow);
-    ncq += __popcll(m);
+    if constexpr (NW == 1) {
+      if (ncq + __popcll(m) > CQ) m = 0;  // queue full: evaluate in-lane
+      if ((m >> lane) & 1ull) cardq[ncq + __popcll(m & lanemask_lt())] = r;
+      else if (ok) eval_row(r, crow);
+      ncq += __popcll(m);
+    } else {
+      int pos = CQ;
+      if (m) {
+        int b = 0;
+        if (lane == 0) b = atomicAdd(&scal[S_NK], __popcll(m));
+        pos = __shfl(b, 0) + __popcll(m & lanemask_lt());
+      }
+      if (card && pos < CQ) cardq[pos] = r;
+      else if (ok) eval_row(r, crow);  // queue full: evaluate in-lane
+    }
   }
 
-  // AtMost rows, one at a time, lanes over positions (oracle: eval_row):
-  // counts by ballot; a variable listed m times is a run of m positions,
-  // forced false when the count plus m exceeds the bound.
+  // AtMost rows, one at a time per wavefront, lanes over positions (oracle:
+  // eval_row): counts by ballot; a variable listed m times is a run of m
+  // positions, forced false when the count plus m exceeds the bound.
   __device__ __forceinline__ void flush_cards(int& crow, int ncq) {
-    if (ncq == 0) return;
-    wsync();
-    for (int q = 0; q < ncq; ++q) {
-      const int r = cardq[q], k = r - nc;
+    int q0, qs;
+    if constexpr (NW == 1) {
+      if (ncq == 0) return;
+      wsync();
+      q0 = 0; qs = 1;
+    } else {
+      __syncthreads();
+      ncq = min(scal[S_NK], CQ);
+      q0 = wid; qs = NW;
+    }
+    for (int q = q0; q < ncq; q += qs) {
+      const int r = DP_CHK(cardq[q], nc, nrows, 3), k = r - nc;
       const int a = card_off[k], len = (int)card_off[k + 1] - a, bound = card_bound[k];
       if (len > 64) {  // long rows: one lane
         if (lane == 0) eval_row(r, crow);
@@ -338,16 +498,18 @@ struct Wave {
     }
   }
 
-  // learned rows are evaluated in every round (lanes over rows)
+  // learned rows are evaluated in every round (threads over rows)
   __device__ __forceinline__ void eval_learned(int& crow) {
     if (!learn_on) return;
-    for (int j = lane; j < nl; j += 64) eval_row(nrows + j, crow);
+    for (int j = tid; j < nl; j += NT) eval_row(nrows + j, crow);
   }
 
   __device__ __forceinline__ void clear_touched(int nt) {
-    for (int i = lane; i < nt; i += 64) imp[(int)touched[i]] = (uint32_t)INF;
-    if (lane == 0) scal[S_NTOUCHED] = 0;
-    wsync();
+    if constexpr (NW > 1) __syncthreads();  // every read of imp in this round is done
+    for (int i = tid; i < nt; i += NT) imp[(int)touched[i]] = (uint32_t)INF;
+    gsync();
+    if (tid == 0) scal[S_NTOUCHED] = 0;
+    gsync();
   }
 
   __device__ __forceinline__ void commit(int l, int r, int start, int i) {
@@ -356,81 +518,89 @@ struct Wave {
     reason[v] = enc(r);
     rs[v] = enc(start);
     dix[v] = enc(-1);
-    trail[start + i] = enc(l);
+    trail[DP_CHK(start + i, 0, nv, 9)] = enc(l);
     imp[l] = (uint32_t)INF;
   }
 
   // Commit the implications of the round, or report its conflict: the lowest
   // conflicting row, else the lowest variable implied both ways.
   __device__ __forceinline__ int finish_round(int crow) {
-    wsync();
-    const int nt = scal[S_NTOUCHED];
-    if (__ballot(crow != INF)) {
-      c_row = wave_min(crow);
+    gsync();
+    const int nt = DP_CHK(scal[S_NTOUCHED], 0, 2 * nv + 1, 4);
+    if constexpr (NW > 1) {
+      if (tid == 0) scal[S_NK] = 0;  // the AtMost queue was flushed
+    }
+    if (g_any(crow != INF)) {
+      c_row = g_min(crow);
       clear_touched(nt);
       ck = CK_ROW;
       return -1;
     }
     const int start = tlen;
-    if (nt <= 64) {  // one literal per lane: a single pass
-      const int l = lane < nt ? (int)touched[lane] : 0;
-      const uint32_t r = lane < nt ? imp[l] : 0u, rn = lane < nt ? imp[l ^ 1] : (uint32_t)INF;
+    if (nt <= NT) {  // one literal per thread: a single pass
+      const int l = tid < nt ? DP_CHK((int)touched[tid], 0, 2 * nv, 5) : 0;
+      const uint32_t r = tid < nt ? (uint32_t)DP_CHK((int)ld_imp(&imp[l]), 0, nrows + nl, 6) : 0u,
+                     rn = tid < nt ? ld_imp(&imp[l ^ 1]) : (uint32_t)INF;
       const int cv = rn != (uint32_t)INF ? (l >> 1) : INF;
-      if (__ballot(cv != INF)) {
-        c_var = wave_min(cv);
-        c_rp = (int)imp[2 * c_var]; c_rn = (int)imp[2 * c_var + 1];
+      if (g_any(cv != INF)) {
+        c_var = g_min(cv);
+        c_rp = (int)ld_imp(&imp[2 * c_var]); c_rn = (int)ld_imp(&imp[2 * c_var + 1]);
         ck = CK_VAR; c_row = tlen;  // bound: every variable assigned so far
         clear_touched(nt);
         return -1;
       }
-      if (lane < nt) commit(l, (int)r, start, lane);
+      if (tid < nt) commit(l, (int)r, start, tid);
     } else {
       int cv = INF;
-      for (int i = lane; i < nt; i += 64) {
+      for (int i = tid; i < nt; i += NT) {
         const int l = touched[i];
-        if (imp[l ^ 1] != (uint32_t)INF) cv = min(cv, l >> 1);
+        if (ld_imp(&imp[l ^ 1]) != (uint32_t)INF) cv = min(cv, l >> 1);
       }
-      if (__ballot(cv != INF)) {
-        c_var = wave_min(cv);
-        c_rp = (int)imp[2 * c_var]; c_rn = (int)imp[2 * c_var + 1];
+      if (g_any(cv != INF)) {
+        c_var = g_min(cv);
+        c_rp = (int)ld_imp(&imp[2 * c_var]); c_rn = (int)ld_imp(&imp[2 * c_var + 1]);
         ck = CK_VAR; c_row = tlen;
         clear_touched(nt);
         return -1;
       }
-      for (int i = lane; i < nt; i += 64) {
-        const int l = touched[i];
-        commit(l, (int)imp[l], start, i);
+      for (int i = tid; i < nt; i += NT) {
+        const int l = DP_CHK((int)touched[i], 0, 2 * nv, 7);
+        commit(l, DP_CHK((int)ld_imp(&imp[l]), 0, nrows + nl, 8), start, i);
       }
     }
-    if (lane == 0) scal[S_NTOUCHED] = 0;
+    if (tid == 0) scal[S_NTOUCHED] = 0;
     tlen += nt;
-    wsync();
+    gsync();
     return 0;
   }
 
   __device__ __forceinline__ int extra_check() {
     int cnt = 0, nun = 0;
-    for (int b = 0; b < nv; b += 64) {
-      const int v = b + lane;
+    for (int b = 0; b < nv; b += NT) {
+      const int v = b + tid;
       const bool ex = v < nv && getb(extra, v);
       const int x = ex ? val[v] : 0;
-      cnt += __popcll(__ballot(ex && x > 0));
-      nun += __popcll(__ballot(ex && x == 0));
+      cnt += ex && x > 0;
+      nun += ex && x == 0;
     }
+    cnt = g_sum(cnt);
+    nun = g_sum(nun);
     if (cnt > extra_w) { ck = CK_EXTRA; return -1; }
     if (cnt == extra_w && nun > 0) {
       const int start = tlen;
-      for (int b = 0; b < nv; b += 64) {
-        const int v = b + lane;
+      int run = tlen;
+      for (int b = 0; b < nv; b += NT) {
+        const int v = b + tid;
         const bool f = v < nv && getb(extra, v) && val[v] == 0;
-        const uint64_t m = __ballot(f);
+        const int at = claim(f, run);
         if (f) {
           val[v] = -1; reason[v] = enc(R_EXTRA); rs[v] = enc(start); dix[v] = enc(-1);
-          trail[tlen + __popcll(m & lanemask_lt())] = enc(2 * v + 1);
+          trail[DP_CHK(at, 0, nv, 28)] = enc(2 * v + 1);
         }
-        tlen += __popcll(m);
       }
-      wsync();
+      claim_end(run);
+      tlen = run;
+      gsync();
       return 1;
     }
     return 0;
@@ -455,36 +625,51 @@ struct Wave {
       DP_ACC(3, hi - lo == 1);
 #endif
       int ncq = 0;
-      if (hi - lo == 1) {  // one new literal: lanes over its watch list
-        const int l = trail[lo];
+      if (hi - lo == 1) {  // one new literal: threads over its watch list
+        const int l = DP_CHK((int)trail[lo], 0, 2 * nv, 10);
         const int a = w_off[l], e = w_off[l + 1];
-        for (int k0 = a; k0 < e; k0 += 64) visit(k0 + lane < e ? (int)w[k0 + lane] : -1, crow, ncq);
-      } else
-      for (int b = lo; b < hi; b += 64) {
-        const int i = b + lane;
-        int cnt = 0, a = 0;
-        if (i < hi) {
-          const int l = trail[i];
-          a = w_off[l];
-          cnt = (int)w_off[l + 1] - a;
-        }
-        const int incl = wave_incl_scan(cnt);
-        const int total = __builtin_amdgcn_readlane(incl, 63);
-        if (total <= WBUF) {
-          // flatten: every frontier literal writes its watch range into the list
-          for (int k = 0, at = incl - cnt; k < cnt; ++k) wbuf[at + k] = enc(a + k);
-          wsync();
-          for (int t0 = 0; t0 < total; t0 += 64)
-            visit(t0 + lane < total ? (int)w[wbuf[t0 + lane]] : -1, crow, ncq);
-          wsync();
-        } else {
-          // a very large chunk: one frontier literal at a time
-          const int n = min(64, hi - b);
-          for (int e = 0; e < n; ++e) {
-            const int l = trail[b + e];
-            const int a2 = w_off[l], e2 = w_off[l + 1];
-            for (int k0 = a2; k0 < e2; k0 += 64)
-              visit(k0 + lane < e2 ? (int)w[k0 + lane] : -1, crow, ncq);
+        for (int k0 = a; k0 < e; k0 += NT) visit(k0 + tid < e ? (int)w[k0 + tid] : -1, crow, ncq);
+      } else {
+        for (int b = lo; b < hi; b += NT) {
+          const int i = b + tid;
+          int cnt = 0, a = 0;
+          if (i < hi) {
+            const int l = DP_CHK((int)trail[i], 0, 2 * nv, 11);
+            a = w_off[l];
+            cnt = (int)w_off[l + 1] - a;
+          }
+          // flatten: a group-wide prefix sum of the watch-range lengths
+          const int incl = wave_incl_scan(cnt);
+          int total = __builtin_amdgcn_readlane(incl, 63), before = 0;
+          if constexpr (NW > 1) {
+            if (lane == 63) scal[S_SLOT + wid] = incl;
+            __syncthreads();
+            total = 0;
+#pragma unroll
+            for (int q = 0; q < NW; ++q) {
+              const int c = scal[S_SLOT + q];
+              before += q < wid ? c : 0;
+              total += c;
+            }
+            __syncthreads();
+          }
+          if (total <= WBUF) {
+            // every frontier literal writes its watch range into the list
+            for (int k = 0, at = before + incl - cnt; k < cnt; ++k) wbuf[at + k] = enc(a + k);
+            gsync();
+            for (int t0 = 0; t0 < total; t0 += NT)
+              visit(t0 + tid < total ? DP_CHK((int)w[DP_CHK((int)wbuf[t0 + tid], 0, nwatch, 12)], 0, nrows, 13) : -1,
+                    crow, ncq);
+            gsync();
+          } else {
+            // a very large chunk: one frontier literal at a time
+            const int n = min(NT, hi - b);
+            for (int e = 0; e < n; ++e) {
+              const int l = trail[b + e];
+              const int a2 = w_off[l], e2 = w_off[l + 1];
+              for (int k0 = a2; k0 < e2; k0 += NT)
+                visit(k0 + tid < e2 ? (int)w[k0 + tid] : -1, crow, ncq);
+            }
           }
         }
       }
@@ -507,7 +692,7 @@ struct Wave {
   // on the empty assignment only the rows of the base list can fire.
   __device__ __forceinline__ int base_propagate() {
     int crow = INF, ncq = 0;
-    for (int i0 = 0; i0 < nbase; i0 += 64) visit(i0 + lane < nbase ? (int)base_rows[i0 + lane] : -1, crow, ncq);
+    for (int i0 = 0; i0 < nbase; i0 += NT) visit(i0 + tid < nbase ? (int)base_rows[i0 + tid] : -1, crow, ncq);
     flush_cards(crow, ncq);
     eval_learned(crow);
     if (finish_round(crow) < 0) return -1;
@@ -515,9 +700,10 @@ struct Wave {
   }
 
   __device__ __forceinline__ void truncate_to(int mark) {
-    for (int i = mark + lane; i < tlen; i += 64) val[(int)trail[i] >> 1] = 0;
+    gsync();
+    for (int i = mark + tid; i < tlen; i += NT) val[DP_CHK((int)trail[i], 0, 2 * nv, 14) >> 1] = 0;
     tlen = qhead = mark;
-    wsync();
+    gsync();
   }
 
   // gini Untest() (search.go:84): the learned rows decide the restored scope
@@ -533,13 +719,13 @@ struct Wave {
   }
 
   __device__ __forceinline__ void assign_one(int l, int why, int decision) {
-    if (lane == 0) {
-      const int v = l >> 1;
+    if (tid == 0) {
+      const int v = DP_CHK(l, 0, 2 * nv, 30) >> 1;
       val[v] = (l & 1) ? -1 : 1; reason[v] = enc(why); rs[v] = enc(tlen);
-      dix[v] = enc(decision); trail[tlen] = enc(l);
+      dix[v] = enc(decision); trail[DP_CHK(tlen, 0, nv, 31)] = enc(l);
     }
     ++tlen;
-    wsync();
+    gsync();
   }
 
   // gini Assume(m) + Test() (search.go:75-76)
@@ -563,13 +749,18 @@ struct Wave {
   __device__ __forceinline__ void set_bit_atomic(uint32_t* b, int i) { atomicOr(&b[i >> 5], 1u << (i & 31)); }
 
   // antecedents of row r for variable u, whose round started at trail
-  // position bound (serial in the calling lane)
+  // position bound (serial in the calling thread)
   __device__ __forceinline__ void ante_serial(int r, int u, int bound) {
+    r = DP_CHK(r, 0, nrows + nl, 15);
     if (r < nc || r >= nrows) {
       const IX* lits = clause_lits;
       int a, b;
       if (r < nc) { a = clause_off[r]; b = clause_off[r + 1]; set_bit_atomic(used, clause_id[r]); }
-      else { lits = l_lits; a = l_off[r - nrows]; b = l_off[r - nrows + 1]; }
+      else {
+        lits = l_lits;
+        a = DP_CHK((int)l_off[r - nrows], 0, lcap + 1, 35);
+        b = DP_CHK((int)l_off[r - nrows + 1], 0, lcap + 1, 36);
+      }
       for (int j = a; j < b; ++j) {
         const int v = (int)lits[j] >> 1;
         if (v != u) mark_push(v);
@@ -583,41 +774,43 @@ struct Wave {
       }
     }
   }
+  // the epilogue bound's antecedents (true extras assigned before bound)
   __device__ __forceinline__ void extra_serial(int u, int bound) {
     for (int v = 0; v < nv; ++v)
       if (v != u && getb(extra, v) && val[v] > 0 && (int)rs[v] < bound) mark_push(v);
   }
 
   __device__ __forceinline__ void analyze() {
-    if (lane == 0) scal[S_NWORK] = 0;
-    wsync();
-    if (lane == 0) {
+    gsync();
+    if (tid == 0) {
+      scal[S_NWORK] = 0;
       if (ck == CK_ROW) ante_serial(c_row, -1, INF);
       else if (ck == CK_VAR) { ante_serial(c_rp, c_var, c_row); ante_serial(c_rn, c_var, c_row); }
       else if (ck == CK_EXTRA) extra_serial(-1, INF);
     }
-    wsync();
+    gsync();
     int head = 0;
     for (;;) {
       const int nw = scal[S_NWORK];
+      if constexpr (NW > 1) __syncthreads();  // every thread read nw before any grows it
       if (head >= nw) break;
-      for (int i = head + lane; i < nw; i += 64) {
-        const int u = touched[i];
+      for (int i = head + tid; i < nw; i += NT) {
+        const int u = DP_CHK((int)touched[i], 0, nv, 16);
         const int r = dec(reason[u]);
         if (r >= 0) ante_serial(r, u, rs[u]);
         else if (r == R_EXTRA) extra_serial(u, rs[u]);
-        else if (dec(dix[u]) >= 0) set_bit_atomic(dset, dix[u]);
+        else if (dec(dix[u]) >= 0) set_bit_atomic(dset, DP_CHK((int)dix[u], 0, nv, 32));
         else if (collect_guess && getb(inS, u)) set_bit_atomic(fg, u);
       }
       head = nw;
-      wsync();
+      gsync();
     }
     const int nw = scal[S_NWORK];
-    for (int i = lane; i < nw; i += 64) {
+    for (int i = tid; i < nw; i += NT) {
       const int v = touched[i];
       atomicAnd(&seen[v >> 5], ~(1u << (v & 31)));
     }
-    wsync();
+    gsync();
   }
 
   // ------------------------------------------------------------------
@@ -645,11 +838,11 @@ struct Wave {
   // unassigned positive literal (the decision), or -1.  Such a row has a
   // positive literal but no true one, and every negative literal on a true
   // variable, so it is in the watch list of some true positive literal:
-  // lanes scan the watch lists of the variables assigned true instead of
+  // threads scan the watch lists of the variables assigned true instead of
   // every clause row (same answer as the oracle's full scan).
   __device__ __forceinline__ int first_violated() {
     int best = INF;
-    for (int i = lane; i < tlen; i += 64) {
+    for (int i = tid; i < tlen; i += NT) {
       const int l = trail[i];
       if (l & 1) continue;  // only variables assigned true own violations
       for (int k = w_off[l]; k < (int)w_off[l + 1]; ++k) {
@@ -658,28 +851,29 @@ struct Wave {
         if (c < nc && c < best && row_on(c) && violated(c, fu)) best = c;
       }
     }
-    if (!__ballot(best != INF)) return -1;
-    best = wave_min(best);
+    best = g_min(best);
+    if (best == INF) return -1;
     int fu;
     violated(best, fu);
     return fu;
   }
 
   __device__ __forceinline__ void save_model() {
-    for (int b = 0; b < nv; b += 64) {
-      const int v = b + lane;
+    for (int b = 0; b < nv; b += NT) {
+      const int v = b + tid;
       const uint64_t m = __ballot(v < nv && val[v] > 0);
-      if (lane == 0) {
-        model[b >> 5] = (uint32_t)m;
-        if ((b >> 5) + 1 < nbv) model[(b >> 5) + 1] = (uint32_t)(m >> 32);
+      const int wd = (b + 64 * wid) >> 5;
+      if (lane == 0 && wd < nbv) {
+        model[wd] = (uint32_t)m;
+        if (wd + 1 < nbv) model[wd + 1] = (uint32_t)(m >> 32);
       }
     }
-    wsync();
+    gsync();
   }
 
   __device__ __forceinline__ void clear_bits(uint32_t* bs, int n) {
-    for (int i = lane; i < bits_words(n); i += 64) bs[i] = 0;
-    wsync();
+    for (int i = tid; i < bits_words(n); i += NT) bs[i] = 0;
+    gsync();
   }
 
   __device__ __forceinline__ int dpll() {
@@ -691,7 +885,7 @@ struct Wave {
         const int l = first_violated();
         if (l < 0) { save_model(); r = RS_SAT; break; }
         if (++steps > budget) { budget_hit = true; r = RS_BUDGET; break; }
-        if (lane == 0) {
+        if (tid == 0) {
           d_lit[nd] = enc(l); d_mark[nd] = enc(tlen);
           d_flip[nd >> 5] &= ~(1u << (nd & 31));
         }
@@ -706,39 +900,39 @@ struct Wave {
       // h = highest decision reached, b = the next one below (or -1)
       int h = -1, b = -1, n = 0;
       for (int wi = bits_words(nd) - 1; wi >= 0 && b < 0; --wi) {
-        uint32_t x = dset[wi];
+        uint32_t x = ld_bits(&dset[wi]);
         while (x && b < 0) {
           const int i = wi * 32 + 31 - __clz(x);
           x &= ~(1u << (i & 31));
           if (h < 0) h = i; else b = i;
         }
       }
-      for (int wi = 0; wi < bits_words(nd); ++wi) n += __popc(dset[wi]);
+      for (int wi = 0; wi < bits_words(nd); ++wi) n += __popc(ld_bits(&dset[wi]));
       if (h < 0) { r = RS_UNSAT; break; }
       if (++steps > budget) { budget_hit = true; r = RS_BUDGET; break; }
-      const int lat = l_off[nl];
+      const int lat = DP_CHK((int)l_off[nl], 0, lcap + 1, 26);
       if (nl < L_MAX && lat + n <= lcap) {
-        // learned row: negated decisions, ascending decision index
-        int at = lat;
-        for (int base = 0; base < nd; base += 64) {
-          const int i = base + lane;
-          const bool in = i < nd && getb(dset, i);
-          const uint64_t m = __ballot(in);
-          if (in) l_lits[at + __popcll(m & lanemask_lt())] = enc((int)d_lit[i] ^ 1);
-          at += __popcll(m);
+        // learned row: the negated decisions it met
+        int run = lat;
+        for (int base = 0; base < nd; base += NT) {
+          const int i = base + tid;
+          const bool in = i < nd && ((ld_bits(&dset[i >> 5]) >> (i & 31)) & 1u);
+          const int at = claim(in, run);
+          if (in) l_lits[DP_CHK(at, 0, lcap, 27)] = enc((int)d_lit[i] ^ 1);
         }
-        if (lane == 0) l_off[nl + 1] = enc(at);
+        claim_end(run);
+        if (tid == 0) l_off[nl + 1] = enc(run);
         ++nl;
-        wsync();
+        gsync();
         nd = b + 1;
-        truncate_to(d_mark[nd]);
+        truncate_to(DP_CHK((int)d_mark[nd], 0, nv + 1, 24));
         assign_one((int)d_lit[h] ^ 1, nrows + nl - 1, -1);
       } else {
         while (nd > 0 && getb(d_flip, nd - 1)) --nd;
         if (nd == 0) { r = RS_UNSAT; break; }
-        truncate_to(d_mark[nd - 1]);
-        if (lane == 0) d_flip[(nd - 1) >> 5] |= 1u << ((nd - 1) & 31);
-        wsync();
+        truncate_to(DP_CHK((int)d_mark[nd - 1], 0, nv + 1, 25));
+        if (tid == 0) d_flip[(nd - 1) >> 5] |= 1u << ((nd - 1) & 31);
+        gsync();
         assign_one((int)d_lit[nd - 1] ^ 1, R_DEC, nd - 1);
       }
     }
@@ -762,26 +956,26 @@ struct Wave {
   }
   __device__ __forceinline__ void dq_push_back(int list, int idx) {
     const int at = (dq_head + dq_n) % cap;
-    if (lane == 0) { dq[2 * at] = enc(list); dq[2 * at + 1] = enc(idx); }
+    if (tid == 0) { dq[2 * at] = enc(list); dq[2 * at + 1] = enc(idx); }
     ++dq_n;
   }
   __device__ __forceinline__ void dq_push_front(int list, int idx) {
     dq_head = (dq_head + cap - 1) % cap;
-    if (lane == 0) { dq[2 * dq_head] = enc(list); dq[2 * dq_head + 1] = enc(idx); }
+    if (tid == 0) { dq[2 * dq_head] = enc(list); dq[2 * dq_head + 1] = enc(idx); }
     ++dq_n;
   }
 
   // PushGuess, search.go:34-77
   __device__ __forceinline__ void push_guess() {
-    wsync();
-    const int list = dq[2 * dq_head], idx = dq[2 * dq_head + 1];
+    gsync();
+    const int list = DP_CHK((int)dq[2 * dq_head], 0, nch + nv, 17), idx = DP_CHK((int)dq[2 * dq_head + 1], 0, nv + 1, 18);
     dq_head = (dq_head + 1) % cap;
     --dq_n;
     const int len = list_len(list);
     int m = idx < len ? list_at(list, idx) : -1;
     bool any = false;
-    for (int i = lane; i < len; i += 64) any |= getb(inS, list_at(list, i));
-    if (__ballot(any)) m = -1;
+    for (int i = tid; i < len; i += NT) any |= getb(inS, list_at(list, i));
+    if (g_any(any)) m = -1;
     else if (idx >= len) class_b = true;  // exhausted choice
     int children = 0;
     if (m >= 0)
@@ -789,13 +983,13 @@ struct Wave {
         dq_push_back(r, 0);
         ++children;
       }
-    if (lane == 0) {
+    if (tid == 0) {
       IX* g = stk + 5 * ng;
       g[0] = enc(list); g[1] = enc(idx); g[2] = enc(m); g[3] = enc(children); g[4] = enc(tlen);
       if (m >= 0) inS[m >> 5] |= 1u << (m & 31);
     }
     ++ng;
-    wsync();
+    gsync();
     if (m < 0) return;
     if (steps >= budget) { budget_hit = true; result = 0; return; }
     result = test_assume(2 * m);
@@ -804,20 +998,22 @@ struct Wave {
 
   // PopGuess, search.go:79-98
   __device__ __forceinline__ void pop_guess() {
-    wsync();
+    gsync();
     --ng;
     const IX* g = stk + 5 * ng;
-    const int list = g[0], idx = g[1], m = dec(g[2]), children = g[3], mark = g[4];
-    wsync();
+    const int list = DP_CHK((int)g[0], 0, nch + nv, 19), idx = DP_CHK((int)g[1], 0, nv + 1, 20),
+              m = DP_CHK(dec(g[2]), -1, nv, 21), children = DP_CHK((int)g[3], 0, cap, 22),
+              mark = DP_CHK((int)g[4], 0, nv + 1, 23);
+    gsync();
     if (m >= 0) {
-      if (lane == 0) inS[m >> 5] &= ~(1u << (m & 31));
-      wsync();
+      if (tid == 0) inS[m >> 5] &= ~(1u << (m & 31));
+      gsync();
       result = untest_to(mark);
       last_solve = false;
     }
     dq_n -= children;
     dq_push_front(list, idx + (m >= 0 ? 1 : 0));
-    wsync();
+    gsync();
   }
 
   // Solve() within the search: a failure learns the nogood of the guesses its
@@ -829,20 +1025,21 @@ struct Wave {
     collect_guess = false;
     if (r == RS_UNSAT) {
       int n = 0;
-      for (int wi = 0; wi < nbv; ++wi) n += __popc(fg[wi]);
+      for (int wi = tid; wi < nbv; wi += NT) n += __popc(ld_bits(&fg[wi]));
+      n = g_sum(n);
       const int lat = l_off[nl];
       if (nl < L_MAX && lat + n <= lcap) {
-        int at = lat;
-        for (int b = 0; b < nv; b += 64) {
-          const int v = b + lane;
-          const bool in = v < nv && getb(fg, v);
-          const uint64_t m = __ballot(in);
-          if (in) l_lits[at + __popcll(m & lanemask_lt())] = enc(2 * v + 1);
-          at += __popcll(m);
+        int run = lat;
+        for (int b = 0; b < nv; b += NT) {
+          const int v = b + tid;
+          const bool in = v < nv && ((ld_bits(&fg[v >> 5]) >> (v & 31)) & 1u);
+          const int at = claim(in, run);
+          if (in) l_lits[at] = enc(2 * v + 1);
         }
-        if (lane == 0) l_off[nl + 1] = enc(at);
+        claim_end(run);
+        if (tid == 0) l_off[nl + 1] = enc(run);
         ++nl;
-        wsync();
+        gsync();
       }
     }
     return r;
@@ -854,7 +1051,7 @@ struct Wave {
     result = 0;
     class_b = solve_unsat = last_solve = false;
     for (int i = 0; i < na; ++i) dq_push_back(nch + (int)anchors[i], 0);
-    wsync();
+    gsync();
     for (;;) {
       if (dq_n == 0 && result == 0) {
         const int r = search_solve();
@@ -890,16 +1087,16 @@ struct Wave {
 
   __device__ __forceinline__ void fill_bits(uint32_t* bs, int n, bool ones) {
     const int nw = bits_words(n);
-    for (int i = lane; i < nw; i += 64) {
+    for (int i = tid; i < nw; i += NT) {
       uint32_t x = 0;
       if (ones) x = (i == nw - 1 && (n & 31)) ? ((1u << (n & 31)) - 1u) : 0xffffffffu;
       bs[i] = x;
     }
-    wsync();
+    gsync();
   }
   __device__ __forceinline__ void copy_bits(uint32_t* dst, const uint32_t* src, int n) {
-    for (int i = lane; i < bits_words(n); i += 64) dst[i] = src[i];
-    wsync();
+    for (int i = tid; i < bits_words(n); i += NT) dst[i] = ld_bits(&src[i]);
+    gsync();
   }
 
   __device__ __forceinline__ int refute(const uint32_t* K) {
@@ -925,20 +1122,36 @@ struct Wave {
     if (r == RS_UNSAT) {
       copy_bits(en, used, nid);
       for (int id = 0; id < nid; ++id) {
+        if ((id & 31) == 0 && en[id >> 5] == 0) { id += 31; continue; }  // empty word
         if (!getb(en, id)) continue;
         copy_bits(en2, en, nid);
-        if (lane == 0) en2[id >> 5] &= ~(1u << (id & 31));
-        wsync();
+        if (tid == 0) en2[id >> 5] &= ~(1u << (id & 31));
+        gsync();
         r = refute(en2);
         if (r == RS_UNSAT) copy_bits(en, used, nid);
         else if (r == RS_BUDGET) { flags |= DP_F_CORE_BUDGET; break; }
       }
-      for (int b = 0; b < nid; b += 64) {  // ascending identity ids
-        const int id = b + lane;
-        const bool in = id < nid && getb(en, id);
-        const uint64_t m = __ballot(in);
-        if (in) out[len + __popcll(m & lanemask_lt())] = id;
-        len += __popcll(m);
+      // ascending identity ids: the kept bits of each word, in word order
+      for (int b = 0; b < nbi; b += NT) {
+        const int i = b + tid;
+        const uint32_t x = i < nbi ? en[i] : 0u;
+        const int c = __popc(x);
+        const int incl = wave_incl_scan(c);
+        int before = incl - c, total = __builtin_amdgcn_readlane(incl, 63);
+        if constexpr (NW > 1) {
+          if (lane == 63) scal[S_SLOT + wid] = incl;
+          __syncthreads();
+          total = 0;
+#pragma unroll
+          for (int q = 0; q < NW; ++q) {
+            const int s = scal[S_SLOT + q];
+            before += q < wid ? s : 0;
+            total += s;
+          }
+          __syncthreads();
+        }
+        for (uint32_t y = x; y; y &= y - 1) out[len + before++] = 32 * i + __ffs(y) - 1;
+        len += total;
       }
     } else {
       flags |= DP_F_CORE_BUDGET;
@@ -952,12 +1165,15 @@ struct Wave {
   // SAT epilogue, solve.go:86-110 (oracle: epilogue)
   // ------------------------------------------------------------------
   __device__ __forceinline__ int epilogue(int32_t& flags, uint32_t* __restrict__ out) {
-    for (int i = lane; i < nbv; i += 64) extra[i] = model[i] & ~inS[i];
-    wsync();
     int ne = 0;
-    for (int i = 0; i < nbv; ++i) ne += __popc(extra[i]);
+    for (int i = tid; i < nbv; i += NT) {
+      const uint32_t x = model[i] & ~inS[i];
+      extra[i] = x;
+      ne += __popc(x);
+    }
+    ne = g_sum(ne);
     if (ne == 0) {
-      for (int i = lane; i < nbv; i += 64) out[i] = inS[i];
+      for (int i = tid; i < nbv; i += NT) out[i] = inS[i];
       return DP_SAT;
     }
     flags |= DP_F_EPILOGUE;
@@ -965,8 +1181,9 @@ struct Wave {
     if (base_propagate() < 0) return DP_ERROR;
     const int start = tlen;
     bool bad = false;
-    for (int b = 0; b < nv; b += 64) {
-      const int v = b + lane;
+    int run = tlen;
+    for (int b = 0; b < nv; b += NT) {
+      const int v = b + tid;
       bool f = false;
       int l = 0;
       if (v < nv && !getb(extra, v)) {
@@ -974,22 +1191,21 @@ struct Wave {
         if (val[v] == -want) bad = true;
         if (val[v] == 0) { f = true; l = 2 * v + (want < 0 ? 1 : 0); }
       }
-      const uint64_t m = __ballot(f);
+      const int at = claim(f, run);
       if (f) {
         val[v] = (l & 1) ? -1 : 1; reason[v] = enc(R_DEC); rs[v] = enc(start); dix[v] = enc(-1);
-        trail[tlen + __popcll(m & lanemask_lt())] = enc(l);
+        trail[DP_CHK(at, 0, nv, 29)] = enc(l);
       }
-      tlen += __popcll(m);
     }
-    wsync();
-    if (__ballot(bad)) return DP_ERROR;
+    claim_end(run);
+    tlen = run;
+    gsync();
+    if (g_any(bad)) return DP_ERROR;
     if (propagate() < 0) return DP_ERROR;
     const int mark = tlen;
     int f = 0;
-    for (int b = 0; b < nv; b += 64) {
-      const int v = b + lane;
-      f += __popcll(__ballot(v < nv && getb(extra, v) && val[v] > 0));
-    }
+    for (int v = tid; v < nv; v += NT) f += getb(extra, v) && val[v] > 0;
+    f = g_sum(f);
     extra_mode = true;
     for (int wv = f; wv <= ne; ++wv) {
       truncate_to(mark);
@@ -998,7 +1214,7 @@ struct Wave {
       const int r = dpll();
       if (r == RS_SAT) {
         extra_mode = false;
-        for (int i = lane; i < nbv; i += 64) out[i] = model[i];
+        for (int i = tid; i < nbv; i += NT) out[i] = model[i];
         return DP_SAT;
       }
       if (r == RS_BUDGET) { extra_mode = false; return DP_INCOMPLETE; }
@@ -1010,30 +1226,30 @@ struct Wave {
 
 }  // namespace
 
-// One wavefront per problem; blockIdx.x indexes `order` (problems bucketed by
-// working-set footprint; the HBM instantiation works in HBM scratch).
+// One problem per workgroup; blockIdx.x indexes `order` (problems bucketed by
+// working-set footprint; the multi-wave modes work partly in HBM scratch).
 // Outputs: status / flags / installed / core / steps (oracle_solve).
-
-template <bool HBM>
-__global__ void __launch_bounds__(64) solve_kernel(KernelArgs a) {
+template <int MODE>
+__global__ void __launch_bounds__(64 * mode_waves(MODE)) solve_kernel(KernelArgs a) {
   extern __shared__ int4 lds4[];
 #ifdef DP_STAMPS
   int64_t t[6];
-#endif
-#ifdef DP_STAMPS
   const int64_t wall0 = wallclock();
 #endif
   DP_STAMP(0);
   const int pid = a.order[blockIdx.x];
   const int32_t* grec = a.rec + a.rec_off[pid];
-  Wave<HBM> W;
-  if constexpr (HBM) W.init(reinterpret_cast<char*>(a.scratch + a.scratch_off[blockIdx.x]), grec);
-  else W.init(reinterpret_cast<char*>(lds4), grec);
+  Group<MODE> W;
+  char* hbm = MODE == M_LDS ? nullptr : reinterpret_cast<char*>(a.scratch + a.scratch_off[blockIdx.x]);
+  W.init(reinterpret_cast<char*>(lds4), hbm, grec);
+#ifdef DP_STAMPS
+  if (a.stamps) W.dbg = reinterpret_cast<unsigned long long*>(a.stamps + (int64_t)DP_NSTAMP * pid + 12);
+#endif
   W.budget = a.budget;
   uint32_t* inst = a.installed + a.inst_off[pid];
   int32_t flags = 0;
   int status;
-  for (int i = W.lane; i < W.nbv; i += 64) inst[i] = 0;
+  for (int i = W.tid; i < W.nbv; i += Group<MODE>::NT) inst[i] = 0;
   DP_STAMP(1);
   const int base = W.base_propagate();
   DP_STAMP(2);
@@ -1065,7 +1281,7 @@ __global__ void __launch_bounds__(64) solve_kernel(KernelArgs a) {
   if (status == DP_UNSAT) clen = W.core(a.core + a.core_off[pid], flags);
   DP_STAMP(5);
 #ifdef DP_STAMPS
-  if (W.lane == 0 && a.stamps) {
+  if (W.tid == 0 && a.stamps) {
     int64_t* o = a.stamps + (int64_t)DP_NSTAMP * pid;
     for (int i = 0; i < 5; ++i) o[i] = t[i + 1] - t[i];
     for (int i = 0; i < 5; ++i) o[5 + i] = W.acc[i];
@@ -1073,7 +1289,7 @@ __global__ void __launch_bounds__(64) solve_kernel(KernelArgs a) {
     o[11] = wallclock();
   }
 #endif
-  if (W.lane == 0) {
+  if (W.tid == 0) {
     a.status[pid] = (int8_t)status;
     a.flags[pid] = flags;
     a.core_len[pid] = clen;
@@ -1081,19 +1297,17 @@ __global__ void __launch_bounds__(64) solve_kernel(KernelArgs a) {
   }
 }
 
-hipError_t launch_solve(const KernelArgs& a, int n_blocks, int lds_bytes, hipStream_t stream) {
-  if (n_blocks <= 0) return hipSuccess;
-  if (a.scratch)
-    hipLaunchKernelGGL(solve_kernel<true>, dim3((unsigned)n_blocks), dim3(64), 0, stream, a);
-  else
-    hipLaunchKernelGGL(solve_kernel<false>, dim3((unsigned)n_blocks), dim3(64), (size_t)lds_bytes,
-                       stream, a);
-  return hipGetLastError();
-}
-
-hipError_t configure_solve_kernel(int max_lds_bytes) {
-  return hipFuncSetAttribute(reinterpret_cast<const void*>(&solve_kernel<false>),
-                             hipFuncAttributeMaxDynamicSharedMemorySize, max_lds_bytes);
-}
+// Instantiate and launch one mode (included once per translation unit).
+#define DP_DEFINE_MODE(MODE, NAME)                                                          \
+  hipError_t NAME(const KernelArgs& a, int n_blocks, int lds_bytes, hipStream_t stream) {   \
+    if (n_blocks <= 0) return hipSuccess;                                                   \
+    hipLaunchKernelGGL(solve_kernel<MODE>, dim3((unsigned)n_blocks), dim3(64 * mode_waves(MODE)), \
+                       (size_t)lds_bytes, stream, a);                                       \
+    return hipGetLastError();                                                               \
+  }                                                                                         \
+  hipError_t NAME##_configure(int max_lds_bytes) {                                          \
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&solve_kernel<MODE>),          \
+                               hipFuncAttributeMaxDynamicSharedMemorySize, max_lds_bytes);  \
+  }
 
 }  // namespace dp

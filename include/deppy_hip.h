@@ -199,8 +199,17 @@ typedef struct dp_opts {
   int32_t first_device; /* HIP device ordinal of the first device used     */
   int32_t n_devices;    /* 0 = every visible device from first_device       */
   int64_t step_budget;  /* per-problem budget (BCP invocations); 0 = default */
-  int32_t flags;        /* reserved, 0                                      */
+  int32_t flags;        /* enum dp_opt_flag bits, normally 0                 */
 } dp_opts;
+
+/* Placement overrides (testing and measurement): by default a problem whose
+ * working set fits a CU's LDS is solved by one wavefront out of LDS, and a
+ * larger one by one multi-wave workgroup (per-variable state in LDS when it
+ * fits, else in HBM).  These flags send every problem to a multi-wave path. */
+enum dp_opt_flag {
+  DP_OPT_FORCE_GROUP = 1 << 0, /* every problem: multi-wave workgroup */
+  DP_OPT_FORCE_HBM = 1 << 1    /* every problem: multi-wave workgroup, state in HBM */
+};
 
 typedef struct dp_ctx dp_ctx;
 

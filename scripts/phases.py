@@ -14,7 +14,7 @@ import numpy as np  # noqa: E402
 from deppy_amd import _lib  # noqa: E402
 from tests.gpu_common import lowered_config  # noqa: E402
 
-NS = 12
+NS = 16
 NAMES = ["init", "base", "search", "epilogue", "core", "round_eval", "round_finish", "rounds",
          "rounds_1lit", "push_guess"]
 L = _lib.lib()

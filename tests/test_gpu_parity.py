@@ -109,6 +109,34 @@ def test_generated_bit_exact(ctx, config, n, seed):
           "class B", int(((g["flags"] & 2) != 0).sum()), file=sys.stderr)
 
 
+@pytest.mark.parametrize("config,n,seed", [(4, 6, 31)])
+def test_olm_scale_bit_exact(ctx, config, n, seed):
+    """Config 4: OLM-scale catalogs (V~55k), one multi-wave workgroup each."""
+    lw = lowered_config(config, n, seed)
+    assert min(int(lw.record(p)[1]) for p in range(n)) > 50000
+    g = ctx.solve(lw.rec_off, lw.rec)
+    o = oracle.solve_batch(lw.rec_off, lw.rec, 0, 16)
+    bad = compare_results(g, o, n)
+    assert bad == [], bad[:10]
+    assert (g["status"] == 1).all()
+
+
+@pytest.mark.parametrize("flags", [_lib.OPT_FORCE_GROUP, _lib.OPT_FORCE_HBM], ids=["split", "hbm"])
+@pytest.mark.parametrize("config,n,seed", [(2, 300, 41), (5, 120, 42), (3, 500, 43)])
+def test_multiwave_paths_bit_exact(config, n, seed, flags):
+    """The workgroup-per-problem kernels (M_SPLIT, M_HBM) on small catalogs,
+    where the oracle is cheap and every path (learning, epilogue, cores) is hit."""
+    c = _lib.Context(0, 1, flags=flags)
+    try:
+        lw = lowered_config(config, n, seed)
+        g = c.solve(lw.rec_off, lw.rec)
+    finally:
+        c.close()
+    o = oracle.solve_batch(lw.rec_off, lw.rec, 0, 16)
+    bad = compare_results(g, o, n)
+    assert bad == [], bad[:10]
+
+
 @pytest.mark.parametrize("config,n,seed", [(2, 400, 21), (5, 60, 22)])
 def test_models_and_cores_verified(ctx, config, n, seed):
     """Every SAT answer satisfies every row; every core is UNSAT on its own and
