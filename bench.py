@@ -77,8 +77,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--depth", type=int, default=3, help="steps in flight (1 = launch+wait per step)")
-    ap.add_argument("--pmc-json", default=None,
-                    help="per-dispatch HBM bytes measured by a separate rocprofv3 --pmc pass")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic_config2.json"),
+                    help="HBM bytes per solve run measured by separate rocprofv3 --pmc passes "
+                         "(scripts/gpu_check.sh); used for roofline.traffic on the config it was taken on")
     args = ap.parse_args()
 
     g = shard.init_from_env("nccl")
@@ -135,7 +136,9 @@ def main():
     traffic = None
     if args.pmc_json and os.path.exists(args.pmc_json):
         with open(args.pmc_json) as f:
-            traffic = json.load(f).get("hbm_bytes_per_dispatch")
+            pmc = json.load(f)
+        if pmc.get("config") == args.config and pmc.get("problems") == args.problems:
+            traffic = pmc.get("hbm_bytes_per_dispatch")
 
     line = {
         "metric": METRIC,

@@ -16,5 +16,6 @@ timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/p
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o pmc -- python3 bench.py --no-cpu --steps 5 --warmup 0 --depth 1 $BARGS > $OUT/pmc_fetch.log 2>&1 && \
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o pmc -- python3 bench.py --no-cpu --steps 5 --warmup 0 --depth 1 $BARGS > $OUT/pmc_write.log 2>&1
 rc=$?
+[ $rc -eq 0 ] && python scripts/pmc_traffic.py $OUT/pmc_fetch $OUT/pmc_write 9 > $OUT/pmc_traffic.json
 tail -3 $OUT/gpu_tests.log; cat $OUT/bench.log | tail -2
 exit $rc

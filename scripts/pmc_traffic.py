@@ -4,6 +4,10 @@ FETCH_SIZE is in KiB and reads half the bytes of wide (16 B/lane) coalesced
 reads on gfx950, so it is doubled; WRITE_SIZE is taken as reported.
 
 usage: python scripts/pmc_traffic.py <fetch_dir> <write_dir> <runs> > pmc.json
+
+<runs> = solve runs (dp_run / dp_launch) in the profiled bench.py command:
+1 PCIe-inclusive solve + 3 serial runs + warmup + steps (bench.py --steps 5
+--warmup 0 --depth 1 -> 9).  A run is one launch of every footprint bucket.
 """
 import csv
 import glob
@@ -25,7 +29,7 @@ write = total(sys.argv[2], "WRITE_SIZE")
 runs = int(sys.argv[3])
 fb = 2 * 1024 * sum(fetch.values()) / runs
 wb = 1024 * sum(write.values()) / runs
-print(json.dumps({"hbm_bytes_per_dispatch": round(fb + wb), "fetch_bytes_per_run": round(fb),
+print(json.dumps({"hbm_bytes_per_dispatch": round(fb + wb), "unit": "bytes per solve run (all buckets)","fetch_bytes_per_run": round(fb),
                   "write_bytes_per_run": round(wb), "dispatches_fetch": len(fetch),
                   "dispatches_write": len(write), "runs": runs,
                   "correction": "FETCH_SIZE x2 (gfx950 wide-read half count), KiB->B"}))
