@@ -16,6 +16,8 @@ LIB_PATH = os.path.join(HERE, "libdeppy_hip.so")
 # dp_opt_flag (include/deppy_hip.h): placement overrides
 OPT_FORCE_GROUP = 1 << 0
 OPT_FORCE_HBM = 1 << 1
+# dp_flag bits used on the host
+F_TRACE_TRUNCATED = 1 << 8
 if os.environ.get("DEPPY_STAMPS") == "1":  # diagnostic phase-stamp build (scripts/ only)
     LIB_PATH = os.path.join(HERE, os.environ.get("DEPPY_STAMPS_LIB", "libdeppy_hip_stamps.so"))
 
@@ -31,7 +33,7 @@ EXPORTS = [
     "dp_lowered_ident_con", "dp_lowered_error", "dp_result_layout", "dp_create", "dp_destroy",
     "dp_last_error", "dp_last_global_error", "dp_num_devices", "dp_solve", "dp_upload", "dp_run",
     "dp_launch", "dp_wait", "dp_download", "dp_resident_free", "dp_last_kernel_ms", "dp_gen_catalogs", "dp_gen_wire",
-    "dp_gen_free",
+    "dp_gen_free", "dp_upload_traced", "dp_download_trace", "dp_solve_traced",
 ]
 
 
@@ -100,6 +102,10 @@ def lib():
     L.dp_num_devices.argtypes = [vp]
     L.dp_solve.argtypes = [vp, ctypes.POINTER(Batch), ctypes.POINTER(Result)]
     L.dp_upload.argtypes = [vp, ctypes.POINTER(Batch), ctypes.POINTER(vp)]
+    L.dp_upload_traced.argtypes = [vp, ctypes.POINTER(Batch), ctypes.c_int32, ctypes.POINTER(vp)]
+    L.dp_download_trace.argtypes = [vp, vp, c_i32p, c_i32p]
+    L.dp_solve_traced.argtypes = [vp, ctypes.POINTER(Batch), ctypes.c_int32, ctypes.POINTER(Result),
+                                  c_i32p, c_i32p]
     L.dp_run.argtypes = [vp, vp]
     L.dp_launch.argtypes = [vp, vp]
     L.dp_wait.argtypes = [vp, vp]
@@ -245,14 +251,19 @@ class Context:
     def error(self) -> str:
         return lib().dp_last_error(self.h).decode()
 
-    def upload(self, rec_off: np.ndarray, rec: np.ndarray) -> "Resident":
-        return Resident(self, rec_off, rec)
+    def upload(self, rec_off: np.ndarray, rec: np.ndarray, trace_cap: int = 0) -> "Resident":
+        return Resident(self, rec_off, rec, trace_cap)
 
-    def solve(self, rec_off: np.ndarray, rec: np.ndarray) -> dict:
-        r = self.upload(rec_off, rec)
+    def solve(self, rec_off: np.ndarray, rec: np.ndarray, trace_cap: int = 0) -> dict:
+        """Upload, solve, download.  trace_cap > 0 also returns the search
+        trace (dp_upload_traced): trace[P, trace_cap], trace_len[P]."""
+        r = self.upload(rec_off, rec, trace_cap)
         try:
             r.run()
-            return r.download()
+            out = r.download()
+            if trace_cap > 0:
+                out.update(r.download_trace())
+            return out
         finally:
             r.free()
 
@@ -273,8 +284,9 @@ def _batch(rec_off, rec):
 class Resident:
     """A batch resident in HBM (dp_upload); run() solves it in place."""
 
-    def __init__(self, ctx: Context, rec_off, rec):
+    def __init__(self, ctx: Context, rec_off, rec, trace_cap: int = 0):
         self.ctx = ctx
+        self.trace_cap = trace_cap
         self.rec_off = np.ascontiguousarray(rec_off, np.int64)
         self.rec = np.ascontiguousarray(rec if len(rec) else np.zeros(1, np.int32), np.int32)
         n = len(self.rec_off) - 1
@@ -284,7 +296,7 @@ class Resident:
         self.core_off = np.zeros(n + 1, np.int64)
         lib().dp_result_layout(ctypes.byref(b), _p(self.inst_off, c_i64p), _p(self.core_off, c_i64p))
         h = ctypes.c_void_p()
-        if lib().dp_upload(ctx.h, ctypes.byref(b), ctypes.byref(h)) != 0:
+        if lib().dp_upload_traced(ctx.h, ctypes.byref(b), trace_cap, ctypes.byref(h)) != 0:
             raise RuntimeError("dp_upload: " + ctx.error())
         self.h = h
 
@@ -319,6 +331,14 @@ class Resident:
             out[k] = out[k][:n]
         return out
 
+    def download_trace(self) -> dict:
+        n = self.n
+        tr = np.zeros((max(n, 1), max(self.trace_cap, 1)), np.int32)
+        tl = np.zeros(max(n, 1), np.int32)
+        if lib().dp_download_trace(self.ctx.h, self.h, _p(tr, c_i32p), _p(tl, c_i32p)) != 0:
+            raise RuntimeError("dp_download_trace: " + self.ctx.error())
+        return dict(trace=tr[:n], trace_len=tl[:n])
+
     def free(self):
         if self.h:
             lib().dp_resident_free(self.ctx.h, self.h)
@@ -335,6 +355,20 @@ def generate(config: int, n: int, seed: int) -> dict:
         return wire_to_numpy(L.dp_gen_wire(g).contents)
     finally:
         L.dp_gen_free(g)
+
+
+def trace_events(res: dict, p: int) -> list:
+    """The search-trace events of problem p: [(guessed variables, identities)]."""
+    t = res["trace"][p][:int(res["trace_len"][p])]
+    ev, i = [], 0
+    while i < len(t):
+        n = int(t[i])
+        vs = [int(x) for x in t[i + 1:i + 1 + n]]
+        i += 1 + n
+        m = int(t[i])
+        ev.append((vs, [int(x) for x in t[i + 1:i + 1 + m]]))
+        i += 1 + m
+    return ev
 
 
 def installed_list(res: dict, p: int, nv: int) -> list[int]:

@@ -30,6 +30,11 @@ struct KernelArgs {
   const int64_t* scratch_off;
   // diagnostic builds only (-DDP_STAMPS): per-problem phase cycle counts
   int64_t* stamps;
+  // search trace (Tracer, search.go:173); null: not traced.  trace_cap words
+  // per problem, indexed by problem like status
+  int32_t* trace;
+  int32_t* trace_len;
+  int32_t trace_cap;
 };
 
 // Launch one workgroup per problem of order[0..n_blocks) with lds_bytes of

@@ -77,6 +77,9 @@ struct DevSlice {
   int32_t* scratch = nullptr;
   int64_t* scratch_off = nullptr;
   int64_t* stamps = nullptr;  // diagnostic builds only
+  int32_t* trace = nullptr;   // search trace: trace_cap words per problem
+  int32_t* trace_len = nullptr;
+  int32_t trace_cap = 0;
   hipStream_t stream = nullptr;  // lane of the last launch (context-owned)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // bucket launches run concurrently on the other lanes, joined back by events
@@ -122,7 +125,7 @@ void free_slice(DevSlice& s) {
   (void)hipSetDevice(s.device);
   void* ptrs[] = {s.rec, s.rec_off, s.order, s.status, s.flags, s.installed,
                   s.inst_off, s.core, s.core_off, s.core_len, s.steps, s.scratch, s.scratch_off,
-                  s.stamps};
+                  s.stamps, s.trace, s.trace_len};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s.ev0) (void)hipEventDestroy(s.ev0);
@@ -193,7 +196,7 @@ int64_t build_image(const int32_t* rec, std::vector<int32_t>& out) {
 
 // Build one device's slice: device images, bucketed launch order, outputs.
 int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_off,
-                const int64_t* core_off, int32_t opt_flags) {
+                const int64_t* core_off, int32_t opt_flags, int32_t trace_cap) {
   HIP_OK(hipSetDevice(s.device));
   s.stream = L.s[0];
   HIP_OK(hipEventCreate(&s.ev0));
@@ -278,6 +281,12 @@ int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_of
   HIP_OK(hipMalloc(&s.stamps, std::max<size_t>((size_t)n, 1) * dp::DP_NSTAMP * 8));
   HIP_OK(hipMemsetAsync(s.stamps, 0, std::max<size_t>((size_t)n, 1) * dp::DP_NSTAMP * 8, s.stream));
 #endif
+  if (trace_cap > 0) {
+    s.trace_cap = trace_cap;
+    HIP_OK(hipMalloc(&s.trace, std::max<size_t>((size_t)n, 1) * (size_t)trace_cap * 4));
+    HIP_OK(hipMalloc(&s.trace_len, std::max<size_t>((size_t)n, 1) * 4));
+    HIP_OK(hipMemsetAsync(s.trace_len, 0, std::max<size_t>((size_t)n, 1) * 4, s.stream));
+  }
   HIP_OK(hipMalloc(&s.installed, (size_t)std::max<int64_t>(s.n_inst, 1) * 4));
   HIP_OK(hipMalloc(&s.core, (size_t)std::max<int64_t>(s.n_core, 1) * 4));
   // problems that fit no bucket are reported DP_ERROR | DP_F_TOO_LARGE
@@ -315,6 +324,9 @@ int launch_slice(DevSlice& s, Lanes& L, int64_t budget) {
   a.scratch = nullptr;
   a.scratch_off = nullptr;
   a.stamps = s.stamps;
+  a.trace = s.trace;
+  a.trace_len = s.trace_len;
+  a.trace_cap = s.trace_cap;
   // the multi-wave launches (long-running large catalogs) first, then the
   // largest buckets, so they start earliest
   std::vector<int> launch_order;
@@ -470,7 +482,11 @@ int dp_result_layout(const dp_batch* b, int64_t* inst_off, int64_t* core_off) {
 }
 
 int dp_upload(dp_ctx* ctx, const dp_batch* b, dp_resident** out) {
-  if (!ctx || !b || !out) return -1;
+  return dp_upload_traced(ctx, b, 0, out);
+}
+
+int dp_upload_traced(dp_ctx* ctx, const dp_batch* b, int32_t trace_cap, dp_resident** out) {
+  if (!ctx || !b || !out || trace_cap < 0) return -1;
   std::lock_guard<std::mutex> lk(ctx->mu);
   t_ctx = ctx;
   const int32_t P = b->n_problems;
@@ -500,7 +516,8 @@ int dp_upload(dp_ctx* ctx, const dp_batch* b, dp_resident** out) {
     r->slices.push_back(s);
   }
   int rc = for_slices(ctx, r, [&](DevSlice& s) {
-    return build_slice(s, lanes_of(ctx, s.device), b, inst_off.data(), core_off.data(), ctx->flags);
+    return build_slice(s, lanes_of(ctx, s.device), b, inst_off.data(), core_off.data(), ctx->flags,
+                       trace_cap);
   });
   if (rc) {
     dp_resident_free(ctx, r);
@@ -565,6 +582,38 @@ int dp_download(dp_ctx* ctx, dp_resident* r, dp_result* res) {
   t_ctx = ctx;
   if (wait_locked(ctx, r)) return -1;
   return for_slices(ctx, r, [&](DevSlice& s) { return download_slice(s, res); });
+}
+
+int dp_download_trace(dp_ctx* ctx, dp_resident* r, int32_t* trace, int32_t* trace_len) {
+  if (!ctx || !r || !trace || !trace_len) return -1;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  t_ctx = ctx;
+  if (wait_locked(ctx, r)) return -1;
+  return for_slices(ctx, r, [&](DevSlice& s) {
+    HIP_OK(hipSetDevice(s.device));
+    const int32_t n = s.p1 - s.p0;
+    if (!s.trace) {
+      fail("dp_download_trace: the batch was not uploaded with dp_upload_traced");
+      return -1;
+    }
+    if (n == 0) return 0;
+    HIP_OK(hipMemcpyAsync(trace_len + s.p0, s.trace_len, (size_t)n * 4, hipMemcpyDeviceToHost, s.stream));
+    HIP_OK(hipMemcpyAsync(trace + (int64_t)s.trace_cap * s.p0, s.trace, (size_t)n * s.trace_cap * 4,
+                          hipMemcpyDeviceToHost, s.stream));
+    HIP_OK(hipStreamSynchronize(s.stream));
+    return 0;
+  });
+}
+
+int dp_solve_traced(dp_ctx* ctx, const dp_batch* b, int32_t trace_cap, dp_result* res,
+                    int32_t* trace, int32_t* trace_len) {
+  dp_resident* r = nullptr;
+  if (dp_upload_traced(ctx, b, trace_cap, &r)) return -1;
+  int rc = dp_run(ctx, r);
+  if (!rc) rc = dp_download(ctx, r, res);
+  if (!rc) rc = dp_download_trace(ctx, r, trace, trace_len);
+  dp_resident_free(ctx, r);
+  return rc;
 }
 
 void dp_resident_free(dp_ctx* ctx, dp_resident* r) {

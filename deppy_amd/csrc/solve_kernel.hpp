@@ -168,6 +168,9 @@ struct Group {
   const uint32_t* enabled;  // nullptr: every row
   bool extra_mode;
   int extra_w;
+  int32_t* tr;  // search trace of this problem (nullptr: not traced)
+  int tr_cap, tr_len;
+  bool tr_stop;
 #ifdef DP_STAMPS
   int64_t acc[5];  // round eval cycles, round finish cycles, rounds, 1-literal rounds, push+pop cycles
   unsigned long long* dbg;  // [first code, value, bound, failures]
@@ -349,6 +352,9 @@ struct Group {
     enabled = nullptr;
     extra_mode = false;
     extra_w = 0;
+    tr = nullptr;
+    tr_cap = tr_len = 0;
+    tr_stop = false;
 #ifdef DP_STAMPS
     for (int i = 0; i < 5; ++i) acc[i] = 0;
     dbg = nullptr;
@@ -787,6 +793,7 @@ struct Group {
       if (ck == CK_ROW) ante_serial(c_row, -1, INF);
       else if (ck == CK_VAR) { ante_serial(c_rp, c_var, c_row); ante_serial(c_rn, c_var, c_row); }
       else if (ck == CK_EXTRA) extra_serial(-1, INF);
+      else if (ck == CK_ASSUME) mark_push(c_var);  // the assumed literal is false: its reasons
     }
     gsync();
     int head = 0;
@@ -1052,17 +1059,22 @@ struct Group {
     class_b = solve_unsat = last_solve = false;
     for (int i = 0; i < na; ++i) dq_push_back(nch + (int)anchors[i], 0);
     gsync();
+    bool from_solve = false;
     for (;;) {
       if (dq_n == 0 && result == 0) {
+        if (tr) fill_bits(used, nid, false);
         const int r = search_solve();
+        from_solve = true;
         if (r == RS_BUDGET) { result = RS_BUDGET; break; }
         result = r;
         last_solve = (r == RS_SAT);
         if (r == RS_UNSAT) solve_unsat = true;
       }
       if (result < 0) {
+        if (tr) trace_event(from_solve);  // h.tracer.Trace(h), search.go:173
         if (ng == 0) break;
         pop_guess();
+        from_solve = false;
         continue;
       }
       if (dq_n == 0) break;
@@ -1073,6 +1085,7 @@ struct Group {
 #else
       push_guess();
 #endif
+      from_solve = false;
       if (budget_hit) { result = RS_BUDGET; break; }
     }
     // Value() after an ending on Test()==1 reads that scope's full assignment
@@ -1084,6 +1097,67 @@ struct Group {
   // NotSatisfiable (oracle: refute / core_extract)
   // ------------------------------------------------------------------
   __device__ __forceinline__ void reset_all() { truncate_to(0); }
+
+  // The set bits of bits[0..nw) as ascending indices into out; returns their
+  // number.  Every thread writes the bits of its words at their exclusive
+  // prefix (DPP scan per wavefront, per-wave slots across wavefronts).
+  __device__ __forceinline__ int emit_bits(const uint32_t* bits, int nw, int32_t* out) {
+    int len = 0;
+    for (int b = 0; b < nw; b += NT) {
+      const int i = b + tid;
+      const uint32_t x = i < nw ? ld_bits(&bits[i]) : 0u;
+      const int c = __popc(x);
+      const int incl = wave_incl_scan(c);
+      int before = incl - c, total = __builtin_amdgcn_readlane(incl, 63);
+      if constexpr (NW > 1) {
+        if (lane == 63) scal[S_SLOT + wid] = incl;
+        __syncthreads();
+        total = 0;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+          const int s = scal[S_SLOT + q];
+          before += q < wid ? s : 0;
+          total += s;
+        }
+        __syncthreads();
+      }
+      for (uint32_t y = x; y; y &= y - 1) out[len + before++] = 32 * i + __ffs(y) - 1;
+      len += total;
+    }
+    return len;
+  }
+
+  // Tracer.Trace(SearchPosition) at an unsatisfiable search step
+  // (search.go:173; oracle: trace_event).  Record [n, guessed variables in
+  // stack order, m, identities ascending]: the identities of the failure's
+  // conflict analysis -- a failed Test/Untest is analysed here, a failed
+  // Solve() left the union of its refutation's analyses in `used`.
+  __device__ __forceinline__ void trace_event(bool from_solve) {
+    if (tr_stop) return;
+    if (!from_solve) {
+      fill_bits(used, nid, false);
+      analyze();
+    }
+    int ngv = 0, ni = 0;
+    for (int i = tid; i < ng; i += NT) ngv += dec(stk[5 * i + 2]) >= 0;
+    for (int i = tid; i < nbi; i += NT) ni += __popc(ld_bits(&used[i]));
+    ngv = g_sum(ngv);
+    ni = g_sum(ni);
+    if (tr_len + 2 + ngv + ni > tr_cap) { tr_stop = true; return; }
+    int32_t* o = tr + tr_len;
+    if (tid == 0) {
+      int k = 0;
+      o[k++] = ngv;
+      for (int i = 0; i < ng; ++i) {
+        const int m = dec(stk[5 * i + 2]);
+        if (m >= 0) o[k++] = m;
+      }
+      o[k] = ni;
+    }
+    emit_bits(used, nbi, o + 2 + ngv);
+    tr_len += 2 + ngv + ni;
+    gsync();
+  }
 
   __device__ __forceinline__ void fill_bits(uint32_t* bs, int n, bool ones) {
     const int nw = bits_words(n);
@@ -1131,28 +1205,7 @@ struct Group {
         if (r == RS_UNSAT) copy_bits(en, used, nid);
         else if (r == RS_BUDGET) { flags |= DP_F_CORE_BUDGET; break; }
       }
-      // ascending identity ids: the kept bits of each word, in word order
-      for (int b = 0; b < nbi; b += NT) {
-        const int i = b + tid;
-        const uint32_t x = i < nbi ? en[i] : 0u;
-        const int c = __popc(x);
-        const int incl = wave_incl_scan(c);
-        int before = incl - c, total = __builtin_amdgcn_readlane(incl, 63);
-        if constexpr (NW > 1) {
-          if (lane == 63) scal[S_SLOT + wid] = incl;
-          __syncthreads();
-          total = 0;
-#pragma unroll
-          for (int q = 0; q < NW; ++q) {
-            const int s = scal[S_SLOT + q];
-            before += q < wid ? s : 0;
-            total += s;
-          }
-          __syncthreads();
-        }
-        for (uint32_t y = x; y; y &= y - 1) out[len + before++] = 32 * i + __ffs(y) - 1;
-        len += total;
-      }
+      len = emit_bits(en, nbi, out);  // ascending identity ids
     } else {
       flags |= DP_F_CORE_BUDGET;
     }
@@ -1246,6 +1299,10 @@ __global__ void __launch_bounds__(64 * mode_waves(MODE)) solve_kernel(KernelArgs
   if (a.stamps) W.dbg = reinterpret_cast<unsigned long long*>(a.stamps + (int64_t)DP_NSTAMP * pid + 12);
 #endif
   W.budget = a.budget;
+  if (a.trace) {
+    W.tr = a.trace + (int64_t)a.trace_cap * pid;
+    W.tr_cap = a.trace_cap;
+  }
   uint32_t* inst = a.installed + a.inst_off[pid];
   int32_t flags = 0;
   int status;
@@ -1289,7 +1346,9 @@ __global__ void __launch_bounds__(64 * mode_waves(MODE)) solve_kernel(KernelArgs
     o[11] = wallclock();
   }
 #endif
+  if (W.tr_stop) flags |= DP_F_TRACE_TRUNCATED;
   if (W.tid == 0) {
+    if (a.trace) a.trace_len[pid] = W.tr_len;
     a.status[pid] = (int8_t)status;
     a.flags[pid] = flags;
     a.core_len[pid] = clen;

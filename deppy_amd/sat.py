@@ -407,12 +407,47 @@ def _duplicate(variables) -> Optional[DuplicateIdentifier]:
     return None
 
 
+class _Position(SearchPosition):
+    """One unsatisfiable search step as the GPU recorded it (search.go:205-217)."""
+
+    def __init__(self, variables: list, conflicts: list):
+        self._v, self._c = variables, conflicts
+
+    def Variables(self) -> list:
+        return list(self._v)
+
+    def Conflicts(self) -> list:
+        return list(self._c)
+
+
+# trace words reserved per problem (dp_upload_traced); a truncated trace is
+# re-solved alone with a larger reservation
+TRACE_CAP = 1 << 12
+TRACE_CAP_MAX = 1 << 24
+
+
+def _replay_trace(tracer: Tracer, variables: list, lw, p: int, res: dict, j: int) -> None:
+    """Deliver the recorded steps to the tracer in search order (search.go:173)."""
+    i0 = int(lw.ident_off[p])
+    for vs, ids in _lib.trace_events(res, j):
+        conflicts = []
+        for ident in ids:
+            var = variables[int(lw.ident_var[i0 + ident])]
+            conflicts.append(AppliedConstraint(var, var.Constraints()[int(lw.ident_con[i0 + ident])]))
+        tracer.Trace(_Position([variables[v] for v in vs], conflicts))
+
+
 def SolveBatch(inputs: Sequence[Sequence[Variable]], tracer: Optional[Tracer] = None,
                context: Optional[_lib.Context] = None) -> list:
     """Solve many independent problems in one GPU launch.
 
+    With a tracer other than DefaultTracer the GPU records every
+    unsatisfiable search step and the steps are replayed through
+    tracer.Trace, problem by problem, before this returns.
+
     Returns [(installed | None, error | None)] in input order."""
     inputs = [list(v) for v in inputs]
+    traced = tracer is not None and not isinstance(tracer, DefaultTracer)
     lw = _lib.Lowered(encode_inputs(inputs))
     out: list = [None] * len(inputs)
     ok = [p for p in range(len(inputs)) if lw.err[p] == 0]
@@ -431,9 +466,16 @@ def SolveBatch(inputs: Sequence[Sequence[Variable]], tracer: Optional[Tracer] = 
             offs.append(offs[-1] + len(r))
         rec = np.concatenate(parts).astype(np.int32)
         ctx = context or device_context()
-        res = ctx.solve(np.array(offs, np.int64), rec)
+        res = ctx.solve(np.array(offs, np.int64), rec, TRACE_CAP if traced else 0)
         for j, p in enumerate(ok):
             variables = inputs[p]
+            if traced:
+                rj, jj, cap = res, j, TRACE_CAP
+                while rj["flags"][jj] & _lib.F_TRACE_TRUNCATED and cap < TRACE_CAP_MAX:
+                    cap *= 16
+                    r1 = lw.record(p).astype(np.int32)
+                    rj, jj = ctx.solve(np.array([0, len(r1)], np.int64), r1, cap), 0
+                _replay_trace(tracer, variables, lw, p, rj, jj)
             st = int(res["status"][j])
             if st == SAT:
                 inst = _lib.installed_list(res, j, len(variables))

@@ -192,7 +192,8 @@ enum dp_flag {
   DP_F_BASE_UNSAT = 1 << 4,     /* base Test returned -1                                 */
   DP_F_CORE_BUDGET = 1 << 5,    /* core not fully minimised within the step budget        */
   DP_F_BUDGET = 1 << 6,         /* step budget exhausted -> DP_INCOMPLETE                 */
-  DP_F_TOO_LARGE = 1 << 7       /* record does not fit the device path                    */
+  DP_F_TOO_LARGE = 1 << 7,      /* record does not fit the device path                    */
+  DP_F_TRACE_TRUNCATED = 1 << 8 /* search trace stopped: an event exceeded the capacity   */
 };
 
 typedef struct dp_opts {
@@ -261,6 +262,19 @@ int dp_launch(dp_ctx* ctx, dp_resident* r);
 int dp_wait(dp_ctx* ctx, dp_resident* r);
 int dp_download(dp_ctx* ctx, dp_resident* r, dp_result* res);
 void dp_resident_free(dp_ctx* ctx, dp_resident* r);
+/* Search trace (WithTracer, solve.go:141-146; Tracer.Trace at every
+ * unsatisfiable search step, search.go:173).  dp_upload_traced reserves
+ * trace_cap int32 words per problem; the solve writes one event record per
+ * step: [n, variable indices of the guesses in stack order (SearchPosition
+ * .Variables(), search.go:205-213), m, identity ids ascending (.Conflicts(),
+ * search.go:215-217)].  An event that does not fit stops the problem's trace
+ * and sets DP_F_TRACE_TRUNCATED.  dp_download_trace fills trace[P*trace_cap]
+ * (problem p at p*trace_cap) and trace_len[P] (words written). */
+int dp_upload_traced(dp_ctx* ctx, const dp_batch* b, int32_t trace_cap, dp_resident** out);
+int dp_download_trace(dp_ctx* ctx, dp_resident* r, int32_t* trace, int32_t* trace_len);
+int dp_solve_traced(dp_ctx* ctx, const dp_batch* b, int32_t trace_cap, dp_result* res,
+                    int32_t* trace, int32_t* trace_len);
+
 /* Device time of the solve kernel(s) of the last waited launch (dp_run,
  * dp_wait, dp_solve), measured with HIP events on its stream (max over devices). */
 int dp_last_kernel_ms(const dp_ctx* ctx, double* ms);

@@ -40,6 +40,9 @@ def lib():
         L.oracle_solve_batch.argtypes = [ctypes.c_int32, _i64p, _i32p, ctypes.c_int64,
                                          ctypes.c_int32, _i8p, _i32p, _u32p, _i64p, _i32p,
                                          _i64p, _i32p, _i64p]
+        L.oracle_solve_batch_traced.argtypes = [ctypes.c_int32, _i64p, _i32p, ctypes.c_int64,
+                                                ctypes.c_int32, _i8p, _i32p, _u32p, _i64p, _i32p,
+                                                _i64p, _i32p, _i64p, _i32p, ctypes.c_int32, _i32p]
         L.oracle_search_scripted.argtypes = [_i32p, _i32p, ctypes.c_int32, _i32p, ctypes.c_int32,
                                              ctypes.POINTER(ctypes.c_int32), _i32p,
                                              ctypes.POINTER(ctypes.c_int32),
@@ -73,8 +76,10 @@ def solve(rec: np.ndarray, budget: int = 0):
     return st, flags.value, installed, list(core[:clen.value]), steps.value
 
 
-def solve_batch(rec_off: np.ndarray, rec: np.ndarray, budget: int = 0, nthreads: int = 1):
-    """Batch solve; returns dict of arrays (same layout as dp_result)."""
+def solve_batch(rec_off: np.ndarray, rec: np.ndarray, budget: int = 0, nthreads: int = 1,
+                trace_cap: int = 0):
+    """Batch solve; returns dict of arrays (same layout as dp_result).  With
+    trace_cap > 0 also the search trace: trace[P, trace_cap], trace_len[P]."""
     rec_off = np.ascontiguousarray(rec_off, dtype=np.int64)
     rec = np.ascontiguousarray(rec, dtype=np.int32)
     n = len(rec_off) - 1
@@ -89,6 +94,14 @@ def solve_batch(rec_off: np.ndarray, rec: np.ndarray, budget: int = 0, nthreads:
         installed=np.zeros(max(1, int(inst_off[-1])), np.uint32), inst_off=inst_off,
         core=np.zeros(max(1, int(core_off[-1])), np.int32), core_off=core_off,
         core_len=np.zeros(n, np.int32), steps=np.zeros(n, np.int64))
+    if trace_cap > 0:
+        out["trace"] = np.zeros((n, trace_cap), np.int32)
+        out["trace_len"] = np.zeros(n, np.int32)
+        lib().oracle_solve_batch_traced(n, rec_off, rec, budget, nthreads, out["status"],
+                                        out["flags"], out["installed"], inst_off, out["core"],
+                                        core_off, out["core_len"], out["steps"], out["trace"],
+                                        trace_cap, out["trace_len"])
+        return out
     lib().oracle_solve_batch(n, rec_off, rec, budget, nthreads, out["status"], out["flags"],
                              out["installed"], inst_off, out["core"], core_off, out["core_len"],
                              out["steps"])

@@ -91,6 +91,9 @@ typedef struct {
   uint8_t* fg; /* guesses met by the refutation of the current Solve() */
   int32_t* dix;    /* decision index of a Solve() decision variable, else -1 */
   uint8_t* dset;   /* decisions met by the last conflict analysis */
+  /* search trace (Tracer, search.go:173): event records, see oracle_solve_traced */
+  int32_t* trace;
+  int32_t trace_cap, trace_len, trace_stop;
 } st_t;
 
 /* learned-row store: at most L_MAX rows and 2*nv+64 literals */
@@ -418,7 +421,10 @@ static void analyze(st_t* s) {
     push_ante(s, s->c_rp, s->c_var, s->c_row);
     push_ante(s, s->c_rn, s->c_var, s->c_row);
   } else if (s->ck == CK_EXTRA) push_extra(s, -1, INF);
-  else return;
+  else if (s->ck == CK_ASSUME) {  /* the assumed literal is false: its variable's reasons */
+    s->seen[s->c_var] = 1;
+    s->work[s->nwork++] = s->c_var;
+  } else return;
   for (int i = 0; i < s->nwork; ++i) {
     int u = s->work[i];
     int r = s->reason[u];
@@ -596,6 +602,17 @@ static void pop_guess(search_t* h, st_t* s, const backend_t* be) {
   dq_push_front(h, (choice_t){g.list, g.idx + (g.m >= 0)});
 }
 
+/* Tracer.Trace(SearchPosition) at an unsatisfiable search step (search.go:173).
+ * Variables(): the guessed variables, stack order (search.go:205-213).
+ * Conflicts(): restated as the identities the failure's conflict analysis
+ * reaches, ascending -- for a failed Test/Untest the analysis of its BCP
+ * conflict, for a failed Solve() the union over its refutation's analyses
+ * (gini's Why, lit_mapping.go:198-207; the reference only logs traces,
+ * solve_test.go:302-353, so their content is parity-unpinned).
+ * Record: [n, variables..., m, identities...]; an event that does not fit the
+ * remaining capacity stops the trace (DP_F_TRACE_TRUNCATED). */
+static void trace_event(search_t* h, st_t* s, int from_solve);
+
 /* Do, search.go:158-203.  Returns the result; leaves the guessed variables of
  * the final stack (search.Lits()) in lits[0..*nlits) and pops every guess. */
 static int search_do(search_t* h, st_t* s, const backend_t* be, int32_t* lits, int32_t* nlits) {
@@ -606,21 +623,26 @@ static int search_do(search_t* h, st_t* s, const backend_t* be, int32_t* lits, i
   h->head = h->n = h->ng = 0;
   h->result = 0;
   for (int i = 0; i < p->na; ++i) dq_push_back(h, (choice_t){~p->anchors[i], 0});
+  int from_solve = 0;
   for (;;) {
     if (h->n == 0 && h->result == 0) {
+      if (s->trace) memset(s->used, 0, (size_t)p->nid);
       h->result = be->solve(be->u, s);
       h->last_solve = (h->result == 1);
+      from_solve = 1;
       if (h->result == R_BUDGET) break;
       if (h->result < 0) h->solve_unsat = 1;
     }
     if (h->result < 0) {
-      /* tracer.Trace(h) would run here (search.go:173) */
+      if (s->trace) trace_event(h, s, from_solve);  /* h.tracer.Trace(h), search.go:173 */
       if (h->ng == 0) break;
       pop_guess(h, s, be);
+      from_solve = 0;
       continue;
     }
     if (h->n == 0) break;
     push_guess(h, s, be);
+    from_solve = 0;
     if (s->budget_hit) { h->result = R_BUDGET; break; }
   }
   /* Value() after a Test()==1 ending reads the full assignment of that scope */
@@ -635,6 +657,27 @@ static int search_do(search_t* h, st_t* s, const backend_t* be, int32_t* lits, i
   free(h->dq);
   free(h->g);
   return result;
+}
+
+static void trace_event(search_t* h, st_t* s, int from_solve) {
+  if (s->trace_stop) return;
+  const prob_t* p = &s->p;
+  if (!from_solve) {
+    memset(s->used, 0, (size_t)p->nid);
+    analyze(s);
+  }
+  int ng = 0, ni = 0;
+  for (int i = 0; i < h->ng; ++i) ng += h->g[i].m >= 0;
+  for (int i = 0; i < p->nid; ++i) ni += s->used[i];
+  if (s->trace_len + 2 + ng + ni > s->trace_cap) { s->trace_stop = 1; return; }
+  int32_t* o = s->trace + s->trace_len;
+  *o++ = ng;
+  for (int i = 0; i < h->ng; ++i)
+    if (h->g[i].m >= 0) *o++ = h->g[i].m;
+  *o++ = ni;
+  for (int i = 0; i < p->nid; ++i)
+    if (s->used[i]) *o++ = i;
+  s->trace_len += 2 + ng + ni;
 }
 
 /* the real backend: our BCP */
@@ -789,9 +832,17 @@ static int epilogue(st_t* s, int32_t* flags, uint32_t* installed) {
 
 int oracle_solve(const int32_t* rec, int64_t budget, int32_t* flags, uint32_t* installed,
                  int32_t* core, int32_t* core_len, int64_t* steps) {
+  return oracle_solve_traced(rec, budget, flags, installed, core, core_len, steps, NULL, 0, NULL);
+}
+
+int oracle_solve_traced(const int32_t* rec, int64_t budget, int32_t* flags, uint32_t* installed,
+                        int32_t* core, int32_t* core_len, int64_t* steps, int32_t* trace,
+                        int32_t trace_cap, int32_t* trace_len) {
   st_t s;
   st_init(&s, rec);
   s.budget = budget > 0 ? budget : (1 << 16);
+  s.trace = trace;
+  s.trace_cap = trace_cap;
   int nv = s.p.nv, nw = (nv + 31) / 32;
   *flags = 0;
   *core_len = 0;
@@ -829,6 +880,8 @@ int oracle_solve(const int32_t* rec, int64_t budget, int32_t* flags, uint32_t* i
   }
   if (status == DP_UNSAT) *core_len = core_extract(&s, core, flags);
   if (steps) *steps = s.steps;
+  if (trace_len) *trace_len = s.trace_len;
+  if (s.trace_stop) *flags |= DP_F_TRACE_TRUNCATED;
   st_free(&s);
   return status;
 }
@@ -902,6 +955,9 @@ typedef struct {
   const int64_t* core_off;
   int32_t* core_len;
   int64_t* steps;
+  int32_t* trace; /* NULL: no tracing; else trace_cap words per problem */
+  int32_t trace_cap;
+  int32_t* trace_len;
   int32_t next; /* shared work counter */
   pthread_mutex_t mu;
 } batch_t;
@@ -917,9 +973,11 @@ static void* batch_worker(void* arg) {
     int i1 = i0 + 16 < b->n ? i0 + 16 : b->n;
     for (int i = i0; i < i1; ++i) {
       int64_t st = 0;
-      b->status[i] = (int8_t)oracle_solve(b->rec + b->rec_off[i], b->budget, &b->flags[i],
-                                          b->installed + b->inst_off[i], b->core + b->core_off[i],
-                                          &b->core_len[i], &st);
+      b->status[i] = (int8_t)oracle_solve_traced(
+          b->rec + b->rec_off[i], b->budget, &b->flags[i], b->installed + b->inst_off[i],
+          b->core + b->core_off[i], &b->core_len[i], &st,
+          b->trace ? b->trace + (int64_t)b->trace_cap * i : NULL, b->trace_cap,
+          b->trace ? &b->trace_len[i] : NULL);
       if (b->steps) b->steps[i] = st;
     }
   }
@@ -930,8 +988,17 @@ int oracle_solve_batch(int32_t n, const int64_t* rec_off, const int32_t* rec, in
                        int32_t nthreads, int8_t* status, int32_t* flags, uint32_t* installed,
                        const int64_t* inst_off, int32_t* core, const int64_t* core_off,
                        int32_t* core_len, int64_t* steps) {
+  return oracle_solve_batch_traced(n, rec_off, rec, budget, nthreads, status, flags, installed,
+                                   inst_off, core, core_off, core_len, steps, NULL, 0, NULL);
+}
+
+int oracle_solve_batch_traced(int32_t n, const int64_t* rec_off, const int32_t* rec,
+                              int64_t budget, int32_t nthreads, int8_t* status, int32_t* flags,
+                              uint32_t* installed, const int64_t* inst_off, int32_t* core,
+                              const int64_t* core_off, int32_t* core_len, int64_t* steps,
+                              int32_t* trace, int32_t trace_cap, int32_t* trace_len) {
   batch_t b = {n, rec_off, rec, budget, status, flags, installed, inst_off, core, core_off,
-               core_len, steps, 0, PTHREAD_MUTEX_INITIALIZER};
+               core_len, steps, trace, trace_cap, trace_len, 0, PTHREAD_MUTEX_INITIALIZER};
   if (nthreads < 1) nthreads = 1;
   pthread_t* th = xcalloc((size_t)nthreads, sizeof(pthread_t));
   for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, batch_worker, &b);

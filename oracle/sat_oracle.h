@@ -27,11 +27,24 @@ extern "C" {
 int oracle_solve(const int32_t* rec, int64_t budget, int32_t* flags, uint32_t* installed,
                  int32_t* core, int32_t* core_len, int64_t* steps);
 
-/* Batch form on nthreads host threads (the CPU baseline). */
+/* oracle_solve with the search trace (Tracer, search.go:173): trace_cap
+ * int32 words of event records [n, variables..., m, identities...], one per
+ * unsatisfiable search step; *trace_len = words written; an event that does
+ * not fit stops the trace and sets DP_F_TRACE_TRUNCATED. */
+int oracle_solve_traced(const int32_t* rec, int64_t budget, int32_t* flags, uint32_t* installed,
+                        int32_t* core, int32_t* core_len, int64_t* steps, int32_t* trace,
+                        int32_t trace_cap, int32_t* trace_len);
+
+/* Batch forms on nthreads host threads (the CPU baseline). */
 int oracle_solve_batch(int32_t n, const int64_t* rec_off, const int32_t* rec, int64_t budget,
                        int32_t nthreads, int8_t* status, int32_t* flags, uint32_t* installed,
                        const int64_t* inst_off, int32_t* core, const int64_t* core_off,
                        int32_t* core_len, int64_t* steps);
+int oracle_solve_batch_traced(int32_t n, const int64_t* rec_off, const int32_t* rec,
+                              int64_t budget, int32_t nthreads, int8_t* status, int32_t* flags,
+                              uint32_t* installed, const int64_t* inst_off, int32_t* core,
+                              const int64_t* core_off, int32_t* core_len, int64_t* steps,
+                              int32_t* trace, int32_t trace_cap, int32_t* trace_len);
 
 /* search.Do with a scripted inter.S (the counterfeiter FakeS of
  * pkg/sat/zz_search_test.go): Test()/Untest() return the scripted values in

@@ -54,3 +54,33 @@ def not_satisfiable_string(variables, applied_sorted):
         return "constraints not satisfiable"
     return "constraints not satisfiable: " + ", ".join(
         cstr(a["var"], by[a["var"]]["constraints"][a["constraint"]]) for a in applied_sorted)
+
+
+def wire_problem_variables(w, p):
+    """Problem p of a generated wire batch (_lib.generate) as sat Variables."""
+    from deppy_amd import sat
+    from tests.test_lowering import V
+
+    so, sb = w["str_off"], w["str_bytes"].tobytes()
+
+    def s(i):
+        return sb[so[i]:so[i + 1]].decode()
+
+    out = []
+    for v in range(int(w["prob_var_off"][p]), int(w["prob_var_off"][p + 1])):
+        cons = []
+        for c in range(int(w["var_con_off"][v]), int(w["var_con_off"][v + 1])):
+            k, n = int(w["con_kind"][c]), int(w["con_n"][c])
+            args = [s(int(a)) for a in w["con_arg"][w["con_arg_off"][c]:w["con_arg_off"][c + 1]]]
+            if k == 1:
+                cons.append(sat.Mandatory())
+            elif k == 2:
+                cons.append(sat.Prohibited())
+            elif k == 3:
+                cons.append(sat.Dependency(*args))
+            elif k == 4:
+                cons.append(sat.Conflict(args[0]))
+            else:
+                cons.append(sat.AtMost(n, *args))
+        out.append(V(s(int(w["var_id"][v])), *cons))
+    return out
