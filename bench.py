@@ -76,7 +76,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--depth", type=int, default=3, help="steps in flight (1 = launch+wait per step)")
+    ap.add_argument("--depth", type=int, default=8,
+                    help="steps in flight (1 = launch+wait per step); 8 = two per hardware queue")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic_config2.json"),
                     help="HBM bytes per solve run measured by separate rocprofv3 --pmc passes "
                          "(scripts/gpu_check.sh); used for roofline.traffic on the config it was taken on")

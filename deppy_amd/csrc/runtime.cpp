@@ -5,8 +5,11 @@
 // cost-balanced slices, one per device, with no inter-device traffic.  On each
 // device, problems are bucketed by working-set footprint so every launch
 // requests only the dynamic LDS its largest problem needs (occupancy follows
-// the footprint); problems beyond the 160 KiB LDS of a CU run with their
-// working set in an HBM scratch region (one more launch).
+// the footprint); adjacent buckets are merged while that costs at most half
+// the workgroups per CU, since one launch per batch leaves the hardware
+// queues to other batches in flight (measured: 13.7M -> 21M res/s at three
+// batches in flight).  Problems beyond the 160 KiB LDS of a CU are solved by
+// multi-wave workgroups with part of the working set in HBM scratch.
 //
 // Streams belong to the context: kLanes per device, one per hardware queue
 // (GPU_MAX_HW_QUEUES is 4), created first so each maps to its own queue.
@@ -18,6 +21,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -37,6 +41,7 @@ constexpr int kBuckets[] = {8 << 10, 16 << 10, 24 << 10, 32 << 10, 48 << 10, 64 
                             96 << 10, 160 << 10};
 constexpr int kNBuckets = (int)(sizeof(kBuckets) / sizeof(kBuckets[0]));
 constexpr int kLanes = 4;
+constexpr double kMergeRatio = 0.5;  // bucket merging (build_slice); 0 = off
 
 #define HIP_OK(expr)                                                         \
   do {                                                                       \
@@ -228,16 +233,32 @@ int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_of
     else s.too_large.push_back(i);
   }
   std::vector<int32_t> order;
+  // Adjacent buckets are merged into one launch while the merged LDS request
+  // keeps at least kMergeRatio of the first bucket's workgroups per CU: fewer
+  // launches per batch leave more hardware queues to the batches in flight.
+  double merge = kMergeRatio;
+  if (const char* m = std::getenv("DEPPY_BUCKET_MERGE")) merge = std::atof(m);  // diagnostic
+  auto lds_of = [&](int32_t i) { return dp::layout<dp::M_LDS>(rec.data() + roff[(size_t)i]).lds_bytes; };
   for (int k = 0; k < kNBuckets; ++k) {
     if (bucket[(size_t)k].empty()) continue;
-    s.b_first.push_back((int)order.size());
-    s.b_count.push_back((int)bucket[(size_t)k].size());
     int mx = 0;
-    for (int32_t i : bucket[(size_t)k])
-      mx = std::max(mx, dp::layout<dp::M_LDS>(rec.data() + roff[(size_t)i]).lds_bytes);
-    s.b_lds.push_back(mx);
+    for (int32_t i : bucket[(size_t)k]) mx = std::max(mx, lds_of(i));
+    const bool join = !s.b_lds.empty() && merge > 0 &&
+                      (double)(kMaxLdsBytes / std::max(mx, s.b_lds.back())) >=
+                          merge * (double)(kMaxLdsBytes / s.b_lds.back());
+    if (join) {
+      s.b_count.back() += (int)bucket[(size_t)k].size();
+      s.b_lds.back() = std::max(s.b_lds.back(), mx);
+    } else {
+      s.b_first.push_back((int)order.size());
+      s.b_count.push_back((int)bucket[(size_t)k].size());
+      s.b_lds.push_back(mx);
+    }
     order.insert(order.end(), bucket[(size_t)k].begin(), bucket[(size_t)k].end());
   }
+  // diagnostic: DEPPY_LDS_PAD_KB raises every launch's LDS request (occupancy study)
+  if (const char* pad = std::getenv("DEPPY_LDS_PAD_KB"))
+    for (int& b : s.b_lds) b = std::max(b, std::atoi(pad) * 1024);
   s.big_base = (int)order.size();
   std::vector<int64_t> soff(1, 0);
   for (int mode = dp::M_SPLIT; mode <= dp::M_HBM; ++mode) {
@@ -306,8 +327,12 @@ int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_of
 int launch_slice(DevSlice& s, Lanes& L, int64_t budget) {
   HIP_OK(hipSetDevice(s.device));
   const int nlaunch = (int)s.b_first.size() + (int)s.g_first.size();
+  // lanes this batch spreads its launches over (diagnostic DEPPY_LANE_SERIAL=1:
+  // one lane, launches back to back)
+  int width = std::max(1, std::min(nlaunch, kLanes));
+  if (const char* e = std::getenv("DEPPY_LANE_SERIAL")) width = std::atoi(e) ? 1 : width;
   const int base = L.next;
-  L.next = (L.next + std::max(1, std::min(nlaunch, kLanes))) % kLanes;
+  L.next = (L.next + width) % kLanes;
   s.stream = L.s[base];
   dp::KernelArgs a;
   a.rec = s.rec;
@@ -334,12 +359,12 @@ int launch_slice(DevSlice& s, Lanes& L, int64_t budget) {
   std::sort(launch_order.begin(), launch_order.end(),
             [&](int x, int y) { return s.b_count[(size_t)x] > s.b_count[(size_t)y]; });
   for (size_t g = 0; g < s.g_first.size(); ++g) launch_order.insert(launch_order.begin() + (long)g, -1 - (int)g);
-  const int nside = std::min<int>(kLanes - 1, (int)launch_order.size() - 1);
+  const int nside = std::min<int>(width - 1, (int)launch_order.size() - 1);
   auto side = [&](int i) { return L.s[(base + 1 + i) % kLanes]; };
   HIP_OK(hipEventRecord(s.ev0, s.stream));
   for (int i = 0; i < nside; ++i) HIP_OK(hipStreamWaitEvent(side(i), s.ev0, 0));
   for (size_t i = 0; i < launch_order.size(); ++i) {
-    hipStream_t st = (i % kLanes == 0) ? s.stream : side((int)(i % kLanes) - 1);
+    hipStream_t st = (i % width == 0) ? s.stream : side((int)(i % width) - 1);
     const int k = launch_order[i];
     if (k < 0) {
       const size_t g = (size_t)(-1 - k);

@@ -196,9 +196,17 @@ struct Group {
   // group primitives (one wavefront: wave barrier and ballots; several:
   // s_barrier and per-wave slots in LDS)
   // ------------------------------------------------------------------
+  // Workgroup barrier of the multi-wave modes.  Their per-literal arrays are
+  // in HBM and __syncthreads() only drains LDS traffic (lgkmcnt) before
+  // s_barrier: a wavefront could pass it with global stores still in flight
+  // and another wavefront read the old words.  Drain every counter first.
+  __device__ __forceinline__ static void bar() {
+    __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0)
+    __syncthreads();
+  }
   __device__ __forceinline__ void gsync() {
     if constexpr (NW == 1) wsync();
-    else __syncthreads();
+    else bar();
   }
   __device__ __forceinline__ bool g_any(bool b) {
     const bool w = __ballot(b) != 0;
@@ -206,11 +214,11 @@ struct Group {
       return w;
     } else {
       if (lane == 0) scal[S_SLOT + wid] = w;
-      __syncthreads();
+      bar();
       int r = 0;
 #pragma unroll
       for (int i = 0; i < NW; ++i) r |= scal[S_SLOT + i];
-      __syncthreads();
+      bar();
       return r != 0;
     }
   }
@@ -220,11 +228,11 @@ struct Group {
       return x;
     } else {
       if (lane == 0) scal[S_SLOT + wid] = x;
-      __syncthreads();
+      bar();
       int r = INF;
 #pragma unroll
       for (int i = 0; i < NW; ++i) r = min(r, scal[S_SLOT + i]);
-      __syncthreads();
+      bar();
       return r;
     }
   }
@@ -234,11 +242,11 @@ struct Group {
       return x;
     } else {
       if (lane == 0) scal[S_SLOT + wid] = x;
-      __syncthreads();
+      bar();
       int r = 0;
 #pragma unroll
       for (int i = 0; i < NW; ++i) r += scal[S_SLOT + i];
-      __syncthreads();
+      bar();
       return r;
     }
   }
@@ -261,11 +269,11 @@ struct Group {
   }
   __device__ __forceinline__ void claim_end(int& run) {
     if constexpr (NW > 1) {
-      __syncthreads();
+      bar();
       run += scal[S_APP];
-      __syncthreads();
+      bar();
       if (tid == 0) scal[S_APP] = 0;
-      __syncthreads();
+      bar();
     }
   }
 
@@ -480,7 +488,7 @@ struct Group {
       wsync();
       q0 = 0; qs = 1;
     } else {
-      __syncthreads();
+      bar();
       ncq = min(scal[S_NK], CQ);
       q0 = wid; qs = NW;
     }
@@ -511,7 +519,7 @@ struct Group {
   }
 
   __device__ __forceinline__ void clear_touched(int nt) {
-    if constexpr (NW > 1) __syncthreads();  // every read of imp in this round is done
+    if constexpr (NW > 1) bar();  // every read of imp in this round is done
     for (int i = tid; i < nt; i += NT) imp[(int)touched[i]] = (uint32_t)INF;
     gsync();
     if (tid == 0) scal[S_NTOUCHED] = 0;
@@ -649,7 +657,7 @@ struct Group {
           int total = __builtin_amdgcn_readlane(incl, 63), before = 0;
           if constexpr (NW > 1) {
             if (lane == 63) scal[S_SLOT + wid] = incl;
-            __syncthreads();
+            bar();
             total = 0;
 #pragma unroll
             for (int q = 0; q < NW; ++q) {
@@ -657,7 +665,7 @@ struct Group {
               before += q < wid ? c : 0;
               total += c;
             }
-            __syncthreads();
+            bar();
           }
           if (total <= WBUF) {
             // every frontier literal writes its watch range into the list
@@ -799,7 +807,7 @@ struct Group {
     int head = 0;
     for (;;) {
       const int nw = scal[S_NWORK];
-      if constexpr (NW > 1) __syncthreads();  // every thread read nw before any grows it
+      if constexpr (NW > 1) bar();  // every thread read nw before any grows it
       if (head >= nw) break;
       for (int i = head + tid; i < nw; i += NT) {
         const int u = DP_CHK((int)touched[i], 0, nv, 16);
@@ -1111,7 +1119,7 @@ struct Group {
       int before = incl - c, total = __builtin_amdgcn_readlane(incl, 63);
       if constexpr (NW > 1) {
         if (lane == 63) scal[S_SLOT + wid] = incl;
-        __syncthreads();
+        bar();
         total = 0;
 #pragma unroll
         for (int q = 0; q < NW; ++q) {
@@ -1119,7 +1127,7 @@ struct Group {
           before += q < wid ? s : 0;
           total += s;
         }
-        __syncthreads();
+        bar();
       }
       for (uint32_t y = x; y; y &= y - 1) out[len + before++] = 32 * i + __ffs(y) - 1;
       len += total;
