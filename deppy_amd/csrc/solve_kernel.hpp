@@ -172,7 +172,9 @@ struct Group {
   int tr_cap, tr_len;
   bool tr_stop;
 #ifdef DP_STAMPS
-  int64_t acc[5];  // round eval cycles, round finish cycles, rounds, 1-literal rounds, push+pop cycles
+  // round eval cycles, round finish cycles, rounds, 1-literal rounds, push_guess cycles,
+  // search Solve() cycles, pop_guess cycles, push_guess calls
+  int64_t acc[8];
   unsigned long long* dbg;  // [first code, value, bound, failures]
   __device__ __noinline__ int chk_fail(int x, int hi, int code) {
     if (dbg) {
@@ -302,6 +304,30 @@ struct Group {
       IX* b = reinterpret_cast<IX*>(lds + L.body);
       const int groups = (h[DP_H_IMG] - DP_H_SIZE + 3) >> 2;
       const int4* src = reinterpret_cast<const int4*>(grec + DP_H_SIZE);
+      if (L.body == 0 && ((groups + 63) >> 6) * 1024 <= L.lds_bytes) {
+        // Stage the int32 image into the allocation with LDS-DMA (every
+        // 1 KiB piece in flight at once: one memory latency), then narrow it
+        // in place: piece c is read from [1024c, +1024) and written to
+        // [512c, +512), below every piece not yet read.  The arrays the
+        // staging overwrites are initialised after this.
+        for (int c = 0; c < groups; c += 64) {
+          const int i = min(c + lane, groups - 1);
+          __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src + i),
+                                           (__attribute__((address_space(3))) void*)(lds + 16 * c), 16, 0, 0);
+        }
+        __builtin_amdgcn_s_waitcnt(0);
+        wsync();
+        for (int c = 0; c < groups; c += 64) {
+          const int i = c + lane;
+          const int4 x = reinterpret_cast<const int4*>(lds)[min(i, groups - 1)];
+          if (i < groups) {  // the store depends on the load: this piece is read first
+            uint2 y;
+            y.x = (uint32_t)(x.x & 0xffff) | ((uint32_t)x.y << 16);
+            y.y = (uint32_t)(x.z & 0xffff) | ((uint32_t)x.w << 16);
+            reinterpret_cast<uint2*>(b)[i] = y;
+          }
+        }
+      } else
       for (int i = tid; i < groups; i += NT) {
         const int4 x = src[i];
         uint2 y;
@@ -364,7 +390,7 @@ struct Group {
     tr_cap = tr_len = 0;
     tr_stop = false;
 #ifdef DP_STAMPS
-    for (int i = 0; i < 5; ++i) acc[i] = 0;
+    for (int i = 0; i < 8; ++i) acc[i] = 0;
     dbg = nullptr;
 #endif
 
@@ -857,6 +883,19 @@ struct Group {
   // every clause row (same answer as the oracle's full scan).
   __device__ __forceinline__ int first_violated() {
     int best = INF;
+    if (nc <= 4 * NT) {
+      // few rows: every thread scans its rows in ascending order (the
+      // oracle's scan, a short dependent chain per thread)
+      for (int c = tid; c < nc; c += NT) {
+        int fu;
+        if (row_on(c) && violated(c, fu)) { best = c; break; }
+      }
+      best = g_min(best);
+      if (best == INF) return -1;
+      int fu;
+      violated(best, fu);
+      return fu;
+    }
     for (int i = tid; i < tlen; i += NT) {
       const int l = trail[i];
       if (l & 1) continue;  // only variables assigned true own violations
@@ -1071,7 +1110,13 @@ struct Group {
     for (;;) {
       if (dq_n == 0 && result == 0) {
         if (tr) fill_bits(used, nid, false);
+#ifdef DP_STAMPS
+        const int64_t ts = stamp();
         const int r = search_solve();
+        DP_ACC(5, stamp() - ts);
+#else
+        const int r = search_solve();
+#endif
         from_solve = true;
         if (r == RS_BUDGET) { result = RS_BUDGET; break; }
         result = r;
@@ -1081,7 +1126,13 @@ struct Group {
       if (result < 0) {
         if (tr) trace_event(from_solve);  // h.tracer.Trace(h), search.go:173
         if (ng == 0) break;
+#ifdef DP_STAMPS
+        const int64_t tq = stamp();
         pop_guess();
+        DP_ACC(6, stamp() - tq);
+#else
+        pop_guess();
+#endif
         from_solve = false;
         continue;
       }
@@ -1090,6 +1141,7 @@ struct Group {
       const int64_t tp = stamp();
       push_guess();
       DP_ACC(4, stamp() - tp);
+      DP_ACC(7, 1);
 #else
       push_guess();
 #endif
@@ -1352,6 +1404,7 @@ __global__ void __launch_bounds__(64 * mode_waves(MODE)) solve_kernel(KernelArgs
     for (int i = 0; i < 5; ++i) o[5 + i] = W.acc[i];
     o[10] = wall0;
     o[11] = wallclock();
+    for (int i = 5; i < 8; ++i) o[11 + i] = W.acc[i];
   }
 #endif
   if (W.tr_stop) flags |= DP_F_TRACE_TRUNCATED;

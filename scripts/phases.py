@@ -14,9 +14,10 @@ import numpy as np  # noqa: E402
 from deppy_amd import _lib  # noqa: E402
 from tests.gpu_common import lowered_config  # noqa: E402
 
-NS = 16
+NS = 20
 NAMES = ["init", "base", "search", "epilogue", "core", "round_eval", "round_finish", "rounds",
          "rounds_1lit", "push_guess"]
+EXTRA = {16: "search_solve", 17: "pop_guess", 18: "pushes"}
 L = _lib.lib()
 L.dp_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _lib.c_i64p]
 config = int(sys.argv[1]) if len(sys.argv) > 1 else 2
@@ -40,6 +41,7 @@ for n in sizes:
             continue
         out[cls] = {"count": int(mask.sum()),
                     **{nm: [int(np.mean(st[mask, i])), int(np.percentile(st[mask, i], 99))] for i, nm in enumerate(NAMES)},
+                    **{nm: [int(np.mean(st[mask, i])), int(np.percentile(st[mask, i], 99))] for i, nm in EXTRA.items()},
                     "total_mean": int(cyc[mask].mean()), "total_max": int(cyc[mask].max())}
     # wall-clock timeline (us): when waves start / end relative to the first start
     w0 = st[:, 10].min()
