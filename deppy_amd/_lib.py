@@ -20,6 +20,8 @@ OPT_FORCE_HBM = 1 << 1
 F_TRACE_TRUNCATED = 1 << 8
 if os.environ.get("DEPPY_STAMPS") == "1":  # diagnostic phase-stamp build (scripts/ only)
     LIB_PATH = os.path.join(HERE, os.environ.get("DEPPY_STAMPS_LIB", "libdeppy_hip_stamps.so"))
+elif os.environ.get("DEPPY_VARIANT_LIB"):  # a tagged release variant (measurement scripts only)
+    LIB_PATH = os.path.join(HERE, os.environ["DEPPY_VARIANT_LIB"])
 
 c_i32p = ctypes.POINTER(ctypes.c_int32)
 c_i64p = ctypes.POINTER(ctypes.c_int64)

@@ -34,8 +34,8 @@ def build(verbose: bool = False, extra: list[str] | None = None, stamps: bool = 
     if stamps:
         extra = (extra or []) + ["-DDP_STAMPS"]
         obj, lib = OBJ + "_stamps" + tag, STAMPS_LIB.replace(".so", tag + ".so")
-    else:
-        obj, lib = OBJ, LIB
+    else:  # a tagged release variant (measurement only) never replaces the product library
+        obj, lib = OBJ + tag, LIB.replace(".so", tag + ".so")
     return _build(verbose, extra, obj, lib)
 
 

@@ -205,6 +205,9 @@ struct Group {
   __device__ __forceinline__ static void bar() {
     __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0)
     __syncthreads();
+#ifdef DP_BAR_INV
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // diagnostic: drop L1 after each barrier
+#endif
   }
   __device__ __forceinline__ void gsync() {
     if constexpr (NW == 1) wsync();
@@ -759,6 +762,11 @@ struct Group {
   }
 
   __device__ __forceinline__ void assign_one(int l, int why, int decision) {
+    // Callers decide on reads of val (test_assume's lit_val, dpll's
+    // violated): with several wavefronts, no thread may still be reading when
+    // thread 0 writes, or a late wavefront sees the new value and branches
+    // differently (one wavefront reads before it writes, in program order).
+    if constexpr (NW > 1) bar();
     if (tid == 0) {
       const int v = DP_CHK(l, 0, 2 * nv, 30) >> 1;
       val[v] = (l & 1) ? -1 : 1; reason[v] = enc(why); rs[v] = enc(tlen);
