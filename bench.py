@@ -40,6 +40,19 @@ METRIC = "resolutions/sec (node) on synthetic catalogs at 1/2/4/8 GPUs; BCP HBM 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
+# BASELINE.json configs as bench workloads: (default catalogs per GPU, description)
+WORKLOADS = {
+    2: (10000, "config2: %d synthetic operator catalogs per GPU (P=40 packages, ~240 variables; "
+               "Dependency+Conflict+AtMost), one wavefront per catalog"),
+    3: (125000, "config3: %d small catalogs per GPU (P~U{4..12}, ~20-70 variables; 1M over 8 GPUs "
+                "by host partition), one wavefront per catalog"),
+    4: (256, "config4: %d OLM-scale catalogs per GPU (P=5000, ~55k variables, deep dependency "
+             "chains), one 8-wave workgroup per catalog"),
+    5: (10000, "config5: %d mixed-size catalogs per GPU (P~U{4..400}, 50%% with injected "
+               "infeasibility), UNSAT-heavy"),
+}
+
+
 def lowered_config(config, n, seed):
     w = _lib.generate(config, n, seed)
     wa = _lib.WireArrays(**{k: w[k] for k in (
@@ -71,7 +84,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=2)
-    ap.add_argument("--problems", type=int, default=10000)
+    ap.add_argument("--problems", type=int, default=0,
+                    help="catalogs per GPU (0: the config's default, WORKLOADS)")
     ap.add_argument("--seed", type=int, default=1000)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -82,6 +96,8 @@ def main():
                     help="HBM bytes per solve run measured by separate rocprofv3 --pmc passes "
                          "(scripts/gpu_check.sh); used for roofline.traffic on the config it was taken on")
     args = ap.parse_args()
+    if args.problems <= 0:
+        args.problems = WORKLOADS[args.config][0]
 
     g = shard.init_from_env("nccl")
     rank, world, local = g.rank, g.world, g.local
@@ -154,10 +170,7 @@ def main():
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic",
-        "config": {"workload": "config2: %d synthetic operator catalogs per GPU (P=40 packages,"
-                               " ~240 variables; Dependency+Conflict+AtMost), one wavefront per"
-                               " catalog" % args.problems if args.config == 2 else
-                               "config%d: %d catalogs per GPU" % (args.config, args.problems),
+        "config": {"workload": WORKLOADS[args.config][1] % args.problems,
                    "catalogs_per_gpu": args.problems, "parallelism": "dp%d (host partition)" % world,
                    "seed": args.seed},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,

@@ -113,13 +113,70 @@ namespace {
 
 constexpr int32_t kF = 0, kT = 1;
 
+// Open-addressing hash map from 64-bit keys to int32 values, with
+// generation-stamped slots: reset() is O(1), so one table serves every
+// problem a worker lowers (std::unordered_map cost ~0.3 s per OLM-scale
+// catalog in node allocation alone).
+struct FlatMap {
+  std::vector<uint64_t> key;
+  std::vector<int32_t> val;
+  std::vector<uint32_t> gen;
+  uint32_t cur = 1;
+  size_t count = 0, mask = 0;
+  FlatMap() { grow(1024); }
+  void grow(size_t cap) {
+    std::vector<uint64_t> k2(cap);
+    std::vector<int32_t> v2(cap);
+    std::vector<uint32_t> g2(cap, 0);
+    const size_t m2 = cap - 1;
+    for (size_t i = 0; i < key.size(); ++i)
+      if (gen[i] == cur) {
+        size_t h = hash(key[i]) & m2;
+        while (g2[h] == cur) h = (h + 1) & m2;
+        k2[h] = key[i]; v2[h] = val[i]; g2[h] = cur;
+      }
+    key.swap(k2); val.swap(v2); gen.swap(g2);
+    mask = m2;
+  }
+  static size_t hash(uint64_t x) {
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33;
+    return (size_t)x;
+  }
+  void reset() {
+    count = 0;
+    if (++cur == 0) {  // generation wrap: clear for real
+      std::fill(gen.begin(), gen.end(), 0u);
+      cur = 1;
+    }
+  }
+  // the value of k, or -1
+  int32_t find(uint64_t k) const {
+    for (size_t h = hash(k) & mask; gen[h] == cur; h = (h + 1) & mask)
+      if (key[h] == k) return val[h];
+    return -1;
+  }
+  // insert k -> v (k must be absent)
+  void insert(uint64_t k, int32_t v) {
+    if (2 * (count + 1) > key.size()) grow(2 * key.size());
+    size_t h = hash(k) & mask;
+    while (gen[h] == cur) h = (h + 1) & mask;
+    key[h] = k; val[h] = v; gen[h] = cur;
+    ++count;
+  }
+  int32_t* find_slot(uint64_t k) {
+    for (size_t h = hash(k) & mask; gen[h] == cur; h = (h + 1) & mask)
+      if (key[h] == k) return &val[h];
+    return nullptr;
+  }
+};
+
 // And-inverter graph with structural hashing (gini logic.C).
 struct Aig {
   int32_t next_node = 1;
-  std::unordered_map<uint64_t, int32_t> strash;
+  FlatMap strash;
   void reset(int nv) {
     next_node = 1 + nv;
-    strash.clear();
+    strash.reset();
   }
   static int32_t input(int v) { return 2 * (v + 1); }
   int32_t And(int32_t a, int32_t b) {
@@ -130,29 +187,33 @@ struct Aig {
     if (a == (b ^ 1)) return kF;
     if (a > b) std::swap(a, b);
     uint64_t key = ((uint64_t)(uint32_t)a << 32) | (uint32_t)b;
-    auto it = strash.find(key);
-    if (it != strash.end()) return it->second;
+    const int32_t hit = strash.find(key);
+    if (hit >= 0) return hit;
     int32_t g = 2 * next_node++;
-    strash.emplace(key, g);
+    strash.insert(key, g);
     return g;
   }
   int32_t Or(int32_t a, int32_t b) { return And(a ^ 1, b ^ 1) ^ 1; }
 };
 
-// Batcher odd-even merge sort comparators for n = 2^k (gini CardSort, recalled).
+// Batcher odd-even merge sort comparators for n = 2^k (gini CardSort,
+// recalled).  Built once per k (k < 31), then read without a lock.
 const std::vector<std::pair<int, int>>& batcher(int n) {
   static std::mutex mu;
-  static std::unordered_map<int, std::vector<std::pair<int, int>>> cache;
+  static std::atomic<const std::vector<std::pair<int, int>>*> table[31];
+  int k = 0;
+  while ((1 << k) < n) ++k;
+  if (const auto* t = table[k].load(std::memory_order_acquire)) return *t;
   std::lock_guard<std::mutex> lk(mu);
-  auto it = cache.find(n);
-  if (it != cache.end()) return it->second;
-  std::vector<std::pair<int, int>> v;
+  if (const auto* t = table[k].load(std::memory_order_relaxed)) return *t;
+  auto* v = new std::vector<std::pair<int, int>>();  // kept for the process lifetime
   for (int p = 1; p < n; p <<= 1)
-    for (int k = p; k >= 1; k >>= 1)
-      for (int j = k % p; j < n - k; j += 2 * k)
-        for (int i = 0; i < std::min(k, n - j - k); ++i)
-          if ((i + j) / (2 * p) == (i + j + k) / (2 * p)) v.emplace_back(i + j, i + j + k);
-  return cache.emplace(n, std::move(v)).first->second;
+    for (int q = p; q >= 1; q >>= 1)
+      for (int j = q % p; j < n - q; j += 2 * q)
+        for (int i = 0; i < std::min(q, n - j - q); ++i)
+          if ((i + j) / (2 * p) == (i + j + q) / (2 * p)) v->emplace_back(i + j, i + j + q);
+  table[k].store(v, std::memory_order_release);
+  return *v;
 }
 
 struct Out {  // per-thread output chunk
@@ -168,7 +229,7 @@ struct Work {  // per-thread scratch
   Aig aig;
   std::vector<int64_t> stamp;  // interned path: string -> (tag << 32 | var)
   std::unordered_map<std::string_view, int32_t> names;
-  std::unordered_map<int32_t, int32_t> key_ident;
+  FlatMap key_ident;  // gate literal -> identity
   std::vector<int32_t> owner_v, owner_c;
   std::vector<int32_t> clause_off, clause_lits, clause_id;
   std::vector<int32_t> card_off, card_lits, card_bound, card_id;
@@ -226,7 +287,7 @@ struct Lowerer {
 
     Aig& aig = W.aig;
     aig.reset(nv);
-    W.key_ident.clear();
+    W.key_ident.reset();
     W.owner_v.clear(); W.owner_c.clear();
     W.clause_off.assign(1, 0); W.clause_lits.clear(); W.clause_id.clear();
     W.card_off.assign(1, 0); W.card_lits.clear(); W.card_bound.clear(); W.card_id.clear();
@@ -270,16 +331,16 @@ struct Lowerer {
           }
         }
         if (bad || !W.errs.empty() || m == kT) continue;
-        auto it = W.key_ident.find(m);
-        if (it == W.key_ident.end()) {
+        int32_t* slot = W.key_ident.find_slot((uint64_t)(uint32_t)m);
+        if (!slot) {
           int32_t ident = (int32_t)W.owner_v.size();
-          W.key_ident.emplace(m, ident);
+          W.key_ident.insert((uint64_t)(uint32_t)m, ident);
           W.owner_v.push_back(vi);
           W.owner_c.push_back(ci);
           emit_rows(W, m, nv, kind, vi, w.con_n[c], a0, a1, ident);
         } else {
-          W.owner_v[it->second] = vi;  // last writer wins, lit_mapping.go:69-72
-          W.owner_c[it->second] = ci;
+          W.owner_v[*slot] = vi;  // last writer wins, lit_mapping.go:69-72
+          W.owner_c[*slot] = ci;
         }
       }
     }
@@ -471,8 +532,10 @@ int dp_lower(const dp_wire* wire, dp_lowered** out) {
   const int32_t P = wire->n_problems;
   unsigned hw = std::thread::hardware_concurrency();
   int nt = (int)std::min<unsigned>(hw ? hw : 1, 16);
-  if (P < 256) nt = 1;
-  const int32_t chunk = 64;
+  // threads by work (constraint arguments), chunks small enough to balance
+  const int64_t work = P ? wire->con_arg_off[wire->var_con_off[wire->prob_var_off[P]]] : 0;
+  if (work < 200000) nt = 1;
+  const int32_t chunk = (int32_t)std::max<int64_t>(1, std::min<int64_t>(64, P / (8 * (int64_t)nt)));
   const int32_t nchunks = (P + chunk - 1) / chunk;
   std::vector<dp::Out> outs((size_t)std::max(nchunks, 1));
   dp::Lowerer L(*wire);
