@@ -163,7 +163,8 @@ struct Group {
   int64_t steps, budget;
   bool budget_hit;
   int ck, c_row, c_var, c_rp, c_rn;
-  bool collect_guess, learn_on;
+  bool collect_guess;
+  int learn_lo;  // learned rows below learn_lo are switched off (core refutations)
   int nl;
   const uint32_t* enabled;  // nullptr: every row
   bool extra_mode;
@@ -384,7 +385,7 @@ struct Group {
     budget_hit = false;
     ck = CK_NONE; c_row = c_var = c_rp = c_rn = 0;
     collect_guess = false;
-    learn_on = true;
+    learn_lo = 0;
     nl = 0;
     enabled = nullptr;
     extra_mode = false;
@@ -543,8 +544,7 @@ struct Group {
 
   // learned rows are evaluated in every round (threads over rows)
   __device__ __forceinline__ void eval_learned(int& crow) {
-    if (!learn_on) return;
-    for (int j = tid; j < nl; j += NT) eval_row(nrows + j, crow);
+    for (int j = learn_lo + tid; j < nl; j += NT) eval_row(nrows + j, crow);
   }
 
   __device__ __forceinline__ void clear_touched(int nt) {
@@ -752,7 +752,7 @@ struct Group {
   // gini Untest() (search.go:84): the learned rows decide the restored scope
   __device__ __forceinline__ int untest_to(int mark) {
     truncate_to(mark);
-    if (learn_on && nl > 0) {
+    if (nl > learn_lo) {
       int crow = INF;
       eval_learned(crow);
       if (finish_round(crow) < 0) return -1;
@@ -1008,6 +1008,7 @@ struct Group {
   // ------------------------------------------------------------------
   int dq_head, dq_n, ng, result;
   bool class_b, solve_unsat, last_solve;
+  bool final_from_solve;  // the search's last failure came from Solve() (else Test/Untest)
 
   // choice lists: rows 0..nch-1; the singleton list of anchor v is nch + v
   __device__ __forceinline__ int list_len(int list) const {
@@ -1113,11 +1114,20 @@ struct Group {
     result = 0;
     class_b = solve_unsat = last_solve = false;
     for (int i = 0; i < na; ++i) dq_push_back(nch + (int)anchors[i], 0);
-    gsync();
+    // `used` collects the identities of every conflict analysis of the
+    // search's Solve() calls (the derivations of its learned nogoods): with
+    // the final root conflict, an unsatisfiable set when the search fails
+    // (oracle: search_do).  With tracing, `used` holds the current step's
+    // identities and `en` the rest of the union.
+    fill_bits(used, nid, false);
+    fill_bits(en, nid, false);
     bool from_solve = false;
     for (;;) {
       if (dq_n == 0 && result == 0) {
-        if (tr) fill_bits(used, nid, false);
+        if (tr) {
+          or_bits(en, used, nid);
+          fill_bits(used, nid, false);
+        }
 #ifdef DP_STAMPS
         const int64_t ts = stamp();
         const int r = search_solve();
@@ -1156,6 +1166,8 @@ struct Group {
       from_solve = false;
       if (budget_hit) { result = RS_BUDGET; break; }
     }
+    final_from_solve = from_solve;
+    or_bits(used, en, nid);
     // Value() after an ending on Test()==1 reads that scope's full assignment
     if (result == 1 && !last_solve) save_model();
     return result;
@@ -1202,7 +1214,8 @@ struct Group {
   // Solve() left the union of its refutation's analyses in `used`.
   __device__ __forceinline__ void trace_event(bool from_solve) {
     if (tr_stop) return;
-    if (!from_solve) {
+    if (!from_solve) {  // a trace-only analysis: kept out of the union
+      or_bits(en, used, nid);
       fill_bits(used, nid, false);
       analyze();
     }
@@ -1211,7 +1224,11 @@ struct Group {
     for (int i = tid; i < nbi; i += NT) ni += __popc(ld_bits(&used[i]));
     ngv = g_sum(ngv);
     ni = g_sum(ni);
-    if (tr_len + 2 + ngv + ni > tr_cap) { tr_stop = true; return; }
+    if (tr_len + 2 + ngv + ni > tr_cap) {
+      tr_stop = true;
+      if (!from_solve) fill_bits(used, nid, false);
+      return;
+    }
     int32_t* o = tr + tr_len;
     if (tid == 0) {
       int k = 0;
@@ -1225,6 +1242,7 @@ struct Group {
     emit_bits(used, nbi, o + 2 + ngv);
     tr_len += 2 + ngv + ni;
     gsync();
+    if (!from_solve) fill_bits(used, nid, false);
   }
 
   __device__ __forceinline__ void fill_bits(uint32_t* bs, int n, bool ones) {
@@ -1240,10 +1258,17 @@ struct Group {
     for (int i = tid; i < bits_words(n); i += NT) dst[i] = ld_bits(&src[i]);
     gsync();
   }
+  __device__ __forceinline__ void or_bits(uint32_t* dst, const uint32_t* src, int n) {
+    for (int i = tid; i < bits_words(n); i += NT) dst[i] |= ld_bits(&src[i]);
+    gsync();
+  }
 
   __device__ __forceinline__ int refute(const uint32_t* K) {
     reset_all();
-    learn_on = false;
+    // the search's learned rows are not part of the base formula; the rows
+    // this refutation's own Solve() learns are (oracle: refute)
+    const int lo = learn_lo;
+    learn_lo = nl;
     enabled = K;
     fill_bits(used, nid, false);
     int r;
@@ -1251,7 +1276,7 @@ struct Group {
     else r = dpll();
     reset_all();
     enabled = nullptr;
-    learn_on = true;
+    learn_lo = lo;
     return r;
   }
 
@@ -1259,10 +1284,14 @@ struct Group {
     const int64_t saved = steps;
     steps = 0;
     int len = 0;
-    fill_bits(en, nid, true);
-    int r = refute(en);
+    // start from the identities of the solve's own refutation (`used`: the
+    // base conflict, or the search's union), an unsatisfiable set: no fresh
+    // refutation of the whole catalog (oracle: core_extract)
+    copy_bits(en, used, nid);
+    int any = 0;
+    for (int i = tid; i < nbi; i += NT) any |= en[i] != 0u;
+    int r = g_any(any) ? RS_UNSAT : RS_BUDGET;
     if (r == RS_UNSAT) {
-      copy_bits(en, used, nid);
       for (int id = 0; id < nid; ++id) {
         if ((id & 31) == 0 && en[id >> 5] == 0) { id += 31; continue; }  // empty word
         if (!getb(en, id)) continue;
@@ -1382,6 +1411,8 @@ __global__ void __launch_bounds__(64 * mode_waves(MODE)) solve_kernel(KernelArgs
   if (base < 0) {
     flags |= DP_F_BASE_UNSAT;
     status = DP_UNSAT;
+    W.fill_bits(W.used, W.nid, false);
+    W.analyze();  // the base conflict's identities start the explanation
   } else if (base == 1) {
     flags |= DP_F_SEARCH_SKIPPED;
     W.save_model();
@@ -1396,6 +1427,7 @@ __global__ void __launch_bounds__(64 * mode_waves(MODE)) solve_kernel(KernelArgs
       status = DP_INCOMPLETE;
     } else if (r < 0) {
       status = DP_UNSAT;
+      if (!W.final_from_solve) W.analyze();  // the final root conflict (an Untest)
     } else {
       status = W.epilogue(flags, inst);
       if (status == DP_INCOMPLETE) flags |= DP_F_BUDGET;

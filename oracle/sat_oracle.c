@@ -87,10 +87,11 @@ typedef struct {
   uint8_t* d_flip;
   /* learned nogoods of failed Solve() calls: rows nrows.. (see learn()) */
   int32_t *l_off, *l_lits;
-  int32_t nl, lcap, learn_on, collect_guess;
+  int32_t nl, lcap, learn_lo, collect_guess; /* rows below learn_lo are switched off */
   uint8_t* fg; /* guesses met by the refutation of the current Solve() */
   int32_t* dix;    /* decision index of a Solve() decision variable, else -1 */
   uint8_t* dset;   /* decisions met by the last conflict analysis */
+  uint8_t* uacc; /* identities of the search's refutation (union over its analyses) */
   /* search trace (Tracer, search.go:173): event records, see oracle_solve_traced */
   int32_t* trace;
   int32_t trace_cap, trace_len, trace_stop;
@@ -163,6 +164,7 @@ static int st_init(st_t* s, const int32_t* rec) {
   s->is_extra = xcalloc((size_t)nv, 1);
   s->seen = xcalloc((size_t)nv, 1);
   s->used = xcalloc((size_t)p->nid, 1);
+  s->uacc = xcalloc((size_t)p->nid + 1, 1);
   s->work = xcalloc((size_t)nv, sizeof(int32_t));
   s->inS = xcalloc((size_t)nv, 1);
   s->model = xcalloc((size_t)(nv + 31) / 32, sizeof(uint32_t));
@@ -175,14 +177,14 @@ static int st_init(st_t* s, const int32_t* rec) {
   s->fg = xcalloc((size_t)nv, 1);
   s->dix = xcalloc((size_t)nv, sizeof(int32_t));
   s->dset = xcalloc((size_t)nv + 1, 1);
-  s->learn_on = 1;
+  s->learn_lo = 0;
   return 0;
 }
 
 static void st_free(st_t* s) {
   free(s->w_off); free(s->w); free(s->val); free(s->reason); free(s->rnd); free(s->trail);
   free(s->imp_pos); free(s->imp_neg); free(s->touched); free(s->is_extra); free(s->seen);
-  free(s->used); free(s->work); free(s->inS); free(s->model); free(s->d_lit); free(s->d_mark);
+  free(s->used); free(s->uacc); free(s->work); free(s->inS); free(s->model); free(s->d_lit); free(s->d_mark);
   free(s->d_flip); free(s->l_off); free(s->l_lits); free(s->fg); free(s->dix); free(s->dset);
 }
 
@@ -308,10 +310,10 @@ static int extra_check(st_t* s) {
   return 0;
 }
 
-/* Learned rows are evaluated in every round (they are few). */
+/* Learned rows are evaluated in every round (they are few); a core
+ * refutation switches off the rows learned before it (learn_lo). */
 static void eval_learned(st_t* s, int* crow) {
-  if (!s->learn_on) return;
-  for (int j = 0; j < s->nl; ++j) eval_row(s, s->p.nrows + j, crow);
+  for (int j = s->learn_lo; j < s->nl; ++j) eval_row(s, s->p.nrows + j, crow);
 }
 
 static int propagate(st_t* s) {
@@ -356,7 +358,7 @@ static void truncate_to(st_t* s, int mark) {
  * under unit propagation, learned rows included (search.go:84). */
 static int untest_to(st_t* s, int mark) {
   truncate_to(s, mark);
-  if (s->learn_on && s->nl > 0) {
+  if (s->nl > s->learn_lo) {
     int rd = ++s->round, crow = INF;
     eval_learned(s, &crow);
     if (finish_round(s, rd, crow) < 0) return -1;
@@ -544,6 +546,7 @@ struct search_s {
   int ng;
   int result;
   int class_b, solve_unsat, last_solve;
+  int final_from_solve; /* the last failure came from Solve() (else Test/Untest) */
 };
 
 static inline int list_len(const prob_t* p, int list) {
@@ -623,10 +626,20 @@ static int search_do(search_t* h, st_t* s, const backend_t* be, int32_t* lits, i
   h->head = h->n = h->ng = 0;
   h->result = 0;
   for (int i = 0; i < p->na; ++i) dq_push_back(h, (choice_t){~p->anchors[i], 0});
+  /* used[] collects the identities of every conflict analysis of the
+   * search's Solve() calls: the derivations of its learned nogoods, and so
+   * (with the final root conflict, analysed by the caller) an unsatisfiable
+   * identity set when the search fails.  With tracing, used[] holds the
+   * current step's identities and uacc[] the rest of the union. */
+  memset(s->used, 0, (size_t)p->nid);
+  memset(s->uacc, 0, (size_t)p->nid);
   int from_solve = 0;
   for (;;) {
     if (h->n == 0 && h->result == 0) {
-      if (s->trace) memset(s->used, 0, (size_t)p->nid);
+      if (s->trace) {
+        for (int i = 0; i < p->nid; ++i) s->uacc[i] |= s->used[i];
+        memset(s->used, 0, (size_t)p->nid);
+      }
       h->result = be->solve(be->u, s);
       h->last_solve = (h->result == 1);
       from_solve = 1;
@@ -645,6 +658,8 @@ static int search_do(search_t* h, st_t* s, const backend_t* be, int32_t* lits, i
     from_solve = 0;
     if (s->budget_hit) { h->result = R_BUDGET; break; }
   }
+  h->final_from_solve = from_solve;
+  for (int i = 0; i < p->nid; ++i) s->used[i] |= s->uacc[i];
   /* Value() after a Test()==1 ending reads the full assignment of that scope */
   if (h->result == 1 && !h->last_solve) save_model(s);
   int k = 0;
@@ -662,14 +677,19 @@ static int search_do(search_t* h, st_t* s, const backend_t* be, int32_t* lits, i
 static void trace_event(search_t* h, st_t* s, int from_solve) {
   if (s->trace_stop) return;
   const prob_t* p = &s->p;
-  if (!from_solve) {
+  if (!from_solve) {  /* a trace-only analysis: kept out of the union */
+    for (int i = 0; i < p->nid; ++i) s->uacc[i] |= s->used[i];
     memset(s->used, 0, (size_t)p->nid);
     analyze(s);
   }
   int ng = 0, ni = 0;
   for (int i = 0; i < h->ng; ++i) ng += h->g[i].m >= 0;
   for (int i = 0; i < p->nid; ++i) ni += s->used[i];
-  if (s->trace_len + 2 + ng + ni > s->trace_cap) { s->trace_stop = 1; return; }
+  if (s->trace_len + 2 + ng + ni > s->trace_cap) {
+    s->trace_stop = 1;
+    if (!from_solve) memset(s->used, 0, (size_t)p->nid);
+    return;
+  }
   int32_t* o = s->trace + s->trace_len;
   *o++ = ng;
   for (int i = 0; i < h->ng; ++i)
@@ -678,6 +698,7 @@ static void trace_event(search_t* h, st_t* s, int from_solve) {
   for (int i = 0; i < p->nid; ++i)
     if (s->used[i]) *o++ = i;
   s->trace_len += 2 + ng + ni;
+  if (!from_solve) memset(s->used, 0, (size_t)p->nid);
 }
 
 /* the real backend: our BCP */
@@ -732,7 +753,10 @@ static void reset_all(st_t* s) {
  * identities of every conflict the refutation met. */
 static int refute(st_t* s, const uint8_t* en) {
   reset_all(s);
-  s->learn_on = 0;
+  /* the search's learned rows are not part of the base formula; the rows
+   * this refutation's own Solve() learns are (they prune its search) */
+  const int lo = s->learn_lo;
+  s->learn_lo = s->nl;
   s->enabled = en;
   memset(s->used, 0, (size_t)s->p.nid);
   s->collect = 1;
@@ -742,7 +766,7 @@ static int refute(st_t* s, const uint8_t* en) {
   s->collect = 0;
   reset_all(s);
   s->enabled = NULL;
-  s->learn_on = 1;
+  s->learn_lo = lo;
   return r;
 }
 
@@ -750,12 +774,16 @@ static int core_extract(st_t* s, int32_t* core, int32_t* flags) {
   int nid = s->p.nid, len = 0;
   uint8_t* K = xcalloc((size_t)nid, 1);
   uint8_t* K2 = xcalloc((size_t)nid, 1);
-  memset(K, 1, (size_t)nid);
   int64_t saved_steps = s->steps;
   s->steps = 0; /* the explanation has its own budget */
-  int r = refute(s, K);
+  /* start from the identities of the solve's own refutation (used[]: the
+   * base conflict, or the search's union), an unsatisfiable set: no fresh
+   * refutation of the whole catalog */
+  memcpy(K, s->used, (size_t)nid);
+  int any = 0;
+  for (int id = 0; id < nid; ++id) any |= K[id];
+  int r = any ? R_UNSAT : R_BUDGET;
   if (r == R_UNSAT) {
-    memcpy(K, s->used, (size_t)nid);
     for (int id = 0; id < nid; ++id) {
       if (!K[id]) continue;
       memcpy(K2, K, (size_t)nid);
@@ -852,6 +880,8 @@ int oracle_solve_traced(const int32_t* rec, int64_t budget, int32_t* flags, uint
   if (base < 0) {
     *flags |= DP_F_BASE_UNSAT;
     status = DP_UNSAT;
+    memset(s.used, 0, (size_t)s.p.nid);
+    analyze(&s); /* the base conflict's identities start the explanation */
   } else if (base == 1) {
     *flags |= DP_F_SEARCH_SKIPPED;
     save_model(&s);
@@ -870,6 +900,7 @@ int oracle_solve_traced(const int32_t* rec, int64_t budget, int32_t* flags, uint
       status = DP_INCOMPLETE;
     } else if (r < 0) {
       status = DP_UNSAT;
+      if (!h.final_from_solve) analyze(&s); /* the final root conflict (an Untest) */
     } else {
       memset(s.inS, 0, (size_t)nv);
       for (int i = 0; i < nl; ++i) s.inS[lits[i]] = 1;
