@@ -208,15 +208,40 @@ int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_of
   HIP_OK(hipEventCreate(&s.ev1));
   for (auto& e : s.done) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   const int32_t n = s.p1 - s.p0;
+  // device images, built by up to 16 host threads into contiguous parts
+  // (each part is uploaded in place, no concatenation)
+  const unsigned hw = std::thread::hardware_concurrency();
+  const int T = (int)std::max<int64_t>(1, std::min<int64_t>({16, hw ? (int64_t)hw : 1, n / 256}));
+  std::vector<std::vector<int32_t>> parts((size_t)T);
+  std::vector<int64_t> len((size_t)n);
+  auto part_lo = [&](int t) { return (int32_t)((int64_t)n * t / T); };
+  auto build_part = [&](int t) {
+    std::vector<int32_t>& out = parts[(size_t)t];
+    for (int32_t i = part_lo(t); i < part_lo(t + 1); ++i) {
+      const size_t at = out.size();
+      build_image(b->rec + b->rec_off[s.p0 + i], out);
+      len[(size_t)i] = (int64_t)(out.size() - at);
+    }
+  };
+  if (T == 1) build_part(0);
+  else {
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t) th.emplace_back(build_part, t);
+    for (auto& x : th) x.join();
+  }
   std::vector<int64_t> roff((size_t)n + 1, 0);
-  std::vector<int32_t> rec;
-  for (int32_t i = 0; i < n; ++i) {
-    build_image(b->rec + b->rec_off[s.p0 + i], rec);
-    roff[(size_t)i + 1] = (int64_t)rec.size();
+  std::vector<const int32_t*> img((size_t)n);
+  for (int t = 0; t < T; ++t) {
+    size_t at = 0;
+    for (int32_t i = part_lo(t); i < part_lo(t + 1); ++i) {
+      img[(size_t)i] = parts[(size_t)t].data() + at;
+      at += (size_t)len[(size_t)i];
+      roff[(size_t)i + 1] = roff[(size_t)i] + len[(size_t)i];
+    }
   }
   std::vector<std::vector<int32_t>> bucket(kNBuckets), big(3);
   for (int32_t i = 0; i < n; ++i) {
-    const int32_t* r = rec.data() + roff[(size_t)i];
+    const int32_t* r = img[(size_t)i];
     const bool forced = opt_flags & (DP_OPT_FORCE_GROUP | DP_OPT_FORCE_HBM);
     const int64_t lds = dp::fits16(r) && !forced ? (int64_t)dp::layout<dp::M_LDS>(r).lds_bytes : INT64_MAX;
     int k = 0;
@@ -238,7 +263,7 @@ int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_of
   // launches per batch leave more hardware queues to the batches in flight.
   double merge = kMergeRatio;
   if (const char* m = std::getenv("DEPPY_BUCKET_MERGE")) merge = std::atof(m);  // diagnostic
-  auto lds_of = [&](int32_t i) { return dp::layout<dp::M_LDS>(rec.data() + roff[(size_t)i]).lds_bytes; };
+  auto lds_of = [&](int32_t i) { return dp::layout<dp::M_LDS>(img[(size_t)i]).lds_bytes; };
   for (int k = 0; k < kNBuckets; ++k) {
     if (bucket[(size_t)k].empty()) continue;
     int mx = 0;
@@ -268,7 +293,7 @@ int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_of
     s.g_mode.push_back(mode);
     int mx = 0;
     for (int32_t i : big[(size_t)mode]) {
-      const int32_t* r = rec.data() + roff[(size_t)i];
+      const int32_t* r = img[(size_t)i];
       const dp::Layout L = mode == dp::M_SPLIT ? dp::layout<dp::M_SPLIT>(r) : dp::layout<dp::M_HBM>(r);
       mx = std::max(mx, L.lds_bytes);
       soff.push_back(soff.back() + ((int64_t)L.bytes + 15) / 16 * 4);  // int32 words, 16-byte aligned
@@ -285,7 +310,11 @@ int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_of
     li[(size_t)i] = inst_off[s.p0 + i] - s.inst0;
     lc[(size_t)i] = core_off[s.p0 + i] - s.core0;
   }
-  if (upload_vec(&s.rec, rec.data(), rec.size(), s.stream)) return -1;
+  HIP_OK(hipMalloc(&s.rec, std::max<size_t>((size_t)roff[(size_t)n], 1) * 4));
+  for (int t = 0; t < T; ++t)
+    if (!parts[(size_t)t].empty())
+      HIP_OK(hipMemcpyAsync(s.rec + roff[(size_t)part_lo(t)], parts[(size_t)t].data(),
+                            parts[(size_t)t].size() * 4, hipMemcpyHostToDevice, s.stream));
   if (upload_vec(&s.rec_off, roff.data(), (size_t)n, s.stream)) return -1;
   if (upload_vec(&s.order, order.data(), order.size(), s.stream)) return -1;
   if (upload_vec(&s.inst_off, li.data(), (size_t)n + 1, s.stream)) return -1;
