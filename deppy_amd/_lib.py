@@ -35,7 +35,7 @@ EXPORTS = [
     "dp_lowered_ident_con", "dp_lowered_error", "dp_result_layout", "dp_create", "dp_destroy",
     "dp_last_error", "dp_last_global_error", "dp_num_devices", "dp_solve", "dp_upload", "dp_run",
     "dp_launch", "dp_wait", "dp_download", "dp_resident_free", "dp_last_kernel_ms", "dp_gen_catalogs", "dp_gen_wire",
-    "dp_gen_free", "dp_upload_traced", "dp_download_trace", "dp_solve_traced",
+    "dp_gen_free", "dp_upload_traced", "dp_download_trace", "dp_solve_traced", "dp_lowered_errors",
 ]
 
 
@@ -94,6 +94,7 @@ def lib():
         getattr(L, f).argtypes = [vp]
         getattr(L, f).restype = c_i32p
     L.dp_lowered_error.argtypes = [vp, ctypes.c_int32, ctypes.POINTER(ctypes.c_char_p)]
+    L.dp_lowered_errors.argtypes = [vp, c_i32p]
     L.dp_result_layout.argtypes = [ctypes.POINTER(Batch), c_i64p, c_i64p]
     L.dp_create.argtypes = [ctypes.POINTER(Opts)]
     L.dp_create.restype = vp
@@ -212,13 +213,14 @@ class Lowered:
             else:
                 self.ident_var = np.zeros(0, np.int32)
                 self.ident_con = np.zeros(0, np.int32)
-            self.err = np.zeros(P, np.int32)
+            self.err = np.zeros(max(P, 1), np.int32)
             self.msg = [None] * P
             m = ctypes.c_char_p()
-            for p in range(P):
-                self.err[p] = L.dp_lowered_error(h, p, ctypes.byref(m))
-                if self.err[p]:
+            if L.dp_lowered_errors(h, _p(self.err, c_i32p)):
+                for p in np.nonzero(self.err[:P])[0]:
+                    L.dp_lowered_error(h, int(p), ctypes.byref(m))
                     self.msg[p] = m.value.decode("utf-8", "surrogateescape")
+            self.err = self.err[:P]
         finally:
             L.dp_lowered_free(h)
 

@@ -546,7 +546,11 @@ int dp_lower(const dp_wire* wire, dp_lowered** out) {
     for (;;) {
       int c = next.fetch_add(1);
       if (c >= nchunks) break;
-      for (int32_t p = c * chunk; p < std::min(P, (c + 1) * chunk); ++p) L.lower_one(p, W, outs[(size_t)c]);
+      // fill a chunk in thread-local storage, then move it into place: the
+      // Out headers of neighbouring chunks share cache lines
+      dp::Out local;
+      for (int32_t p = c * chunk; p < std::min(P, (c + 1) * chunk); ++p) L.lower_one(p, W, local);
+      outs[(size_t)c] = std::move(local);
     }
   };
   if (nt == 1) worker();
@@ -590,6 +594,15 @@ int32_t dp_lowered_error(const dp_lowered* lw, int32_t p, const char** msg) {
   if (p < 0 || p >= lw->n) return -1;
   if (msg) *msg = lw->msg[(size_t)p].c_str();
   return lw->err[(size_t)p];
+}
+
+int32_t dp_lowered_errors(const dp_lowered* lw, int32_t* err) {
+  int32_t bad = 0;
+  for (int32_t p = 0; p < lw->n; ++p) {
+    err[p] = lw->err[(size_t)p];
+    bad += err[p] != DP_LOWER_OK;
+  }
+  return bad;
 }
 
 int dp_rec_validate(const int32_t* rec, int64_t words) {

@@ -42,6 +42,7 @@ constexpr int kBuckets[] = {8 << 10, 16 << 10, 24 << 10, 32 << 10, 48 << 10, 64 
 constexpr int kNBuckets = (int)(sizeof(kBuckets) / sizeof(kBuckets[0]));
 constexpr int kLanes = 4;
 constexpr double kMergeRatio = 0.5;  // bucket merging (build_slice); 0 = off
+constexpr double kSplitPct = 0.0;    // outlier split (build_slice); 0 = off
 
 #define HIP_OK(expr)                                                         \
   do {                                                                       \
@@ -73,6 +74,7 @@ struct DevSlice {
   int64_t n_inst = 0, n_core = 0;
   // launches: [bucket] -> (first order index, count, lds bytes)
   std::vector<int> b_first, b_count, b_lds;
+  std::vector<int> b_chain;  // 1: runs after the previous bucket launch, on its queue
   std::vector<int32_t> too_large;             // local indices (-> DP_ERROR)
   // multi-wave launches for problems over the LDS limit: [i] -> (first order
   // index, count, mode, lds bytes); their scratch offsets are indexed from
@@ -281,6 +283,31 @@ int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_of
     }
     order.insert(order.end(), bucket[(size_t)k].begin(), bucket[(size_t)k].end());
   }
+  // A launch requests its largest problem's LDS.  When a few outliers cost a
+  // workgroup per CU, they are split off into a launch of their own that
+  // follows on the same queue (b_chain), so the bulk runs at the higher
+  // occupancy (kSplitPct: the footprint percentile the bulk is sized to).
+  s.b_chain.assign(s.b_first.size(), 0);
+  double pct = kSplitPct;
+  if (const char* e = std::getenv("DEPPY_LDS_PCT")) pct = std::atof(e);  // diagnostic
+  if (pct > 0 && pct < 100) {
+    std::vector<int> f2, c2, l2, ch2;
+    for (size_t g = 0; g < s.b_first.size(); ++g) {
+      auto first = order.begin() + s.b_first[g], last = first + s.b_count[g];
+      std::stable_sort(first, last, [&](int32_t x, int32_t y) { return lds_of(x) < lds_of(y); });
+      const int cut = (int)((double)s.b_count[g] * pct / 100.0);
+      const int q = cut > 0 ? lds_of(*(first + cut - 1)) : s.b_lds[g];
+      int k = cut;  // bulk = every problem with footprint <= q
+      while (k < s.b_count[g] && lds_of(*(first + k)) <= q) ++k;
+      if (k < s.b_count[g] && kMaxLdsBytes / q > kMaxLdsBytes / s.b_lds[g]) {
+        f2.push_back(s.b_first[g]); c2.push_back(k); l2.push_back(q); ch2.push_back(0);
+        f2.push_back(s.b_first[g] + k); c2.push_back(s.b_count[g] - k); l2.push_back(s.b_lds[g]); ch2.push_back(1);
+      } else {
+        f2.push_back(s.b_first[g]); c2.push_back(s.b_count[g]); l2.push_back(s.b_lds[g]); ch2.push_back(0);
+      }
+    }
+    s.b_first = f2; s.b_count = c2; s.b_lds = l2; s.b_chain = ch2;
+  }
   // diagnostic: DEPPY_LDS_PAD_KB raises every launch's LDS request (occupancy study)
   if (const char* pad = std::getenv("DEPPY_LDS_PAD_KB"))
     for (int& b : s.b_lds) b = std::max(b, std::atoi(pad) * 1024);
@@ -355,7 +382,27 @@ int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_of
 // use and the two overlap.
 int launch_slice(DevSlice& s, Lanes& L, int64_t budget) {
   HIP_OK(hipSetDevice(s.device));
-  const int nlaunch = (int)s.b_first.size() + (int)s.g_first.size();
+  // queue groups: launches that run back to back on one queue.  The
+  // multi-wave launches (long-running large catalogs) first, then the bucket
+  // launches by size (a chained launch follows its predecessor), so the
+  // largest start earliest.
+  std::vector<std::vector<int>> groups;
+  for (size_t g = 0; g < s.g_first.size(); ++g) groups.push_back({-1 - (int)g});
+  std::vector<std::vector<int>> bg;
+  for (size_t k = 0; k < s.b_first.size(); ++k) {
+    if (k < s.b_chain.size() && s.b_chain[k] && !bg.empty()) bg.back().push_back((int)k);
+    else bg.push_back({(int)k});
+  }
+  auto cnt = [&](const std::vector<int>& v) {
+    int c = 0;
+    for (int k : v) c += s.b_count[(size_t)k];
+    return c;
+  };
+  std::stable_sort(bg.begin(), bg.end(), [&](const std::vector<int>& x, const std::vector<int>& y) {
+    return cnt(x) > cnt(y);
+  });
+  groups.insert(groups.end(), bg.begin(), bg.end());
+  const int nlaunch = (int)groups.size();
   // lanes this batch spreads its launches over (diagnostic DEPPY_LANE_SERIAL=1:
   // one lane, launches back to back)
   int width = std::max(1, std::min(nlaunch, kLanes));
@@ -381,20 +428,13 @@ int launch_slice(DevSlice& s, Lanes& L, int64_t budget) {
   a.trace = s.trace;
   a.trace_len = s.trace_len;
   a.trace_cap = s.trace_cap;
-  // the multi-wave launches (long-running large catalogs) first, then the
-  // largest buckets, so they start earliest
-  std::vector<int> launch_order;
-  for (size_t k = 0; k < s.b_first.size(); ++k) launch_order.push_back((int)k);
-  std::sort(launch_order.begin(), launch_order.end(),
-            [&](int x, int y) { return s.b_count[(size_t)x] > s.b_count[(size_t)y]; });
-  for (size_t g = 0; g < s.g_first.size(); ++g) launch_order.insert(launch_order.begin() + (long)g, -1 - (int)g);
-  const int nside = std::min<int>(width - 1, (int)launch_order.size() - 1);
+  const int nside = std::min<int>(width - 1, nlaunch - 1);
   auto side = [&](int i) { return L.s[(base + 1 + i) % kLanes]; };
   HIP_OK(hipEventRecord(s.ev0, s.stream));
   for (int i = 0; i < nside; ++i) HIP_OK(hipStreamWaitEvent(side(i), s.ev0, 0));
-  for (size_t i = 0; i < launch_order.size(); ++i) {
+  for (size_t i = 0; i < groups.size(); ++i)
+  for (const int k : groups[i]) {
     hipStream_t st = (i % width == 0) ? s.stream : side((int)(i % width) - 1);
-    const int k = launch_order[i];
     if (k < 0) {
       const size_t g = (size_t)(-1 - k);
       a.order = s.order + s.g_first[g];

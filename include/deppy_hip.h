@@ -176,6 +176,9 @@ const int32_t* dp_lowered_ident_var(const dp_lowered* lw);
 const int32_t* dp_lowered_ident_con(const dp_lowered* lw);
 /* enum dp_lower_err; *msg (may be NULL) receives the reference's error text. */
 int32_t dp_lowered_error(const dp_lowered* lw, int32_t p, const char** msg);
+/* Every problem's enum dp_lower_err at once (err[n_problems]); returns the
+ * number of problems with an error (fetch their text with dp_lowered_error). */
+int32_t dp_lowered_errors(const dp_lowered* lw, int32_t* err);
 
 /* ------------------------------------------------------------------------ */
 /* 3. Solving                                                                 */
