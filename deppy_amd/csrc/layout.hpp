@@ -46,8 +46,9 @@ __host__ __device__ constexpr int32_t mode_waves(int mode) { return mode == M_LD
 __host__ __device__ constexpr int32_t mode_wbuf(int mode) { return mode == M_LDS ? 256 : 4096; }
 // AtMost rows queued for wave-cooperative evaluation in one round
 __host__ __device__ constexpr int32_t mode_cq(int mode) { return mode == M_LDS ? 64 : 512; }
-// wave-shared scalars (S_*), then per-wave reduction slots
+// wave-shared scalars (S_*), then (multi-wave modes) per-wave reduction slots
 constexpr int32_t NSCAL = 64;
+__host__ __device__ constexpr int32_t mode_nscal(int mode) { return mode == M_LDS ? 8 : NSCAL; }
 
 // dp_rec_layout_of (include/deppy_hip.h) for host and device code.
 __host__ __device__ inline dp_rec_layout rec_layout(const int32_t* h) {
@@ -99,14 +100,12 @@ __host__ __device__ inline ImgLayout img_layout(const int32_t* h) {
 struct Layout {
   int32_t body;      // M_LDS only: image arrays (header dropped), one IX per image word
   int32_t val;       // int8[nv]: 0 unassigned, 1 true, -1 false                  [LDS unless M_HBM]
-  int32_t reason;    // IX[nv] implying row; R_DEC / R_EXTRA
+  int32_t reason;    // IX[nv] implying row; R_DEC / R_EXTRA / a Solve() decision (-3 - index)
   int32_t rs;        // IX[nv] trail position where the assigning round started
   int32_t trail;     // IX[nv] true literals in assignment order
   int32_t touched;   // IX[2nv] literals implied this round; analysis work list
-  int32_t d_lit;     // IX[nv] Solve() decision literals
-  int32_t d_mark;    // IX[nv] trail length before each decision
-  int32_t dix;       // IX[nv] decision index of a variable (NONE otherwise)
-  int32_t imp;       // u32[2nv] lowest row implying literal l this round (INF: none)
+  int32_t d_mark;    // IX[nv] trail length before each Solve() decision (its literal is trail[d_mark])
+  int32_t imp;       // IX[2nv] lowest row implying literal l this round (all ones: none)
   int32_t d_flip;    // bits[nv] decision already flipped                          [LDS unless M_HBM]
   int32_t inS;       // bits[nv] guessed set (search.assumptions)                  [LDS unless M_HBM]
   int32_t extra;     // bits[nv] SAT-epilogue extras                               [LDS unless M_HBM]
@@ -120,10 +119,10 @@ struct Layout {
   int32_t l_off;     // IX[L_MAX+1] learned rows (rows nrows..)
   int32_t l_lits;    // IX[lcap]
   int32_t dq;        // IX[2*cap] deque of choices (list, idx)
-  int32_t stk;       // IX[5*cap] guess stack (list, idx, m, children, mark)
+  int32_t stk;       // IX[3*cap] guess stack (list, idx | G_SKIP, mark)
   int32_t wbuf;      // IX[wbuf] flattened work list (watch-list positions)       [LDS]
-  int32_t cardq;     // i32[cq] AtMost rows queued this round                     [LDS]
-  int32_t scal;      // i32[NSCAL] wave-shared scalars and reduction slots        [LDS]
+  int32_t cardq;     // IX[cq] AtMost rows queued this round                      [LDS]
+  int32_t scal;      // i32[nscal] wave-shared scalars and reduction slots        [LDS]
   int32_t bytes;     // HBM scratch bytes (0 for M_LDS)
   int32_t lds_bytes; // LDS bytes
   int32_t cap, lcap;
@@ -150,11 +149,11 @@ __host__ __device__ inline Layout layout(const int32_t* h) {
   };
   enum { COLD = 0, HOT = 1, WORK = 2 };
   L.cap = h[DP_H_NA] + h[DP_H_NCH] + 2;
-  L.lcap = 2 * nv + 64;
+  L.lcap = nv + 64;
   L.body = MODE == M_LDS ? take((h[DP_H_IMG] - DP_H_SIZE + 4) * ix, COLD) : 0;  // +4: dwordx4 copy slack
-  L.scal = take(NSCAL * 4, WORK);
+  L.scal = take(mode_nscal(MODE) * 4, WORK);
   L.wbuf = take(mode_wbuf(MODE) * ix, WORK);
-  L.cardq = take(mode_cq(MODE) * 4, WORK);
+  L.cardq = take(mode_cq(MODE) * ix, WORK);
   L.val = take(nv, HOT);
   L.d_flip = take(nbv * 4, HOT);
   L.inS = take(nbv * 4, HOT);
@@ -170,26 +169,25 @@ __host__ __device__ inline Layout layout(const int32_t* h) {
   L.rs = take(nv * ix, COLD);
   L.trail = take(nv * ix, COLD);
   L.touched = take(2 * nv * ix, COLD);
-  L.d_lit = take(nv * ix, COLD);
   L.d_mark = take(nv * ix, COLD);
-  L.dix = take(nv * ix, COLD);
-  L.imp = take(2 * nv * 4, COLD);
+  L.imp = take(2 * nv * ix, COLD);
   L.l_off = take((L_MAX + 1) * ix, COLD);
   L.l_lits = take(L.lcap * ix, COLD);
   L.dq = take(2 * L.cap * ix, COLD);
-  L.stk = take(5 * L.cap * ix, COLD);
+  L.stk = take(3 * L.cap * ix, COLD);
   L.bytes = og;
   L.lds_bytes = ol;
   return L;
 }
 
 // Can the record run on the 16-bit LDS image?  Every index it holds, and every
-// value the solve stores per variable / row, must stay below 0xfffe (0xffff and
-// 0xfffe encode the no-row reasons).
+// value the solve stores per variable / row, must stay below the encodings of
+// the no-row reasons (0xffff R_DEC, 0xfffe R_EXTRA, 0xfffd - d decision d).
 __host__ __device__ inline bool fits16(const int32_t* h) {
   const int32_t nv = h[DP_H_NV];
+  // reasons encode Solve() decision d as 0xfffd - d above every row id
   return h[DP_H_WORDS] < 65000 && nv < 16000 && h[DP_H_NID] < 65000 &&
-         h[DP_H_NC] + h[DP_H_NK] + L_MAX < 65000 && h[DP_H_NA] + h[DP_H_NCH] < 65000 &&
+         h[DP_H_NC] + h[DP_H_NK] + L_MAX + nv < 65000 && h[DP_H_NA] + h[DP_H_NCH] < 65000 &&
          h[DP_H_NCL] + h[DP_H_NKL] < 65000;
 }
 

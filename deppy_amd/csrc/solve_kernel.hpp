@@ -122,10 +122,19 @@ struct Group {
   static constexpr int WBUF = mode_wbuf(MODE);
   static constexpr int CQ = mode_cq(MODE);
 
-  // IX <-> int for the signed values (reasons R_DEC / R_EXTRA, "none" = -1)
-  __device__ __forceinline__ static int dec(IX x) {
+  // the lowest implying row per literal: 16-bit in LDS, 32-bit (global
+  // atomics) in the multi-wave modes; IMP_NONE = no implication this round
+  using IMP = typename std::conditional<MODE == M_LDS, uint16_t, uint32_t>::type;
+  static constexpr uint32_t IMP_NONE = MODE == M_LDS ? 0xffffu : (uint32_t)INF;
+  // guess-stack flag: the choice was already satisfied by a guess (m = none)
+  static constexpr int G_SKIP = MODE == M_LDS ? 0x8000 : 0x40000000;
+
+  // IX <-> int for the signed values: reasons R_DEC (-1), R_EXTRA (-2) and
+  // Solve() decision d (-3 - d); in 16 bits every value from dthr up is one of
+  // them (fits16 keeps rows below and decisions above)
+  __device__ __forceinline__ int dec(IX x) const {
     if constexpr (MODE != M_LDS) return x;
-    else return x >= 0xfffe ? (int)x - 0x10000 : (int)x;
+    else return (int)x >= dthr ? (int)x - 0x10000 : (int)x;
   }
   __device__ __forceinline__ static IX enc(int x) { return (IX)x; }
 
@@ -133,7 +142,7 @@ struct Group {
   // bitsets) are read from L2: the atomics are performed there and a plain
   // load from another wavefront of the workgroup can hit a stale L1 line.
   // LDS words need no such care.
-  __device__ __forceinline__ static uint32_t ld_imp(const uint32_t* p) {
+  __device__ __forceinline__ static uint32_t ld_imp(const IMP* p) {
     if constexpr (MODE == M_LDS) return *p;
     else return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -148,14 +157,14 @@ struct Group {
   const IX *card_off, *card_lits, *card_bound, *card_id;
   const IX *var_choice_off, *choice_off, *choice_lits, *anchors;
   const IX *w_off, *w, *base_rows;
-  int nbase, nwatch;
+  int nbase, nwatch, dthr;
   // ---- working set ----
   int8_t* val;
-  IX *reason, *rs, *trail, *touched, *d_lit, *d_mark, *dix, *l_off, *l_lits, *dq, *stk;
-  uint32_t* imp;  // imp[l] = lowest row implying literal l this round
+  IX *reason, *rs, *trail, *touched, *d_mark, *l_off, *l_lits, *dq, *stk;
+  IMP* imp;  // imp[l] = lowest row implying literal l this round
   uint32_t *d_flip, *inS, *extra, *seen, *model, *used, *en, *en2, *dset, *fg;
-  IX* wbuf;
-  int32_t *cardq, *scal;
+  IX *wbuf, *cardq;
+  int32_t* scal;
   int cap, lcap;
   int tid, lane, wid;
   // ---- group-uniform state (registers, identical in every thread) ----
@@ -351,6 +360,7 @@ struct Group {
     w_off = rv(X.w_off); w = rv(X.w); base_rows = rv(X.base);
     nbase = h[DP_H_NBASE];
     nwatch = h[DP_H_NCL] + h[DP_H_NKL];
+    dthr = nrows + L_MAX;
     char* hot = MODE == M_HBM ? hbm : lds;   // val and the bitsets
     char* cold = MODE == M_LDS ? lds : hbm;  // per-literal arrays
     val = reinterpret_cast<int8_t*>(hot + L.val);
@@ -358,10 +368,8 @@ struct Group {
     rs = reinterpret_cast<IX*>(cold + L.rs);
     trail = reinterpret_cast<IX*>(cold + L.trail);
     touched = reinterpret_cast<IX*>(cold + L.touched);
-    d_lit = reinterpret_cast<IX*>(cold + L.d_lit);
     d_mark = reinterpret_cast<IX*>(cold + L.d_mark);
-    dix = reinterpret_cast<IX*>(cold + L.dix);
-    imp = reinterpret_cast<uint32_t*>(cold + L.imp);
+    imp = reinterpret_cast<IMP*>(cold + L.imp);
     d_flip = reinterpret_cast<uint32_t*>(hot + L.d_flip);
     inS = reinterpret_cast<uint32_t*>(hot + L.inS);
     extra = reinterpret_cast<uint32_t*>(hot + L.extra);
@@ -377,7 +385,7 @@ struct Group {
     dq = reinterpret_cast<IX*>(cold + L.dq);
     stk = reinterpret_cast<IX*>(cold + L.stk);
     wbuf = reinterpret_cast<IX*>(lds + L.wbuf);
-    cardq = reinterpret_cast<int32_t*>(lds + L.cardq);
+    cardq = reinterpret_cast<IX*>(lds + L.cardq);
     scal = reinterpret_cast<int32_t*>(lds + L.scal);
     cap = L.cap; lcap = L.lcap;
     tlen = qhead = 0;
@@ -403,11 +411,11 @@ struct Group {
     } else {
       for (int v = tid; v < (nv + 3) / 4; v += NT) reinterpret_cast<uint32_t*>(val)[v] = 0;
     }
-    for (int l = tid; l < 2 * nv; l += NT) imp[l] = (uint32_t)INF;
+    for (int l = tid; l < 2 * nv; l += NT) imp[l] = (IMP)IMP_NONE;
     for (int i = tid; i < nbv; i += NT) {
       d_flip[i] = 0; inS[i] = 0; extra[i] = 0; seen[i] = 0; model[i] = 0; dset[i] = 0; fg[i] = 0;
     }
-    if (tid < NSCAL) scal[tid] = 0;
+    if (tid < mode_nscal(MODE)) scal[tid] = 0;
     if (tid == 0) l_off[0] = 0;
     gsync();
   }
@@ -424,11 +432,35 @@ struct Group {
     return (l & 1) ? -x : x;
   }
 
+  // imp[l] as an int (INF: none this round)
+  __device__ __forceinline__ int imp_get(int l) const {
+    const uint32_t x = ld_imp(&imp[l]);
+    return x == IMP_NONE ? INF : (int)x;
+  }
+  // imp[l] = min(imp[l], r); true on the round's first implication of l.
+  // 16-bit: a compare-and-swap on the 32-bit word holding l and l ^ 1.
+  __device__ __forceinline__ bool imp_min(int l, int r) {
+    if constexpr (MODE == M_LDS) {
+      uint32_t* w32 = reinterpret_cast<uint32_t*>(imp) + (l >> 1);
+      const int sh = (l & 1) * 16;
+      uint32_t old = *w32;
+      for (;;) {
+        const uint32_t cur = (old >> sh) & 0xffffu;
+        if ((uint32_t)r >= cur) return false;
+        const uint32_t nw = (old & ~(0xffffu << sh)) | ((uint32_t)r << sh);
+        const uint32_t prev = atomicCAS(w32, old, nw);
+        if (prev == old) return cur == IMP_NONE;
+        old = prev;
+      }
+    } else {
+      return atomicMin(&imp[l], (uint32_t)r) == IMP_NONE;
+    }
+  }
   // record "row r implies literal l" (lowest row wins, oracle: note); the
   // first implication of a literal in the round lists it
   __device__ __forceinline__ void note(int l, int r) {
     l = DP_CHK(l, 0, 2 * nv, 1);
-    if (atomicMin(&imp[l], (uint32_t)r) == (uint32_t)INF)
+    if (imp_min(l, r))
       touched[DP_CHK(atomicAdd(&scal[S_NTOUCHED], 1), 0, 2 * nv, 2)] = enc(l);
   }
 
@@ -493,7 +525,7 @@ struct Group {
     uint64_t m = __ballot(card);
     if constexpr (NW == 1) {
       if (ncq + __popcll(m) > CQ) m = 0;  // queue full: evaluate in-lane
-      if ((m >> lane) & 1ull) cardq[ncq + __popcll(m & lanemask_lt())] = r;
+      if ((m >> lane) & 1ull) cardq[ncq + __popcll(m & lanemask_lt())] = enc(r);
       else if (ok) eval_row(r, crow);
       ncq += __popcll(m);
     } else {
@@ -503,7 +535,7 @@ struct Group {
         if (lane == 0) b = atomicAdd(&scal[S_NK], __popcll(m));
         pos = __shfl(b, 0) + __popcll(m & lanemask_lt());
       }
-      if (card && pos < CQ) cardq[pos] = r;
+      if (card && pos < CQ) cardq[pos] = enc(r);
       else if (ok) eval_row(r, crow);  // queue full: evaluate in-lane
     }
   }
@@ -523,7 +555,7 @@ struct Group {
       q0 = wid; qs = NW;
     }
     for (int q = q0; q < ncq; q += qs) {
-      const int r = DP_CHK(cardq[q], nc, nrows, 3), k = r - nc;
+      const int r = DP_CHK((int)cardq[q], nc, nrows, 3), k = r - nc;
       const int a = card_off[k], len = (int)card_off[k + 1] - a, bound = card_bound[k];
       if (len > 64) {  // long rows: one lane
         if (lane == 0) eval_row(r, crow);
@@ -549,7 +581,7 @@ struct Group {
 
   __device__ __forceinline__ void clear_touched(int nt) {
     if constexpr (NW > 1) bar();  // every read of imp in this round is done
-    for (int i = tid; i < nt; i += NT) imp[(int)touched[i]] = (uint32_t)INF;
+    for (int i = tid; i < nt; i += NT) imp[(int)touched[i]] = (IMP)IMP_NONE;
     gsync();
     if (tid == 0) scal[S_NTOUCHED] = 0;
     gsync();
@@ -560,9 +592,8 @@ struct Group {
     val[v] = (l & 1) ? -1 : 1;
     reason[v] = enc(r);
     rs[v] = enc(start);
-    dix[v] = enc(-1);
     trail[DP_CHK(start + i, 0, nv, 9)] = enc(l);
-    imp[l] = (uint32_t)INF;
+    imp[l] = (IMP)IMP_NONE;
   }
 
   // Commit the implications of the round, or report its conflict: the lowest
@@ -582,33 +613,33 @@ struct Group {
     const int start = tlen;
     if (nt <= NT) {  // one literal per thread: a single pass
       const int l = tid < nt ? DP_CHK((int)touched[tid], 0, 2 * nv, 5) : 0;
-      const uint32_t r = tid < nt ? (uint32_t)DP_CHK((int)ld_imp(&imp[l]), 0, nrows + nl, 6) : 0u,
-                     rn = tid < nt ? ld_imp(&imp[l ^ 1]) : (uint32_t)INF;
-      const int cv = rn != (uint32_t)INF ? (l >> 1) : INF;
+      const int r = tid < nt ? DP_CHK(imp_get(l), 0, nrows + nl, 6) : 0,
+                rn = tid < nt ? imp_get(l ^ 1) : INF;
+      const int cv = rn != INF ? (l >> 1) : INF;
       if (g_any(cv != INF)) {
         c_var = g_min(cv);
-        c_rp = (int)ld_imp(&imp[2 * c_var]); c_rn = (int)ld_imp(&imp[2 * c_var + 1]);
+        c_rp = imp_get(2 * c_var); c_rn = imp_get(2 * c_var + 1);
         ck = CK_VAR; c_row = tlen;  // bound: every variable assigned so far
         clear_touched(nt);
         return -1;
       }
-      if (tid < nt) commit(l, (int)r, start, tid);
+      if (tid < nt) commit(l, r, start, tid);
     } else {
       int cv = INF;
       for (int i = tid; i < nt; i += NT) {
         const int l = touched[i];
-        if (ld_imp(&imp[l ^ 1]) != (uint32_t)INF) cv = min(cv, l >> 1);
+        if (imp_get(l ^ 1) != INF) cv = min(cv, l >> 1);
       }
       if (g_any(cv != INF)) {
         c_var = g_min(cv);
-        c_rp = (int)ld_imp(&imp[2 * c_var]); c_rn = (int)ld_imp(&imp[2 * c_var + 1]);
+        c_rp = imp_get(2 * c_var); c_rn = imp_get(2 * c_var + 1);
         ck = CK_VAR; c_row = tlen;
         clear_touched(nt);
         return -1;
       }
       for (int i = tid; i < nt; i += NT) {
         const int l = DP_CHK((int)touched[i], 0, 2 * nv, 7);
-        commit(l, DP_CHK((int)ld_imp(&imp[l]), 0, nrows + nl, 8), start, i);
+        commit(l, DP_CHK(imp_get(l), 0, nrows + nl, 8), start, i);
       }
     }
     if (tid == 0) scal[S_NTOUCHED] = 0;
@@ -637,7 +668,7 @@ struct Group {
         const bool f = v < nv && getb(extra, v) && val[v] == 0;
         const int at = claim(f, run);
         if (f) {
-          val[v] = -1; reason[v] = enc(R_EXTRA); rs[v] = enc(start); dix[v] = enc(-1);
+          val[v] = -1; reason[v] = enc(R_EXTRA); rs[v] = enc(start);
           trail[DP_CHK(at, 0, nv, 28)] = enc(2 * v + 1);
         }
       }
@@ -769,8 +800,8 @@ struct Group {
     if constexpr (NW > 1) bar();
     if (tid == 0) {
       const int v = DP_CHK(l, 0, 2 * nv, 30) >> 1;
-      val[v] = (l & 1) ? -1 : 1; reason[v] = enc(why); rs[v] = enc(tlen);
-      dix[v] = enc(decision); trail[DP_CHK(tlen, 0, nv, 31)] = enc(l);
+      val[v] = (l & 1) ? -1 : 1; reason[v] = enc(decision >= 0 ? -3 - decision : why);
+      rs[v] = enc(tlen); trail[DP_CHK(tlen, 0, nv, 31)] = enc(l);
     }
     ++tlen;
     gsync();
@@ -848,7 +879,7 @@ struct Group {
         const int r = dec(reason[u]);
         if (r >= 0) ante_serial(r, u, rs[u]);
         else if (r == R_EXTRA) extra_serial(u, rs[u]);
-        else if (dec(dix[u]) >= 0) set_bit_atomic(dset, DP_CHK((int)dix[u], 0, nv, 32));
+        else if (r <= -3) set_bit_atomic(dset, DP_CHK(-3 - r, 0, nv, 32));  // Solve() decision
         else if (collect_guess && getb(inS, u)) set_bit_atomic(fg, u);
       }
       head = nw;
@@ -938,6 +969,11 @@ struct Group {
     gsync();
   }
 
+  // Solve() decision i's literal: the trail entry at its mark, unflipped
+  __device__ __forceinline__ int dlit(int i) const {
+    return (int)trail[(int)d_mark[i]] ^ (int)getb(d_flip, i);
+  }
+
   __device__ __forceinline__ int dpll() {
     const int root = tlen, nl0 = nl;
     int nd = 0, r;
@@ -948,7 +984,7 @@ struct Group {
         if (l < 0) { save_model(); r = RS_SAT; break; }
         if (++steps > budget) { budget_hit = true; r = RS_BUDGET; break; }
         if (tid == 0) {
-          d_lit[nd] = enc(l); d_mark[nd] = enc(tlen);
+          d_mark[nd] = enc(tlen);  // the decision's literal is trail[d_mark[nd]]
           d_flip[nd >> 5] &= ~(1u << (nd & 31));
         }
         assign_one(l, R_DEC, nd);
@@ -980,22 +1016,24 @@ struct Group {
           const int i = base + tid;
           const bool in = i < nd && ((ld_bits(&dset[i >> 5]) >> (i & 31)) & 1u);
           const int at = claim(in, run);
-          if (in) l_lits[DP_CHK(at, 0, lcap, 27)] = enc((int)d_lit[i] ^ 1);
+          if (in) l_lits[DP_CHK(at, 0, lcap, 27)] = enc(dlit(i) ^ 1);
         }
         claim_end(run);
         if (tid == 0) l_off[nl + 1] = enc(run);
         ++nl;
         gsync();
+        const int lh = dlit(h);
         nd = b + 1;
         truncate_to(DP_CHK((int)d_mark[nd], 0, nv + 1, 24));
-        assign_one((int)d_lit[h] ^ 1, nrows + nl - 1, -1);
+        assign_one(lh ^ 1, nrows + nl - 1, -1);
       } else {
         while (nd > 0 && getb(d_flip, nd - 1)) --nd;
         if (nd == 0) { r = RS_UNSAT; break; }
+        const int lf = dlit(nd - 1);  // before its flip bit is set
         truncate_to(DP_CHK((int)d_mark[nd - 1], 0, nv + 1, 25));
         if (tid == 0) d_flip[(nd - 1) >> 5] |= 1u << ((nd - 1) & 31);
         gsync();
-        assign_one((int)d_lit[nd - 1] ^ 1, R_DEC, nd - 1);
+        assign_one(lf ^ 1, R_DEC, nd - 1);
       }
     }
     truncate_to(root);
@@ -1028,6 +1066,12 @@ struct Group {
     ++dq_n;
   }
 
+  // the guessed variable of a stack entry (list, idx | G_SKIP), or -1
+  __device__ __forceinline__ int guess_m(int list, int idxf) const {
+    const int idx = idxf & ~G_SKIP;
+    return !(idxf & G_SKIP) && idx < list_len(list) ? list_at(list, idx) : -1;
+  }
+
   // PushGuess, search.go:34-77
   __device__ __forceinline__ void push_guess() {
     gsync();
@@ -1038,17 +1082,14 @@ struct Group {
     int m = idx < len ? list_at(list, idx) : -1;
     bool any = false;
     for (int i = tid; i < len; i += NT) any |= getb(inS, list_at(list, i));
-    if (g_any(any)) m = -1;
+    const bool skip = g_any(any);
+    if (skip) m = -1;
     else if (idx >= len) class_b = true;  // exhausted choice
-    int children = 0;
-    if (m >= 0)
-      for (int r = var_choice_off[m]; r < (int)var_choice_off[m + 1]; ++r) {
-        dq_push_back(r, 0);
-        ++children;
-      }
+    if (m >= 0)  // its children: one choice per choice row (pop_guess recounts them)
+      for (int r = var_choice_off[m]; r < (int)var_choice_off[m + 1]; ++r) dq_push_back(r, 0);
     if (tid == 0) {
-      IX* g = stk + 5 * ng;
-      g[0] = enc(list); g[1] = enc(idx); g[2] = enc(m); g[3] = enc(children); g[4] = enc(tlen);
+      IX* g = stk + 3 * ng;
+      g[0] = enc(list); g[1] = enc(idx | (skip ? G_SKIP : 0)); g[2] = enc(tlen);
       if (m >= 0) inS[m >> 5] |= 1u << (m & 31);
     }
     ++ng;
@@ -1063,10 +1104,12 @@ struct Group {
   __device__ __forceinline__ void pop_guess() {
     gsync();
     --ng;
-    const IX* g = stk + 5 * ng;
-    const int list = DP_CHK((int)g[0], 0, nch + nv, 19), idx = DP_CHK((int)g[1], 0, nv + 1, 20),
-              m = DP_CHK(dec(g[2]), -1, nv, 21), children = DP_CHK((int)g[3], 0, cap, 22),
-              mark = DP_CHK((int)g[4], 0, nv + 1, 23);
+    const IX* g = stk + 3 * ng;
+    const int list = DP_CHK((int)g[0], 0, nch + nv, 19), idxf = (int)g[1],
+              mark = DP_CHK((int)g[2], 0, nv + 1, 23);
+    const int idx = DP_CHK(idxf & ~G_SKIP, 0, nv + 1, 20);
+    const int m = DP_CHK(guess_m(list, idxf), -1, nv, 21);
+    const int children = m >= 0 ? (int)var_choice_off[m + 1] - (int)var_choice_off[m] : 0;
     gsync();
     if (m >= 0) {
       if (tid == 0) inS[m >> 5] &= ~(1u << (m & 31));
@@ -1220,7 +1263,7 @@ struct Group {
       analyze();
     }
     int ngv = 0, ni = 0;
-    for (int i = tid; i < ng; i += NT) ngv += dec(stk[5 * i + 2]) >= 0;
+    for (int i = tid; i < ng; i += NT) ngv += guess_m(stk[3 * i], stk[3 * i + 1]) >= 0;
     for (int i = tid; i < nbi; i += NT) ni += __popc(ld_bits(&used[i]));
     ngv = g_sum(ngv);
     ni = g_sum(ni);
@@ -1234,7 +1277,7 @@ struct Group {
       int k = 0;
       o[k++] = ngv;
       for (int i = 0; i < ng; ++i) {
-        const int m = dec(stk[5 * i + 2]);
+        const int m = guess_m(stk[3 * i], stk[3 * i + 1]);
         if (m >= 0) o[k++] = m;
       }
       o[k] = ni;
@@ -1343,7 +1386,7 @@ struct Group {
       }
       const int at = claim(f, run);
       if (f) {
-        val[v] = (l & 1) ? -1 : 1; reason[v] = enc(R_DEC); rs[v] = enc(start); dix[v] = enc(-1);
+        val[v] = (l & 1) ? -1 : 1; reason[v] = enc(R_DEC); rs[v] = enc(start);
         trail[DP_CHK(at, 0, nv, 29)] = enc(l);
       }
     }

@@ -97,7 +97,7 @@ typedef struct {
   int32_t trace_cap, trace_len, trace_stop;
 } st_t;
 
-/* learned-row store: at most L_MAX rows and 2*nv+64 literals */
+/* learned-row store: at most L_MAX rows and nv+64 literals */
 #define L_MAX 64
 
 /* ------------------------------------------------------------------ */
@@ -171,7 +171,7 @@ static int st_init(st_t* s, const int32_t* rec) {
   s->d_lit = xcalloc((size_t)nv, sizeof(int32_t));
   s->d_mark = xcalloc((size_t)nv, sizeof(int32_t));
   s->d_flip = xcalloc((size_t)nv, 1);
-  s->lcap = 2 * nv + 64;
+  s->lcap = nv + 64;
   s->l_off = xcalloc(L_MAX + 1, sizeof(int32_t));
   s->l_lits = xcalloc((size_t)s->lcap, sizeof(int32_t));
   s->fg = xcalloc((size_t)nv, 1);
