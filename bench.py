@@ -81,8 +81,8 @@ def _same(a, b) -> bool:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--problems", type=int, default=0,
                     help="catalogs per GPU (0: the config's default, WORKLOADS)")

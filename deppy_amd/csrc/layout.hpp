@@ -43,9 +43,22 @@ constexpr int32_t BIG_WAVES = DP_BIG_WAVES;
 
 __host__ __device__ constexpr int32_t mode_waves(int mode) { return mode == M_LDS ? 1 : BIG_WAVES; }
 // work list of one propagation chunk (rows watched by <= 64*waves frontier literals)
-__host__ __device__ constexpr int32_t mode_wbuf(int mode) { return mode == M_LDS ? 256 : 4096; }
+#ifndef DP_WBUF_LDS
+#define DP_WBUF_LDS 256
+#endif
+#ifndef DP_CQ_LDS
+#define DP_CQ_LDS 64
+#endif
+__host__ __device__ constexpr int32_t mode_wbuf(int mode) { return mode == M_LDS ? DP_WBUF_LDS : 4096; }
 // AtMost rows queued for wave-cooperative evaluation in one round
-__host__ __device__ constexpr int32_t mode_cq(int mode) { return mode == M_LDS ? 64 : 512; }
+__host__ __device__ constexpr int32_t mode_cq(int mode) { return mode == M_LDS ? DP_CQ_LDS : 512; }
+// M_LDS stores imp (the lowest implying row per literal) in 16 bits, updated
+// by a compare-and-swap, or in 32 bits, updated by atomicMin
+#ifndef DP_IMP16
+#define DP_IMP16 1
+#endif
+constexpr bool IMP16_LDS = DP_IMP16;
+
 // wave-shared scalars (S_*), then (multi-wave modes) per-wave reduction slots
 constexpr int32_t NSCAL = 64;
 __host__ __device__ constexpr int32_t mode_nscal(int mode) { return mode == M_LDS ? 8 : NSCAL; }
@@ -170,7 +183,7 @@ __host__ __device__ inline Layout layout(const int32_t* h) {
   L.trail = take(nv * ix, COLD);
   L.touched = take(2 * nv * ix, COLD);
   L.d_mark = take(nv * ix, COLD);
-  L.imp = take(2 * nv * ix, COLD);
+  L.imp = take(2 * nv * (MODE == M_LDS && IMP16_LDS ? 2 : 4), COLD);
   L.l_off = take((L_MAX + 1) * ix, COLD);
   L.l_lits = take(L.lcap * ix, COLD);
   L.dq = take(2 * L.cap * ix, COLD);

@@ -124,8 +124,9 @@ struct Group {
 
   // the lowest implying row per literal: 16-bit in LDS, 32-bit (global
   // atomics) in the multi-wave modes; IMP_NONE = no implication this round
-  using IMP = typename std::conditional<MODE == M_LDS, uint16_t, uint32_t>::type;
-  static constexpr uint32_t IMP_NONE = MODE == M_LDS ? 0xffffu : (uint32_t)INF;
+  static constexpr bool IMP16 = MODE == M_LDS && IMP16_LDS;
+  using IMP = typename std::conditional<IMP16, uint16_t, uint32_t>::type;
+  static constexpr uint32_t IMP_NONE = IMP16 ? 0xffffu : (uint32_t)INF;
   // guess-stack flag: the choice was already satisfied by a guess (m = none)
   static constexpr int G_SKIP = MODE == M_LDS ? 0x8000 : 0x40000000;
 
@@ -440,7 +441,7 @@ struct Group {
   // imp[l] = min(imp[l], r); true on the round's first implication of l.
   // 16-bit: a compare-and-swap on the 32-bit word holding l and l ^ 1.
   __device__ __forceinline__ bool imp_min(int l, int r) {
-    if constexpr (MODE == M_LDS) {
+    if constexpr (IMP16) {
       uint32_t* w32 = reinterpret_cast<uint32_t*>(imp) + (l >> 1);
       const int sh = (l & 1) * 16;
       uint32_t old = *w32;
