@@ -49,8 +49,13 @@ enum { RS_SAT = 1, RS_UNSAT = -1, RS_BUDGET = 2 };
 
 // Lanes of the wave hand values to each other through the working set (LDS,
 // or HBM): complete every access before the next phase.
+#ifndef DP_WSYNC_FENCE
+#define DP_WSYNC_FENCE 1
+#endif
 __device__ __forceinline__ void wsync() {
+#if DP_WSYNC_FENCE
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+#endif
   __builtin_amdgcn_wave_barrier();
 }
 
@@ -1423,8 +1428,14 @@ struct Group {
 // One problem per workgroup; blockIdx.x indexes `order` (problems bucketed by
 // working-set footprint; the multi-wave modes work partly in HBM scratch).
 // Outputs: status / flags / installed / core / steps (oracle_solve).
+#ifndef DP_LDS_MIN_WAVES
+#define DP_LDS_MIN_WAVES 1
+#endif
+// (DP_LDS_MIN_WAVES: minimum waves per SIMD the one-wavefront kernel is
+// compiled for; above 4 the compiler caps VGPRs and spills)
 template <int MODE>
-__global__ void __launch_bounds__(64 * mode_waves(MODE)) solve_kernel(KernelArgs a) {
+__global__ void __launch_bounds__(64 * mode_waves(MODE), MODE == M_LDS ? DP_LDS_MIN_WAVES : 1)
+solve_kernel(KernelArgs a) {
   extern __shared__ int4 lds4[];
 #ifdef DP_STAMPS
   int64_t t[6];
