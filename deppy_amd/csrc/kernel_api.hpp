@@ -9,7 +9,7 @@ namespace dp {
 // diagnostic stamps per problem: 5 phase cycles, 5 counters, wall-clock
 // start/end, then the first failed index check (code, value, bound) and the
 // number of failed checks, then 3 more counters (Solve, pop_guess, pushes)
-constexpr int DP_NSTAMP = 20;
+constexpr int DP_NSTAMP = 32;
 
 struct KernelArgs {
   const int32_t* rec;      // records, each 16-byte aligned

@@ -47,6 +47,12 @@ constexpr int32_t R_EXTRA = -2;  // epilogue bound over the extras
 enum { CK_NONE = 0, CK_ROW, CK_VAR, CK_ASSUME, CK_EXTRA };
 enum { RS_SAT = 1, RS_UNSAT = -1, RS_BUDGET = 2 };
 
+// One wavefront: flush the AtMost queue before a visit that could overflow
+// it (1), or evaluate the overflowing rows in-lane (0).
+#ifndef DP_MAKE_ROOM
+#define DP_MAKE_ROOM 0
+#endif
+
 // Lanes of the wave hand values to each other through the working set (LDS,
 // or HBM): complete every access before the next phase.
 #ifndef DP_WSYNC_FENCE
@@ -126,6 +132,7 @@ struct Group {
   static constexpr int NT = 64 * NW;           // threads per problem
   static constexpr int WBUF = mode_wbuf(MODE);
   static constexpr int CQ = mode_cq(MODE);
+  static_assert(NW > 1 || !DP_MAKE_ROOM || CQ >= 64, "make_room: the AtMost queue holds one visit");
 
   // the lowest implying row per literal: 16-bit in LDS, 32-bit (global
   // atomics) in the multi-wave modes; IMP_NONE = no implication this round
@@ -189,8 +196,11 @@ struct Group {
   bool tr_stop;
 #ifdef DP_STAMPS
   // round eval cycles, round finish cycles, rounds, 1-literal rounds, push_guess cycles,
-  // search Solve() cycles, pop_guess cycles, push_guess calls
-  int64_t acc[8];
+  // search Solve() cycles, pop_guess cycles, push_guess calls; within a
+  // round: 1-literal visit cycles, flattened-frontier cycles, AtMost flush
+  // cycles, learned-row cycles, watch entries visited, frontier literals of
+  // flattened rounds, learned rows evaluated, AtMost rows flushed
+  int64_t acc[16];
   unsigned long long* dbg;  // [first code, value, bound, failures]
   __device__ __noinline__ int chk_fail(int x, int hi, int code) {
     if (dbg) {
@@ -408,7 +418,7 @@ struct Group {
     tr_cap = tr_len = 0;
     tr_stop = false;
 #ifdef DP_STAMPS
-    for (int i = 0; i < 8; ++i) acc[i] = 0;
+    for (int i = 0; i < 16; ++i) acc[i] = 0;
     dbg = nullptr;
 #endif
 
@@ -470,8 +480,16 @@ struct Group {
       touched[DP_CHK(atomicAdd(&scal[S_NTOUCHED], 1), 0, 2 * nv, 2)] = enc(l);
   }
 
-  // clause row evaluation; the literal loads are issued four at a time
-  __device__ __forceinline__ void eval_clause(int r, const IX* lits, int a, int b, int& crow) {
+  // The same from wave-converged code: every lane passes its literal (or -1).
+  // (Measured: a register count with ballot-placed appends instead of the LDS
+  // counter raised the kernel's VGPRs 149 -> 156 and ran 3% slower.)
+  __device__ __forceinline__ void note_all(int l, int r) {
+    if (l >= 0) note(l, r);
+  }
+
+  // clause row evaluation; the literal loads are issued four at a time.
+  // Returns the row's one unassigned literal when it is unit, else -1.
+  __device__ __forceinline__ int eval_clause(int r, const IX* lits, int a, int b, int& crow) {
     int nun = 0, ul = -1;
     for (int j = a; j < b; j += 4) {
       int l[4];
@@ -482,39 +500,50 @@ struct Group {
       for (int k = 0; k < 4; ++k) x[k] = l[k] >= 0 ? lit_val(l[k]) : -1;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        if (x[k] > 0) return;  // satisfied
+        if (x[k] > 0) return -1;  // satisfied
         if (x[k] == 0) { ++nun; ul = l[k]; }
       }
     }
     if (nun == 0) crow = min(crow, r);
-    else if (nun == 1) note(ul, r);
+    return nun == 1 ? ul : -1;
+  }
+  // a clause row (r < nc) or a learned row (r >= nrows)
+  __device__ __forceinline__ int clause_unit(int r, int& crow) {
+    if (r < nc) return eval_clause(r, clause_lits, clause_off[r], clause_off[r + 1], crow);
+    const int j = r - nrows;
+    return eval_clause(r, l_lits, DP_CHK((int)l_off[j], 0, lcap + 1, 33), DP_CHK((int)l_off[j + 1], 0, lcap + 1, 34), crow);
   }
 
-  __device__ __forceinline__ void eval_row(int r, int& crow) {
-    if (r < nc) {
-      eval_clause(r, clause_lits, clause_off[r], clause_off[r + 1], crow);
-    } else if (r >= nrows) {
-      const int j = r - nrows;
-      eval_clause(r, l_lits, DP_CHK((int)l_off[j], 0, lcap + 1, 33), DP_CHK((int)l_off[j + 1], 0, lcap + 1, 34), crow);
-    } else {
-      const int k = r - nc, a = card_off[k], b = card_off[k + 1];
-      int cnt = 0, nun = 0;
-      for (int j = a; j < b; ++j) {
-        const int x = val[card_lits[j]];
-        cnt += (x > 0);
-        nun += (x == 0);
+  // an AtMost row in one lane (several wavefronts, AtMost queue full)
+  __device__ __forceinline__ void card_serial(int r, int& crow) {
+    const int k = r - nc, a = card_off[k], b = card_off[k + 1];
+    int cnt = 0, nun = 0;
+    for (int j = a; j < b; ++j) {
+      const int x = val[card_lits[j]];
+      cnt += (x > 0);
+      nun += (x == 0);
+    }
+    const int bound = card_bound[k];
+    if (cnt > bound) crow = min(crow, r);
+    else if (nun > 0) {
+      // a variable repeated m times is a run of m positions
+      for (int j = a; j < b;) {
+        const int v = card_lits[j];
+        int e = j + 1;
+        while (e < b && (int)card_lits[e] == v) ++e;
+        if (val[v] == 0 && cnt + (e - j) > bound) note(2 * v + 1, r);
+        j = e;
       }
-      const int bound = card_bound[k];
-      if (cnt > bound) crow = min(crow, r);
-      else if (nun > 0) {
-        // a variable repeated m times is a run of m positions
-        for (int j = a; j < b;) {
-          const int v = card_lits[j];
-          int e = j + 1;
-          while (e < b && (int)card_lits[e] == v) ++e;
-          if (val[v] == 0 && cnt + (e - j) > bound) note(2 * v + 1, r);
-          j = e;
-        }
+    }
+  }
+
+  // One wavefront: before a visit, evaluate the AtMost queue if the visit
+  // might overflow it (the round's outcome does not depend on the order).
+  __device__ __forceinline__ void make_room(int& crow, int& ncq) {
+    if constexpr (NW == 1 && DP_MAKE_ROOM) {
+      if (ncq > CQ - 64) {
+        flush_cards(crow, ncq);
+        ncq = 0;
       }
     }
   }
@@ -528,12 +557,20 @@ struct Group {
   __device__ __forceinline__ void visit(int r, int& crow, int& ncq) {
     const bool ok = r >= 0 && row_on(r);
     const bool card = ok && r >= nc && r < nrows;
-    uint64_t m = __ballot(card);
-    if constexpr (NW == 1) {
-      if (ncq + __popcll(m) > CQ) m = 0;  // queue full: evaluate in-lane
-      if ((m >> lane) & 1ull) cardq[ncq + __popcll(m & lanemask_lt())] = enc(r);
-      else if (ok) eval_row(r, crow);
+    const uint64_t m = __ballot(card);
+    if constexpr (NW == 1 && DP_MAKE_ROOM) {
+      if (card) cardq[ncq + __popcll(m & lanemask_lt())] = enc(r);
+      note_all(ok && !card ? clause_unit(r, crow) : -1, r);
       ncq += __popcll(m);
+    } else if constexpr (NW == 1) {
+      const bool q = ncq + __popcll(m) <= CQ;  // queue full: evaluate in-lane
+      if (card && q) cardq[ncq + __popcll(m & lanemask_lt())] = enc(r);
+      else if (card) card_serial(r, crow);
+      else if (ok) {
+        const int ul = clause_unit(r, crow);
+        if (ul >= 0) note(ul, r);
+      }
+      if (q) ncq += __popcll(m);
     } else {
       int pos = CQ;
       if (m) {
@@ -542,7 +579,11 @@ struct Group {
         pos = __shfl(b, 0) + __popcll(m & lanemask_lt());
       }
       if (card && pos < CQ) cardq[pos] = enc(r);
-      else if (ok) eval_row(r, crow);  // queue full: evaluate in-lane
+      else if (card) card_serial(r, crow);  // queue full: evaluate in-lane
+      else if (ok) {
+        const int ul = clause_unit(r, crow);
+        if (ul >= 0) note(ul, r);
+      }
     }
   }
 
@@ -563,8 +604,8 @@ struct Group {
     for (int q = q0; q < ncq; q += qs) {
       const int r = DP_CHK((int)cardq[q], nc, nrows, 3), k = r - nc;
       const int a = card_off[k], len = (int)card_off[k + 1] - a, bound = card_bound[k];
-      if (len > 64) {  // long rows: one lane
-        if (lane == 0) eval_row(r, crow);
+      if (len > 64) {  // long rows: the wavefront in chunks of 64 positions
+        card_long(r, a, len, bound, crow);
         continue;
       }
       const int v = lane < len ? (int)card_lits[a + lane] : -1;
@@ -576,13 +617,39 @@ struct Group {
       const uint64_t ms = __ballot(start);
       const uint64_t after = lane < 63 ? ms >> (lane + 1) : 0ull;
       const int run = (after ? lane + 1 + __ffsll((unsigned long long)after) - 1 : len) - lane;
-      if (start && x == 0 && cnt + run > bound) note(2 * v + 1, r);
+      note_all(start && x == 0 && cnt + run > bound ? 2 * v + 1 : -1, r);
+    }
+  }
+  __device__ __forceinline__ void card_long(int r, int a, int len, int bound, int& crow) {
+    int cnt = 0;
+    bool any = false;
+    for (int j0 = 0; j0 < len; j0 += 64) {
+      const int j = j0 + lane;
+      const int v = j < len ? (int)card_lits[a + j] : -1;
+      const int x = v >= 0 ? val[v] : 0;
+      cnt += __popcll(__ballot(v >= 0 && x > 0));
+      any |= __ballot(v >= 0 && x == 0) != 0ull;
+    }
+    if (cnt > bound) { crow = min(crow, r); return; }
+    if (!any) return;
+    for (int j0 = 0; j0 < len; j0 += 64) {
+      const int j = j0 + lane;
+      const int v = j < len ? (int)card_lits[a + j] : -1;
+      const bool start = v >= 0 && (j == 0 || (int)card_lits[a + j - 1] != v);
+      int e = j + 1;
+      if (start)
+        while (e < len && (int)card_lits[a + e] == v) ++e;
+      const bool f = start && val[v] == 0 && cnt + (e - j) > bound;
+      note_all(f ? 2 * v + 1 : -1, r);
     }
   }
 
   // learned rows are evaluated in every round (threads over rows)
   __device__ __forceinline__ void eval_learned(int& crow) {
-    for (int j = learn_lo + tid; j < nl; j += NT) eval_row(nrows + j, crow);
+    for (int j0 = learn_lo; j0 < nl; j0 += NT) {
+      const int j = j0 + tid;
+      note_all(j < nl ? clause_unit(nrows + j, crow) : -1, nrows + j);
+    }
   }
 
   __device__ __forceinline__ void clear_touched(int nt) {
@@ -708,7 +775,14 @@ struct Group {
       if (hi - lo == 1) {  // one new literal: threads over its watch list
         const int l = DP_CHK((int)trail[lo], 0, 2 * nv, 10);
         const int a = w_off[l], e = w_off[l + 1];
-        for (int k0 = a; k0 < e; k0 += NT) visit(k0 + tid < e ? (int)w[k0 + tid] : -1, crow, ncq);
+        for (int k0 = a; k0 < e; k0 += NT) {
+          make_room(crow, ncq);
+          visit(k0 + tid < e ? (int)w[k0 + tid] : -1, crow, ncq);
+        }
+#ifdef DP_STAMPS
+        DP_ACC(8, stamp() - t0);
+        DP_ACC(12, e - a);
+#endif
       } else {
         for (int b = lo; b < hi; b += NT) {
           const int i = b + tid;
@@ -737,9 +811,11 @@ struct Group {
             // every frontier literal writes its watch range into the list
             for (int k = 0, at = before + incl - cnt; k < cnt; ++k) wbuf[at + k] = enc(a + k);
             gsync();
-            for (int t0 = 0; t0 < total; t0 += NT)
+            for (int t0 = 0; t0 < total; t0 += NT) {
+              make_room(crow, ncq);
               visit(t0 + tid < total ? DP_CHK((int)w[DP_CHK((int)wbuf[t0 + tid], 0, nwatch, 12)], 0, nrows, 13) : -1,
                     crow, ncq);
+            }
             gsync();
           } else {
             // a very large chunk: one frontier literal at a time
@@ -747,14 +823,31 @@ struct Group {
             for (int e = 0; e < n; ++e) {
               const int l = trail[b + e];
               const int a2 = w_off[l], e2 = w_off[l + 1];
-              for (int k0 = a2; k0 < e2; k0 += NT)
+              for (int k0 = a2; k0 < e2; k0 += NT) {
+                make_room(crow, ncq);
                 visit(k0 + tid < e2 ? (int)w[k0 + tid] : -1, crow, ncq);
+              }
             }
           }
         }
+#ifdef DP_STAMPS
+        DP_ACC(9, stamp() - t0);
+        DP_ACC(13, hi - lo);
+#endif
       }
+#ifdef DP_STAMPS
+      const int64_t tf = stamp();
+      DP_ACC(15, NW == 1 ? ncq : min(scal[S_NK], CQ));
+      flush_cards(crow, ncq);
+      const int64_t tl = stamp();
+      DP_ACC(10, tl - tf);
+      DP_ACC(14, nl - learn_lo);
+      eval_learned(crow);
+      DP_ACC(11, stamp() - tl);
+#else
       flush_cards(crow, ncq);
       eval_learned(crow);
+#endif
 #ifdef DP_STAMPS
       const int64_t t1 = stamp();
       const int fr = finish_round(crow);
@@ -772,7 +865,10 @@ struct Group {
   // on the empty assignment only the rows of the base list can fire.
   __device__ __forceinline__ int base_propagate() {
     int crow = INF, ncq = 0;
-    for (int i0 = 0; i0 < nbase; i0 += NT) visit(i0 + tid < nbase ? (int)base_rows[i0 + tid] : -1, crow, ncq);
+    for (int i0 = 0; i0 < nbase; i0 += NT) {
+      make_room(crow, ncq);
+      visit(i0 + tid < nbase ? (int)base_rows[i0 + tid] : -1, crow, ncq);
+    }
     flush_cards(crow, ncq);
     eval_learned(crow);
     if (finish_round(crow) < 0) return -1;
@@ -1062,12 +1158,13 @@ struct Group {
     return list >= nch ? list - nch : (int)choice_lits[(int)choice_off[list] + i];
   }
   __device__ __forceinline__ void dq_push_back(int list, int idx) {
-    const int at = (dq_head + dq_n) % cap;
+    int at = dq_head + dq_n;
+    if (at >= cap) at -= cap;
     if (tid == 0) { dq[2 * at] = enc(list); dq[2 * at + 1] = enc(idx); }
     ++dq_n;
   }
   __device__ __forceinline__ void dq_push_front(int list, int idx) {
-    dq_head = (dq_head + cap - 1) % cap;
+    dq_head = dq_head == 0 ? cap - 1 : dq_head - 1;
     if (tid == 0) { dq[2 * dq_head] = enc(list); dq[2 * dq_head + 1] = enc(idx); }
     ++dq_n;
   }
@@ -1082,7 +1179,7 @@ struct Group {
   __device__ __forceinline__ void push_guess() {
     gsync();
     const int list = DP_CHK((int)dq[2 * dq_head], 0, nch + nv, 17), idx = DP_CHK((int)dq[2 * dq_head + 1], 0, nv + 1, 18);
-    dq_head = (dq_head + 1) % cap;
+    dq_head = dq_head + 1 == cap ? 0 : dq_head + 1;
     --dq_n;
     const int len = list_len(list);
     int m = idx < len ? list_at(list, idx) : -1;
@@ -1499,7 +1596,7 @@ solve_kernel(KernelArgs a) {
     for (int i = 0; i < 5; ++i) o[5 + i] = W.acc[i];
     o[10] = wall0;
     o[11] = wallclock();
-    for (int i = 5; i < 8; ++i) o[11 + i] = W.acc[i];
+    for (int i = 5; i < 16; ++i) o[11 + i] = W.acc[i];
   }
 #endif
   if (W.tr_stop) flags |= DP_F_TRACE_TRUNCATED;

@@ -15,7 +15,7 @@ from deppy_amd import _lib  # noqa: E402
 from oracle import oracle  # noqa: E402  (checker only)
 from tests.gpu_common import compare_results, lowered_config  # noqa: E402
 
-NS = 20
+NS = 32
 config, n, flags = (int(x) for x in sys.argv[1:4])
 L = _lib.lib()
 L.dp_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _lib.c_i64p]
