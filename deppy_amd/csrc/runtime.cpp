@@ -36,10 +36,17 @@ namespace {
 
 constexpr int kMaxLdsBytes = 160 * 1024;          // LDS per CU on gfx950
 constexpr int64_t kDefaultBudget = 1 << 16;        // BCP invocations per problem
-// LDS bucket ceilings (bytes); one launch per non-empty bucket
-constexpr int kBuckets[] = {8 << 10, 16 << 10, 24 << 10, 32 << 10, 48 << 10, 64 << 10,
-                            96 << 10, 160 << 10};
-constexpr int kNBuckets = (int)(sizeof(kBuckets) / sizeof(kBuckets[0]));
+// LDS bucket ceilings (bytes); one launch per non-empty bucket (after
+// merging).  Diagnostic DEPPY_LDS_LEVELS=1: one bucket per occupancy level
+// instead (bucket k = the problems of which exactly kMaxLevel - k fit one
+// CU's LDS).  Measured worse: more launches per batch take more of the four
+// hardware queues, and batches in flight stop overlapping (config 2 at merge
+// 0.75: 27.0M -> 18.3M res/s; config 5 at 0.5: 583k -> 568k).
+constexpr int kMaxLevel = 16;
+constexpr int kLdsGran = 512;
+constexpr int kCeilings[] = {8 << 10, 16 << 10, 24 << 10, 32 << 10, 48 << 10, 64 << 10,
+                             96 << 10, 160 << 10};
+constexpr int kNBuckets = kMaxLevel;
 constexpr int kLanes = 4;
 constexpr double kMergeRatio = 0.5;  // bucket merging (build_slice); 0 = off
 constexpr double kSplitPct = 0.0;    // outlier split (build_slice); 0 = off
@@ -242,12 +249,22 @@ int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_of
     }
   }
   std::vector<std::vector<int32_t>> bucket(kNBuckets), big(3);
+  bool levels = false;
+  if (const char* e = std::getenv("DEPPY_LDS_LEVELS")) levels = std::atoi(e) != 0;  // diagnostic
   for (int32_t i = 0; i < n; ++i) {
     const int32_t* r = img[(size_t)i];
     const bool forced = opt_flags & (DP_OPT_FORCE_GROUP | DP_OPT_FORCE_HBM);
     const int64_t lds = dp::fits16(r) && !forced ? (int64_t)dp::layout<dp::M_LDS>(r).lds_bytes : INT64_MAX;
-    int k = 0;
-    while (k < kNBuckets && lds > kBuckets[k]) ++k;
+    int k = kNBuckets;
+    if (lds <= kMaxLdsBytes) {
+      if (levels) {
+        const int64_t q = kMaxLdsBytes / ((lds + kLdsGran - 1) / kLdsGran * kLdsGran);
+        k = kMaxLevel - (int)std::min<int64_t>(q, kMaxLevel);
+      } else {
+        k = 0;
+        while (lds > kCeilings[k]) ++k;
+      }
+    }
     if (k < kNBuckets) {
       bucket[(size_t)k].push_back(i);
       continue;
@@ -266,13 +283,15 @@ int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_of
   double merge = kMergeRatio;
   if (const char* m = std::getenv("DEPPY_BUCKET_MERGE")) merge = std::atof(m);  // diagnostic
   auto lds_of = [&](int32_t i) { return dp::layout<dp::M_LDS>(img[(size_t)i]).lds_bytes; };
+  int first_lds = 0;  // largest footprint of the first bucket of the open launch
   for (int k = 0; k < kNBuckets; ++k) {
     if (bucket[(size_t)k].empty()) continue;
     int mx = 0;
     for (int32_t i : bucket[(size_t)k]) mx = std::max(mx, lds_of(i));
     const bool join = !s.b_lds.empty() && merge > 0 &&
                       (double)(kMaxLdsBytes / std::max(mx, s.b_lds.back())) >=
-                          merge * (double)(kMaxLdsBytes / s.b_lds.back());
+                          merge * (double)(kMaxLdsBytes / first_lds);
+    if (!join) first_lds = mx;
     if (join) {
       s.b_count.back() += (int)bucket[(size_t)k].size();
       s.b_lds.back() = std::max(s.b_lds.back(), mx);
@@ -308,6 +327,20 @@ int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_of
     }
     s.b_first = f2; s.b_count = c2; s.b_lds = l2; s.b_chain = ch2;
   }
+  // Within a launch, workgroups are dispatched in blockIdx order: largest
+  // image first (longest-processing-time-first, the image size standing in
+  // for the unknown solve time), so the long solves do not start last and
+  // form the launch's tail.  (Results are indexed by problem: the order
+  // changes nothing but the schedule.)
+  bool lpt = true;
+  if (const char* e = std::getenv("DEPPY_LPT")) lpt = std::atoi(e) != 0;  // diagnostic
+  if (lpt)
+    for (size_t g = 0; g < s.b_first.size(); ++g) {
+      auto first = order.begin() + s.b_first[g], last = first + s.b_count[g];
+      std::stable_sort(first, last, [&](int32_t x, int32_t y) {
+        return img[(size_t)x][dp::DP_H_IMG] > img[(size_t)y][dp::DP_H_IMG];
+      });
+    }
   // diagnostic: DEPPY_LDS_PAD_KB raises every launch's LDS request (occupancy study)
   if (const char* pad = std::getenv("DEPPY_LDS_PAD_KB"))
     for (int& b : s.b_lds) b = std::max(b, std::atoi(pad) * 1024);
@@ -315,6 +348,10 @@ int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_of
   std::vector<int64_t> soff(1, 0);
   for (int mode = dp::M_SPLIT; mode <= dp::M_HBM; ++mode) {
     if (big[(size_t)mode].empty()) continue;
+    if (lpt)
+      std::stable_sort(big[(size_t)mode].begin(), big[(size_t)mode].end(), [&](int32_t x, int32_t y) {
+        return img[(size_t)x][dp::DP_H_IMG] > img[(size_t)y][dp::DP_H_IMG];
+      });
     s.g_first.push_back((int)order.size());
     s.g_count.push_back((int)big[(size_t)mode].size());
     s.g_mode.push_back(mode);

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Same-box A/B of an environment knob: alternating bench runs per config.
+#   usage (via gpurun): bash scripts/ab_env.sh <tag> "<configs>" <steps> VAR "v1 v2 ..."
+TAG=$1; CONFIGS=$2; STEPS=$3; VAR=$4; VALS=$5
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+for rep in 1 2; do
+  for c in $CONFIGS; do
+    for v in $VALS; do
+      env $VAR=$v timeout -k 10 200 python -u bench.py --config $c --steps $STEPS --warmup 4 --cpu-seconds 1 > $OUT/$v.$c.$rep.log 2>&1 || exit 1
+      python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().splitlines()[-1]); print(sys.argv[2], d['value'], d['ms_per_step'], d['roofline']['kernel_ms'], d['verified_bit_exact_vs_oracle'])" $OUT/$v.$c.$rep.log "$VAR=$v config$c rep$rep"
+    done
+  done
+done
