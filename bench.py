@@ -65,8 +65,11 @@ def lowered_config(config, n, seed):
 
 
 def compulsory_bytes(lw, res) -> int:
-    """Input record words + every output word the kernel writes."""
-    rec_bytes = 4 * int(lw.rec_off[-1])
+    """Input records + every output word the kernel writes.
+    Records count in their device form: LDS-path problems are stored in
+    16-bit form (2 bytes per word after the int32 header; "B/2-equivalents
+    when int16 literals are used"), the others at 4 bytes per word."""
+    rec_bytes, _ = _lib.device_bytes(lw.rec_off, lw.rec)
     n = lw.n
     out = n * (1 + 4 + 4 + 8)  # status, flags, core_len, steps
     out += 4 * int(res["inst_off"][-1])  # installed bitmaps

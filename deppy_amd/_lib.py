@@ -36,6 +36,7 @@ EXPORTS = [
     "dp_last_error", "dp_last_global_error", "dp_num_devices", "dp_solve", "dp_upload", "dp_run",
     "dp_launch", "dp_wait", "dp_download", "dp_resident_free", "dp_last_kernel_ms", "dp_gen_catalogs", "dp_gen_wire",
     "dp_gen_free", "dp_upload_traced", "dp_download_trace", "dp_solve_traced", "dp_lowered_errors",
+    "dp_device_bytes",
 ]
 
 
@@ -120,6 +121,7 @@ def lib():
     L.dp_gen_wire.argtypes = [vp]
     L.dp_gen_wire.restype = ctypes.POINTER(Wire)
     L.dp_gen_free.argtypes = [vp]
+    L.dp_device_bytes.argtypes = [ctypes.POINTER(Batch), ctypes.c_int32, c_i64p, c_i64p]
     _lib = L
     return L
 
@@ -347,6 +349,16 @@ class Resident:
         if self.h:
             lib().dp_resident_free(self.ctx.h, self.h)
             self.h = None
+
+
+def device_bytes(rec_off, rec, flags: int = 0) -> tuple[int, int]:
+    """(record bytes, image bytes) of a batch in its device form (dp_device_bytes)."""
+    rec_off = np.ascontiguousarray(rec_off, np.int64)
+    rec = np.ascontiguousarray(rec if len(rec) else np.zeros(1, np.int32), np.int32)
+    rb, ib = ctypes.c_int64(), ctypes.c_int64()
+    if lib().dp_device_bytes(ctypes.byref(_batch(rec_off, rec)), flags, ctypes.byref(rb), ctypes.byref(ib)) != 0:
+        raise RuntimeError("dp_device_bytes failed")
+    return rb.value, ib.value
 
 
 def generate(config: int, n: int, seed: int) -> dict:

@@ -91,7 +91,12 @@ __host__ __device__ inline dp_rec_layout rec_layout(const int32_t* h) {
 //                             (clauses of length <= 1; AtMost rows in which
 //                             some variable's multiplicity exceeds the bound)
 // Two reserved header words of the device copy carry the extension sizes.
-enum { DP_H_NBASE = 14, DP_H_IMG = 15 };
+// A third marks the 16-bit form (DP_FMT_U16): images of problems solved on
+// the LDS path are narrowed by the host (the int32 header stays, every word
+// after it becomes a uint16), so init stages half the bytes and has nothing
+// to convert.
+enum { DP_H_FMT = 13, DP_H_NBASE = 14, DP_H_IMG = 15 };
+enum { DP_FMT_I32 = 0, DP_FMT_U16 = 1 };
 
 struct ImgLayout {
   int32_t w_off, w, base, words;

@@ -156,9 +156,15 @@ int upload_vec(T** dst, const T* src, size_t n, hipStream_t st) {
   return 0;
 }
 
+// Does an image (its header) run on the one-wavefront LDS path?  The same
+// test places it in a bucket (build_slice).
+bool lds_path(const int32_t* h) {
+  return dp::fits16(h) && (int64_t)dp::layout<dp::M_LDS>(h).lds_bytes <= kMaxLdsBytes;
+}
+
 // Device image of one record (layout.hpp img_layout): the record, then its
 // watch lists and base rows.  Returns the image length.
-int64_t build_image(const int32_t* rec, std::vector<int32_t>& out) {
+int64_t build_image(const int32_t* rec, std::vector<int32_t>& out, bool narrow) {
   const dp_rec_layout R = dp::rec_layout(rec);
   const int32_t nv = rec[DP_H_NV], nc = rec[DP_H_NC], nk = rec[DP_H_NK];
   const int32_t* clause_off = rec + R.clause_off;
@@ -202,10 +208,42 @@ int64_t build_image(const int32_t* rec, std::vector<int32_t>& out) {
     if (fires) { out.push_back(nc + k); ++nbase; }
   }
   const int64_t words = (int64_t)(out.size() - at);
+  out[at + dp::DP_H_FMT] = dp::DP_FMT_I32;
   out[at + dp::DP_H_NBASE] = nbase;
   out[at + dp::DP_H_IMG] = (int32_t)words;
-  out.resize(at + (size_t)((words + 3) & ~3LL), 0);  // 16-byte aligned images
+  if (narrow && lds_path(out.data() + at)) {
+    // 16-bit form: body word j (after the header) -> uint16 j, two per int32
+    int32_t* x = out.data() + at;
+    const int64_t nb = words - DP_H_SIZE;
+    for (int64_t j = 0; j < nb; j += 2) {
+      const uint32_t lo = (uint32_t)x[DP_H_SIZE + j] & 0xffffu;
+      const uint32_t hi = j + 1 < nb ? (uint32_t)x[DP_H_SIZE + j + 1] & 0xffffu : 0u;
+      x[DP_H_SIZE + j / 2] = (int32_t)(lo | (hi << 16));
+    }
+    x[dp::DP_H_FMT] = dp::DP_FMT_U16;
+    out.resize(at + (size_t)DP_H_SIZE + (size_t)((nb + 1) / 2));
+  }
+  const int64_t stored = (int64_t)(out.size() - at);
+  out.resize(at + (size_t)((stored + 3) & ~3LL), 0);  // 16-byte aligned images
   return words;
+}
+
+extern "C" int dp_device_bytes(const dp_batch* b, int32_t opt_flags, int64_t* rec_bytes, int64_t* img_bytes) {
+  if (!b || (b->n_problems > 0 && (!b->rec || !b->rec_off))) return -1;
+  const bool forced = opt_flags & (DP_OPT_FORCE_GROUP | DP_OPT_FORCE_HBM);
+  int64_t rb = 0, ib = 0;
+  std::vector<int32_t> tmp;
+  for (int32_t p = 0; p < b->n_problems; ++p) {
+    const int32_t* rec = b->rec + b->rec_off[p];
+    tmp.clear();
+    build_image(rec, tmp, !forced);
+    const int64_t w = rec[DP_H_WORDS];
+    rb += tmp[dp::DP_H_FMT] == dp::DP_FMT_U16 ? 4 * DP_H_SIZE + 2 * (w - DP_H_SIZE) : 4 * w;
+    ib += 4 * (int64_t)tmp.size();
+  }
+  if (rec_bytes) *rec_bytes = rb;
+  if (img_bytes) *img_bytes = ib;
+  return 0;
 }
 
 // Build one device's slice: device images, bucketed launch order, outputs.
@@ -222,13 +260,14 @@ int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_of
   const unsigned hw = std::thread::hardware_concurrency();
   const int T = (int)std::max<int64_t>(1, std::min<int64_t>({16, hw ? (int64_t)hw : 1, n / 256}));
   std::vector<std::vector<int32_t>> parts((size_t)T);
+  const bool forced = opt_flags & (DP_OPT_FORCE_GROUP | DP_OPT_FORCE_HBM);
   std::vector<int64_t> len((size_t)n);
   auto part_lo = [&](int t) { return (int32_t)((int64_t)n * t / T); };
   auto build_part = [&](int t) {
     std::vector<int32_t>& out = parts[(size_t)t];
     for (int32_t i = part_lo(t); i < part_lo(t + 1); ++i) {
       const size_t at = out.size();
-      build_image(b->rec + b->rec_off[s.p0 + i], out);
+      build_image(b->rec + b->rec_off[s.p0 + i], out, !forced);
       len[(size_t)i] = (int64_t)(out.size() - at);
     }
   };
@@ -253,8 +292,7 @@ int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_of
   if (const char* e = std::getenv("DEPPY_LDS_LEVELS")) levels = std::atoi(e) != 0;  // diagnostic
   for (int32_t i = 0; i < n; ++i) {
     const int32_t* r = img[(size_t)i];
-    const bool forced = opt_flags & (DP_OPT_FORCE_GROUP | DP_OPT_FORCE_HBM);
-    const int64_t lds = dp::fits16(r) && !forced ? (int64_t)dp::layout<dp::M_LDS>(r).lds_bytes : INT64_MAX;
+    const int64_t lds = lds_path(r) && !forced ? (int64_t)dp::layout<dp::M_LDS>(r).lds_bytes : INT64_MAX;
     int k = kNBuckets;
     if (lds <= kMaxLdsBytes) {
       if (levels) {

@@ -327,12 +327,31 @@ struct Group {
     nbv = bits_words(nv); nbi = bits_words(nid);
     const IX* body;
     if constexpr (MODE == M_LDS) {
-      // device image (record + host-built watch lists and base rows): HBM
-      // int32 -> LDS uint16 with dwordx4 loads (images are 16-byte aligned and
-      // padded to 4 words)
+      // device image (record + host-built watch lists and base rows) -> LDS
+      // uint16 with dwordx4 loads (images are 16-byte aligned and padded to 4
+      // words).  The host stores LDS-path images in 16-bit form (DP_FMT_U16):
+      // they are copied as they are.
       IX* b = reinterpret_cast<IX*>(lds + L.body);
-      const int groups = (h[DP_H_IMG] - DP_H_SIZE + 3) >> 2;
       const int4* src = reinterpret_cast<const int4*>(grec + DP_H_SIZE);
+      if (h[DP_H_FMT] == DP_FMT_U16) {
+        const int groups = (h[DP_H_IMG] - DP_H_SIZE + 7) >> 3;
+        if (L.body == 0 && ((groups + 63) >> 6) * 1024 <= L.lds_bytes) {
+          // LDS-DMA, every 1 KiB piece in flight at once (lanes past the
+          // image re-read its last piece into LDS the later arrays own; they
+          // are initialised after this)
+          for (int c = 0; c < groups; c += 64) {
+            const int i = min(c + lane, groups - 1);
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src + i),
+                                             (__attribute__((address_space(3))) void*)(lds + 16 * c), 16, 0, 0);
+          }
+          __builtin_amdgcn_s_waitcnt(0);
+          wsync();
+        } else {
+          for (int i = tid; i < groups; i += NT) reinterpret_cast<int4*>(b)[i] = src[i];
+          wsync();
+        }
+      } else {
+      const int groups = (h[DP_H_IMG] - DP_H_SIZE + 3) >> 2;
       if (L.body == 0 && ((groups + 63) >> 6) * 1024 <= L.lds_bytes) {
         // Stage the int32 image into the allocation with LDS-DMA (every
         // 1 KiB piece in flight at once: one memory latency), then narrow it
@@ -363,6 +382,7 @@ struct Group {
         y.x = (uint32_t)(x.x & 0xffff) | ((uint32_t)x.y << 16);
         y.y = (uint32_t)(x.z & 0xffff) | ((uint32_t)x.w << 16);
         reinterpret_cast<uint2*>(b)[i] = y;
+      }
       }
       body = b;
     } else {

@@ -278,6 +278,14 @@ int dp_download_trace(dp_ctx* ctx, dp_resident* r, int32_t* trace, int32_t* trac
 int dp_solve_traced(dp_ctx* ctx, const dp_batch* b, int32_t trace_cap, dp_result* res,
                     int32_t* trace, int32_t* trace_len);
 
+/* Measurement helper (no reference counterpart): bytes of the batch as the
+ * device stores it.  rec_bytes = the records (the compulsory input of SURVEY
+ * §8(d)): 4 bytes per word, or for problems on the LDS path, whose images are
+ * kept in 16-bit form, 64 header bytes + 2 per word.  img_bytes = the whole
+ * device images (records + watch lists + base rows, 16-byte aligned).
+ * opt_flags as dp_opts.flags.  Returns 0 or -1. */
+int dp_device_bytes(const dp_batch* b, int32_t opt_flags, int64_t* rec_bytes, int64_t* img_bytes);
+
 /* Device time of the solve kernel(s) of the last waited launch (dp_run,
  * dp_wait, dp_solve), measured with HIP events on its stream (max over devices). */
 int dp_last_kernel_ms(const dp_ctx* ctx, double* ms);

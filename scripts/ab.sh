@@ -4,7 +4,7 @@
 TAG=$1; CONFIGS=$2; STEPS=$3; shift 3
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
-for rep in 1 2; do
+for rep in ${REPS:-1 2}; do
   for c in $CONFIGS; do
     for lib in "$@"; do
       DEPPY_VARIANT_LIB=$lib timeout -k 10 150 python -u bench.py --config $c --steps $STEPS --warmup 8 --cpu-seconds 1 > $OUT/$lib.$c.$rep.log 2>&1 || exit 1

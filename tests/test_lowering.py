@@ -138,3 +138,17 @@ def test_no_gpu_fails_loudly():
         pytest.skip("a GPU is present")
     with pytest.raises(RuntimeError):
         _lib.Context(0, 1)
+
+
+def test_device_bytes_16bit_form():
+    """LDS-path records are stored in 16-bit form (64 header bytes + 2 per
+    word); forcing the multi-wave path keeps them at 4 bytes per word."""
+    from tests.gpu_common import lowered_config
+    lw = lowered_config(2, 50, 1000)
+    off, rec = np.asarray(lw.rec_off), np.asarray(lw.rec)
+    words = off[1:] - off[:-1]
+    rb, ib = _lib.device_bytes(off, rec)
+    assert rb == int((64 + 2 * (words - 16)).sum())
+    assert ib > rb
+    rb32, ib32 = _lib.device_bytes(off, rec, flags=1)  # DP_OPT_FORCE_GROUP
+    assert rb32 == 4 * int(words.sum()) and ib32 > ib
