@@ -44,8 +44,10 @@ constexpr int64_t kDefaultBudget = 1 << 16;        // BCP invocations per proble
 // 0.75: 27.0M -> 18.3M res/s; config 5 at 0.5: 583k -> 568k).
 constexpr int kMaxLevel = 16;
 constexpr int kLdsGran = 512;
-constexpr int kCeilings[] = {8 << 10, 16 << 10, 24 << 10, 32 << 10, 48 << 10, 64 << 10,
-                             96 << 10, 160 << 10};
+// (160 KiB / 10, / 5, / 3, / 2, / 1.  Config 5, 30 steps: 588k res/s with
+// the earlier 8/16/24/32/48/64/96/160 ceilings, 608k with these;
+// scripts/ab_ceil.sh.  Configs 2 and 3 make one launch either way.)
+constexpr int kCeilings[] = {16 << 10, 32 << 10, 53 << 10, 80 << 10, 160 << 10};
 constexpr int kNBuckets = kMaxLevel;
 constexpr int kLanes = 4;
 constexpr double kMergeRatio = 0.5;  // bucket merging (build_slice); 0 = off
@@ -288,6 +290,17 @@ int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_of
     }
   }
   std::vector<std::vector<int32_t>> bucket(kNBuckets), big(3);
+  std::vector<int> ceil(std::begin(kCeilings), std::end(kCeilings));
+  if (const char* e = std::getenv("DEPPY_LDS_CEILINGS")) {  // diagnostic: KiB list, ascending, last 160
+    ceil.clear();
+    for (const char* q = e; *q;) {
+      ceil.push_back((int)(std::atof(q) * 1024));
+      while (*q && *q != ',') ++q;
+      if (*q == ',') ++q;
+    }
+    if (ceil.empty() || ceil.back() < kMaxLdsBytes || (int)ceil.size() > kNBuckets)
+      ceil.assign(std::begin(kCeilings), std::end(kCeilings));
+  }
   bool levels = false;
   if (const char* e = std::getenv("DEPPY_LDS_LEVELS")) levels = std::atoi(e) != 0;  // diagnostic
   for (int32_t i = 0; i < n; ++i) {
@@ -300,7 +313,7 @@ int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_of
         k = kMaxLevel - (int)std::min<int64_t>(q, kMaxLevel);
       } else {
         k = 0;
-        while (lds > kCeilings[k]) ++k;
+        while (lds > ceil[(size_t)k]) ++k;
       }
     }
     if (k < kNBuckets) {
