@@ -1546,10 +1546,12 @@ struct Group {
 // working-set footprint; the multi-wave modes work partly in HBM scratch).
 // Outputs: status / flags / installed / core / steps (oracle_solve).
 #ifndef DP_LDS_MIN_WAVES
-#define DP_LDS_MIN_WAVES 1
+#define DP_LDS_MIN_WAVES 4
 #endif
 // (DP_LDS_MIN_WAVES: minimum waves per SIMD the one-wavefront kernel is
-// compiled for; above 4 the compiler caps VGPRs and spills)
+// compiled for.  4 caps it at 128 VGPRs (151 unbounded, 3 waves per SIMD):
+// small catalogs run 16 per CU instead of 12, config 3 70.8M -> 86.0M res/s;
+// LDS-bound config 2 is unchanged, config 5 -0.7%.  Above 4 it spills hard.)
 template <int MODE>
 __global__ void __launch_bounds__(64 * mode_waves(MODE), MODE == M_LDS ? DP_LDS_MIN_WAVES : 1)
 solve_kernel(KernelArgs a) {
