@@ -1548,12 +1548,15 @@ struct Group {
 #ifndef DP_LDS_MIN_WAVES
 #define DP_LDS_MIN_WAVES 4
 #endif
-// (DP_LDS_MIN_WAVES: minimum waves per SIMD the one-wavefront kernel is
-// compiled for.  4 caps it at 128 VGPRs (151 unbounded, 3 waves per SIMD):
-// small catalogs run 16 per CU instead of 12, config 3 70.8M -> 86.0M res/s;
-// LDS-bound config 2 is unchanged, config 5 -0.7%.  Above 4 it spills hard.)
-template <int MODE>
-__global__ void __launch_bounds__(64 * mode_waves(MODE), MODE == M_LDS ? DP_LDS_MIN_WAVES : 1)
+// (MINW: minimum waves per SIMD the kernel is compiled for.  The one-wavefront
+// kernel has two builds: unbounded (151 VGPRs, 3 waves per SIMD, no spills)
+// and DP_LDS_MIN_WAVES = 4 (128 VGPRs, 21 VGPRs + 338 SGPRs spilled to
+// scratch).  The capped build only pays where LDS would let more than 12
+// problems share a CU (small catalogs: config 3 70.8M -> 86.0M res/s); at 9
+// per CU (config 2) its spills are ~40 MB of extra scratch writes per run for
+// no throughput.  launch_solve picks the build per launch by footprint.)
+template <int MODE, int MINW>
+__global__ void __launch_bounds__(64 * mode_waves(MODE), MINW)
 solve_kernel(KernelArgs a) {
   extern __shared__ int4 lds4[];
 #ifdef DP_STAMPS
@@ -1632,15 +1635,15 @@ solve_kernel(KernelArgs a) {
 }
 
 // Instantiate and launch one mode (included once per translation unit).
-#define DP_DEFINE_MODE(MODE, NAME)                                                          \
+#define DP_DEFINE_MODE(MODE, MINW, NAME)                                                    \
   hipError_t NAME(const KernelArgs& a, int n_blocks, int lds_bytes, hipStream_t stream) {   \
     if (n_blocks <= 0) return hipSuccess;                                                   \
-    hipLaunchKernelGGL(solve_kernel<MODE>, dim3((unsigned)n_blocks), dim3(64 * mode_waves(MODE)), \
+    hipLaunchKernelGGL((solve_kernel<MODE, MINW>), dim3((unsigned)n_blocks), dim3(64 * mode_waves(MODE)), \
                        (size_t)lds_bytes, stream, a);                                       \
     return hipGetLastError();                                                               \
   }                                                                                         \
   hipError_t NAME##_configure(int max_lds_bytes) {                                          \
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&solve_kernel<MODE>),          \
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&solve_kernel<MODE, MINW>),          \
                                hipFuncAttributeMaxDynamicSharedMemorySize, max_lds_bytes);  \
   }
 

@@ -5,20 +5,33 @@
 namespace dp {
 
 hipError_t launch_lds(const KernelArgs&, int, int, hipStream_t);
+hipError_t launch_lds_dense(const KernelArgs&, int, int, hipStream_t);
 hipError_t launch_split(const KernelArgs&, int, int, hipStream_t);
 hipError_t launch_hbm(const KernelArgs&, int, int, hipStream_t);
 hipError_t launch_lds_configure(int);
+hipError_t launch_lds_dense_configure(int);
 hipError_t launch_split_configure(int);
 hipError_t launch_hbm_configure(int);
 
+// The unbounded one-wavefront build runs 3 waves per SIMD (12 per CU).  A
+// launch whose footprint lets LDS hold more problems than that per CU takes
+// the register-capped build (4 per SIMD, 16 per CU); larger footprints are
+// LDS-bound and keep the build without spills (solve_kernel.hpp).
+constexpr int kUnboundedWavesPerCU = 12;
+constexpr int kLdsPerCU = 160 * 1024;
+
 hipError_t launch_solve(const KernelArgs& a, int mode, int n_blocks, int lds_bytes, hipStream_t stream) {
-  if (mode == M_LDS) return launch_lds(a, n_blocks, lds_bytes, stream);
+  if (mode == M_LDS) {
+    const bool dense = lds_bytes > 0 && kLdsPerCU / lds_bytes > kUnboundedWavesPerCU;
+    return dense ? launch_lds_dense(a, n_blocks, lds_bytes, stream) : launch_lds(a, n_blocks, lds_bytes, stream);
+  }
   if (mode == M_SPLIT) return launch_split(a, n_blocks, lds_bytes, stream);
   return launch_hbm(a, n_blocks, lds_bytes, stream);
 }
 
 hipError_t configure_solve_kernel(int max_lds_bytes) {
   hipError_t e = launch_lds_configure(max_lds_bytes);
+  if (e == hipSuccess) e = launch_lds_dense_configure(max_lds_bytes);
   if (e == hipSuccess) e = launch_split_configure(max_lds_bytes);
   if (e == hipSuccess) e = launch_hbm_configure(max_lds_bytes);
   return e;
