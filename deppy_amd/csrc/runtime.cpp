@@ -158,10 +158,27 @@ int upload_vec(T** dst, const T* src, size_t n, hipStream_t st) {
   return 0;
 }
 
+// Problems whose one-wavefront LDS footprint exceeds kGroupAbove run as
+// multi-wave workgroups (M_SPLIT) instead: over 80 KiB only one of them fits
+// a CU, and a lone wavefront leaves three of its four SIMDs idle.  Config 5,
+// 30 steps, same box: 608k res/s with every LDS-fitting problem on one wave,
+// 701k at 80 KiB; 96 KiB 675k, 128 KiB 539k, 64 KiB 613k, 48 KiB 474k (the
+// 2-per-CU bucket is better on one wave).  profiles/r01_group_above_ab.jsonl.
+// DEPPY_GROUP_ABOVE=<bytes> overrides it (diagnostic; 163840 = off).
+constexpr int64_t kGroupAbove = 80 << 10;
+int64_t group_above() {
+  static const int64_t v = [] {
+    const char* e = std::getenv("DEPPY_GROUP_ABOVE");
+    const int64_t x = e ? std::atoll(e) : 0;
+    return x > 0 ? std::min<int64_t>(x, kMaxLdsBytes) : kGroupAbove;
+  }();
+  return v;
+}
+
 // Does an image (its header) run on the one-wavefront LDS path?  The same
 // test places it in a bucket (build_slice).
 bool lds_path(const int32_t* h) {
-  return dp::fits16(h) && (int64_t)dp::layout<dp::M_LDS>(h).lds_bytes <= kMaxLdsBytes;
+  return dp::fits16(h) && (int64_t)dp::layout<dp::M_LDS>(h).lds_bytes <= group_above();
 }
 
 // Device image of one record (layout.hpp img_layout): the record, then its
