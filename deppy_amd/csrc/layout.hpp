@@ -35,13 +35,21 @@ constexpr int32_t L_MAX = 64;
 //           LDS
 //   M_HBM   the same workgroup with everything but the work lists in HBM
 //           (catalogs whose per-variable state exceeds the LDS)
-enum Mode { M_LDS = 0, M_SPLIT = 1, M_HBM = 2 };
+// M_SPLIT4: M_SPLIT with MID_WAVES wavefronts (catalogs routed off the LDS
+// path for their size, not for overflowing it; runtime.cpp kMidMaxVars)
+enum Mode { M_LDS = 0, M_SPLIT = 1, M_HBM = 2, M_SPLIT4 = 3 };
 #ifndef DP_BIG_WAVES
 #define DP_BIG_WAVES 8
 #endif
 constexpr int32_t BIG_WAVES = DP_BIG_WAVES;
 
-__host__ __device__ constexpr int32_t mode_waves(int mode) { return mode == M_LDS ? 1 : BIG_WAVES; }
+#ifndef DP_MID_WAVES
+#define DP_MID_WAVES 4
+#endif
+constexpr int32_t MID_WAVES = DP_MID_WAVES;
+__host__ __device__ constexpr int32_t mode_waves(int mode) {
+  return mode == M_LDS ? 1 : mode == M_SPLIT4 ? MID_WAVES : BIG_WAVES;
+}
 // work list of one propagation chunk (rows watched by <= 64*waves frontier literals)
 #ifndef DP_WBUF_LDS
 #define DP_WBUF_LDS 256
@@ -159,7 +167,7 @@ __host__ __device__ inline Layout layout(const int32_t* h) {
   // every array 16-byte aligned; `hot` arrays go to LDS unless M_HBM, the
   // per-literal arrays to LDS only in M_LDS, the work lists always to LDS
   auto take = [&](int32_t nbytes, int kind) {
-    const bool lds = MODE == M_LDS || kind == 2 || (kind == 1 && MODE == M_SPLIT);
+    const bool lds = MODE == M_LDS || kind == 2 || (kind == 1 && (MODE == M_SPLIT || MODE == M_SPLIT4));
     int32_t& o = lds ? ol : og;
     const int32_t at = o;
     o += (nbytes + 15) & ~15;

@@ -166,6 +166,11 @@ int upload_vec(T** dst, const T* src, size_t n, hipStream_t st) {
 // 2-per-CU bucket is better on one wave).  profiles/r01_group_above_ab.jsonl.
 // DEPPY_GROUP_ABOVE=<bytes> overrides it (diagnostic; 163840 = off).
 constexpr int64_t kGroupAbove = 80 << 10;
+// Routed-off catalogs under kMidMaxVars variables run in 4-wave groups
+// (M_SPLIT4), larger ones in 8-wave groups: config 5 (up to ~2.4k variables)
+// 701k -> 737k res/s with 4 waves for all multi-wave work, while config 4
+// (~55k variables) fell 6.3k -> 5.3k (profiles/r01_group_waves_ab.jsonl).
+constexpr int32_t kMidMaxVars = 8192;
 int64_t group_above() {
   static const int64_t v = [] {
     const char* e = std::getenv("DEPPY_GROUP_ABOVE");
@@ -306,7 +311,7 @@ int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_of
       roff[(size_t)i + 1] = roff[(size_t)i] + len[(size_t)i];
     }
   }
-  std::vector<std::vector<int32_t>> bucket(kNBuckets), big(3);
+  std::vector<std::vector<int32_t>> bucket(kNBuckets), big(4);
   std::vector<int> ceil(std::begin(kCeilings), std::end(kCeilings));
   if (const char* e = std::getenv("DEPPY_LDS_CEILINGS")) {  // diagnostic: KiB list, ascending, last 160
     ceil.clear();
@@ -340,7 +345,8 @@ int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_of
     const dp::Layout ls = dp::layout<dp::M_SPLIT>(r), lh = dp::layout<dp::M_HBM>(r);
     // (layout arithmetic is int32: variables are capped well below its range)
     const bool sized = r[DP_H_NV] < (1 << 24) && r[DP_H_NID] < (1 << 26);
-    if (sized && ls.lds_bytes <= kMaxLdsBytes && !(opt_flags & DP_OPT_FORCE_HBM)) big[dp::M_SPLIT].push_back(i);
+    if (sized && ls.lds_bytes <= kMaxLdsBytes && !(opt_flags & DP_OPT_FORCE_HBM))
+      big[!forced && r[DP_H_NV] < kMidMaxVars ? dp::M_SPLIT4 : dp::M_SPLIT].push_back(i);
     else if (sized && lh.lds_bytes <= kMaxLdsBytes) big[dp::M_HBM].push_back(i);
     else s.too_large.push_back(i);
   }
@@ -414,7 +420,7 @@ int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_of
     for (int& b : s.b_lds) b = std::max(b, std::atoi(pad) * 1024);
   s.big_base = (int)order.size();
   std::vector<int64_t> soff(1, 0);
-  for (int mode = dp::M_SPLIT; mode <= dp::M_HBM; ++mode) {
+  for (int mode : {(int)dp::M_SPLIT4, (int)dp::M_SPLIT, (int)dp::M_HBM}) {
     if (big[(size_t)mode].empty()) continue;
     if (lpt)
       std::stable_sort(big[(size_t)mode].begin(), big[(size_t)mode].end(), [&](int32_t x, int32_t y) {
@@ -426,7 +432,9 @@ int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_of
     int mx = 0;
     for (int32_t i : big[(size_t)mode]) {
       const int32_t* r = img[(size_t)i];
-      const dp::Layout L = mode == dp::M_SPLIT ? dp::layout<dp::M_SPLIT>(r) : dp::layout<dp::M_HBM>(r);
+      const dp::Layout L = mode == dp::M_SPLIT    ? dp::layout<dp::M_SPLIT>(r)
+                           : mode == dp::M_SPLIT4 ? dp::layout<dp::M_SPLIT4>(r)
+                                                  : dp::layout<dp::M_HBM>(r);
       mx = std::max(mx, L.lds_bytes);
       soff.push_back(soff.back() + ((int64_t)L.bytes + 15) / 16 * 4);  // int32 words, 16-byte aligned
     }

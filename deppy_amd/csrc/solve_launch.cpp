@@ -7,10 +7,12 @@ namespace dp {
 hipError_t launch_lds(const KernelArgs&, int, int, hipStream_t);
 hipError_t launch_lds_dense(const KernelArgs&, int, int, hipStream_t);
 hipError_t launch_split(const KernelArgs&, int, int, hipStream_t);
+hipError_t launch_split4(const KernelArgs&, int, int, hipStream_t);
 hipError_t launch_hbm(const KernelArgs&, int, int, hipStream_t);
 hipError_t launch_lds_configure(int);
 hipError_t launch_lds_dense_configure(int);
 hipError_t launch_split_configure(int);
+hipError_t launch_split4_configure(int);
 hipError_t launch_hbm_configure(int);
 
 // The unbounded one-wavefront build runs 3 waves per SIMD (12 per CU).  A
@@ -26,6 +28,7 @@ hipError_t launch_solve(const KernelArgs& a, int mode, int n_blocks, int lds_byt
     return dense ? launch_lds_dense(a, n_blocks, lds_bytes, stream) : launch_lds(a, n_blocks, lds_bytes, stream);
   }
   if (mode == M_SPLIT) return launch_split(a, n_blocks, lds_bytes, stream);
+  if (mode == M_SPLIT4) return launch_split4(a, n_blocks, lds_bytes, stream);
   return launch_hbm(a, n_blocks, lds_bytes, stream);
 }
 
@@ -33,6 +36,7 @@ hipError_t configure_solve_kernel(int max_lds_bytes) {
   hipError_t e = launch_lds_configure(max_lds_bytes);
   if (e == hipSuccess) e = launch_lds_dense_configure(max_lds_bytes);
   if (e == hipSuccess) e = launch_split_configure(max_lds_bytes);
+  if (e == hipSuccess) e = launch_split4_configure(max_lds_bytes);
   if (e == hipSuccess) e = launch_hbm_configure(max_lds_bytes);
   return e;
 }
