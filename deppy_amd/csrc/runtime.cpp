@@ -254,7 +254,7 @@ int64_t build_image(const int32_t* rec, std::vector<int32_t>& out, bool narrow) 
 
 extern "C" int dp_device_bytes(const dp_batch* b, int32_t opt_flags, int64_t* rec_bytes, int64_t* img_bytes) {
   if (!b || (b->n_problems > 0 && (!b->rec || !b->rec_off))) return -1;
-  const bool forced = opt_flags & (DP_OPT_FORCE_GROUP | DP_OPT_FORCE_HBM);
+  const bool forced = opt_flags & (DP_OPT_FORCE_GROUP | DP_OPT_FORCE_HBM | DP_OPT_FORCE_MID);
   int64_t rb = 0, ib = 0;
   std::vector<int32_t> tmp;
   for (int32_t p = 0; p < b->n_problems; ++p) {
@@ -284,7 +284,7 @@ int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_of
   const unsigned hw = std::thread::hardware_concurrency();
   const int T = (int)std::max<int64_t>(1, std::min<int64_t>({16, hw ? (int64_t)hw : 1, n / 256}));
   std::vector<std::vector<int32_t>> parts((size_t)T);
-  const bool forced = opt_flags & (DP_OPT_FORCE_GROUP | DP_OPT_FORCE_HBM);
+  const bool forced = opt_flags & (DP_OPT_FORCE_GROUP | DP_OPT_FORCE_HBM | DP_OPT_FORCE_MID);
   std::vector<int64_t> len((size_t)n);
   auto part_lo = [&](int t) { return (int32_t)((int64_t)n * t / T); };
   auto build_part = [&](int t) {
@@ -346,7 +346,8 @@ int build_slice(DevSlice& s, Lanes& L, const dp_batch* b, const int64_t* inst_of
     // (layout arithmetic is int32: variables are capped well below its range)
     const bool sized = r[DP_H_NV] < (1 << 24) && r[DP_H_NID] < (1 << 26);
     if (sized && ls.lds_bytes <= kMaxLdsBytes && !(opt_flags & DP_OPT_FORCE_HBM))
-      big[!forced && r[DP_H_NV] < kMidMaxVars ? dp::M_SPLIT4 : dp::M_SPLIT].push_back(i);
+      big[(opt_flags & DP_OPT_FORCE_MID) || (!forced && r[DP_H_NV] < kMidMaxVars) ? dp::M_SPLIT4 : dp::M_SPLIT]
+          .push_back(i);
     else if (sized && lh.lds_bytes <= kMaxLdsBytes) big[dp::M_HBM].push_back(i);
     else s.too_large.push_back(i);
   }

@@ -212,7 +212,8 @@ typedef struct dp_opts {
  * fits, else in HBM).  These flags send every problem to a multi-wave path. */
 enum dp_opt_flag {
   DP_OPT_FORCE_GROUP = 1 << 0, /* every problem: multi-wave workgroup */
-  DP_OPT_FORCE_HBM = 1 << 1    /* every problem: multi-wave workgroup, state in HBM */
+  DP_OPT_FORCE_HBM = 1 << 1,   /* every problem: multi-wave workgroup, state in HBM */
+  DP_OPT_FORCE_MID = 1 << 2    /* every problem: 4-wave workgroup (the mid-size path) */
 };
 
 typedef struct dp_ctx dp_ctx;

@@ -121,10 +121,11 @@ def test_olm_scale_bit_exact(ctx, config, n, seed):
     assert (g["status"] == 1).all()
 
 
-@pytest.mark.parametrize("flags", [_lib.OPT_FORCE_GROUP, _lib.OPT_FORCE_HBM], ids=["split", "hbm"])
+@pytest.mark.parametrize("flags", [_lib.OPT_FORCE_GROUP, _lib.OPT_FORCE_MID, _lib.OPT_FORCE_HBM],
+                         ids=["split", "split4", "hbm"])
 @pytest.mark.parametrize("config,n,seed", [(2, 300, 41), (5, 120, 42), (3, 500, 43)])
 def test_multiwave_paths_bit_exact(config, n, seed, flags):
-    """The workgroup-per-problem kernels (M_SPLIT, M_HBM) on small catalogs,
+    """The workgroup-per-problem kernels (M_SPLIT, M_SPLIT4, M_HBM) on small catalogs,
     where the oracle is cheap and every path (learning, epilogue, cores) is hit."""
     c = _lib.Context(0, 1, flags=flags)
     try:
