@@ -159,13 +159,16 @@ int upload_vec(T** dst, const T* src, size_t n, hipStream_t st) {
 }
 
 // Problems whose one-wavefront LDS footprint exceeds kGroupAbove run as
-// multi-wave workgroups (M_SPLIT) instead: over 80 KiB only one of them fits
-// a CU, and a lone wavefront leaves three of its four SIMDs idle.  Config 5,
-// 30 steps, same box: 608k res/s with every LDS-fitting problem on one wave,
-// 701k at 80 KiB; 96 KiB 675k, 128 KiB 539k, 64 KiB 613k, 48 KiB 474k (the
-// 2-per-CU bucket is better on one wave).  profiles/r01_group_above_ab.jsonl.
+// multi-wave workgroups (M_SPLIT4 / M_SPLIT) instead: at two or one per CU, a
+// lone wavefront per problem leaves SIMDs idle.  Config 5, 30 steps, same box,
+// with 8-wave groups: 608k res/s with every LDS-fitting problem on one wave,
+// 701k at 80 KiB (96 KiB 675k, 128 KiB 539k, 64 KiB 613k, 48 KiB 474k).  With
+// 4-wave groups below kMidMaxVars: 737k at 80 KiB, 798k at 64 KiB (60 KiB
+// 686k, 53 KiB 682k, 68 KiB 777k, 72 KiB 734k, 96 KiB 666k).  The optimum
+// sits on the 53/80 KiB bucket structure of this workload; it is a tuning
+// point, not a derived constant.  profiles/r01_group_above_ab.jsonl.
 // DEPPY_GROUP_ABOVE=<bytes> overrides it (diagnostic; 163840 = off).
-constexpr int64_t kGroupAbove = 80 << 10;
+constexpr int64_t kGroupAbove = 64 << 10;
 // Routed-off catalogs under kMidMaxVars variables run in 4-wave groups
 // (M_SPLIT4), larger ones in 8-wave groups: config 5 (up to ~2.4k variables)
 // 701k -> 737k res/s with 4 waves for all multi-wave work, while config 4
