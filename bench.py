@@ -1,31 +1,45 @@
-"""Benchmark: batched pkg/sat resolution on MI355X.
+"""Benchmark: batched pkg/sat resolution on MI355X, host memory to host memory.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
+                    [--scaling weak|strong]
 
-One step = one pass of the solve kernel over one batch of BASELINE config 2:
-10,000 synthetic operator catalogs (~200 bundle entities, Dependency +
-Conflict + AtMost; SURVEY.md §8(d) generator), resident in HBM when the timed
-region starts.  Steps are pipelined `--depth` deep (default 3) as a serving
-loop would run them: the batch is resident in `depth` slots, step i launches
-slot i % depth (dp_launch) after waiting for that slot's previous step
-(dp_wait), so one step's tail of hard catalogs overlaps the next step's bulk.
-Every step still resolves its whole batch; `serial_ms_per_step` reports the
-unpipelined launch+wait time beside it.  With N > 1 (torchrun, one process per GPU) every rank solves
-its own 10,000 catalogs (distinct seeds): weak scaling, no collective on the
-data path (torch.distributed is used only for the barrier and the max-over-
-ranks of the timing).
+The reference's Solve is a host-memory-to-host-memory call
+(pkg/sat/solve.go:53-119) and its benchmark times that whole call
+(pkg/sat/bench_test.go:66-77).  One step here is the same contract for a batch:
+lowered records in host memory -> dp_submit (stage, H2D, solve, D2H) ->
+results in host memory (dp_job_wait), for one batch of BASELINE config 2 by
+default: 10,000 synthetic operator catalogs (~200 bundle entities,
+Dependency + Conflict + AtMost; SURVEY.md §8(d) generator).  `--depth` jobs
+are in flight, as a serving loop keeps them (default 2): step i is submitted
+before step i-2 is collected.  Every step resolves its whole batch, and every
+result lands in host memory.
 
-Rank 0 prints one JSON line.  `value` = resolutions/s over all ranks.
-`roofline.achieved` = compulsory bytes of the batch (input records + outputs,
-DESIGN.md §Measurement) / the solve kernel's mean device time (HIP events on
-its stream).  `cpu_baseline` = the CPU restatement (oracle/, "port") on the
-host, on the same batch repeated for a bounded time.
+`value` = resolutions/s over all ranks, host to host.  Secondary figures:
+`kernel_only` (the batch resident in HBM, relaunched: the rate the solve
+kernel alone sustains), `host_lowering_res_per_s` (wire format -> records,
+dp_lower, not in `value`), `latency` (one catalog alone, host to host, beside
+one CPU thread of the oracle).
+
+Multi-GPU: one process per GPU (torchrun); without WORLD_SIZE and --gpus N>1
+this script relaunches itself under torch.distributed.run before touching any
+GPU.  Problems are independent: no data-path collective;
+torch.distributed carries only the barrier and the max-over-ranks of the
+timing.  --scaling weak (default): every rank solves its own batch.
+--scaling strong: the config's total (config 3: 1,000,000 catalogs) is split
+across the ranks.
+
+`roofline.achieved` = algorithmic bytes of a chunk (staged records + outputs,
+DESIGN.md §4.2) / the chunk's solve-kernel device time (HIP events on its
+stream, dp_get_stats), averaged over the timed region.  `cpu_baseline` = the
+CPU restatement (oracle/, "port") on this process's CPU share (cgroup quota),
+one solver per core, on the same batch repeated for a bounded time.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -34,26 +48,53 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from deppy_amd import _lib, shard  # noqa: E402
-
 METRIC = "resolutions/sec (node) on synthetic catalogs at 1/2/4/8 GPUs; BCP HBM GB/s"
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
+PCIE_PEAK_GBS = 64.0   # PCIe Gen5 x16, one direction
 
-
-# BASELINE.json configs as bench workloads: (default catalogs per GPU, description)
+# BASELINE.json configs as bench workloads: (catalogs per GPU, strong-scaling
+# total, description)
 WORKLOADS = {
-    2: (10000, "config2: %d synthetic operator catalogs per GPU (P=40 packages, ~240 variables; "
-               "Dependency+Conflict+AtMost), one wavefront per catalog"),
-    3: (125000, "config3: %d small catalogs per GPU (P~U{4..12}, ~20-70 variables; 1M over 8 GPUs "
-                "by host partition), one wavefront per catalog"),
-    4: (256, "config4: %d OLM-scale catalogs per GPU (P=5000, ~55k variables, deep dependency "
-             "chains), one 8-wave workgroup per catalog"),
-    5: (10000, "config5: %d mixed-size catalogs per GPU (P~U{4..400}, 50%% with injected "
-               "infeasibility), UNSAT-heavy"),
+    2: (10000, 80000, "config2: %d synthetic operator catalogs per step (P=40 packages, ~240 variables; "
+                      "Dependency+Conflict+AtMost), one wavefront per catalog"),
+    3: (125000, 1000000, "config3: %d small catalogs per step (P~U{4..12}, ~20-70 variables; 1M over the "
+                         "node by host partition), one wavefront per catalog"),
+    4: (256, 2048, "config4: %d OLM-scale catalogs per step (P=5000, ~55k variables, deep dependency "
+                   "chains), one 8-wave workgroup per catalog"),
+    5: (10000, 80000, "config5: %d mixed-size catalogs per step (P~U{4..400}, 50%% with injected "
+                      "infeasibility), UNSAT-heavy"),
 }
 
 
+def cpu_share() -> dict:
+    """Cores this process may use: the cgroup cpu.max quota when set (the GPU
+    box gives each GPU 16), else the affinity mask."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = max(1, int(float(q) / float(p)))
+    except (OSError, ValueError):
+        pass
+    return {"nproc": os.cpu_count(), "affinity": aff, "cgroup_quota": quota,
+            "cores": min(aff, quota) if quota else aff}
+
+
+def maybe_relaunch(args) -> None:
+    """--gpus N > 1 without torchrun: run this script under
+    torch.distributed.run (a child process, started before any GPU call)."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(29500 + os.getpid() % 1000),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    sys.exit(subprocess.call(cmd, env=env))
+
+
 def lowered_config(config, n, seed):
+    from deppy_amd import _lib
     w = _lib.generate(config, n, seed)
     wa = _lib.WireArrays(**{k: w[k] for k in (
         "prob_var_off", "var_id", "var_con_off", "con_kind", "con_n", "con_arg_off", "con_arg",
@@ -64,21 +105,35 @@ def lowered_config(config, n, seed):
     return lw, t_lower
 
 
-def compulsory_bytes(lw, res) -> int:
-    """Input records + every output word the kernel writes.
-    Records count in their device form: LDS-path problems are stored in
-    16-bit form (2 bytes per word after the int32 header; "B/2-equivalents
-    when int16 literals are used"), the others at 4 bytes per word."""
-    rec_bytes, _ = _lib.device_bytes(lw.rec_off, lw.rec)
-    n = lw.n
-    out = n * (1 + 4 + 4 + 8)  # status, flags, core_len, steps
-    out += 4 * int(res["inst_off"][-1])  # installed bitmaps
-    out += 4 * int(res["core_len"].sum())  # cores
-    return rec_bytes + out
+def output_bytes(res) -> int:
+    """Every output word the kernel writes."""
+    n = len(res["status"])
+    return n * (1 + 4 + 4 + 4 + 8) + 4 * int(res["inst_off"][-1]) + 4 * int(res["core_len"].sum())
 
 
-def _same(a, b) -> bool:
-    return all(np.array_equal(a[k], b[k]) for k in ("status", "flags", "installed", "core_len", "core", "steps"))
+def class_mix(res) -> dict:
+    """A / B / UNSAT-BCP / UNSAT-search / budget (dp_flag bits)."""
+    st, fl = res["status"], res["flags"]
+    sat, unsat = st == 1, st == -1
+    return {"sat": int(sat.sum()), "unsat": int(unsat.sum()), "incomplete": int((st == 0).sum()),
+            "error": int((st == -2).sum()),
+            "class_a": int((sat & ((fl & 2) == 0)).sum()), "class_b": int((sat & ((fl & 2) != 0)).sum()),
+            "unsat_bcp": int((unsat & ((fl & 16) != 0)).sum()),
+            "unsat_search": int((unsat & ((fl & 16) == 0)).sum()),
+            "budget": int(((fl & 64) != 0).sum())}
+
+
+KEYS = ("status", "flags", "installed", "core_len", "steps")
+
+
+def same_results(a, b) -> bool:
+    if not all(np.array_equal(a[k], b[k]) for k in KEYS):
+        return False
+    for p in np.flatnonzero(a["core_len"]):
+        c0, c1 = int(a["core_off"][p]), int(a["core_off"][p]) + int(a["core_len"][p])
+        if not np.array_equal(a["core"][c0:c1], b["core"][c0:c1]):
+            return False
+    return True
 
 
 def main():
@@ -87,79 +142,81 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
     ap.add_argument("--problems", type=int, default=0,
-                    help="catalogs per GPU (0: the config's default, WORKLOADS)")
+                    help="catalogs per step and rank (weak) or in total (strong); 0: WORKLOADS")
     ap.add_argument("--seed", type=int, default=1000)
+    ap.add_argument("--depth", type=int, default=2, help="host-to-host jobs in flight")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--depth", type=int, default=8,
-                    help="steps in flight (1 = launch+wait per step); 8 = two per hardware queue")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic_config2.json"),
-                    help="HBM bytes per solve run measured by separate rocprofv3 --pmc passes "
-                         "(scripts/gpu_check.sh); used for roofline.traffic on the config it was taken on")
+    ap.add_argument("--kernel-steps", type=int, default=20,
+                    help="steps of the device-resident (kernel-only) secondary figure; 0: skip")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02_pmc_traffic.json"),
+                    help="HBM bytes per solve kernel dispatch from separate rocprofv3 --pmc passes; "
+                         "used for roofline.traffic when its config/problems match")
     args = ap.parse_args()
-    if args.problems <= 0:
-        args.problems = WORKLOADS[args.config][0]
+    maybe_relaunch(args)
+
+    from deppy_amd import _lib, shard  # noqa: E402  (after the relaunch decision)
 
     g = shard.init_from_env("nccl")
     rank, world, local = g.rank, g.world, g.local
-
-    lw, t_lower = lowered_config(args.config, args.problems, shard.shard_seed(args.seed, rank, args.problems))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    wl = WORKLOADS[args.config]
+    if args.scaling == "weak":
+        n = args.problems or wl[0]
+        first = shard.shard_seed(args.seed, rank, n)
+    else:
+        total = args.problems or wl[1]
+        lo, hi = shard.strong_range(total, rank, world)
+        n, first = hi - lo, args.seed + lo
+    lw, t_lower = lowered_config(args.config, n, first)
     ctx = _lib.Context(local, 1)
 
-    # PCIe-inclusive single pass (host records -> host results), reported only
-    t0 = time.perf_counter()
-    ctx.solve(lw.rec_off, lw.rec)
-    t_pcie = time.perf_counter() - t0
-
+    # host-to-host: depth jobs in flight, each the whole batch
     depth = max(1, args.depth)
-    slots = [ctx.upload(lw.rec_off, lw.rec) for _ in range(depth)]
+    outs = [_lib.result_arrays(lw.rec_off, lw.rec) for _ in range(depth)]
 
-    def steps(n, kms):
-        for i in range(n):
-            r = slots[i % depth]
-            if i >= depth:
-                r.wait()
-                kms.append(ctx.last_kernel_ms())
-            r.launch()
-        for i in range(max(0, n - depth), n):
-            slots[i % depth].wait()
-            kms.append(ctx.last_kernel_ms())
+    def run_steps(k):
+        jobs = []
+        for i in range(k):
+            if len(jobs) == depth:
+                jobs.pop(0).wait()
+            jobs.append(ctx.submit(lw.rec_off, lw.rec, outs[i % depth]))
+        for j in jobs:
+            j.wait()
 
-    # unpipelined reference figure (not the metric): launch + wait per step
-    serial = []
-    for _ in range(3):
-        t0 = time.perf_counter()
-        slots[0].run()
-        serial.append(time.perf_counter() - t0)
-
-    steps(args.warmup, [])
+    run_steps(max(args.warmup, 1))
+    first_res = ctx.submit(lw.rec_off, lw.rec).wait()  # cold-free single call, for the check
     g.barrier()
-    kms = []
+    ctx.stats(reset=True)
     t0 = time.perf_counter()
-    steps(args.steps, kms)
+    run_steps(args.steps)
     t1 = time.perf_counter()
     g.barrier()
+    st = ctx.stats(reset=True)
     elapsed = g.max(t1 - t0)
-    res = slots[0].download()
-    same = all(_same(res, x.download()) for x in slots[1:])
-    for x in slots:
-        x.free()
+    res = ctx.submit(lw.rec_off, lw.rec).wait()
+    deterministic = same_results(res, first_res) and all(
+        same_results(res, {**o, "status": o["status"][:n], "flags": o["flags"][:n],
+                           "core_len": o["core_len"][:n], "steps": o["steps"][:n]}) for o in outs)
 
-    value = shard.aggregate_rate(args.problems, world, args.steps, elapsed)
-    st = res["status"]
-    kernel_ms = float(np.mean(kms))
-    nbytes = compulsory_bytes(lw, res)
-    achieved = nbytes / (kernel_ms * 1e-3) / 1e9
-
+    value = world * n * args.steps / elapsed if args.scaling == "weak" else \
+        (args.problems or wl[1]) * args.steps / elapsed
+    # roofline of the solve kernel, per chunk (HIP events on its stream)
+    chunks = max(st["chunks"], 1)
+    kernel_ms = st["kernel_ms"] / chunks
+    out_b = output_bytes(res)
+    alg_per_chunk = (st["rec_bytes"] / max(args.steps, 1) + out_b) / (chunks / max(args.steps, 1))
+    achieved = alg_per_chunk / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
     traffic = None
     if args.pmc_json and os.path.exists(args.pmc_json):
         with open(args.pmc_json) as f:
             pmc = json.load(f)
-        if pmc.get("config") == args.config and pmc.get("problems") == args.problems:
+        if pmc.get("config") == args.config and pmc.get("chunk_problems") == int(round(n / (chunks / args.steps))):
             traffic = pmc.get("hbm_bytes_per_dispatch")
-
+    step_s = elapsed / args.steps
     line = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -167,38 +224,72 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "ms_per_step": round(step_s * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic",
-        "config": {"workload": WORKLOADS[args.config][1] % args.problems,
-                   "catalogs_per_gpu": args.problems, "parallelism": "dp%d (host partition)" % world,
-                   "seed": args.seed},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                     "traffic": traffic, "kernel_ms": round(kernel_ms, 4),
-                     "algorithmic_bytes_per_launch": nbytes,
-                     "effective_GBs_per_step": round(nbytes / (elapsed / args.steps) / 1e9, 3)},
-        "pipeline_depth": depth,
-        "serial_ms_per_step": round(float(np.median(serial)) * 1e3, 4),
-        "slots_identical": bool(same),
-        "classes": {"sat": int((st == 1).sum()), "unsat": int((st == -1).sum()),
-                    "incomplete": int((st == 0).sum()), "error": int((st == -2).sum()),
-                    "class_b": int(((res["flags"] & 2) != 0).sum())},
-        "pcie_inclusive_res_per_s": round(args.problems / t_pcie, 1),
-        "host_lowering_res_per_s": round(args.problems / t_lower, 1),
+        "config": {"workload": wl[2] % n, "catalogs_per_step_per_gpu": n,
+                   "parallelism": "dp%d (host partition)" % world, "seed": args.seed,
+                   "path": "host memory -> host memory (dp_submit/dp_job_wait), %d jobs in flight" % depth},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
+                     "kernel_ms_per_chunk": round(kernel_ms, 4),
+                     "algorithmic_bytes_per_chunk": int(alg_per_chunk),
+                     "chunks_per_step": round(chunks / args.steps, 2),
+                     "note": "per-chunk kernel time is measured while up to 4 chunks share the GPU"},
+        "pcie": {"h2d_GBs": round(st["h2d_bytes"] / (elapsed if world == 1 else step_s * args.steps) / 1e9, 2),
+                 "d2h_GBs": round(st["d2h_bytes"] / (elapsed if world == 1 else step_s * args.steps) / 1e9, 2),
+                 "h2d_bytes_per_step": st["h2d_bytes"] // args.steps, "peak_GBs": PCIE_PEAK_GBS},
+        "classes": class_mix(res),
+        "deterministic": bool(deterministic),
+        "host_lowering_res_per_s": round(n / t_lower, 1),
     }
+
+    if args.kernel_steps > 0:
+        # secondary: the batch resident in HBM, relaunched (kernel-only rate)
+        slots = [ctx.upload(lw.rec_off, lw.rec) for _ in range(4)]
+        for s in slots:
+            s.run()
+        t0 = time.perf_counter()
+        for i in range(args.kernel_steps):
+            s = slots[i % 4]
+            if i >= 4:
+                s.wait()
+            s.launch()
+        for s in slots:
+            s.wait()
+        tk = time.perf_counter() - t0
+        kres = slots[0].download()
+        for s in slots:
+            s.free()
+        line["kernel_only"] = {"res_per_s": round(n * args.kernel_steps / tk, 1),
+                               "ms_per_step": round(tk / args.kernel_steps * 1e3, 4),
+                               "identical_to_host_path": bool(same_results(kres, res))}
 
     if rank == 0 and not args.no_cpu:
         from oracle import oracle  # CPU baseline + checker only
-        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        share = cpu_share()
+        threads = share["cores"]
         o = oracle.solve_batch(lw.rec_off, lw.rec, 0, threads)  # also the parity check
-        ok = (np.array_equal(o["status"], st) and np.array_equal(o["flags"], res["flags"])
-              and np.array_equal(o["installed"], res["installed"])
-              and np.array_equal(o["core_len"], res["core_len"])
-              and np.array_equal(o["steps"], res["steps"]))
+        ok = same_results(res, o)
+        # latency: single catalogs alone, host to host, beside one oracle thread
+        lat_g, lat_c = [], []
+        for p in range(min(n, 5)):
+            a, b = int(lw.rec_off[p]), int(lw.rec_off[p + 1])
+            one_off = np.array([0, b - a], np.int64)
+            one = np.ascontiguousarray(lw.rec[a:b])
+            ctx.solve(one_off, one)
+            t0 = time.perf_counter()
+            ctx.solve(one_off, one)
+            lat_g.append(time.perf_counter() - t0)
+            t0 = time.perf_counter()
+            oracle.solve_batch(one_off, one, 0, 1)
+            lat_c.append(time.perf_counter() - t0)
+        line["latency"] = {"gpu_ms_median": round(float(np.median(lat_g)) * 1e3, 3),
+                           "cpu_1thread_ms_median": round(float(np.median(lat_c)) * 1e3, 3),
+                           "catalogs": len(lat_g), "note": "one catalog alone, host to host"}
         reps, t0 = 0, time.perf_counter()
         while True:
             oracle.solve_batch(lw.rec_off, lw.rec, 0, threads)
@@ -206,11 +297,13 @@ def main():
             if time.perf_counter() - t0 >= args.cpu_seconds:
                 break
         cpu_t = time.perf_counter() - t0
-        line["cpu_baseline"] = {"value": round(reps * args.problems / cpu_t, 1),
-                                "unit": "resolutions/s", "cores": threads, "kind": "port",
+        line["cpu_baseline"] = {"value": round(reps * n / cpu_t, 1), "unit": "resolutions/s",
+                                "cores": threads, "kind": "port",
                                 "sample": "the timed batch (%d catalogs) solved %d times by "
-                                          "oracle/sat_oracle.c on %d host threads (%.1f s)"
-                                          % (args.problems, reps, threads, cpu_t)}
+                                          "oracle/sat_oracle.c, one solver thread per core (%.1f s); "
+                                          "nproc %s, affinity %d, cgroup quota %s"
+                                          % (n, reps, cpu_t, share["nproc"], share["affinity"],
+                                             share["cgroup_quota"])}
         line["verified_bit_exact_vs_oracle"] = bool(ok)
     if rank == 0:
         print(json.dumps(line), flush=True)

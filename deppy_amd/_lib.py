@@ -37,7 +37,7 @@ EXPORTS = [
     "dp_last_error", "dp_last_global_error", "dp_num_devices", "dp_solve", "dp_upload", "dp_run",
     "dp_launch", "dp_wait", "dp_download", "dp_resident_free", "dp_last_kernel_ms", "dp_gen_catalogs", "dp_gen_wire",
     "dp_gen_free", "dp_upload_traced", "dp_download_trace", "dp_solve_traced", "dp_lowered_errors",
-    "dp_device_bytes",
+    "dp_device_bytes", "dp_submit", "dp_job_wait", "dp_get_stats",
 ]
 
 
@@ -61,6 +61,12 @@ class Wire(ctypes.Structure):
 class Opts(ctypes.Structure):
     _fields_ = [("first_device", ctypes.c_int32), ("n_devices", ctypes.c_int32),
                 ("step_budget", ctypes.c_int64), ("flags", ctypes.c_int32)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("problems", ctypes.c_int64), ("chunks", ctypes.c_int64), ("launches", ctypes.c_int64),
+                ("kernel_ms", ctypes.c_double), ("h2d_bytes", ctypes.c_int64), ("d2h_bytes", ctypes.c_int64),
+                ("rec_bytes", ctypes.c_int64)]
 
 
 class Batch(ctypes.Structure):
@@ -111,6 +117,9 @@ def lib():
     L.dp_download_trace.argtypes = [vp, vp, c_i32p, c_i32p]
     L.dp_solve_traced.argtypes = [vp, ctypes.POINTER(Batch), ctypes.c_int32, ctypes.POINTER(Result),
                                   c_i32p, c_i32p]
+    L.dp_submit.argtypes = [vp, ctypes.POINTER(Batch), ctypes.POINTER(Result), ctypes.POINTER(vp)]
+    L.dp_job_wait.argtypes = [vp, vp]
+    L.dp_get_stats.argtypes = [vp, ctypes.POINTER(Stats), ctypes.c_int32]
     L.dp_run.argtypes = [vp, vp]
     L.dp_launch.argtypes = [vp, vp]
     L.dp_wait.argtypes = [vp, vp]
@@ -262,17 +271,29 @@ class Context:
         return Resident(self, rec_off, rec, trace_cap)
 
     def solve(self, rec_off: np.ndarray, rec: np.ndarray, trace_cap: int = 0) -> dict:
-        """Upload, solve, download.  trace_cap > 0 also returns the search
-        trace (dp_upload_traced): trace[P, trace_cap], trace_len[P]."""
+        """Host records -> host results (dp_solve).  trace_cap > 0 goes through
+        the device-resident form and also returns the search trace
+        (dp_upload_traced): trace[P, trace_cap], trace_len[P]."""
+        if trace_cap <= 0:
+            return self.submit(rec_off, rec).wait()
         r = self.upload(rec_off, rec, trace_cap)
         try:
             r.run()
             out = r.download()
-            if trace_cap > 0:
-                out.update(r.download_trace())
+            out.update(r.download_trace())
             return out
         finally:
             r.free()
+
+    def submit(self, rec_off: np.ndarray, rec: np.ndarray, out: dict | None = None) -> "Job":
+        """Asynchronous host-to-host solve (dp_submit); Job.wait() -> results.
+        `out` (a previous result dict of the same batch) is reused in place."""
+        return Job(self, rec_off, rec, out)
+
+    def stats(self, reset: bool = False) -> dict:
+        st = Stats()
+        lib().dp_get_stats(self.h, ctypes.byref(st), 1 if reset else 0)
+        return {k: getattr(st, k) for k, _ in Stats._fields_}
 
     def last_kernel_ms(self) -> float:
         ms = ctypes.c_double()
@@ -286,6 +307,53 @@ def _batch(rec_off, rec):
     b.rec_off = _p(rec_off, c_i64p)
     b.rec = _p(rec, c_i32p)
     return b
+
+
+def result_arrays(rec_off, rec) -> dict:
+    """Caller-allocated dp_result arrays for a batch (dp_result_layout)."""
+    rec_off = np.ascontiguousarray(rec_off, np.int64)
+    n = len(rec_off) - 1
+    inst_off = np.zeros(n + 1, np.int64)
+    core_off = np.zeros(n + 1, np.int64)
+    lib().dp_result_layout(ctypes.byref(_batch(rec_off, rec)), _p(inst_off, c_i64p), _p(core_off, c_i64p))
+    return dict(status=np.zeros(max(n, 1), np.int8), flags=np.zeros(max(n, 1), np.int32),
+                installed=np.zeros(max(1, int(inst_off[-1])), np.uint32), inst_off=inst_off,
+                core=np.zeros(max(1, int(core_off[-1])), np.int32), core_off=core_off,
+                core_len=np.zeros(max(n, 1), np.int32), steps=np.zeros(max(n, 1), np.int64))
+
+
+def _result_struct(out: dict) -> Result:
+    return Result(_p(out["status"], c_i8p), _p(out["flags"], c_i32p), _p(out["installed"], c_u32p),
+                  _p(out["inst_off"], c_i64p), _p(out["core"], c_i32p), _p(out["core_off"], c_i64p),
+                  _p(out["core_len"], c_i32p), _p(out["steps"], c_i64p))
+
+
+class Job:
+    """A host-to-host solve in flight (dp_submit); wait() -> result dict."""
+
+    def __init__(self, ctx: Context, rec_off, rec, out: dict | None = None):
+        self.ctx = ctx
+        rec_off = np.ascontiguousarray(rec_off, np.int64)
+        rec = np.ascontiguousarray(rec if len(rec) else np.zeros(1, np.int32), np.int32)
+        self.n = len(rec_off) - 1
+        self.out = out if out is not None else result_arrays(rec_off, rec)
+        self._res = _result_struct(self.out)
+        h = ctypes.c_void_p()
+        if lib().dp_submit(ctx.h, ctypes.byref(_batch(rec_off, rec)), ctypes.byref(self._res),
+                           ctypes.byref(h)) != 0:
+            raise RuntimeError("dp_submit: " + ctx.error())
+        self.h = h
+
+    def wait(self) -> dict:
+        h, self.h = self.h, None
+        if h is None:
+            raise RuntimeError("dp_job_wait: job already waited")
+        if lib().dp_job_wait(self.ctx.h, h) != 0:
+            raise RuntimeError("dp_job_wait: " + self.ctx.error())
+        out = dict(self.out)
+        for k in ("status", "flags", "core_len", "steps"):
+            out[k] = out[k][:self.n]
+        return out
 
 
 class Resident:
@@ -323,15 +391,8 @@ class Resident:
 
     def download(self) -> dict:
         n = self.n
-        out = dict(status=np.zeros(max(n, 1), np.int8), flags=np.zeros(max(n, 1), np.int32),
-                   installed=np.zeros(max(1, int(self.inst_off[-1])), np.uint32),
-                   inst_off=self.inst_off,
-                   core=np.zeros(max(1, int(self.core_off[-1])), np.int32), core_off=self.core_off,
-                   core_len=np.zeros(max(n, 1), np.int32), steps=np.zeros(max(n, 1), np.int64))
-        r = Result(_p(out["status"], c_i8p), _p(out["flags"], c_i32p),
-                   _p(out["installed"], c_u32p), _p(self.inst_off, c_i64p),
-                   _p(out["core"], c_i32p), _p(self.core_off, c_i64p),
-                   _p(out["core_len"], c_i32p), _p(out["steps"], c_i64p))
+        out = result_arrays(self.rec_off, self.rec)
+        r = _result_struct(out)
         if lib().dp_download(self.ctx.h, self.h, ctypes.byref(r)) != 0:
             raise RuntimeError("dp_download: " + self.ctx.error())
         for k in ("status", "flags", "core_len", "steps"):

@@ -12,15 +12,19 @@ namespace dp {
 constexpr int DP_NSTAMP = 32;
 
 struct KernelArgs {
-  const int32_t* rec;      // records, each 16-byte aligned
+  const int32_t* rec;      // staged records (layout.hpp), each 16-byte aligned
   const int64_t* rec_off;  // [n] word offset of each record
   const int32_t* order;    // [grid] problem index of each workgroup
   int8_t* status;
   int32_t* flags;
   uint32_t* installed;
   const int64_t* inst_off;
+  // NotSatisfiable explanations: problem p's core_len[p] identities are at
+  // core[core_at[p]...], claimed from *core_pool_len (the pool holds the sum
+  // of the problems' identity counts, so it cannot overflow)
   int32_t* core;
-  const int64_t* core_off;
+  int32_t* core_at;
+  int32_t* core_pool_len;
   int32_t* core_len;
   int64_t* steps;
   int64_t budget;

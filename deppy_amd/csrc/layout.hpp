@@ -90,41 +90,55 @@ __host__ __device__ inline dp_rec_layout rec_layout(const int32_t* h) {
   return L;
 }
 
-// Device image of a problem = the record followed by an extension the host
-// runtime derives from it (runtime.cpp build_image), all int32 in HBM:
+// The device copy of a problem is its record alone: nothing derived is built
+// on the host or crosses PCIe.  A reserved header word of the device copy
+// marks the 16-bit form (DP_FMT_U16): records of problems solved on the LDS
+// path are narrowed by the host while it stages them (the int32 header stays,
+// every word after it becomes a uint16), so PCIe and the LDS-DMA of init move
+// half the bytes and the kernel has nothing to convert.
+//
+// The kernel extends the record during init (Group::build_watches) with
 //   w_off[2nv+1], w[ncl+nkl]  watch lists: rows to evaluate when literal l
 //                             becomes true (clauses holding ~l; AtMost rows
-//                             holding var(l) when l is positive), row order
-//   base[nbase]               rows that can fire on the empty assignment
-//                             (clauses of length <= 1; AtMost rows in which
-//                             some variable's multiplicity exceeds the bound)
-// Two reserved header words of the device copy carry the extension sizes.
-// A third marks the 16-bit form (DP_FMT_U16): images of problems solved on
-// the LDS path are narrowed by the host (the int32 header stays, every word
-// after it becomes a uint16), so init stages half the bytes and has nothing
-// to convert.
-enum { DP_H_FMT = 13, DP_H_NBASE = 14, DP_H_IMG = 15 };
+//                             holding var(l) when l is positive, one entry
+//                             per distinct variable)
+// right after the record in LDS (M_LDS) or in the problem's HBM scratch (the
+// multi-wave modes).  Rows that can fire on the empty assignment (clauses of
+// length <= 1, AtMost rows in which some variable's multiplicity exceeds the
+// bound) are found by a sweep of the row offsets (Group::base_propagate).
+enum { DP_H_FMT = 13 };
 enum { DP_FMT_I32 = 0, DP_FMT_U16 = 1 };
 
 struct ImgLayout {
-  int32_t w_off, w, base, words;
+  int32_t w_off, w, words;
 };
 
+// Words of the extended record (record + watch lists), in record-word units.
 __host__ __device__ inline ImgLayout img_layout(const int32_t* h) {
   ImgLayout X;
   int32_t o = h[DP_H_WORDS];
   X.w_off = o; o += 2 * h[DP_H_NV] + 1;
   X.w = o;     o += h[DP_H_NCL] + h[DP_H_NKL];
-  X.base = o;  o += h[DP_H_NBASE];
   X.words = o;
   return X;
+}
+
+// Words of the staged (device) copy of a record: 16-byte aligned, the body in
+// 16-bit form when narrow.
+__host__ __device__ inline int64_t staged_words(const int32_t* h, bool narrow) {
+  const int64_t body = (int64_t)h[DP_H_WORDS] - DP_H_SIZE;
+  const int64_t w = DP_H_SIZE + (narrow ? (body + 1) / 2 : body);
+  return (w + 3) & ~3LL;
 }
 
 // Byte offsets of every working-set array.  An offset is into the LDS
 // allocation when the mode places that array in LDS (in_lds below), else into
 // the problem's HBM scratch region.
 struct Layout {
-  int32_t body;      // M_LDS only: image arrays (header dropped), one IX per image word
+  int32_t body;      // M_LDS only: the extended record (header dropped), one IX per word
+  int32_t wx;        // multi-wave modes only: w_off[2nv+1] then w[ncl+nkl], int32 (HBM)
+  int32_t cnt;       // multi-wave modes only: int32[2nv+1] watch-list build counters (HBM);
+                     // M_LDS aliases them on the per-literal arrays (reason..touched)
   int32_t val;       // int8[nv]: 0 unassigned, 1 true, -1 false                  [LDS unless M_HBM]
   int32_t reason;    // IX[nv] implying row; R_DEC / R_EXTRA / a Solve() decision (-3 - index)
   int32_t rs;        // IX[nv] trail position where the assigning round started
@@ -176,7 +190,10 @@ __host__ __device__ inline Layout layout(const int32_t* h) {
   enum { COLD = 0, HOT = 1, WORK = 2 };
   L.cap = h[DP_H_NA] + h[DP_H_NCH] + 2;
   L.lcap = nv + 64;
-  L.body = MODE == M_LDS ? take((h[DP_H_IMG] - DP_H_SIZE + 4) * ix, COLD) : 0;  // +4: dwordx4 copy slack
+  const ImgLayout X = img_layout(h);
+  L.body = MODE == M_LDS ? take((X.words - DP_H_SIZE + 8) * ix, COLD) : 0;  // +8: dwordx4 copy slack
+  L.wx = MODE == M_LDS ? 0 : take((X.words - h[DP_H_WORDS]) * 4, COLD);
+  L.cnt = MODE == M_LDS ? 0 : take((2 * nv + 1) * 4, COLD);
   L.scal = take(mode_nscal(MODE) * 4, WORK);
   L.wbuf = take(mode_wbuf(MODE) * ix, WORK);
   L.cardq = take(mode_cq(MODE) * ix, WORK);

@@ -165,12 +165,12 @@ struct Group {
   }
 
   // ---- record views ----
-  int nv, nc, nk, nid, nrows, nbv, nbi, na, nch;
+  int nv, nc, nk, nid, nrows, nbv, nbi, na, nch, ncl;
   const IX *clause_off, *clause_lits, *clause_id;
   const IX *card_off, *card_lits, *card_bound, *card_id;
   const IX *var_choice_off, *choice_off, *choice_lits, *anchors;
-  const IX *w_off, *w, *base_rows;
-  int nbase, nwatch, dthr;
+  const IX *w_off, *w;  // watch lists, built by build_watches
+  int nwatch, dthr;
   // ---- working set ----
   int8_t* val;
   IX *reason, *rs, *trail, *touched, *d_mark, *l_off, *l_lits, *dq, *stk;
@@ -321,20 +321,20 @@ struct Group {
     const Layout L = layout<MODE>(h);
     const dp_rec_layout R = rec_layout(h);
     const ImgLayout X = img_layout(h);
+    ncl = h[DP_H_NCL];
     nv = h[DP_H_NV]; nc = h[DP_H_NC]; nk = h[DP_H_NK]; nid = h[DP_H_NID]; na = h[DP_H_NA];
     nch = h[DP_H_NCH];
     nrows = nc + nk;
     nbv = bits_words(nv); nbi = bits_words(nid);
     const IX* body;
     if constexpr (MODE == M_LDS) {
-      // device image (record + host-built watch lists and base rows) -> LDS
-      // uint16 with dwordx4 loads (images are 16-byte aligned and padded to 4
-      // words).  The host stores LDS-path images in 16-bit form (DP_FMT_U16):
-      // they are copied as they are.
+      // the record -> LDS uint16 with dwordx4 loads (staged records are
+      // 16-byte aligned and padded to 4 words).  The host stages LDS-path
+      // records in 16-bit form (DP_FMT_U16): they are copied as they are.
       IX* b = reinterpret_cast<IX*>(lds + L.body);
       const int4* src = reinterpret_cast<const int4*>(grec + DP_H_SIZE);
       if (h[DP_H_FMT] == DP_FMT_U16) {
-        const int groups = (h[DP_H_IMG] - DP_H_SIZE + 7) >> 3;
+        const int groups = (h[DP_H_WORDS] - DP_H_SIZE + 7) >> 3;
         if (L.body == 0 && ((groups + 63) >> 6) * 1024 <= L.lds_bytes) {
           // LDS-DMA, every 1 KiB piece in flight at once (lanes past the
           // image re-read its last piece into LDS the later arrays own; they
@@ -351,7 +351,7 @@ struct Group {
           wsync();
         }
       } else {
-      const int groups = (h[DP_H_IMG] - DP_H_SIZE + 3) >> 2;
+      const int groups = (h[DP_H_WORDS] - DP_H_SIZE + 3) >> 2;
       if (L.body == 0 && ((groups + 63) >> 6) * 1024 <= L.lds_bytes) {
         // Stage the int32 image into the allocation with LDS-DMA (every
         // 1 KiB piece in flight at once: one memory latency), then narrow it
@@ -393,8 +393,6 @@ struct Group {
     card_off = rv(R.card_off); card_lits = rv(R.card_lits); card_bound = rv(R.card_bound);
     card_id = rv(R.card_id); var_choice_off = rv(R.var_choice_off); choice_off = rv(R.choice_off);
     choice_lits = rv(R.choice_lits); anchors = rv(R.anchors);
-    w_off = rv(X.w_off); w = rv(X.w); base_rows = rv(X.base);
-    nbase = h[DP_H_NBASE];
     nwatch = h[DP_H_NCL] + h[DP_H_NKL];
     dthr = nrows + L_MAX;
     char* hot = MODE == M_HBM ? hbm : lds;   // val and the bitsets
@@ -441,6 +439,17 @@ struct Group {
     for (int i = 0; i < 16; ++i) acc[i] = 0;
     dbg = nullptr;
 #endif
+    // the watch lists follow the record (M_LDS) or live in the problem's
+    // scratch; M_LDS counts on the per-literal arrays, initialised below
+    if constexpr (MODE == M_LDS) {
+      build_watches(const_cast<IX*>(rv(X.w_off)), const_cast<IX*>(rv(X.w)),
+                    reinterpret_cast<uint32_t*>(lds + L.reason));
+      w_off = rv(X.w_off); w = rv(X.w);
+    } else {
+      IX* wo = reinterpret_cast<IX*>(hbm + L.wx);
+      build_watches(wo, wo + 2 * nv + 1, reinterpret_cast<uint32_t*>(hbm + L.cnt));
+      w_off = wo; w = wo + 2 * nv + 1;
+    }
 
     if constexpr (MODE == M_LDS) {
       for (int v = tid; v < nv; v += NT) val[v] = 0;
@@ -453,6 +462,71 @@ struct Group {
     }
     if (tid < mode_nscal(MODE)) scal[tid] = 0;
     if (tid == 0) l_off[0] = 0;
+    gsync();
+  }
+
+  // Watch lists of the record, built on the device (the host ships the record
+  // alone): per-literal counts, an inclusive scan into w_off, then a fill
+  // through per-literal cursors.  cnt[l + 1] counts the rows literal l wakes:
+  // the clauses holding ~l, and (l positive) the AtMost rows holding var(l),
+  // once per distinct variable.  Row order within a list is left to the
+  // atomics: every outcome of a round is a minimum over rows (reasons,
+  // conflicts, Solve()'s first violated row), so nothing depends on it.
+  __device__ __forceinline__ uint32_t ld_cnt(const uint32_t* p) const {
+    if constexpr (MODE == M_LDS) return *p;
+    else return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __device__ __forceinline__ void build_watches(IX* wo, IX* ww, uint32_t* cnt) {
+    const int n2 = 2 * nv + 1;
+    for (int i = tid; i < n2; i += NT) cnt[i] = 0u;
+    gsync();
+    for (int r = tid; r < nc; r += NT)
+      for (int j = clause_off[r]; j < (int)clause_off[r + 1]; ++j)
+        atomicAdd(&cnt[((int)clause_lits[j] ^ 1) + 1], 1u);
+    for (int k = tid; k < nk; k += NT) {
+      const int a = card_off[k], b = card_off[k + 1];
+      for (int j = a; j < b; ++j)
+        if (j == a || card_lits[j] != card_lits[j - 1]) atomicAdd(&cnt[2 * (int)card_lits[j] + 1], 1u);
+    }
+    gsync();
+    if constexpr (NW == 1) {
+      // lanes over 64 consecutive counters, DPP scan, carry across chunks
+      int carry = 0;
+      for (int b = 0; b < n2; b += 64) {
+        const int i = b + lane;
+        const int x = i < n2 ? (int)cnt[i] : 0;
+        const int incl = wave_incl_scan(x) + carry;
+        if (i < n2) { wo[i] = enc(incl); cnt[i] = (uint32_t)incl; }
+        carry = __builtin_amdgcn_readlane(incl, 63);
+      }
+    } else {
+      // one contiguous segment per thread, a group scan of segment sums
+      const int seg = (n2 + NT - 1) / NT;
+      const int s0 = min(tid * seg, n2), s1 = min(s0 + seg, n2);
+      int sum = 0;
+      for (int i = s0; i < s1; ++i) sum += (int)ld_cnt(&cnt[i]);
+      const int incl = wave_incl_scan(sum);
+      if (lane == 63) scal[S_SLOT + wid] = incl;
+      bar();
+      int run = incl - sum;
+#pragma unroll
+      for (int q = 0; q < NW; ++q) run += q < wid ? scal[S_SLOT + q] : 0;
+      bar();
+      for (int i = s0; i < s1; ++i) {
+        run += (int)ld_cnt(&cnt[i]);
+        wo[i] = enc(run);
+        cnt[i] = (uint32_t)run;
+      }
+    }
+    gsync();
+    for (int r = tid; r < nc; r += NT)
+      for (int j = clause_off[r]; j < (int)clause_off[r + 1]; ++j)
+        ww[atomicAdd(&cnt[(int)clause_lits[j] ^ 1], 1u)] = enc(r);
+    for (int k = tid; k < nk; k += NT) {
+      const int a = card_off[k], b = card_off[k + 1];
+      for (int j = a; j < b; ++j)
+        if (j == a || card_lits[j] != card_lits[j - 1]) ww[atomicAdd(&cnt[2 * (int)card_lits[j]], 1u)] = enc(nc + k);
+    }
     gsync();
   }
 
@@ -881,13 +955,30 @@ struct Group {
     }
   }
 
+  // Can AtMost row k fire on the empty assignment (a variable listed more
+  // times than the bound)?
+  __device__ __forceinline__ bool card_fires(int k) const {
+    const int a = card_off[k], b = card_off[k + 1], bound = card_bound[k];
+    if (b - a <= bound) return false;
+    for (int j = a; j < b;) {
+      int e = j + 1;
+      while (e < b && card_lits[e] == card_lits[j]) ++e;
+      if (e - j > bound) return true;
+      j = e;
+    }
+    return false;
+  }
+
   // The base scope (solve.go:63-79): one round evaluates every (enabled) row;
-  // on the empty assignment only the rows of the base list can fire.
+  // on the empty assignment only clauses of length <= 1 and AtMost rows with
+  // a multiplicity over the bound can fire, so a sweep visits just those.
   __device__ __forceinline__ int base_propagate() {
     int crow = INF, ncq = 0;
-    for (int i0 = 0; i0 < nbase; i0 += NT) {
+    for (int i0 = 0; i0 < nrows; i0 += NT) {
+      const int r = i0 + tid;
+      const bool f = r < nc ? (int)clause_off[r + 1] - (int)clause_off[r] <= 1 : r < nrows && card_fires(r - nc);
       make_room(crow, ncq);
-      visit(i0 + tid < nbase ? (int)base_rows[i0 + tid] : -1, crow, ncq);
+      visit(f ? r : -1, crow, ncq);
     }
     flush_cards(crow, ncq);
     eval_learned(crow);
@@ -1446,7 +1537,22 @@ struct Group {
     return r;
   }
 
-  __device__ __forceinline__ int core(int32_t* out, int32_t& flags) {
+  // thread 0's x in every thread
+  __device__ __forceinline__ int g_bcast0(int x) {
+    if constexpr (NW == 1) {
+      return __shfl(x, 0);
+    } else {
+      if (tid == 0) scal[S_SLOT] = x;
+      bar();
+      x = scal[S_SLOT];
+      bar();
+      return x;
+    }
+  }
+
+  // The explanation goes to a pool shared by the launch: its length is
+  // counted first, then one atomic claims the words (*at = its position).
+  __device__ __forceinline__ int core(int32_t* pool, int32_t* pool_len, int32_t& flags, int& at) {
     const int64_t saved = steps;
     steps = 0;
     int len = 0;
@@ -1468,7 +1574,13 @@ struct Group {
         if (r == RS_UNSAT) copy_bits(en, used, nid);
         else if (r == RS_BUDGET) { flags |= DP_F_CORE_BUDGET; break; }
       }
-      len = emit_bits(en, nbi, out);  // ascending identity ids
+      int c = 0;
+      for (int i = tid; i < nbi; i += NT) c += __popc(ld_bits(&en[i]));
+      c = g_sum(c);
+      int a0 = 0;
+      if (tid == 0 && c > 0) a0 = atomicAdd(pool_len, c);
+      at = g_bcast0(a0);
+      len = emit_bits(en, nbi, pool + at);  // ascending identity ids
     } else {
       flags |= DP_F_CORE_BUDGET;
     }
@@ -1611,8 +1723,8 @@ solve_kernel(KernelArgs a) {
     }
   }
   DP_STAMP(4);
-  int clen = 0;
-  if (status == DP_UNSAT) clen = W.core(a.core + a.core_off[pid], flags);
+  int clen = 0, cat = 0;
+  if (status == DP_UNSAT) clen = W.core(a.core, a.core_pool_len, flags, cat);
   DP_STAMP(5);
 #ifdef DP_STAMPS
   if (W.tid == 0 && a.stamps) {
@@ -1630,6 +1742,7 @@ solve_kernel(KernelArgs a) {
     a.status[pid] = (int8_t)status;
     a.flags[pid] = flags;
     a.core_len[pid] = clen;
+    a.core_at[pid] = cat;
     a.steps[pid] = W.steps;
   }
 }

@@ -18,6 +18,12 @@ def shard_seed(base_seed: int, rank: int, per_rank: int) -> int:
     return base_seed + rank * per_rank
 
 
+def strong_range(total: int, rank: int, world: int) -> tuple[int, int]:
+    """Strong scaling: rank's contiguous share [lo, hi) of `total` catalogs
+    (sizes differ by at most one)."""
+    return total * rank // world, total * (rank + 1) // world
+
+
 @dataclass
 class Group:
     rank: int = 0

@@ -248,9 +248,37 @@ const char* dp_last_error(const dp_ctx* ctx);
 const char* dp_last_global_error(void);
 int32_t dp_num_devices(const dp_ctx* ctx);
 
-/* Synchronous batch solve: H2D, kernel(s), D2H.  Returns 0, or a negative
- * whole-batch error (text in dp_last_error); per-problem outcomes in res. */
+/* Synchronous batch solve, host memory to host memory: the batched form of
+ * (Solver).Solve (solve.go:53-119), which the reference also calls on host
+ * memory.  Returns 0, or a negative whole-batch error (text in
+ * dp_last_error); per-problem outcomes in res.  Equivalent to dp_submit +
+ * dp_job_wait. */
 int dp_solve(dp_ctx* ctx, const dp_batch* b, dp_result* res);
+
+/* Asynchronous host-to-host solve (serving loops; no reference counterpart:
+ * the reference solves one problem per call).  dp_submit stages the batch
+ * chunk by chunk into the context's pinned buffers and enqueues each chunk's
+ * H2D copy, solve and D2H copy on the next lane (stream); it returns once the
+ * last chunk is enqueued.  b's arrays may be reused after dp_submit returns;
+ * res must stay valid until dp_job_wait(job) returns, which delivers the
+ * results and frees the job.  Several jobs may be in flight; a later submit
+ * that needs a busy lane first delivers that lane's chunk to its job. */
+typedef struct dp_job dp_job;
+int dp_submit(dp_ctx* ctx, const dp_batch* b, dp_result* res, dp_job** job);
+int dp_job_wait(dp_ctx* ctx, dp_job* job);
+
+/* Counters of the host-to-host path since the last reset (measurement). */
+typedef struct dp_stats {
+  int64_t problems;  /* problems staged by dp_submit / dp_solve              */
+  int64_t chunks;    /* pipeline chunks                                      */
+  int64_t launches;  /* solve kernel launches (all paths)                    */
+  double kernel_ms;  /* sum over chunks of their kernels' device time (HIP
+                        events on the chunk's stream, around its launches)   */
+  int64_t h2d_bytes; /* bytes copied host -> device                          */
+  int64_t d2h_bytes; /* bytes copied device -> host                          */
+  int64_t rec_bytes; /* staged record bytes (16-bit form on the LDS path)    */
+} dp_stats;
+int dp_get_stats(dp_ctx* ctx, dp_stats* out, int32_t reset);
 
 /* Device-resident form (benchmarks, pipelines): the batch is partitioned over
  * the context's devices and copied once; dp_run solves it in place. */
@@ -281,10 +309,10 @@ int dp_solve_traced(dp_ctx* ctx, const dp_batch* b, int32_t trace_cap, dp_result
 
 /* Measurement helper (no reference counterpart): bytes of the batch as the
  * device stores it.  rec_bytes = the records (the compulsory input of SURVEY
- * §8(d)): 4 bytes per word, or for problems on the LDS path, whose images are
- * kept in 16-bit form, 64 header bytes + 2 per word.  img_bytes = the whole
- * device images (records + watch lists + base rows, 16-byte aligned).
- * opt_flags as dp_opts.flags.  Returns 0 or -1. */
+ * §8(d)): 4 bytes per word, or for problems on the LDS path, whose records
+ * are staged in 16-bit form, 64 header bytes + 2 per word.  img_bytes = the
+ * staged copies as they cross PCIe (16-byte aligned; the kernel builds the
+ * watch lists itself).  opt_flags as dp_opts.flags.  Returns 0 or -1. */
 int dp_device_bytes(const dp_batch* b, int32_t opt_flags, int64_t* rec_bytes, int64_t* img_bytes);
 
 /* Device time of the solve kernel(s) of the last waited launch (dp_run,
