@@ -242,6 +242,7 @@ def main():
         "pcie": {"h2d_GBs": round(st["h2d_bytes"] / (elapsed if world == 1 else step_s * args.steps) / 1e9, 2),
                  "d2h_GBs": round(st["d2h_bytes"] / (elapsed if world == 1 else step_s * args.steps) / 1e9, 2),
                  "h2d_bytes_per_step": st["h2d_bytes"] // args.steps, "peak_GBs": PCIE_PEAK_GBS},
+        "host_ms_per_step": {k: round(st[k] / args.steps, 4) for k in ("stage_ms", "wait_ms", "scatter_ms")},
         "classes": class_mix(res),
         "deterministic": bool(deterministic),
         "host_lowering_res_per_s": round(n / t_lower, 1),

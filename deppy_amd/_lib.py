@@ -37,7 +37,8 @@ EXPORTS = [
     "dp_last_error", "dp_last_global_error", "dp_num_devices", "dp_solve", "dp_upload", "dp_run",
     "dp_launch", "dp_wait", "dp_download", "dp_resident_free", "dp_last_kernel_ms", "dp_gen_catalogs", "dp_gen_wire",
     "dp_gen_free", "dp_upload_traced", "dp_download_trace", "dp_solve_traced", "dp_lowered_errors",
-    "dp_device_bytes", "dp_submit", "dp_job_wait", "dp_get_stats",
+    "dp_device_bytes", "dp_submit", "dp_job_wait", "dp_get_stats", "dp_stage_roundtrip",
+    "dp_stitch_selftest", "dp_partition",
 ]
 
 
@@ -66,7 +67,8 @@ class Opts(ctypes.Structure):
 class Stats(ctypes.Structure):
     _fields_ = [("problems", ctypes.c_int64), ("chunks", ctypes.c_int64), ("launches", ctypes.c_int64),
                 ("kernel_ms", ctypes.c_double), ("h2d_bytes", ctypes.c_int64), ("d2h_bytes", ctypes.c_int64),
-                ("rec_bytes", ctypes.c_int64)]
+                ("rec_bytes", ctypes.c_int64), ("stage_ms", ctypes.c_double), ("wait_ms", ctypes.c_double),
+                ("scatter_ms", ctypes.c_double)]
 
 
 class Batch(ctypes.Structure):
@@ -120,6 +122,10 @@ def lib():
     L.dp_submit.argtypes = [vp, ctypes.POINTER(Batch), ctypes.POINTER(Result), ctypes.POINTER(vp)]
     L.dp_job_wait.argtypes = [vp, vp]
     L.dp_get_stats.argtypes = [vp, ctypes.POINTER(Stats), ctypes.c_int32]
+    L.dp_stage_roundtrip.argtypes = [ctypes.POINTER(Batch), ctypes.c_int32, ctypes.c_int32, ctypes.c_int64,
+                                     c_i32p, c_i32p, ctypes.c_int32]
+    L.dp_stitch_selftest.argtypes = [ctypes.POINTER(Batch), ctypes.c_int32, ctypes.POINTER(Result)]
+    L.dp_partition.argtypes = [c_i64p, ctypes.c_int32, ctypes.c_int32, c_i32p]
     L.dp_run.argtypes = [vp, vp]
     L.dp_launch.argtypes = [vp, vp]
     L.dp_wait.argtypes = [vp, vp]
@@ -421,6 +427,41 @@ def device_bytes(rec_off, rec, flags: int = 0) -> tuple[int, int]:
     if lib().dp_device_bytes(ctypes.byref(_batch(rec_off, rec)), flags, ctypes.byref(rb), ctypes.byref(ib)) != 0:
         raise RuntimeError("dp_device_bytes failed")
     return rb.value, ib.value
+
+
+def stage_roundtrip(rec_off, rec, flags: int = 0, chunk_problems: int = 0, chunk_bytes: int = 0):
+    """Host-only: stage a batch in chunks as dp_submit does and widen it back
+    (dp_stage_roundtrip) -> (records, first problem of each chunk)."""
+    rec_off = np.ascontiguousarray(rec_off, np.int64)
+    rec = np.ascontiguousarray(rec if len(rec) else np.zeros(1, np.int32), np.int32)
+    out = np.zeros_like(rec)
+    firsts = np.zeros(max(len(rec_off), 1), np.int32)
+    k = lib().dp_stage_roundtrip(ctypes.byref(_batch(rec_off, rec)), flags, chunk_problems, chunk_bytes,
+                                 _p(out, c_i32p), _p(firsts, c_i32p), len(firsts))
+    if k < 0:
+        raise ValueError("dp_stage_roundtrip: malformed record")
+    return out, firsts[:k]
+
+
+def stitch_selftest(rec_off, rec, chunk_problems: int) -> dict:
+    """Host-only: synthetic per-problem results scattered chunk by chunk
+    (dp_stitch_selftest)."""
+    rec_off = np.ascontiguousarray(rec_off, np.int64)
+    rec = np.ascontiguousarray(rec, np.int32)
+    out = result_arrays(rec_off, rec)
+    out["installed"][:] = 0xdeadbeef
+    r = _result_struct(out)
+    if lib().dp_stitch_selftest(ctypes.byref(_batch(rec_off, rec)), chunk_problems, ctypes.byref(r)) < 0:
+        raise ValueError("dp_stitch_selftest failed")
+    return out
+
+
+def partition(rec_off, nd: int) -> np.ndarray:
+    rec_off = np.ascontiguousarray(rec_off, np.int64)
+    cut = np.zeros(nd + 1, np.int32)
+    if lib().dp_partition(_p(rec_off, c_i64p), len(rec_off) - 1, nd, _p(cut, c_i32p)) != 0:
+        raise ValueError("dp_partition failed")
+    return cut
 
 
 def generate(config: int, n: int, seed: int) -> dict:

@@ -630,6 +630,7 @@ int dp_rec_validate(const int32_t* rec, int64_t words) {
     if (rec[L.clause_id + r] < 0 || rec[L.clause_id + r] >= nid) return -10;
   for (int32_t k = 0; k < nk; ++k) {
     if (rec[L.card_id + k] < 0 || rec[L.card_id + k] >= nid) return -10;
+    if (rec[L.card_bound + k] < 0) return -15;  // (lowering folds AtMost(n<0) into an empty clause)
     // duplicates of a variable must be consecutive (one run per variable)
     for (int32_t j = rec[L.card_off + k]; j < rec[L.card_off + k + 1]; ++j) {
       int32_t v = rec[L.card_lits + j];

@@ -27,6 +27,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <climits>
 #include <condition_variable>
 #include <cstdlib>
@@ -69,6 +70,10 @@ constexpr int64_t kChunkBytes = 24ll << 20;
 // copied with the fixed outputs; a chunk whose cores need more fetches the
 // rest with a second copy.
 constexpr int64_t kCoreWordsPerProblem = 8;
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 int64_t env_i64(const char* name, int64_t dflt) {
   const char* e = std::getenv(name);
@@ -329,26 +334,78 @@ void plan_chunk(Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0,
       if (L.mode == M_LDS) L.lds = std::max(L.lds, std::atoi(pad) * 1024);
 }
 
+// Narrow n words of s into d, checking lo <= x < hi for each (one pass; the
+// checks vectorise with the stores).
+static inline bool narrow_range(const int32_t* s, uint16_t* d, int32_t n, int32_t lo, int32_t hi) {
+  uint32_t bad = 0;
+  const uint32_t span = (uint32_t)(hi - lo);
+  for (int32_t j = 0; j < n; ++j) {
+    bad |= (uint32_t)((uint32_t)(s[j] - lo) >= span);
+    d[j] = (uint16_t)s[j];
+  }
+  return bad == 0;
+}
+// An offsets array: s[0] == 0, non-decreasing, s[n] == total.
+static inline bool narrow_offsets(const int32_t* s, uint16_t* d, int32_t n, int32_t total) {
+  uint32_t bad = (uint32_t)(s[0] != 0) | (uint32_t)(s[n] != total);
+  for (int32_t j = 0; j < n; ++j) bad |= (uint32_t)(s[j + 1] < s[j]);
+  for (int32_t j = 0; j <= n; ++j) d[j] = (uint16_t)s[j];
+  return bad == 0;
+}
+
+// The 16-bit form of a record whose header passed header_ok and fits16:
+// dp_rec_validate's checks fused into the narrowing pass.  AtMost bounds
+// over the row length are stored as the row length (the same row: neither
+// can be exceeded by the count).
+static bool stage_narrow(const int32_t* src, uint16_t* o) {
+  const dp_rec_layout L = dp_rec_layout_of(src);
+  const int32_t nv = src[DP_H_NV], nc = src[DP_H_NC], nk = src[DP_H_NK], nch = src[DP_H_NCH];
+  const int32_t nid = src[DP_H_NID], ncl = src[DP_H_NCL], nkl = src[DP_H_NKL], nchl = src[DP_H_NCHL];
+  auto d = [&](int32_t word) { return o + (word - DP_H_SIZE); };
+  bool ok = narrow_offsets(src + L.clause_off, d(L.clause_off), nc, ncl) &&
+            narrow_range(src + L.clause_lits, d(L.clause_lits), ncl, 0, 2 * nv) &&
+            narrow_range(src + L.clause_id, d(L.clause_id), nc, 0, nid) &&
+            narrow_offsets(src + L.card_off, d(L.card_off), nk, nkl) &&
+            narrow_range(src + L.card_lits, d(L.card_lits), nkl, 0, nv) &&
+            narrow_range(src + L.card_id, d(L.card_id), nk, 0, nid) &&
+            narrow_offsets(src + L.var_choice_off, d(L.var_choice_off), nv, nch) &&
+            narrow_offsets(src + L.choice_off, d(L.choice_off), nch, nchl) &&
+            narrow_range(src + L.choice_lits, d(L.choice_lits), nchl, 0, nv) &&
+            narrow_range(src + L.anchors, d(L.anchors), src[DP_H_NA], 0, nv);
+  if (!ok) return false;
+  const int32_t* co = src + L.card_off;
+  const int32_t* cl = src + L.card_lits;
+  for (int32_t k = 0; k < nk; ++k) {
+    const int32_t a = co[k], b = co[k + 1], bound = src[L.card_bound + k];
+    if (bound < 0) return false;
+    d(L.card_bound)[k] = (uint16_t)std::min(bound, b - a);
+    // the positions of a variable form one run
+    for (int32_t j = a + 1; j < b; ++j)
+      if (cl[j] != cl[j - 1])
+        for (int32_t i = a; i < j - 1; ++i)
+          if (cl[i] == cl[j]) return false;
+  }
+  return true;
+}
+
 // Stage local problem i of the plan into dst (the staged image area): the
 // int32 header with its format word, then the body in 16-bit or int32 form.
-// Returns false when the record is malformed (dp_rec_validate).
+// Returns false when the record is malformed (the checks of dp_rec_validate).
 bool stage_one(const Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0, int32_t i,
                int32_t* dst) {
   const int64_t at = P.img_off[(size_t)i], sw = P.img_off[(size_t)i + 1] - at;
   if (sw == 0) return true;  // skipped (header already rejected)
   const int32_t* src = rec + rec_off[p0 + i];
-  if (dp_rec_validate(src, rec_off[p0 + i + 1] - rec_off[p0 + i]) != 0) return false;
   int32_t* d = dst + at;
   const int64_t words = src[DP_H_WORDS];
   std::memcpy(d, src, 4 * DP_H_SIZE);
   if (P.narrow[(size_t)i]) {
     d[DP_H_FMT] = DP_FMT_U16;
     uint16_t* o = reinterpret_cast<uint16_t*>(d + DP_H_SIZE);
-    const int32_t* s = src + DP_H_SIZE;
-    const int64_t nb = words - DP_H_SIZE;
-    for (int64_t j = 0; j < nb; ++j) o[j] = (uint16_t)s[j];
-    for (int64_t j = nb; j < 2 * (sw - DP_H_SIZE); ++j) o[j] = 0;
+    if (!stage_narrow(src, o)) return false;
+    for (int64_t j = words - DP_H_SIZE; j < 2 * (sw - DP_H_SIZE); ++j) o[j] = 0;
   } else {
+    if (dp_rec_validate(src, rec_off[p0 + i + 1] - rec_off[p0 + i]) != 0) return false;
     d[DP_H_FMT] = DP_FMT_I32;
     std::memcpy(d + DP_H_SIZE, src + DP_H_SIZE, 4 * (size_t)(words - DP_H_SIZE));
     for (int64_t j = words; j < sw; ++j) d[j] = 0;
@@ -481,12 +538,16 @@ struct Buf {
     if (n <= cap) return hipSuccess;
     release();
     n = std::max<size_t>(al(n + n / 8), 4096);
-    hipError_t e = host ? hipHostMalloc(reinterpret_cast<void**>(&p), n, hipHostMallocPortable)
+    hipError_t e = host ? hipHostMalloc(reinterpret_cast<void**>(&p), n,
+                                        hipHostMallocPortable | hipHostMallocMapped | hipHostMallocCoherent)
                         : hipMalloc(reinterpret_cast<void**>(&p), n);
     if (e != hipSuccess) { p = nullptr; cap = 0; return e; }
+    dev = p;
+    if (host && hipHostGetDevicePointer(reinterpret_cast<void**>(&dev), p, 0) != hipSuccess) dev = p;
     cap = n;
     return hipSuccess;
   }
+  char* dev = nullptr;  // device address of a mapped host buffer (zero-copy)
   void release() {
     if (p) (void)(host ? hipHostFree(p) : hipFree(p));
     p = nullptr;
@@ -504,6 +565,7 @@ struct Lane {
   hipStream_t s = nullptr;
   hipEvent_t k0 = nullptr, k1 = nullptr, done = nullptr;
   Buf h_in{nullptr, 0, true}, d_in, h_out{nullptr, 0, true}, d_out, scratch;
+  bool zc_out = false;  // the chunk's kernels wrote their results straight into h_out
   // the chunk in flight
   dp_job* job = nullptr;
   int32_t p0 = 0;
@@ -536,6 +598,7 @@ struct dp_ctx {
   std::mutex mu;
   Pool* pool = nullptr;
   int next_lane = 0;  // pipeline cursor over (device, lane)
+  bool zc_in = true, zc_out = true;  // zero-copy records / results (start_chunk)
   int32_t chunk_problems = kChunkProblems;
   int64_t chunk_bytes = kChunkBytes;
   dp_stats st{};
@@ -595,26 +658,31 @@ int finish_lane(dp_ctx* ctx, Lane& L) {
   L.job = nullptr;
   job->pending--;
   HIP_OK(hipSetDevice(L.device));
+  const double t0 = now_ms();
   HIP_OK(hipEventSynchronize(L.done));
+  const double t1 = now_ms();
+  ctx->st.wait_ms += t1 - t0;
   float ms = 0.f;
   if (!L.plan.launches.empty() && hipEventElapsedTime(&ms, L.k0, L.k1) == hipSuccess) {
     ctx->st.kernel_ms += ms;
     ctx->last_ms = ms;
   }
-  const int32_t used = *at<int32_t>(L.h_out.p, L.ol.pool_len);
+  const int32_t used = L.zc_out ? 0 : *at<int32_t>(L.h_out.p, L.ol.pool_len);
   const size_t need = L.ol.pool + (size_t)used * 4;
-  if (need > L.ol.d2h) {  // cores beyond the pipelined window
+  if (!L.zc_out && need > L.ol.d2h) {  // cores beyond the pipelined window
     HIP_OK(hipMemcpyAsync(L.h_out.p + L.ol.d2h, L.d_out.p + L.ol.d2h, need - L.ol.d2h, hipMemcpyDeviceToHost, L.s));
     HIP_OK(hipStreamSynchronize(L.s));
     ctx->st.d2h_bytes += (int64_t)(need - L.ol.d2h);
   }
   scatter(L.plan, L.ol, L.h_out.p, L.p0, &job->res);
+  ctx->st.scatter_ms += now_ms() - t1;
   return 0;
 }
 
 // Stage and enqueue problems [p0, p0+n) of a job on lane L.
 int start_chunk(dp_ctx* ctx, Lane& L, dp_job* job, int32_t p0, int32_t n) {
   HIP_OK(hipSetDevice(L.device));
+  const double t0 = now_ms();
   std::vector<uint8_t> bad((size_t)n, 0);
   dp::plan_chunk(L.plan, job->rec, job->rec_off, p0, n, ctx->flags, &bad);
   const InLayout il = in_layout(L.plan);
@@ -637,24 +705,47 @@ int start_chunk(dp_ctx* ctx, Lane& L, dp_job* job, int32_t p0, int32_t n) {
       return 0;  // the chunk is not launched; the job reports the error
     }
   fill_in_tables(P, il, L.h_in.p);
-  HIP_OK(hipMemcpyAsync(L.d_in.p, L.h_in.p, il.end, hipMemcpyHostToDevice, L.s));
+  ctx->st.stage_ms += now_ms() - t0;
+  // Zero-copy: the kernels write their results straight into the lane's
+  // mapped pinned buffer, and (when no multi-wave problem, which re-reads its
+  // record, is in the chunk) read the staged records from it.  With a D2H
+  // copy per chunk instead, copies from every stream queue on the same copy
+  // engine: a chunk's H2D waited behind the previous chunk's D2H, which waits
+  // for that chunk's kernel, and the lanes ran one after another (config 2:
+  // 3.0M res/s with H2D + D2H, 5.9M with zero-copy results, 6.4M with both
+  // zero-copy; profiles/r02_zero_copy_ab.jsonl).
+  const bool zc_in = ctx->zc_in && P.scratch_off.empty();
+  L.zc_out = ctx->zc_out;
+  char* din = zc_in ? L.h_in.dev : L.d_in.p;
+  char* dout = L.zc_out ? L.h_out.dev : L.d_out.p;
+  if (!zc_in) HIP_OK(hipMemcpyAsync(L.d_in.p, L.h_in.p, il.end, hipMemcpyHostToDevice, L.s));
   HIP_OK(hipMemsetAsync(L.d_out.p + L.ol.pool_len, 0, 4, L.s));
-  dp::KernelArgs a = kernel_args(il, L.ol, L.d_in.p, L.d_out.p, reinterpret_cast<int32_t*>(L.scratch.p), ctx->budget);
-  a.order = at<int32_t>(L.d_in.p, il.order);
+  dp::KernelArgs a = kernel_args(il, L.ol, din, dout, reinterpret_cast<int32_t*>(L.scratch.p), ctx->budget);
+  a.core_pool_len = at<int32_t>(L.d_out.p, L.ol.pool_len);
+  a.order = at<int32_t>(din, il.order);
   HIP_OK(hipEventRecord(L.k0, L.s));
   if (enqueue_launches(ctx, P, a, L.s)) return -1;
   HIP_OK(hipEventRecord(L.k1, L.s));
-  HIP_OK(hipMemcpyAsync(L.h_out.p, L.d_out.p, L.ol.d2h, hipMemcpyDeviceToHost, L.s));
+  if (!L.zc_out) HIP_OK(hipMemcpyAsync(L.h_out.p, L.d_out.p, L.ol.d2h, hipMemcpyDeviceToHost, L.s));
   HIP_OK(hipEventRecord(L.done, L.s));
   L.job = job;
   L.p0 = p0;
   job->pending++;
   ctx->st.chunks++;
   ctx->st.problems += n;
-  ctx->st.h2d_bytes += (int64_t)il.end;
-  ctx->st.d2h_bytes += (int64_t)L.ol.d2h;
+  ctx->st.h2d_bytes += zc_in ? 0 : (int64_t)il.end;
+  ctx->st.d2h_bytes += L.zc_out ? 0 : (int64_t)L.ol.d2h;
   ctx->st.rec_bytes += P.rec_bytes;
   return 0;
+}
+
+// The chunk starting at p: up to chunk_problems problems and chunk_bytes
+// record bytes (at least one problem).
+int32_t next_chunk(const int64_t* rec_off, int32_t p, int32_t P, int32_t chunk_problems, int64_t chunk_bytes) {
+  int32_t q = p;
+  const int64_t w0 = rec_off[p];
+  while (q < P && q - p < chunk_problems && (q == p || (rec_off[q + 1] - w0) * 4 <= chunk_bytes)) ++q;
+  return q;
 }
 
 Lane& lane_at(dp_ctx* ctx, int k) {
@@ -666,12 +757,7 @@ int submit_locked(dp_ctx* ctx, dp_job* job) {
   const int32_t P = job->n;
   int32_t p = 0;
   while (p < P) {
-    // chunk: up to chunk_problems problems and chunk_bytes record bytes
-    int32_t q = p;
-    const int64_t w0 = job->rec_off[p];
-    while (q < P && q - p < ctx->chunk_problems &&
-           (q == p || (job->rec_off[q + 1] - w0) * 4 <= ctx->chunk_bytes))
-      ++q;
+    const int32_t q = next_chunk(job->rec_off, p, P, ctx->chunk_problems, ctx->chunk_bytes);
     Lane& L = lane_at(ctx, ctx->next_lane++);
     if (ctx->next_lane >= (int)ctx->dev.size() * kLanes) ctx->next_lane = 0;
     if (finish_lane(ctx, L)) return -1;
@@ -739,6 +825,8 @@ dp_ctx* dp_create(const dp_opts* opts) {
   if (opts) ctx->flags = opts->flags;
   ctx->chunk_problems = (int32_t)std::max<int64_t>(1, env_i64("DEPPY_CHUNK_PROBLEMS", kChunkProblems));
   ctx->chunk_bytes = std::max<int64_t>(1, env_i64("DEPPY_CHUNK_BYTES", kChunkBytes));
+  ctx->zc_in = env_i64("DEPPY_ZC_IN", 1) != 0;   // diagnostic: 0 = H2D copy of every chunk
+  ctx->zc_out = env_i64("DEPPY_ZC_OUT", 1) != 0; // diagnostic: 0 = D2H copy of every chunk
   ctx->pool = new Pool(host_threads());
   return ctx;
 }
@@ -1062,6 +1150,97 @@ int dp_debug_stamps(dp_ctx* ctx, dp_resident* r, int64_t* out) {
 int dp_last_kernel_ms(const dp_ctx* ctx, double* ms) {
   if (!ctx || !ms) return -1;
   *ms = ctx->last_ms;
+  return 0;
+}
+
+// ---- host-only test hooks (include/deppy_hip.h) ----
+
+static Pool& hook_pool() {
+  static Pool pool(host_threads());
+  return pool;
+}
+
+int dp_stage_roundtrip(const dp_batch* b, int32_t opt_flags, int32_t chunk_problems, int64_t chunk_bytes,
+                       int32_t* out_rec, int32_t* chunk_first, int32_t cap) {
+  if (!b || !out_rec || b->n_problems < 0) return -1;
+  if (chunk_problems <= 0) chunk_problems = kChunkProblems;
+  if (chunk_bytes <= 0) chunk_bytes = kChunkBytes;
+  const int32_t P = b->n_problems;
+  int32_t nchunks = 0;
+  Plan plan;
+  std::vector<int32_t> staged;
+  for (int32_t p = 0; p < P;) {
+    const int32_t q = next_chunk(b->rec_off, p, P, chunk_problems, chunk_bytes);
+    if (chunk_first && nchunks < cap) chunk_first[nchunks] = p;
+    ++nchunks;
+    std::vector<uint8_t> bad((size_t)(q - p), 0);
+    dp::plan_chunk(plan, b->rec, b->rec_off, p, q - p, opt_flags, &bad);
+    staged.assign((size_t)plan.img_off[(size_t)plan.n] + 1, 0);
+    hook_pool().run(q - p, [&](int64_t i) {
+      if (!dp::stage_one(plan, b->rec, b->rec_off, p, (int32_t)i, staged.data())) bad[(size_t)i] = 1;
+    }, 32);
+    for (auto x : bad)
+      if (x) return -1;
+    for (int32_t i = 0; i < q - p; ++i) {
+      const int32_t* st = staged.data() + plan.img_off[(size_t)i];
+      int32_t* o = out_rec + b->rec_off[p + i];
+      const int64_t words = b->rec[b->rec_off[p + i] + DP_H_WORDS];
+      std::memcpy(o, st, 4 * DP_H_SIZE);
+      o[dp::DP_H_FMT] = b->rec[b->rec_off[p + i] + dp::DP_H_FMT];
+      if (st[dp::DP_H_FMT] == dp::DP_FMT_U16) {
+        const uint16_t* u = reinterpret_cast<const uint16_t*>(st + DP_H_SIZE);
+        for (int64_t j = DP_H_SIZE; j < words; ++j) o[j] = u[j - DP_H_SIZE];
+      } else {
+        std::memcpy(o + DP_H_SIZE, st + DP_H_SIZE, 4 * (size_t)(words - DP_H_SIZE));
+      }
+    }
+    p = q;
+  }
+  return nchunks;
+}
+
+int dp_stitch_selftest(const dp_batch* b, int32_t chunk_problems, dp_result* res) {
+  if (!b || !res || b->n_problems < 0) return -1;
+  if (chunk_problems <= 0) chunk_problems = kChunkProblems;
+  const int32_t P = b->n_problems;
+  int32_t nchunks = 0;
+  Plan plan;
+  std::vector<char> out;
+  for (int32_t p = 0; p < P; ++nchunks) {
+    const int32_t q = next_chunk(b->rec_off, p, P, chunk_problems, kChunkBytes);
+    dp::plan_chunk(plan, b->rec, b->rec_off, p, q - p, 0, nullptr);
+    const OutLayout ol = out_layout(plan);
+    out.assign(ol.end, 0);
+    int32_t pool_len = 0;
+    for (int32_t i = q - p - 1; i >= 0; --i) {  // pool claims in reverse problem order
+      const int64_t g = p + i;
+      const int32_t* h = b->rec + b->rec_off[g];
+      const int32_t nid = h[DP_H_NID];
+      const bool unsat = g % 3 == 0 && nid > 0;
+      at<int8_t>(out.data(), ol.status)[i] = (int8_t)(unsat ? DP_UNSAT : DP_SAT);
+      at<int32_t>(out.data(), ol.flags)[i] = (int32_t)(g & 0xff);
+      at<int64_t>(out.data(), ol.steps)[i] = 7 * g;
+      uint32_t* inst = at<uint32_t>(out.data(), ol.installed) + plan.inst_off[(size_t)i];
+      for (int64_t w = 0; w < plan.inst_off[(size_t)i + 1] - plan.inst_off[(size_t)i]; ++w)
+        inst[w] = (uint32_t)(g * 2654435761u) ^ (uint32_t)w;
+      const int32_t len = unsat ? std::min<int32_t>(nid, 1 + (int32_t)(g % 4)) : 0;
+      at<int32_t>(out.data(), ol.core_len)[i] = len;
+      at<int32_t>(out.data(), ol.core_at)[i] = pool_len;
+      for (int32_t j = 0; j < len; ++j) at<int32_t>(out.data(), ol.pool)[pool_len + j] = (int32_t)((g + j) % nid);
+      pool_len += len;
+    }
+    *at<int32_t>(out.data(), ol.pool_len) = pool_len;
+    scatter(plan, ol, out.data(), p, res);
+    p = q;
+  }
+  return nchunks;
+}
+
+int dp_partition(const int64_t* rec_off, int32_t n_problems, int32_t nd, int32_t* cut) {
+  if (!rec_off || !cut || nd <= 0 || n_problems < 0) return -1;
+  std::vector<int32_t> c;
+  dp::partition_by_words(rec_off, n_problems, nd, c);
+  std::copy(c.begin(), c.end(), cut);
   return 0;
 }
 

@@ -277,6 +277,9 @@ typedef struct dp_stats {
   int64_t h2d_bytes; /* bytes copied host -> device                          */
   int64_t d2h_bytes; /* bytes copied device -> host                          */
   int64_t rec_bytes; /* staged record bytes (16-bit form on the LDS path)    */
+  double stage_ms;   /* host: planning + staging records into pinned memory  */
+  double wait_ms;    /* host: blocked on a chunk's completion                 */
+  double scatter_ms; /* host: results -> the caller's dp_result              */
 } dp_stats;
 int dp_get_stats(dp_ctx* ctx, dp_stats* out, int32_t reset);
 
@@ -314,6 +317,27 @@ int dp_solve_traced(dp_ctx* ctx, const dp_batch* b, int32_t trace_cap, dp_result
  * staged copies as they cross PCIe (16-byte aligned; the kernel builds the
  * watch lists itself).  opt_flags as dp_opts.flags.  Returns 0 or -1. */
 int dp_device_bytes(const dp_batch* b, int32_t opt_flags, int64_t* rec_bytes, int64_t* img_bytes);
+
+/* Host-only test hooks (no device, no reference counterpart): the chunking,
+ * staging and result stitching of dp_submit, run on the CPU.
+ *   dp_stage_roundtrip: plans b in chunks as dp_submit does (chunk_problems /
+ *     chunk_bytes; 0 = defaults), stages every chunk, and widens the staged
+ *     copies back into out_rec (same offsets as b->rec): a round trip that
+ *     reproduces every record except AtMost bounds over their row length,
+ *     which are staged as the row length.  chunk_first[] receives the first
+ *     problem of each chunk (cap entries at most).  Returns the number of
+ *     chunks, or -1 for a malformed record.
+ *   dp_stitch_selftest: for every chunk, fills the chunk's output region with
+ *     synthetic results of problem p (status, flags, steps, installed words
+ *     and a core, all functions of p) at pool positions in reverse claim
+ *     order, then scatters them into res like a finished chunk.  Returns the
+ *     number of chunks or -1.
+ *   dp_partition: the contiguous per-device slices of a resident batch,
+ *     balanced by record words: cut[nd+1]. */
+int dp_stage_roundtrip(const dp_batch* b, int32_t opt_flags, int32_t chunk_problems, int64_t chunk_bytes,
+                       int32_t* out_rec, int32_t* chunk_first, int32_t cap);
+int dp_stitch_selftest(const dp_batch* b, int32_t chunk_problems, dp_result* res);
+int dp_partition(const int64_t* rec_off, int32_t n_problems, int32_t nd, int32_t* cut);
 
 /* Device time of the solve kernel(s) of the last waited launch (dp_run,
  * dp_wait, dp_solve), measured with HIP events on its stream (max over devices). */

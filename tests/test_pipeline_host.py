@@ -1,0 +1,113 @@
+"""Host-side parts of the host-to-host pipeline (runtime.cpp), on the CPU.
+
+dp_submit cuts a batch into chunks, stages every chunk's records (16-bit form
+for the LDS path, with dp_rec_validate's checks fused in), and stitches each
+chunk's results back into the caller's dp_result by problem index, with the
+explanations read through a per-chunk pool.  These tests run the same code
+through the library's host-only hooks, with no GPU: the staging round trip
+must reproduce every record, the stitching of synthetic per-problem results
+must put every value at its problem, for any chunking, and the per-device
+partition must cover the batch contiguously.
+"""
+import numpy as np
+import pytest
+
+from deppy_amd import _lib
+from tests.gpu_common import lowered_config
+
+
+def _bounds_clamped(rec_off, rec):
+    """The records with every AtMost bound over its row length set to the row
+    length (how the 16-bit staging stores them; the same row)."""
+    out = rec.copy()
+    for p in range(len(rec_off) - 1):
+        r = out[rec_off[p]:rec_off[p + 1]]
+        nc, nk, ncl, nkl = int(r[2]), int(r[3]), int(r[7]), int(r[8])
+        co = 16 + nc + 1 + ncl + nc
+        cb = co + nk + 1 + nkl
+        for k in range(nk):
+            r[cb + k] = min(int(r[cb + k]), int(r[co + k + 1] - r[co + k]))
+    return out
+
+
+@pytest.mark.parametrize("config,n", [(2, 300), (3, 2000), (5, 120)])
+@pytest.mark.parametrize("chunk", [1, 7, 4096])
+def test_stage_roundtrip(config, n, chunk):
+    lw = lowered_config(config, n, 77)
+    out, firsts = _lib.stage_roundtrip(lw.rec_off, lw.rec, chunk_problems=chunk)
+    assert np.array_equal(out, _bounds_clamped(lw.rec_off, lw.rec))
+    assert firsts[0] == 0 and np.all(np.diff(firsts) > 0) and np.all(np.diff(firsts) <= chunk)
+    assert len(firsts) == -(-n // chunk)
+
+
+def test_stage_roundtrip_int32_path():
+    # forced multi-wave placement stages int32 copies (dp_rec_validate path)
+    lw = lowered_config(2, 50, 5)
+    out, _ = _lib.stage_roundtrip(lw.rec_off, lw.rec, flags=_lib.OPT_FORCE_GROUP, chunk_problems=16)
+    assert np.array_equal(out, lw.rec)
+
+
+def test_stage_chunk_bytes_bound():
+    lw = lowered_config(2, 200, 9)
+    words = np.diff(lw.rec_off)
+    cap = int(words.max()) * 4 * 10  # ten of the largest records
+    _, firsts = _lib.stage_roundtrip(lw.rec_off, lw.rec, chunk_bytes=cap)
+    bounds = list(firsts) + [len(words)]
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        assert b - a == 1 or 4 * int(lw.rec_off[b] - lw.rec_off[a]) <= cap
+
+
+def test_stage_rejects_malformed():
+    lw = lowered_config(2, 20, 3)
+    rec = lw.rec.copy()
+    r0 = int(lw.rec_off[5])
+    nc, ncl = int(rec[r0 + 2]), int(rec[r0 + 7])
+    rec[r0 + 16 + nc + 1] = 2 * int(rec[r0 + 1]) + 3  # a clause literal past 2*nv
+    with pytest.raises(ValueError):
+        _lib.stage_roundtrip(lw.rec_off, rec)
+    rec = lw.rec.copy()
+    rec[r0 + 16 + 1] = rec[r0 + 16 + 2] + 1  # clause offsets not monotone
+    if ncl:
+        with pytest.raises(ValueError):
+            _lib.stage_roundtrip(lw.rec_off, rec)
+
+
+def _expected(lw):
+    n = lw.n
+    nv = lw.rec[lw.rec_off[:-1] + 1].astype(np.int64)
+    nid = lw.rec[lw.rec_off[:-1] + 6].astype(np.int64)
+    ref = _lib.result_arrays(lw.rec_off, lw.rec)
+    for p in range(n):
+        unsat = p % 3 == 0 and nid[p] > 0
+        ref["status"][p] = -1 if unsat else 1
+        ref["flags"][p] = p & 0xff
+        ref["steps"][p] = 7 * p
+        a, b = int(ref["inst_off"][p]), int(ref["inst_off"][p + 1])
+        ref["installed"][a:b] = (np.uint32((p * 2654435761) & 0xffffffff) ^ np.arange(b - a, dtype=np.uint32))
+        cl = min(int(nid[p]), 1 + p % 4) if unsat else 0
+        ref["core_len"][p] = cl
+        c0 = int(ref["core_off"][p])
+        ref["core"][c0:c0 + cl] = [(p + j) % int(nid[p]) for j in range(cl)]
+    return ref
+
+
+@pytest.mark.parametrize("chunk", [1, 3, 64, 4096])
+def test_stitching_any_chunking(chunk):
+    lw = lowered_config(3, 500, 21)
+    got = _lib.stitch_selftest(lw.rec_off, lw.rec, chunk)
+    ref = _expected(lw)
+    for k in ("status", "flags", "steps", "installed", "core_len"):
+        assert np.array_equal(got[k][:lw.n], ref[k][:lw.n]), k
+    for p in range(lw.n):
+        c0, cl = int(ref["core_off"][p]), int(ref["core_len"][p])
+        assert np.array_equal(got["core"][c0:c0 + cl], ref["core"][c0:c0 + cl]), p
+
+
+@pytest.mark.parametrize("nd", [1, 2, 3, 8])
+def test_partition_covers_batch(nd):
+    lw = lowered_config(2, 101, 4)
+    cut = _lib.partition(lw.rec_off, nd)
+    assert cut[0] == 0 and cut[-1] == lw.n and np.all(np.diff(cut) >= 0)
+    if nd <= lw.n:
+        words = [int(lw.rec_off[cut[d + 1]] - lw.rec_off[cut[d]]) for d in range(nd)]
+        assert max(words) <= int(lw.rec_off[-1]) / nd + int(np.diff(lw.rec_off).max())
