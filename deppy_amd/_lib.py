@@ -37,7 +37,7 @@ EXPORTS = [
     "dp_last_error", "dp_last_global_error", "dp_num_devices", "dp_solve", "dp_upload", "dp_run",
     "dp_launch", "dp_wait", "dp_download", "dp_resident_free", "dp_last_kernel_ms", "dp_gen_catalogs", "dp_gen_wire",
     "dp_gen_free", "dp_upload_traced", "dp_download_trace", "dp_solve_traced", "dp_lowered_errors",
-    "dp_device_bytes", "dp_submit", "dp_job_wait", "dp_get_stats", "dp_stage_roundtrip",
+    "dp_device_bytes", "dp_lower_into", "dp_lowered_exact_count", "dp_submit", "dp_job_wait", "dp_get_stats", "dp_stage_roundtrip",
     "dp_stitch_selftest", "dp_partition",
 ]
 
@@ -96,6 +96,9 @@ def lib():
     L.dp_rec_validate.argtypes = [c_i32p, ctypes.c_int64]
     L.dp_lower.argtypes = [ctypes.POINTER(Wire), ctypes.POINTER(vp)]
     L.dp_lowered_free.argtypes = [vp]
+    L.dp_lower_into.argtypes = [ctypes.POINTER(Wire), vp]
+    L.dp_lowered_exact_count.argtypes = [vp]
+    L.dp_lowered_exact_count.restype = ctypes.c_int64
     L.dp_lowered_num_problems.argtypes = [vp]
     for f in ("dp_lowered_rec_off", "dp_lowered_ident_off"):
         getattr(L, f).argtypes = [vp]
@@ -208,8 +211,33 @@ def wire_to_numpy(w: Wire) -> dict:
                 str_off=so, str_bytes=np.frombuffer(sb, np.uint8))
 
 
+class _LoweredHandle:
+    """Owns a dp_lowered; numpy views of its arrays keep it alive."""
+
+    def __init__(self, h):
+        self.h = h
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().dp_lowered_free(self.h)
+        except Exception:
+            pass
+
+
+def _view(owner, ptr, n: int, ctype, dtype) -> np.ndarray:
+    """Zero-copy numpy view of n elements at ptr, holding `owner` alive."""
+    if n == 0:
+        return np.zeros(0, dtype)
+    arr = (ctype * n).from_address(ctypes.cast(ptr, ctypes.c_void_p).value)
+    arr._owner = owner
+    return np.frombuffer(arr, dtype)
+
+
 class Lowered:
-    """Result of dp_lower, copied into numpy."""
+    """Result of dp_lower: numpy views of the library-owned arrays (no copy).
+    relower(wire) lowers another batch into the same storage
+    (dp_lower_into), invalidating the previous views' contents."""
 
     def __init__(self, wire: WireArrays):
         L = lib()
@@ -217,30 +245,35 @@ class Lowered:
         ws = wire.struct()
         if L.dp_lower(ctypes.byref(ws), ctypes.byref(h)) != 0:
             raise ValueError(L.dp_last_global_error().decode())
-        try:
-            P = L.dp_lowered_num_problems(h)
-            self.n = P
-            self.rec_off = np.ctypeslib.as_array(L.dp_lowered_rec_off(h), (P + 1,)).copy()
-            nw = int(self.rec_off[-1])
-            self.rec = np.ctypeslib.as_array(L.dp_lowered_rec(h), (max(nw, 1),))[:nw].copy()
-            self.ident_off = np.ctypeslib.as_array(L.dp_lowered_ident_off(h), (P + 1,)).copy()
-            ni = int(self.ident_off[-1])
-            if ni:
-                self.ident_var = np.ctypeslib.as_array(L.dp_lowered_ident_var(h), (ni,)).copy()
-                self.ident_con = np.ctypeslib.as_array(L.dp_lowered_ident_con(h), (ni,)).copy()
-            else:
-                self.ident_var = np.zeros(0, np.int32)
-                self.ident_con = np.zeros(0, np.int32)
-            self.err = np.zeros(max(P, 1), np.int32)
-            self.msg = [None] * P
-            m = ctypes.c_char_p()
-            if L.dp_lowered_errors(h, _p(self.err, c_i32p)):
-                for p in np.nonzero(self.err[:P])[0]:
-                    L.dp_lowered_error(h, int(p), ctypes.byref(m))
-                    self.msg[p] = m.value.decode("utf-8", "surrogateescape")
-            self.err = self.err[:P]
-        finally:
-            L.dp_lowered_free(h)
+        self._owner = _LoweredHandle(h)
+        self._fetch()
+
+    def relower(self, wire: WireArrays) -> "Lowered":
+        ws = wire.struct()
+        if lib().dp_lower_into(ctypes.byref(ws), self._owner.h) != 0:
+            raise ValueError(lib().dp_last_global_error().decode())
+        self._fetch()
+        return self
+
+    def _fetch(self):
+        L, h, o = lib(), self._owner.h, self._owner
+        P = L.dp_lowered_num_problems(h)
+        self.n = P
+        self.n_exact = int(L.dp_lowered_exact_count(h))
+        self.rec_off = _view(o, L.dp_lowered_rec_off(h), P + 1, ctypes.c_int64, np.int64)
+        self.rec = _view(o, L.dp_lowered_rec(h), int(self.rec_off[-1]), ctypes.c_int32, np.int32)
+        self.ident_off = _view(o, L.dp_lowered_ident_off(h), P + 1, ctypes.c_int64, np.int64)
+        ni = int(self.ident_off[-1])
+        self.ident_var = _view(o, L.dp_lowered_ident_var(h), ni, ctypes.c_int32, np.int32)
+        self.ident_con = _view(o, L.dp_lowered_ident_con(h), ni, ctypes.c_int32, np.int32)
+        self.err = np.zeros(max(P, 1), np.int32)
+        self.msg = [None] * P
+        m = ctypes.c_char_p()
+        if L.dp_lowered_errors(h, _p(self.err, c_i32p)):
+            for p in np.nonzero(self.err[:P])[0]:
+                L.dp_lowered_error(h, int(p), ctypes.byref(m))
+                self.msg[p] = m.value.decode("utf-8", "surrogateescape")
+        self.err = self.err[:P]
 
     def record(self, p: int) -> np.ndarray:
         return self.rec[self.rec_off[p]:self.rec_off[p + 1]]

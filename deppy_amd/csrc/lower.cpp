@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "pool.hpp"
 
 namespace dp {
 
@@ -227,7 +228,12 @@ struct Out {  // per-thread output chunk
 
 struct Work {  // per-thread scratch
   Aig aig;
-  std::vector<int64_t> stamp;  // interned path: string -> (tag << 32 | var)
+  // interned path: string id -> variable of the problem being lowered, valid
+  // while st_tag matches the problem's tag (no clearing between problems)
+  std::vector<uint64_t> st_tag;
+  std::vector<int32_t> st_idx;
+  uint64_t gen = 0;  // dp_lower call number of this scratch
+  uint64_t tag_of(int32_t p, bool fast) const { return gen << 33 | (uint64_t)(p + 1) << 1 | (fast ? 1u : 0u); }
   std::unordered_map<std::string_view, int32_t> names;
   FlatMap key_ident;  // gate literal -> identity
   std::vector<int32_t> owner_v, owner_c;
@@ -236,7 +242,50 @@ struct Work {  // per-thread scratch
   std::vector<int32_t> var_choice_off, choice_off, choice_lits, anchors;
   std::vector<int32_t> ms, sorted, order, mult;
   std::vector<std::string> errs;
+  // fast path (lower_fast): identity keys and each identity's first writer
+  FlatMap fkey;
+  std::vector<int32_t> first_c, first_s;
+  std::vector<int32_t> seq, seq2;
 };
+
+// Canonical identity keys of the fast path (Lowerer::lower_fast).  gini's
+// logic.C hash-conses And(a, b) on the unordered operand pair after folding
+// constants, a == b and a == !b, so two constraints share an assumed literal
+// exactly when their folded terms are equal.  The fast path names each term
+// by a key without building the graph:
+//   K_POS v        x_v             Mandatory(v)
+//   K_NEG v        !x_v            Prohibited(v), Dependency(v;), Conflict(v,v),
+//                                  AtMost(0; v)
+//   K_CONF {a,b}   !And(x_a, x_b)  Conflict(a,b), AtMost(1; a,b)   (a != b)
+//   K_NOR {a,b}    And(!x_a, !x_b) AtMost(0; a,b)                  (a != b)
+//   K_DEP (s,d..)  the Or chain    Dependency(s; d1..dn), d1 != s  (hashed;
+//                                  the term is And(..And(x_s,!x_d1)..,!x_dn):
+//                                  each level splits uniquely into a node and
+//                                  an input, so equal terms <=> equal sequences)
+//   K_CARD n, set  !sorted[n]      AtMost(n; m distinct vars), m >= 3 (hashed)
+//   K_F            F               AtMost(n < 0; ...)
+// Terms of different keys compute different Boolean functions, so they are
+// different terms: !sorted[n] of Batcher's network over m distinct inputs is
+// "at most n of the m", antimonotone and dependent on all m (0 <= n < m); a
+// Dependency chain with s not among d is increasing in every d it names (or
+// the constant T once s recurs); Mandatory is increasing, the others are
+// antimonotone in fewer variables.  What the keys cannot decide goes to the
+// exact path (lower_one, the full AIG): an AtMost with a repeated variable,
+// two AtMosts over one set and bound in different orders (same function,
+// structure unknown), a hashed key that matches a different sequence, and any
+// lookup error.
+enum : uint64_t { K_F = 0, K_POS = 1, K_NEG = 2, K_CONF = 3, K_NOR = 4, K_DEP = 5, K_CARD = 6 };
+inline uint64_t key1(uint64_t tag, uint32_t a) { return tag << 60 | a; }
+inline uint64_t key2(uint64_t tag, uint32_t a, uint32_t b) {
+  if (a > b) std::swap(a, b);
+  return tag << 60 | (uint64_t)a << 30 | b;
+}
+inline uint64_t hmix(uint64_t h, uint64_t x) {
+  h ^= x + 0x9e3779b97f4a7c15ULL;
+  h *= 0xbf58476d1ce4e5b9ULL;
+  return h ^ (h >> 31);
+}
+inline uint64_t keyh(uint64_t tag, uint64_t h) { return tag << 60 | (h & ((1ULL << 60) - 1)); }
 
 struct Lowerer {
   const dp_wire& w;
@@ -249,16 +298,15 @@ struct Lowerer {
   void lower_one(int32_t p, Work& W, Out& O) const {
     const int64_t v0 = w.prob_var_off[p], v1 = w.prob_var_off[p + 1];
     const int nv = (int)(v1 - v0);
-    const int64_t tag = (int64_t)p + 1;
+    const uint64_t tag = W.tag_of(p, false);
     // pass 1: one literal per variable, reject duplicates (lit_mapping.go:50-57)
     W.names.clear();
     for (int i = 0; i < nv; ++i) {
       int64_t sid = w.var_id[v0 + i];
       bool dup;
       if (w.interned) {
-        int64_t& st = W.stamp[(size_t)sid];
-        dup = (st >> 32) == tag;
-        if (!dup) st = (tag << 32) | i;
+        dup = W.st_tag[(size_t)sid] == tag;
+        if (!dup) { W.st_tag[(size_t)sid] = tag; W.st_idx[(size_t)sid] = i; }
       } else {
         dup = !W.names.emplace(str(sid), i).second;
       }
@@ -272,8 +320,7 @@ struct Lowerer {
     auto lit_of = [&](int64_t sid) -> int32_t {  // LitOf, lit_mapping.go:81-88
       int32_t v = -1;
       if (w.interned) {
-        int64_t st = W.stamp[(size_t)sid];
-        if ((st >> 32) == tag) v = (int32_t)(st & 0xffffffff);
+        if (W.st_tag[(size_t)sid] == tag) v = W.st_idx[(size_t)sid];
       } else {
         auto it = W.names.find(str(sid));
         if (it != W.names.end()) v = it->second;
@@ -372,6 +419,170 @@ struct Lowerer {
     emit_record(W, O, nv);
   }
 
+  // lower_one's exact result without the And-inverter graph, from the
+  // canonical keys above; false (nothing emitted) when the keys cannot
+  // decide and lower_one must run.
+  bool lower_fast(int32_t p, Work& W, Out& O) const {
+    if (!w.interned) return false;
+    const int64_t v0 = w.prob_var_off[p], v1 = w.prob_var_off[p + 1];
+    const int nv = (int)(v1 - v0);
+    if (nv >= (1 << 28)) return false;
+    // this path's stamps carry a tag of their own (lower_one may follow)
+    const uint64_t tag = W.tag_of(p, true);
+    for (int i = 0; i < nv; ++i) {
+      const size_t sid = (size_t)w.var_id[v0 + i];
+      if (W.st_tag[sid] == tag) return false;  // a duplicate: lower_one reports it
+      W.st_tag[sid] = tag;
+      W.st_idx[sid] = i;
+    }
+    auto var = [&](int64_t sid) -> int32_t {
+      return W.st_tag[(size_t)sid] == tag ? W.st_idx[(size_t)sid] : -1;
+    };
+    W.fkey.reset();
+    W.first_c.clear(); W.first_s.clear();
+    W.owner_v.clear(); W.owner_c.clear();
+    W.clause_off.assign(1, 0); W.clause_lits.clear(); W.clause_id.clear();
+    W.card_off.assign(1, 0); W.card_lits.clear(); W.card_bound.clear(); W.card_id.clear();
+    W.var_choice_off.assign(1, 0); W.choice_off.assign(1, 0); W.choice_lits.clear(); W.anchors.clear();
+    for (int vi = 0; vi < nv; ++vi) {
+      const int64_t c0 = w.var_con_off[v0 + vi], c1 = w.var_con_off[v0 + vi + 1];
+      bool anchor = false;
+      for (int64_t c = c0; c < c1; ++c) {
+        const int32_t kind = w.con_kind[c];
+        const int64_t a0 = w.con_arg_off[c], a1 = w.con_arg_off[c + 1];
+        uint64_t key = 0;
+        bool taut = false, hashed = false;
+        W.seq.clear();
+        switch (kind) {
+          case DP_MANDATORY:
+            key = key1(K_POS, (uint32_t)vi);
+            anchor = true;
+            break;
+          case DP_PROHIBITED:
+            key = key1(K_NEG, (uint32_t)vi);
+            break;
+          case DP_DEPENDENCY: {
+            if (a1 == a0) { key = key1(K_NEG, (uint32_t)vi); break; }
+            uint64_t h = hmix(0x6465707300000000ULL, (uint64_t)vi);
+            for (int64_t a = a0; a < a1; ++a) {
+              const int32_t d = var(w.con_arg[a]);
+              if (d < 0) return false;
+              W.seq.push_back(d);
+              W.choice_lits.push_back(d);  // Order(), search.go:59-69
+              h = hmix(h, (uint64_t)d);
+            }
+            W.choice_off.push_back((int32_t)W.choice_lits.size());
+            if (W.seq[0] == vi) { taut = true; break; }  // Or(!x_s, x_s) = T
+            key = keyh(K_DEP, h);
+            hashed = true;
+            break;
+          }
+          case DP_CONFLICT: {
+            const int32_t t = var(w.con_arg[a0]);
+            if (t < 0) return false;
+            key = t == vi ? key1(K_NEG, (uint32_t)vi) : key2(K_CONF, (uint32_t)vi, (uint32_t)t);
+            break;
+          }
+          case DP_ATMOST: {
+            const int64_t N = a1 - a0;
+            const int32_t n = w.con_n[c];
+            for (int64_t a = a0; a < a1; ++a) {
+              const int32_t d = var(w.con_arg[a]);
+              if (d < 0) return false;
+              W.seq.push_back(d);
+            }
+            if (n < 0) { key = key1(K_F, 0); break; }
+            if (n >= N) { taut = true; break; }
+            W.seq2.assign(W.seq.begin(), W.seq.end());
+            std::sort(W.seq2.begin(), W.seq2.end());
+            for (size_t j = 1; j < W.seq2.size(); ++j)
+              if (W.seq2[j] == W.seq2[j - 1]) return false;  // multiplicity: exact path
+            if (N == 1) key = key1(K_NEG, (uint32_t)W.seq[0]);
+            else if (N == 2) key = key2(n == 0 ? K_NOR : K_CONF, (uint32_t)W.seq[0], (uint32_t)W.seq[1]);
+            else {
+              uint64_t h = hmix(0x63617264ULL, (uint64_t)n);
+              for (int32_t d : W.seq2) h = hmix(h, (uint64_t)d);
+              key = keyh(K_CARD, h);
+              hashed = true;
+            }
+            break;
+          }
+          default:
+            return false;
+        }
+        if (taut) continue;
+        const int ci = (int)(c - c0);
+        int32_t* slot = W.fkey.find_slot(key);
+        if (slot) {
+          const int32_t id = *slot;
+          if (hashed && !same_term(W, id, c, vi, var)) return false;
+          W.owner_v[(size_t)id] = vi;  // last writer wins, lit_mapping.go:69-72
+          W.owner_c[(size_t)id] = ci;
+          continue;
+        }
+        const int32_t id = (int32_t)W.owner_v.size();
+        W.fkey.insert(key, id);
+        W.owner_v.push_back(vi);
+        W.owner_c.push_back(ci);
+        W.first_c.push_back((int32_t)c);
+        W.first_s.push_back(vi);
+        // the rows of a new identity, from its first writer (emit_rows)
+        const uint64_t tg = key >> 60;
+        auto close_clause = [&]() {
+          W.clause_off.push_back((int32_t)W.clause_lits.size());
+          W.clause_id.push_back(id);
+        };
+        if (tg == K_F) {
+          close_clause();
+        } else if (tg == K_POS || tg == K_NEG) {
+          W.clause_lits.push_back(2 * (int32_t)(key & 0x3fffffff) + (tg == K_NEG));
+          close_clause();
+        } else if (kind == DP_DEPENDENCY) {
+          const size_t start = W.clause_lits.size();
+          W.clause_lits.push_back(2 * vi + 1);
+          bool tautology = false;
+          for (int32_t d : W.seq) {
+            if (d == vi) { tautology = true; break; }
+            bool seen = false;
+            for (size_t j = start; j < W.clause_lits.size(); ++j) seen |= W.clause_lits[j] == 2 * d;
+            if (!seen) W.clause_lits.push_back(2 * d);
+          }
+          if (tautology) W.clause_lits.resize(start);  // no row
+          else close_clause();
+        } else if (kind == DP_CONFLICT) {
+          W.clause_lits.push_back(2 * vi + 1);
+          W.clause_lits.push_back(2 * var(w.con_arg[a0]) + 1);
+          close_clause();
+        } else {  // AtMost over distinct variables
+          W.card_lits.insert(W.card_lits.end(), W.seq.begin(), W.seq.end());
+          W.card_off.push_back((int32_t)W.card_lits.size());
+          W.card_bound.push_back(w.con_n[c]);
+          W.card_id.push_back(id);
+        }
+      }
+      W.var_choice_off.push_back((int32_t)W.choice_off.size() - 1);
+      if (anchor) W.anchors.push_back(vi);
+    }
+    emit_record(W, O, nv);
+    return true;
+  }
+
+  // Is the term of constraint c on subject s (a hashed key, W.seq resolved)
+  // the one of identity id's first writer?  Same kind, subject and argument
+  // sequence (and bound) build the same term.
+  template <class Var>
+  bool same_term(const Work& W, int32_t id, int64_t c, int s, const Var& var) const {
+    const int64_t f = W.first_c[(size_t)id];
+    if (w.con_kind[f] != w.con_kind[c]) return false;
+    if (w.con_kind[c] == DP_DEPENDENCY && W.first_s[(size_t)id] != s) return false;
+    if (w.con_kind[c] == DP_ATMOST && w.con_n[f] != w.con_n[c]) return false;
+    const int64_t a0 = w.con_arg_off[f], a1 = w.con_arg_off[f + 1];
+    if (a1 - a0 != (int64_t)W.seq.size()) return false;
+    for (int64_t a = a0; a < a1; ++a)
+      if (var(w.con_arg[a]) != W.seq[(size_t)(a - a0)]) return false;
+    return true;
+  }
+
   static int32_t leq(Aig& aig, Work& W, int32_t n) {
     const int N = (int)W.ms.size();
     if (n < 0) return kF;
@@ -405,7 +616,7 @@ struct Lowerer {
     }
     auto var_of = [&](int64_t a) -> int32_t {
       int64_t sid = w.con_arg[a];
-      if (w.interned) return (int32_t)(W.stamp[(size_t)sid] & 0xffffffff);
+      if (w.interned) return W.st_idx[(size_t)sid];
       return W.names.find(str(sid))->second;
     };
     if (kind == DP_DEPENDENCY) {
@@ -491,6 +702,17 @@ struct dp_lowered {
   std::vector<int64_t> rec_off, ident_off;
   std::vector<int32_t> rec, ivar, icon, err;
   std::vector<std::string> msg;
+  // scratch kept across dp_lower_into calls (once grown, no allocation or
+  // page fault per call): per pool thread, and chunk c's slices of outs[t]
+  std::vector<dp::Work> work;
+  std::vector<dp::Out> outs;
+  struct Piece {
+    int t;
+    size_t r0, r1, i0, i1, q0, q1;
+  };
+  std::vector<Piece> pieces;
+  std::vector<size_t> at_rec, at_id, at_p;
+  std::atomic<int64_t> n_exact{0};  // problems the last call lowered through the full AIG
 };
 
 extern "C" {
@@ -525,66 +747,115 @@ static bool wire_ok(const dp_wire* w) {
 }
 
 int dp_lower(const dp_wire* wire, dp_lowered** out) {
-  if (!out || !wire_ok(wire)) {
-    dp::set_global_error("dp_lower: malformed wire batch");
-    return -1;
-  }
-  const int32_t P = wire->n_problems;
-  unsigned hw = std::thread::hardware_concurrency();
-  int nt = (int)std::min<unsigned>(hw ? hw : 1, 16);
-  // threads by work (constraint arguments), chunks small enough to balance
-  const int64_t work = P ? wire->con_arg_off[wire->var_con_off[wire->prob_var_off[P]]] : 0;
-  if (work < 200000) nt = 1;
-  const int32_t chunk = (int32_t)std::max<int64_t>(1, std::min<int64_t>(64, P / (8 * (int64_t)nt)));
-  const int32_t nchunks = (P + chunk - 1) / chunk;
-  std::vector<dp::Out> outs((size_t)std::max(nchunks, 1));
-  dp::Lowerer L(*wire);
-  std::atomic_int next{0};
-  auto worker = [&]() {
-    dp::Work W;
-    if (wire->interned) W.stamp.assign((size_t)wire->n_strs, 0);
-    for (;;) {
-      int c = next.fetch_add(1);
-      if (c >= nchunks) break;
-      // fill a chunk in thread-local storage, then move it into place: the
-      // Out headers of neighbouring chunks share cache lines
-      dp::Out local;
-      for (int32_t p = c * chunk; p < std::min(P, (c + 1) * chunk); ++p) L.lower_one(p, W, local);
-      outs[(size_t)c] = std::move(local);
-    }
-  };
-  if (nt == 1) worker();
-  else {
-    std::vector<std::thread> th;
-    for (int t = 0; t < nt; ++t) th.emplace_back(worker);
-    for (auto& t : th) t.join();
-  }
+  if (!out) return -1;
   auto* lw = new dp_lowered;
-  lw->n = P;
-  lw->rec_off.assign(1, 0);
-  lw->ident_off.assign(1, 0);
-  size_t tot = 0, toti = 0;
-  for (auto& o : outs) { tot += o.rec.size(); toti += o.ivar.size(); }
-  lw->rec.reserve(tot);
-  lw->ivar.reserve(toti);
-  lw->icon.reserve(toti);
-  for (auto& o : outs) {
-    for (size_t i = 0; i < o.rec_len.size(); ++i) {
-      lw->rec_off.push_back(lw->rec_off.back() + o.rec_len[i]);
-      lw->ident_off.push_back(lw->ident_off.back() + o.ident_len[i]);
-    }
-    lw->rec.insert(lw->rec.end(), o.rec.begin(), o.rec.end());
-    lw->ivar.insert(lw->ivar.end(), o.ivar.begin(), o.ivar.end());
-    lw->icon.insert(lw->icon.end(), o.icon.begin(), o.icon.end());
-    lw->err.insert(lw->err.end(), o.err.begin(), o.err.end());
-    for (auto& m : o.msg) lw->msg.push_back(std::move(m));
+  if (dp_lower_into(wire, lw) != 0) {
+    delete lw;
+    return -1;
   }
   *out = lw;
   return 0;
 }
 
+int dp_lower_into(const dp_wire* wire, dp_lowered* lw) {
+  if (!lw || !wire_ok(wire)) {
+    dp::set_global_error("dp_lower: malformed wire batch");
+    return -1;
+  }
+  const int32_t P = wire->n_problems;
+  // DEPPY_LOWER_EXACT=1: every problem through the full AIG (tests, A/B)
+  const char* ex = std::getenv("DEPPY_LOWER_EXACT");
+  const bool exact = ex && *ex && *ex != '0';
+  dp::Pool& pool = dp::host_pool();
+  int nt = pool.size();
+  // threads by work (constraint arguments), chunks small enough to balance
+  const int64_t work = P ? wire->con_arg_off[wire->var_con_off[wire->prob_var_off[P]]] : 0;
+  if (work < 200000) nt = 1;
+  const int32_t chunk = (int32_t)std::max<int64_t>(1, std::min<int64_t>(64, P / (8 * (int64_t)nt)));
+  const int32_t nchunks = (P + chunk - 1) / chunk;
+  if ((int)lw->work.size() < pool.size()) {
+    lw->work.resize((size_t)pool.size());
+    lw->outs.resize((size_t)pool.size());
+  }
+  for (auto& W : lw->work) {
+    ++W.gen;
+    if (wire->interned && W.st_tag.size() < (size_t)wire->n_strs) {
+      W.st_tag.resize((size_t)wire->n_strs, 0);
+      W.st_idx.resize((size_t)wire->n_strs, 0);
+    }
+  }
+  for (auto& O : lw->outs) {
+    O.rec.clear(); O.rec_len.clear(); O.ivar.clear(); O.icon.clear();
+    O.ident_len.clear(); O.err.clear(); O.msg.clear();
+  }
+  lw->pieces.resize((size_t)nchunks);
+  lw->n_exact.store(0);
+  dp::Lowerer L(*wire);
+  auto lower_chunk = [&](int64_t c, int t) {
+    dp::Work& W = lw->work[(size_t)t];
+    dp::Out& O = lw->outs[(size_t)t];
+    auto& pc = lw->pieces[(size_t)c];
+    pc.t = t;
+    pc.r0 = O.rec.size(); pc.i0 = O.ivar.size(); pc.q0 = O.rec_len.size();
+    for (int32_t p = (int32_t)c * chunk; p < std::min<int32_t>(P, ((int32_t)c + 1) * chunk); ++p)
+      if (exact || !L.lower_fast(p, W, O)) {
+        L.lower_one(p, W, O);
+        lw->n_exact.fetch_add(1, std::memory_order_relaxed);
+      }
+    pc.r1 = O.rec.size(); pc.i1 = O.ivar.size(); pc.q1 = O.rec_len.size();
+  };
+  if (nt == 1)
+    for (int32_t c = 0; c < nchunks; ++c) lower_chunk(c, 0);
+  else
+    pool.run(nchunks, lower_chunk, 1);
+  // pieces -> one batch: offsets serially, the copies in parallel
+  lw->n = P;
+  auto& ar = lw->at_rec;
+  auto& ai = lw->at_id;
+  auto& ap = lw->at_p;
+  ar.assign((size_t)nchunks + 1, 0); ai.assign((size_t)nchunks + 1, 0); ap.assign((size_t)nchunks + 1, 0);
+  for (int32_t c = 0; c < nchunks; ++c) {
+    const auto& pc = lw->pieces[(size_t)c];
+    ar[(size_t)c + 1] = ar[(size_t)c] + (pc.r1 - pc.r0);
+    ai[(size_t)c + 1] = ai[(size_t)c] + (pc.i1 - pc.i0);
+    ap[(size_t)c + 1] = ap[(size_t)c] + (pc.q1 - pc.q0);
+  }
+  lw->rec.resize(ar.back());
+  lw->ivar.resize(ai.back());
+  lw->icon.resize(ai.back());
+  lw->rec_off.resize((size_t)P + 1);
+  lw->ident_off.resize((size_t)P + 1);
+  lw->err.resize((size_t)P);
+  lw->msg.resize((size_t)P);
+  lw->rec_off[0] = lw->ident_off[0] = 0;
+  auto merge = [&](int64_t c) {
+    const auto& pc = lw->pieces[(size_t)c];
+    dp::Out& o = lw->outs[(size_t)pc.t];
+    std::copy(o.rec.begin() + (int64_t)pc.r0, o.rec.begin() + (int64_t)pc.r1, lw->rec.begin() + (int64_t)ar[(size_t)c]);
+    std::copy(o.ivar.begin() + (int64_t)pc.i0, o.ivar.begin() + (int64_t)pc.i1, lw->ivar.begin() + (int64_t)ai[(size_t)c]);
+    std::copy(o.icon.begin() + (int64_t)pc.i0, o.icon.begin() + (int64_t)pc.i1, lw->icon.begin() + (int64_t)ai[(size_t)c]);
+    int64_t r = (int64_t)ar[(size_t)c], d = (int64_t)ai[(size_t)c];
+    for (size_t q = pc.q0; q < pc.q1; ++q) {
+      const size_t p = ap[(size_t)c] + (q - pc.q0);
+      r += o.rec_len[q];
+      d += o.ident_len[q];
+      lw->rec_off[p + 1] = r;
+      lw->ident_off[p + 1] = d;
+      lw->err[p] = o.err[q];
+      if (o.err[q]) lw->msg[p] = std::move(o.msg[q]);
+      else if (!lw->msg[p].empty()) lw->msg[p].clear();
+    }
+  };
+  if (nt == 1)
+    for (int32_t c = 0; c < nchunks; ++c) merge(c);
+  else
+    pool.run(nchunks, std::function<void(int64_t)>(merge), 1);
+  return 0;
+}
+
 void dp_lowered_free(dp_lowered* lw) { delete lw; }
 int32_t dp_lowered_num_problems(const dp_lowered* lw) { return lw->n; }
+int64_t dp_lowered_exact_count(const dp_lowered* lw) { return lw->n_exact.load(); }
 const int64_t* dp_lowered_rec_off(const dp_lowered* lw) { return lw->rec_off.data(); }
 const int32_t* dp_lowered_rec(const dp_lowered* lw) { return lw->rec.data(); }
 const int64_t* dp_lowered_ident_off(const dp_lowered* lw) { return lw->ident_off.data(); }

@@ -42,6 +42,7 @@
 #include "common.hpp"
 #include "kernel_api.hpp"
 #include "layout.hpp"
+#include "pool.hpp"
 
 namespace {
 
@@ -79,95 +80,6 @@ int64_t env_i64(const char* name, int64_t dflt) {
   const char* e = std::getenv(name);
   return e && *e ? std::atoll(e) : dflt;
 }
-
-// Host threads for staging: the CPU share of this process (cgroup cpu.max
-// quota when one is set, else the hardware threads), capped.
-int host_threads() {
-  int64_t n = env_i64("DEPPY_HOST_THREADS", 0);
-  if (n > 0) return (int)std::min<int64_t>(n, 256);
-  unsigned hw = std::thread::hardware_concurrency();
-  n = hw ? hw : 1;
-  std::ifstream f("/sys/fs/cgroup/cpu.max");
-  std::string quota, period;
-  if (f >> quota >> period && quota != "max") {
-    const double q = std::atof(quota.c_str()), p = std::atof(period.c_str());
-    if (q > 0 && p > 0) n = std::min<int64_t>(n, std::max<int64_t>(1, (int64_t)(q / p)));
-  }
-  return (int)std::min<int64_t>(n, 32);
-}
-
-// A persistent pool: run(n, fn) calls fn(i) for every i < n on the workers
-// and the calling thread (dynamic, in blocks), and returns when all are done.
-class Pool {
- public:
-  explicit Pool(int n) {
-    for (int t = 1; t < n; ++t) th_.emplace_back([this] { loop(); });
-  }
-  ~Pool() {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      stop_ = true;
-      ++gen_;
-    }
-    cv_.notify_all();
-    for (auto& t : th_) t.join();
-  }
-  int size() const { return (int)th_.size() + 1; }
-  void run(int64_t n, const std::function<void(int64_t)>& fn, int64_t block = 16) {
-    if (n <= 0) return;
-    if (th_.empty() || n <= block) {
-      for (int64_t i = 0; i < n; ++i) fn(i);
-      return;
-    }
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      fn_ = &fn;
-      n_ = n;
-      block_ = block;
-      next_.store(0);
-      busy_ = (int)th_.size();
-      ++gen_;
-    }
-    cv_.notify_all();
-    work();
-    std::unique_lock<std::mutex> lk(mu_);
-    done_cv_.wait(lk, [this] { return busy_ == 0; });
-    fn_ = nullptr;
-  }
-
- private:
-  void work() {
-    for (;;) {
-      const int64_t lo = next_.fetch_add(block_);
-      if (lo >= n_) break;
-      const int64_t hi = std::min(n_, lo + block_);
-      for (int64_t i = lo; i < hi; ++i) (*fn_)(i);
-    }
-  }
-  void loop() {
-    uint64_t seen = 0;
-    for (;;) {
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return gen_ != seen; });
-        seen = gen_;
-        if (stop_) return;
-      }
-      work();
-      std::lock_guard<std::mutex> lk(mu_);
-      if (--busy_ == 0) done_cv_.notify_one();
-    }
-  }
-  std::vector<std::thread> th_;
-  std::mutex mu_;
-  std::condition_variable cv_, done_cv_;
-  uint64_t gen_ = 0;
-  bool stop_ = false;
-  const std::function<void(int64_t)>* fn_ = nullptr;
-  int64_t n_ = 0, block_ = 1;
-  std::atomic<int64_t> next_{0};
-  int busy_ = 0;
-};
 
 int64_t group_above() {
   static const int64_t v = [] {
@@ -596,7 +508,7 @@ struct dp_ctx {
   std::string err;
   double last_ms = 0.0;
   std::mutex mu;
-  Pool* pool = nullptr;
+  dp::Pool* pool = nullptr;
   int next_lane = 0;  // pipeline cursor over (device, lane)
   bool zc_in = true, zc_out = true;  // zero-copy records / results (start_chunk)
   int32_t chunk_problems = kChunkProblems;
@@ -827,7 +739,7 @@ dp_ctx* dp_create(const dp_opts* opts) {
   ctx->chunk_bytes = std::max<int64_t>(1, env_i64("DEPPY_CHUNK_BYTES", kChunkBytes));
   ctx->zc_in = env_i64("DEPPY_ZC_IN", 1) != 0;   // diagnostic: 0 = H2D copy of every chunk
   ctx->zc_out = env_i64("DEPPY_ZC_OUT", 1) != 0; // diagnostic: 0 = D2H copy of every chunk
-  ctx->pool = new Pool(host_threads());
+  ctx->pool = new dp::Pool(dp::host_threads());
   return ctx;
 }
 
@@ -1155,10 +1067,7 @@ int dp_last_kernel_ms(const dp_ctx* ctx, double* ms) {
 
 // ---- host-only test hooks (include/deppy_hip.h) ----
 
-static Pool& hook_pool() {
-  static Pool pool(host_threads());
-  return pool;
-}
+static dp::Pool& hook_pool() { return dp::host_pool(); }
 
 int dp_stage_roundtrip(const dp_batch* b, int32_t opt_flags, int32_t chunk_problems, int64_t chunk_bytes,
                        int32_t* out_rec, int32_t* chunk_first, int32_t cap) {

@@ -164,8 +164,14 @@ typedef struct dp_lowered dp_lowered; /* host-owned, opaque */
  * problem (dp_lowered_error) and such problems get an empty record.
  * Returns 0, or -1 on malformed input (text in dp_last_global_error()). */
 int dp_lower(const dp_wire* wire, dp_lowered** out);
+/* dp_lower into an existing result, reusing its storage (a serving loop
+ * lowers batch after batch without allocating).  Returns 0 or -1. */
+int dp_lower_into(const dp_wire* wire, dp_lowered* lw);
 void dp_lowered_free(dp_lowered* lw);
 int32_t dp_lowered_num_problems(const dp_lowered* lw);
+/* Problems of the last lowering that went through the full And-inverter
+ * graph instead of the canonical identity keys (measurement; lower.cpp). */
+int64_t dp_lowered_exact_count(const dp_lowered* lw);
 const int64_t* dp_lowered_rec_off(const dp_lowered* lw); /* [P+1] */
 const int32_t* dp_lowered_rec(const dp_lowered* lw);
 /* Identity -> reported AppliedConstraint (last writer, lit_mapping.go:69-72):

@@ -152,3 +152,73 @@ def test_device_bytes_16bit_form():
     assert ib > rb
     rb32, ib32 = _lib.device_bytes(off, rec, flags=1)  # DP_OPT_FORCE_GROUP
     assert rb32 == 4 * int(words.sum()) and ib32 > ib
+
+
+def _random_problems(seed, n_problems, max_vars=7):
+    """Small random problems over a tiny identifier alphabet: identity
+    collisions (Conflict vs AtMost(1;a,b), AtMost(0;a,b) pairs, Prohibited vs
+    Dependency()/Conflict(v,v)/AtMost(0;v), repeated Dependencies, AtMosts over
+    one set in one or two orders, multiplicities) are frequent."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n_problems):
+        nv = int(rng.integers(1, max_vars + 1))
+        names = ["v%d" % i for i in range(nv)]
+        vs = []
+        for i in range(nv):
+            cons = []
+            for _ in range(int(rng.integers(0, 5))):
+                k = int(rng.integers(1, 6))
+                pick = lambda m: [names[j] for j in rng.integers(0, nv, m)]
+                if k == 1:
+                    cons.append(sat.Mandatory())
+                elif k == 2:
+                    cons.append(sat.Prohibited())
+                elif k == 3:
+                    cons.append(sat.Dependency(*pick(int(rng.integers(0, 4)))))
+                elif k == 4:
+                    cons.append(sat.Conflict(pick(1)[0]))
+                else:
+                    m = int(rng.integers(0, 5))
+                    ids = pick(m) if rng.random() < 0.3 else list(rng.permutation(names)[:m])
+                    cons.append(sat.AtMost(int(rng.integers(-1, m + 1)), *ids))
+            vs.append(V(names[i], *cons))
+        out.append(vs)
+    return out
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_fast_lowering_equals_exact_aig(seed, monkeypatch):
+    """The key-based identity path (lower_fast) is record-for-record equal to
+    the full And-inverter graph (lower_one) and to oracle/lower_ref.py."""
+    probs = _random_problems(seed, 400)
+    wire = sat.encode_inputs(probs)
+    fast = _lib.Lowered(wire)
+    monkeypatch.setenv("DEPPY_LOWER_EXACT", "1")
+    exact = _lib.Lowered(wire)
+    assert exact.n_exact == len(probs)
+    # most problems take the key path, collisions included
+    assert fast.n_exact < 0.5 * len(probs), fast.n_exact
+    np.testing.assert_array_equal(fast.rec_off, exact.rec_off)
+    np.testing.assert_array_equal(fast.rec, exact.rec)
+    np.testing.assert_array_equal(fast.ident_var, exact.ident_var)
+    np.testing.assert_array_equal(fast.ident_con, exact.ident_con)
+    assert fast.msg == exact.msg
+    for p, vs in enumerate(probs[:120]):
+        ref = lower_ref.lower_problem([
+            (v.Identifier().encode(), [(c.kind, c.n, [i.encode() for i in c.ids]) for c in v.Constraints()])
+            for v in vs])
+        compare(fast, p, ref)
+
+
+def test_relower_reuses_storage():
+    a, b = _random_problems(7, 50), _random_problems(8, 80)
+    lw = _lib.Lowered(sat.encode_inputs(a))
+    keep = lw.rec.copy()
+    fresh_b = _lib.Lowered(sat.encode_inputs(b))
+    lw.relower(sat.encode_inputs(b))
+    np.testing.assert_array_equal(lw.rec, fresh_b.rec)
+    np.testing.assert_array_equal(lw.rec_off, fresh_b.rec_off)
+    assert lw.msg == fresh_b.msg
+    lw.relower(sat.encode_inputs(a))
+    np.testing.assert_array_equal(lw.rec, keep)
