@@ -164,6 +164,16 @@ struct FlatMap {
     key[h] = k; val[h] = v; gen[h] = cur;
     ++count;
   }
+  // the slot of k, inserted with value v when absent
+  int32_t* find_or_insert(uint64_t k, int32_t v) {
+    if (2 * (count + 1) > key.size()) grow(2 * key.size());
+    size_t h = hash(k) & mask;
+    for (; gen[h] == cur; h = (h + 1) & mask)
+      if (key[h] == k) return &val[h];
+    key[h] = k; val[h] = v; gen[h] = cur;
+    ++count;
+    return &val[h];
+  }
   int32_t* find_slot(uint64_t k) {
     for (size_t h = hash(k) & mask; gen[h] == cur; h = (h + 1) & mask)
       if (key[h] == k) return &val[h];
@@ -217,8 +227,49 @@ const std::vector<std::pair<int, int>>& batcher(int n) {
   return *v;
 }
 
-struct Out {  // per-thread output chunk
+// The fast path's record under construction: raw arrays sized once per
+// problem from its counts (no per-element capacity checks).
+struct Fast {
+  std::vector<int32_t> store;
+  std::vector<int64_t> store64;
+  int32_t *clause_off, *clause_lits, *clause_id, *card_off, *card_lits, *card_bound, *card_id;
+  int32_t *var_choice_off, *choice_off, *choice_lits, *anchors, *owner_v, *owner_c, *first_s, *seq, *seq2;
+  int64_t* first_c;
+  int32_t nc, ncl, nk, nkl, nch, nchl, na, nid;
+  void reset(size_t nv, size_t C, size_t A) {
+    const size_t need = (C + 1) + (A + C) + C + (C + 1) + A + C + C + (nv + 1) + (C + 1) + A + nv + 4 * C + 2 * (A + 1);
+    if (store.size() < need) store.resize(need + need / 4);
+    if (store64.size() < C + 1) store64.resize(C + 1 + C / 4);
+    int32_t* q = store.data();
+    auto take = [&](size_t n) { int32_t* r = q; q += n; return r; };
+    clause_off = take(C + 1); clause_lits = take(A + C); clause_id = take(C);
+    card_off = take(C + 1); card_lits = take(A); card_bound = take(C); card_id = take(C);
+    var_choice_off = take(nv + 1); choice_off = take(C + 1); choice_lits = take(A); anchors = take(nv);
+    owner_v = take(C); owner_c = take(C); first_s = take(C); seq2 = take(A + 1); seq = take(A + 1);
+    (void)take(C);
+    first_c = store64.data();
+    nc = ncl = nk = nkl = nch = nchl = na = nid = 0;
+    clause_off[0] = card_off[0] = var_choice_off[0] = choice_off[0] = 0;
+  }
+  void close_clause(int32_t id) {
+    clause_id[nc] = id;
+    clause_off[++nc] = ncl;
+  }
+};
+
+// Per-thread output and scratch: 128-byte aligned, since their vector headers
+// change with every append and neighbouring threads' would share cache lines.
+struct alignas(128) Out {  // per-thread output chunk
+  // records: rec[0..nrec) (storage grows geometrically and is never
+  // re-initialised, so appending a record writes its words once)
   std::vector<int32_t> rec;
+  size_t nrec = 0;
+  int32_t* extend(size_t n) {
+    if (nrec + n > rec.size()) rec.resize(std::max(2 * rec.size(), nrec + n + 4096));
+    int32_t* r = rec.data() + nrec;
+    nrec += n;
+    return r;
+  }
   std::vector<int64_t> rec_len;  // per problem
   std::vector<int32_t> ivar, icon;
   std::vector<int64_t> ident_len;
@@ -226,7 +277,7 @@ struct Out {  // per-thread output chunk
   std::vector<std::string> msg;
 };
 
-struct Work {  // per-thread scratch
+struct alignas(128) Work {  // per-thread scratch
   Aig aig;
   // interned path: string id -> variable of the problem being lowered, valid
   // while st_tag matches the problem's tag (no clearing between problems)
@@ -242,10 +293,9 @@ struct Work {  // per-thread scratch
   std::vector<int32_t> var_choice_off, choice_off, choice_lits, anchors;
   std::vector<int32_t> ms, sorted, order, mult;
   std::vector<std::string> errs;
-  // fast path (lower_fast): identity keys and each identity's first writer
+  // fast path (lower_fast): identity keys and the record under construction
   FlatMap fkey;
-  std::vector<int32_t> first_c, first_s;
-  std::vector<int32_t> seq, seq2;
+  Fast fast;
 };
 
 // Canonical identity keys of the fast path (Lowerer::lower_fast).  gini's
@@ -420,66 +470,81 @@ struct Lowerer {
   }
 
   // lower_one's exact result without the And-inverter graph, from the
-  // canonical keys above; false (nothing emitted) when the keys cannot
-  // decide and lower_one must run.
-  bool lower_fast(int32_t p, Work& W, Out& O) const {
-    if (!w.interned) return false;
+  // canonical keys above.  Returns 1 (record emitted), 0 (the keys cannot
+  // decide: nothing emitted, lower_one must run) or -1 (malformed problem).
+  // The problem's own arrays are validated on the way (problem_ok's checks).
+  // Arrays are raw buffers sized from the problem's counts: a problem with C
+  // constraints and A arguments has at most C rows, A + C clause literals, A
+  // AtMost positions and A choice literals.
+  int lower_fast(int32_t p, Work& W, Out& O) const {
+    if (!w.interned) return 0;
     const int64_t v0 = w.prob_var_off[p], v1 = w.prob_var_off[p + 1];
     const int nv = (int)(v1 - v0);
-    if (nv >= (1 << 28)) return false;
+    if (nv >= (1 << 28)) return 0;
+    const uint64_t nstr = (uint64_t)w.n_strs;
     // this path's stamps carry a tag of their own (lower_one may follow)
     const uint64_t tag = W.tag_of(p, true);
     for (int i = 0; i < nv; ++i) {
-      const size_t sid = (size_t)w.var_id[v0 + i];
-      if (W.st_tag[sid] == tag) return false;  // a duplicate: lower_one reports it
+      const uint64_t sid = (uint64_t)w.var_id[v0 + i];
+      if (sid >= nstr || w.var_con_off[v0 + i + 1] < w.var_con_off[v0 + i]) return -1;
+      if (W.st_tag[sid] == tag) return 0;  // a duplicate: lower_one reports it
       W.st_tag[sid] = tag;
       W.st_idx[sid] = i;
     }
+    const int64_t cb = nv ? w.var_con_off[v0] : 0, ce = nv ? w.var_con_off[v1] : 0;
+    const int64_t C = ce - cb, A = nv ? w.con_arg_off[ce] - w.con_arg_off[cb] : 0;
+    if (A < 0) return -1;
+    // var of string id sid, -1 if not a variable of this problem, -2 if out of range
     auto var = [&](int64_t sid) -> int32_t {
+      if ((uint64_t)sid >= nstr) return -2;
       return W.st_tag[(size_t)sid] == tag ? W.st_idx[(size_t)sid] : -1;
     };
+    Fast& F = W.fast;
+    F.reset((size_t)nv, (size_t)C, (size_t)A);
     W.fkey.reset();
-    W.first_c.clear(); W.first_s.clear();
-    W.owner_v.clear(); W.owner_c.clear();
-    W.clause_off.assign(1, 0); W.clause_lits.clear(); W.clause_id.clear();
-    W.card_off.assign(1, 0); W.card_lits.clear(); W.card_bound.clear(); W.card_id.clear();
-    W.var_choice_off.assign(1, 0); W.choice_off.assign(1, 0); W.choice_lits.clear(); W.anchors.clear();
     for (int vi = 0; vi < nv; ++vi) {
       const int64_t c0 = w.var_con_off[v0 + vi], c1 = w.var_con_off[v0 + vi + 1];
       bool anchor = false;
       for (int64_t c = c0; c < c1; ++c) {
         const int32_t kind = w.con_kind[c];
         const int64_t a0 = w.con_arg_off[c], a1 = w.con_arg_off[c + 1];
+        if (a1 < a0) return -1;
         uint64_t key = 0;
         bool taut = false, hashed = false;
-        W.seq.clear();
+        int32_t* seq = F.seq;
+        int32_t ns = 0;
         switch (kind) {
           case DP_MANDATORY:
+            if (a1 != a0) return -1;
             key = key1(K_POS, (uint32_t)vi);
             anchor = true;
             break;
           case DP_PROHIBITED:
+            if (a1 != a0) return -1;
             key = key1(K_NEG, (uint32_t)vi);
             break;
           case DP_DEPENDENCY: {
             if (a1 == a0) { key = key1(K_NEG, (uint32_t)vi); break; }
             uint64_t h = hmix(0x6465707300000000ULL, (uint64_t)vi);
+            seq = F.choice_lits + F.nchl;  // the arguments are the Order() list, search.go:59-69
             for (int64_t a = a0; a < a1; ++a) {
               const int32_t d = var(w.con_arg[a]);
-              if (d < 0) return false;
-              W.seq.push_back(d);
-              W.choice_lits.push_back(d);  // Order(), search.go:59-69
+              if (d < 0) return d == -2 ? -1 : 0;
+              seq[ns++] = d;
               h = hmix(h, (uint64_t)d);
             }
-            W.choice_off.push_back((int32_t)W.choice_lits.size());
-            if (W.seq[0] == vi) { taut = true; break; }  // Or(!x_s, x_s) = T
+            F.nchl += ns;
+            F.choice_off[++F.nch] = F.nchl;
+            if (seq[0] == vi) { taut = true; break; }  // Or(!x_s, x_s) = T
             key = keyh(K_DEP, h);
             hashed = true;
             break;
           }
           case DP_CONFLICT: {
+            if (a1 - a0 != 1) return -1;
             const int32_t t = var(w.con_arg[a0]);
-            if (t < 0) return false;
+            if (t < 0) return t == -2 ? -1 : 0;
+            seq[ns++] = t;
             key = t == vi ? key1(K_NEG, (uint32_t)vi) : key2(K_CONF, (uint32_t)vi, (uint32_t)t);
             break;
           }
@@ -488,98 +553,134 @@ struct Lowerer {
             const int32_t n = w.con_n[c];
             for (int64_t a = a0; a < a1; ++a) {
               const int32_t d = var(w.con_arg[a]);
-              if (d < 0) return false;
-              W.seq.push_back(d);
+              if (d < 0) return d == -2 ? -1 : 0;
+              seq[ns++] = d;
             }
             if (n < 0) { key = key1(K_F, 0); break; }
             if (n >= N) { taut = true; break; }
-            W.seq2.assign(W.seq.begin(), W.seq.end());
-            std::sort(W.seq2.begin(), W.seq2.end());
-            for (size_t j = 1; j < W.seq2.size(); ++j)
-              if (W.seq2[j] == W.seq2[j - 1]) return false;  // multiplicity: exact path
-            if (N == 1) key = key1(K_NEG, (uint32_t)W.seq[0]);
-            else if (N == 2) key = key2(n == 0 ? K_NOR : K_CONF, (uint32_t)W.seq[0], (uint32_t)W.seq[1]);
+            int32_t* srt = F.seq2;
+            std::copy(seq, seq + ns, srt);
+            std::sort(srt, srt + ns);
+            for (int32_t j = 1; j < ns; ++j)
+              if (srt[j] == srt[j - 1]) return 0;  // multiplicity: exact path
+            if (N == 1) key = key1(K_NEG, (uint32_t)seq[0]);
+            else if (N == 2) key = key2(n == 0 ? K_NOR : K_CONF, (uint32_t)seq[0], (uint32_t)seq[1]);
             else {
               uint64_t h = hmix(0x63617264ULL, (uint64_t)n);
-              for (int32_t d : W.seq2) h = hmix(h, (uint64_t)d);
+              for (int32_t j = 0; j < ns; ++j) h = hmix(h, (uint64_t)srt[j]);
               key = keyh(K_CARD, h);
               hashed = true;
             }
             break;
           }
           default:
-            return false;
+            return -1;
         }
         if (taut) continue;
         const int ci = (int)(c - c0);
-        int32_t* slot = W.fkey.find_slot(key);
-        if (slot) {
+        int32_t* slot = W.fkey.find_or_insert(key, F.nid);
+        if (*slot != F.nid) {  // a known term
           const int32_t id = *slot;
-          if (hashed && !same_term(W, id, c, vi, var)) return false;
-          W.owner_v[(size_t)id] = vi;  // last writer wins, lit_mapping.go:69-72
-          W.owner_c[(size_t)id] = ci;
+          if (hashed && !same_term(F, id, c, vi, seq, ns, var)) return 0;
+          F.owner_v[id] = vi;  // last writer wins, lit_mapping.go:69-72
+          F.owner_c[id] = ci;
           continue;
         }
-        const int32_t id = (int32_t)W.owner_v.size();
-        W.fkey.insert(key, id);
-        W.owner_v.push_back(vi);
-        W.owner_c.push_back(ci);
-        W.first_c.push_back((int32_t)c);
-        W.first_s.push_back(vi);
+        const int32_t id = F.nid++;
+        F.owner_v[id] = vi;
+        F.owner_c[id] = ci;
+        F.first_c[id] = c;
+        F.first_s[id] = vi;
         // the rows of a new identity, from its first writer (emit_rows)
         const uint64_t tg = key >> 60;
-        auto close_clause = [&]() {
-          W.clause_off.push_back((int32_t)W.clause_lits.size());
-          W.clause_id.push_back(id);
-        };
         if (tg == K_F) {
-          close_clause();
+          F.close_clause(id);
         } else if (tg == K_POS || tg == K_NEG) {
-          W.clause_lits.push_back(2 * (int32_t)(key & 0x3fffffff) + (tg == K_NEG));
-          close_clause();
+          F.clause_lits[F.ncl++] = 2 * (int32_t)(key & 0x3fffffff) + (tg == K_NEG);
+          F.close_clause(id);
         } else if (kind == DP_DEPENDENCY) {
-          const size_t start = W.clause_lits.size();
-          W.clause_lits.push_back(2 * vi + 1);
+          const int32_t start = F.ncl;
+          F.clause_lits[F.ncl++] = 2 * vi + 1;
           bool tautology = false;
-          for (int32_t d : W.seq) {
+          for (int32_t j = 0; j < ns; ++j) {
+            const int32_t d = seq[j];
             if (d == vi) { tautology = true; break; }
             bool seen = false;
-            for (size_t j = start; j < W.clause_lits.size(); ++j) seen |= W.clause_lits[j] == 2 * d;
-            if (!seen) W.clause_lits.push_back(2 * d);
+            for (int32_t k = start; k < F.ncl; ++k) seen |= F.clause_lits[k] == 2 * d;
+            if (!seen) F.clause_lits[F.ncl++] = 2 * d;
           }
-          if (tautology) W.clause_lits.resize(start);  // no row
-          else close_clause();
+          if (tautology) F.ncl = start;  // no row
+          else F.close_clause(id);
         } else if (kind == DP_CONFLICT) {
-          W.clause_lits.push_back(2 * vi + 1);
-          W.clause_lits.push_back(2 * var(w.con_arg[a0]) + 1);
-          close_clause();
+          F.clause_lits[F.ncl++] = 2 * vi + 1;
+          F.clause_lits[F.ncl++] = 2 * seq[0] + 1;
+          F.close_clause(id);
         } else {  // AtMost over distinct variables
-          W.card_lits.insert(W.card_lits.end(), W.seq.begin(), W.seq.end());
-          W.card_off.push_back((int32_t)W.card_lits.size());
-          W.card_bound.push_back(w.con_n[c]);
-          W.card_id.push_back(id);
+          std::copy(seq, seq + ns, F.card_lits + F.nkl);
+          F.nkl += ns;
+          F.card_off[++F.nk] = F.nkl;
+          F.card_bound[F.nk - 1] = w.con_n[c];
+          F.card_id[F.nk - 1] = id;
         }
       }
-      W.var_choice_off.push_back((int32_t)W.choice_off.size() - 1);
-      if (anchor) W.anchors.push_back(vi);
+      F.var_choice_off[vi + 1] = F.nch;
+      if (anchor) F.anchors[F.na++] = vi;
     }
-    emit_record(W, O, nv);
-    return true;
+    emit_fast(F, O, nv);
+    return 1;
   }
 
-  // Is the term of constraint c on subject s (a hashed key, W.seq resolved)
-  // the one of identity id's first writer?  Same kind, subject and argument
-  // sequence (and bound) build the same term.
+  // The record of the fast path (the layout emit_record writes).
+  static void emit_fast(const Fast& F, Out& O, int nv) {
+    int32_t hdr[DP_H_SIZE] = {0};
+    hdr[DP_H_MAGIC] = DP_REC_MAGIC;
+    hdr[DP_H_NV] = nv;
+    hdr[DP_H_NC] = F.nc;
+    hdr[DP_H_NK] = F.nk;
+    hdr[DP_H_NCH] = F.nch;
+    hdr[DP_H_NA] = F.na;
+    hdr[DP_H_NID] = F.nid;
+    hdr[DP_H_NCL] = F.ncl;
+    hdr[DP_H_NKL] = F.nkl;
+    hdr[DP_H_NCHL] = F.nchl;
+    const dp_rec_layout L = dp_rec_layout_of(hdr);
+    hdr[DP_H_WORDS] = L.words;
+    int32_t* r = O.extend((size_t)L.words);
+    auto put = [&](int32_t at, const int32_t* src, int32_t n) { std::memcpy(r + at, src, (size_t)n * 4); };
+    std::memcpy(r, hdr, sizeof hdr);
+    put(L.clause_off, F.clause_off, F.nc + 1);
+    put(L.clause_lits, F.clause_lits, F.ncl);
+    put(L.clause_id, F.clause_id, F.nc);
+    put(L.card_off, F.card_off, F.nk + 1);
+    put(L.card_lits, F.card_lits, F.nkl);
+    put(L.card_bound, F.card_bound, F.nk);
+    put(L.card_id, F.card_id, F.nk);
+    put(L.var_choice_off, F.var_choice_off, nv + 1);
+    put(L.choice_off, F.choice_off, F.nch + 1);
+    put(L.choice_lits, F.choice_lits, F.nchl);
+    put(L.anchors, F.anchors, F.na);
+    O.rec_len.push_back(L.words);
+    O.ivar.insert(O.ivar.end(), F.owner_v, F.owner_v + F.nid);
+    O.icon.insert(O.icon.end(), F.owner_c, F.owner_c + F.nid);
+    O.ident_len.push_back(F.nid);
+    O.err.push_back(DP_LOWER_OK);
+    O.msg.emplace_back();
+  }
+
+  // Is the term of constraint c on subject s (a hashed key, its arguments
+  // resolved in seq[0..ns)) the one of identity id's first writer?  Same
+  // kind, subject and argument sequence (and bound) build the same term.
   template <class Var>
-  bool same_term(const Work& W, int32_t id, int64_t c, int s, const Var& var) const {
-    const int64_t f = W.first_c[(size_t)id];
+  bool same_term(const Fast& F, int32_t id, int64_t c, int s, const int32_t* seq, int32_t ns,
+                 const Var& var) const {
+    const int64_t f = F.first_c[id];
     if (w.con_kind[f] != w.con_kind[c]) return false;
-    if (w.con_kind[c] == DP_DEPENDENCY && W.first_s[(size_t)id] != s) return false;
+    if (w.con_kind[c] == DP_DEPENDENCY && F.first_s[id] != s) return false;
     if (w.con_kind[c] == DP_ATMOST && w.con_n[f] != w.con_n[c]) return false;
     const int64_t a0 = w.con_arg_off[f], a1 = w.con_arg_off[f + 1];
-    if (a1 - a0 != (int64_t)W.seq.size()) return false;
+    if (a1 - a0 != (int64_t)ns) return false;
     for (int64_t a = a0; a < a1; ++a)
-      if (var(w.con_arg[a]) != W.seq[(size_t)(a - a0)]) return false;
+      if (var(w.con_arg[a]) != seq[a - a0]) return false;
     return true;
   }
 
@@ -656,7 +757,7 @@ struct Lowerer {
     int32_t hdr[DP_H_SIZE + 4] = {0};
     hdr[DP_H_MAGIC] = DP_REC_MAGIC;
     hdr[DP_H_WORDS] = dp_rec_layout_of(hdr).words;
-    O.rec.insert(O.rec.end(), hdr, hdr + hdr[DP_H_WORDS]);
+    std::memcpy(O.extend((size_t)hdr[DP_H_WORDS]), hdr, 4 * (size_t)hdr[DP_H_WORDS]);
     O.rec_len.push_back(hdr[DP_H_WORDS]);
     O.ident_len.push_back(0);
     O.err.push_back(code);
@@ -679,13 +780,15 @@ struct Lowerer {
     hdr[DP_H_NCHL] = (int32_t)W.choice_lits.size();
     dp_rec_layout L = dp_rec_layout_of(hdr);
     hdr[DP_H_WORDS] = L.words;
-    size_t base = O.rec.size();
-    O.rec.insert(O.rec.end(), hdr, hdr + DP_H_SIZE);
-    auto app = [&](const std::vector<int32_t>& v) { O.rec.insert(O.rec.end(), v.begin(), v.end()); };
+    size_t base = O.nrec;
+    std::memcpy(O.extend(DP_H_SIZE), hdr, 4 * DP_H_SIZE);
+    auto app = [&](const std::vector<int32_t>& v) {
+      if (!v.empty()) std::memcpy(O.extend(v.size()), v.data(), 4 * v.size());
+    };
     app(W.clause_off); app(W.clause_lits); app(W.clause_id);
     app(W.card_off); app(W.card_lits); app(W.card_bound); app(W.card_id);
     app(W.var_choice_off); app(W.choice_off); app(W.choice_lits); app(W.anchors);
-    O.rec_len.push_back((int64_t)(O.rec.size() - base));
+    O.rec_len.push_back((int64_t)(O.nrec - base));
     O.ivar.insert(O.ivar.end(), W.owner_v.begin(), W.owner_v.end());
     O.icon.insert(O.icon.end(), W.owner_c.begin(), W.owner_c.end());
     O.ident_len.push_back((int64_t)W.owner_v.size());
@@ -719,6 +822,8 @@ extern "C" {
 
 const char* dp_last_global_error(void) { return dp::g_err.c_str(); }
 
+// The batch-level shape of a wire batch (serial, O(problems)); each problem's
+// own arrays are checked by problem_ok on the lowering threads.
 static bool wire_ok(const dp_wire* w) {
   if (!w || w->n_problems < 0 || !w->prob_var_off) return false;
   if (w->n_problems == 0) return true;
@@ -726,14 +831,21 @@ static bool wire_ok(const dp_wire* w) {
   if (w->prob_var_off[0] != 0) return false;
   for (int32_t p = 0; p < w->n_problems; ++p)
     if (w->prob_var_off[p + 1] < w->prob_var_off[p]) return false;
-  if (nvars > 0 && (!w->var_id || !w->var_con_off)) return false;
-  if (nvars == 0) return true;
-  const int64_t ncons = w->var_con_off[nvars];
-  for (int64_t v = 0; v < nvars; ++v) {
+  if (nvars > 0 && (!w->var_id || !w->var_con_off || w->var_con_off[0] != 0)) return false;
+  if (nvars > 0 && w->var_con_off[nvars] > 0 && (!w->con_kind || !w->con_arg_off || w->con_arg_off[0] != 0))
+    return false;
+  return true;
+}
+
+// Problem p's variables, constraints and arguments are well formed.
+static bool problem_ok(const dp_wire* w, int32_t p) {
+  const int64_t v0 = w->prob_var_off[p], v1 = w->prob_var_off[p + 1];
+  for (int64_t v = v0; v < v1; ++v) {
     if (w->var_con_off[v + 1] < w->var_con_off[v]) return false;
     if (w->var_id[v] < 0 || w->var_id[v] >= w->n_strs) return false;
   }
-  for (int64_t c = 0; c < ncons; ++c) {
+  if (v1 == v0) return true;
+  for (int64_t c = w->var_con_off[v0]; c < w->var_con_off[v1]; ++c) {
     int32_t k = w->con_kind[c];
     if (k < DP_MANDATORY || k > DP_ATMOST) return false;
     int64_t na = w->con_arg_off[c + 1] - w->con_arg_off[c];
@@ -785,29 +897,44 @@ int dp_lower_into(const dp_wire* wire, dp_lowered* lw) {
     }
   }
   for (auto& O : lw->outs) {
-    O.rec.clear(); O.rec_len.clear(); O.ivar.clear(); O.icon.clear();
+    O.nrec = 0; O.rec_len.clear(); O.ivar.clear(); O.icon.clear();
     O.ident_len.clear(); O.err.clear(); O.msg.clear();
   }
   lw->pieces.resize((size_t)nchunks);
   lw->n_exact.store(0);
   dp::Lowerer L(*wire);
+  std::atomic<bool> bad{false};
   auto lower_chunk = [&](int64_t c, int t) {
     dp::Work& W = lw->work[(size_t)t];
     dp::Out& O = lw->outs[(size_t)t];
     auto& pc = lw->pieces[(size_t)c];
     pc.t = t;
-    pc.r0 = O.rec.size(); pc.i0 = O.ivar.size(); pc.q0 = O.rec_len.size();
+    pc.r0 = O.nrec; pc.i0 = O.ivar.size(); pc.q0 = O.rec_len.size();
     for (int32_t p = (int32_t)c * chunk; p < std::min<int32_t>(P, ((int32_t)c + 1) * chunk); ++p)
-      if (exact || !L.lower_fast(p, W, O)) {
+    {
+      const int r = exact ? 0 : L.lower_fast(p, W, O);
+      if (r < 0 || (r == 0 && !problem_ok(wire, p))) {
+        bad.store(true, std::memory_order_relaxed);
+        return;
+      }
+      if (r == 0) {
         L.lower_one(p, W, O);
         lw->n_exact.fetch_add(1, std::memory_order_relaxed);
       }
-    pc.r1 = O.rec.size(); pc.i1 = O.ivar.size(); pc.q1 = O.rec_len.size();
+    }
+    pc.r1 = O.nrec; pc.i1 = O.ivar.size(); pc.q1 = O.rec_len.size();
   };
   if (nt == 1)
     for (int32_t c = 0; c < nchunks; ++c) lower_chunk(c, 0);
   else
     pool.run(nchunks, lower_chunk, 1);
+  if (bad.load()) {
+    lw->n = 0;
+    lw->rec_off.assign(1, 0);
+    lw->ident_off.assign(1, 0);
+    dp::set_global_error("dp_lower: malformed wire batch");
+    return -1;
+  }
   // pieces -> one batch: offsets serially, the copies in parallel
   lw->n = P;
   auto& ar = lw->at_rec;
