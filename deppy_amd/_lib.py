@@ -37,7 +37,7 @@ EXPORTS = [
     "dp_last_error", "dp_last_global_error", "dp_num_devices", "dp_solve", "dp_upload", "dp_run",
     "dp_launch", "dp_wait", "dp_download", "dp_resident_free", "dp_last_kernel_ms", "dp_gen_catalogs", "dp_gen_wire",
     "dp_gen_free", "dp_upload_traced", "dp_download_trace", "dp_solve_traced", "dp_lowered_errors",
-    "dp_device_bytes", "dp_lower_into", "dp_lowered_exact_count", "dp_submit", "dp_job_wait", "dp_get_stats", "dp_stage_roundtrip",
+    "dp_device_bytes", "dp_lower_into", "dp_lowered_new", "dp_lowered_exact_count", "dp_submit", "dp_job_wait", "dp_get_stats", "dp_stage_roundtrip",
     "dp_stitch_selftest", "dp_partition",
 ]
 
@@ -67,7 +67,7 @@ class Opts(ctypes.Structure):
 class Stats(ctypes.Structure):
     _fields_ = [("problems", ctypes.c_int64), ("chunks", ctypes.c_int64), ("launches", ctypes.c_int64),
                 ("kernel_ms", ctypes.c_double), ("h2d_bytes", ctypes.c_int64), ("d2h_bytes", ctypes.c_int64),
-                ("rec_bytes", ctypes.c_int64), ("stage_ms", ctypes.c_double), ("wait_ms", ctypes.c_double),
+                ("rec_bytes", ctypes.c_int64), ("stage_ms", ctypes.c_double), ("plan_ms", ctypes.c_double), ("wait_ms", ctypes.c_double),
                 ("scatter_ms", ctypes.c_double)]
 
 
@@ -96,7 +96,8 @@ def lib():
     L.dp_rec_validate.argtypes = [c_i32p, ctypes.c_int64]
     L.dp_lower.argtypes = [ctypes.POINTER(Wire), ctypes.POINTER(vp)]
     L.dp_lowered_free.argtypes = [vp]
-    L.dp_lower_into.argtypes = [ctypes.POINTER(Wire), vp]
+    L.dp_lower_into.argtypes = [ctypes.POINTER(Wire), ctypes.c_int32, vp]
+    L.dp_lowered_new.restype = vp
     L.dp_lowered_exact_count.argtypes = [vp]
     L.dp_lowered_exact_count.restype = ctypes.c_int64
     L.dp_lowered_num_problems.argtypes = [vp]
@@ -239,18 +240,26 @@ class Lowered:
     relower(wire) lowers another batch into the same storage
     (dp_lower_into), invalidating the previous views' contents."""
 
-    def __init__(self, wire: WireArrays):
+    def __init__(self, wire: WireArrays, narrow: bool = False):
+        """narrow: records that fit 16 bits in the DP_FMT_U16 form (the staged
+        form, DP_LOWER_NARROW); default int32 records."""
         L = lib()
         h = ctypes.c_void_p()
         ws = wire.struct()
-        if L.dp_lower(ctypes.byref(ws), ctypes.byref(h)) != 0:
+        self.narrow = narrow
+        if narrow:
+            h = ctypes.c_void_p(L.dp_lowered_new())
+            if L.dp_lower_into(ctypes.byref(ws), 1, h) != 0:
+                L.dp_lowered_free(h)
+                raise ValueError(L.dp_last_global_error().decode())
+        elif L.dp_lower(ctypes.byref(ws), ctypes.byref(h)) != 0:
             raise ValueError(L.dp_last_global_error().decode())
         self._owner = _LoweredHandle(h)
         self._fetch()
 
     def relower(self, wire: WireArrays) -> "Lowered":
         ws = wire.struct()
-        if lib().dp_lower_into(ctypes.byref(ws), self._owner.h) != 0:
+        if lib().dp_lower_into(ctypes.byref(ws), 1 if self.narrow else 0, self._owner.h) != 0:
             raise ValueError(lib().dp_last_global_error().decode())
         self._fetch()
         return self

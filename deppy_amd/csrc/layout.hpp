@@ -106,8 +106,10 @@ __host__ __device__ inline dp_rec_layout rec_layout(const int32_t* h) {
 // multi-wave modes).  Rows that can fire on the empty assignment (clauses of
 // length <= 1, AtMost rows in which some variable's multiplicity exceeds the
 // bound) are found by a sweep of the row offsets (Group::base_propagate).
-enum { DP_H_FMT = 13 };
-enum { DP_FMT_I32 = 0, DP_FMT_U16 = 1 };
+
+// Staged-copy format of a record the host rejected while narrowing it (the
+// kernel reports it as malformed without reading its body).
+enum { DP_FMT_REJECT = 2 };
 
 struct ImgLayout {
   int32_t w_off, w, words;
@@ -223,15 +225,8 @@ __host__ __device__ inline Layout layout(const int32_t* h) {
   return L;
 }
 
-// Can the record run on the 16-bit LDS image?  Every index it holds, and every
-// value the solve stores per variable / row, must stay below the encodings of
-// the no-row reasons (0xffff R_DEC, 0xfffe R_EXTRA, 0xfffd - d decision d).
-__host__ __device__ inline bool fits16(const int32_t* h) {
-  const int32_t nv = h[DP_H_NV];
-  // reasons encode Solve() decision d as 0xfffd - d above every row id
-  return h[DP_H_WORDS] < 65000 && nv < 16000 && h[DP_H_NID] < 65000 &&
-         h[DP_H_NC] + h[DP_H_NK] + L_MAX + nv < 65000 && h[DP_H_NA] + h[DP_H_NCH] < 65000 &&
-         h[DP_H_NCL] + h[DP_H_NKL] < 65000;
-}
+// Can the record run on the 16-bit LDS image?  (dp_rec_fits16: the reasons
+// encode Solve() decision d as 0xfffd - d above every row id.)
+inline bool fits16(const int32_t* h) { return dp_rec_fits16(h) != 0; }
 
 }  // namespace dp

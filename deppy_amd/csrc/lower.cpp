@@ -339,7 +339,23 @@ inline uint64_t keyh(uint64_t tag, uint64_t h) { return tag << 60 | (h & ((1ULL 
 
 struct Lowerer {
   const dp_wire& w;
-  explicit Lowerer(const dp_wire& wire) : w(wire) {}
+  const bool narrow;  // DP_LOWER_NARROW: records that fit 16 bits in the DP_FMT_U16 form
+  Lowerer(const dp_wire& wire, bool narrow16) : w(wire), narrow(narrow16) {}
+
+  // The last record appended to O (int32 words from `base`) in the 16-bit
+  // form, in place (word j -> halfword j never overtakes word j).
+  void narrow_last(Out& O, size_t base) const {
+    int32_t* r = O.rec.data() + base;
+    if (!narrow || !dp_rec_fits16(r)) return;
+    const int64_t words = r[DP_H_WORDS];
+    uint16_t* u = reinterpret_cast<uint16_t*>(r + DP_H_SIZE);
+    for (int64_t j = 0; j < words - DP_H_SIZE; ++j) u[j] = (uint16_t)r[DP_H_SIZE + j];
+    if ((words - DP_H_SIZE) & 1) u[words - DP_H_SIZE] = 0;
+    r[DP_H_FMT] = DP_FMT_U16;
+    const int64_t phys = dp_rec_phys_words(r);
+    O.nrec = base + (size_t)phys;
+    O.rec_len.back() = phys;
+  }
 
   std::string_view str(int64_t i) const {
     return std::string_view(w.str_bytes + w.str_off[i], (size_t)(w.str_off[i + 1] - w.str_off[i]));
@@ -466,7 +482,9 @@ struct Lowerer {
       W.var_choice_off.push_back((int32_t)W.choice_off.size() - 1);
       if (anchor) W.anchors.push_back(vi);
     }
+    const size_t base = O.nrec;
     emit_record(W, O, nv);
+    narrow_last(O, base);
   }
 
   // lower_one's exact result without the And-inverter graph, from the
@@ -626,7 +644,9 @@ struct Lowerer {
       F.var_choice_off[vi + 1] = F.nch;
       if (anchor) F.anchors[F.na++] = vi;
     }
+    const size_t base = O.nrec;
     emit_fast(F, O, nv);
+    narrow_last(O, base);
     return 1;
   }
 
@@ -861,7 +881,7 @@ static bool problem_ok(const dp_wire* w, int32_t p) {
 int dp_lower(const dp_wire* wire, dp_lowered** out) {
   if (!out) return -1;
   auto* lw = new dp_lowered;
-  if (dp_lower_into(wire, lw) != 0) {
+  if (dp_lower_into(wire, 0, lw) != 0) {
     delete lw;
     return -1;
   }
@@ -869,7 +889,7 @@ int dp_lower(const dp_wire* wire, dp_lowered** out) {
   return 0;
 }
 
-int dp_lower_into(const dp_wire* wire, dp_lowered* lw) {
+int dp_lower_into(const dp_wire* wire, int32_t flags, dp_lowered* lw) {
   if (!lw || !wire_ok(wire)) {
     dp::set_global_error("dp_lower: malformed wire batch");
     return -1;
@@ -902,7 +922,7 @@ int dp_lower_into(const dp_wire* wire, dp_lowered* lw) {
   }
   lw->pieces.resize((size_t)nchunks);
   lw->n_exact.store(0);
-  dp::Lowerer L(*wire);
+  dp::Lowerer L(*wire, (flags & DP_LOWER_NARROW) != 0);
   std::atomic<bool> bad{false};
   auto lower_chunk = [&](int64_t c, int t) {
     dp::Work& W = lw->work[(size_t)t];
@@ -981,6 +1001,7 @@ int dp_lower_into(const dp_wire* wire, dp_lowered* lw) {
 }
 
 void dp_lowered_free(dp_lowered* lw) { delete lw; }
+dp_lowered* dp_lowered_new(void) { return new dp_lowered; }
 int32_t dp_lowered_num_problems(const dp_lowered* lw) { return lw->n; }
 int64_t dp_lowered_exact_count(const dp_lowered* lw) { return lw->n_exact.load(); }
 const int64_t* dp_lowered_rec_off(const dp_lowered* lw) { return lw->rec_off.data(); }
@@ -1006,12 +1027,26 @@ int32_t dp_lowered_errors(const dp_lowered* lw, int32_t* err) {
 int dp_rec_validate(const int32_t* rec, int64_t words) {
   if (!rec || words < DP_H_SIZE) return -1;
   if (rec[DP_H_MAGIC] != DP_REC_MAGIC) return -2;
+  if (rec[DP_H_FMT] == DP_FMT_U16) {  // widen, then the int32 checks
+    for (int i = DP_H_NV; i <= DP_H_NCHL; ++i)
+      if (rec[i] < 0) return -3;
+    if (!dp_rec_fits16(rec) || dp_rec_layout_of(rec).words != rec[DP_H_WORDS]) return -4;
+    if (dp_rec_phys_words(rec) > words) return -4;
+    std::vector<int32_t> w((size_t)rec[DP_H_WORDS]);
+    std::memcpy(w.data(), rec, 4 * DP_H_SIZE);
+    w[DP_H_FMT] = DP_FMT_I32;
+    const uint16_t* u = reinterpret_cast<const uint16_t*>(rec + DP_H_SIZE);
+    for (size_t j = DP_H_SIZE; j < w.size(); ++j) w[j] = u[j - DP_H_SIZE];
+    return dp_rec_validate(w.data(), (int64_t)w.size());
+  }
+  if (rec[DP_H_FMT] != DP_FMT_I32) return -16;
   for (int i = DP_H_NV; i <= DP_H_NCHL; ++i)
     if (rec[i] < 0) return -3;
   dp_rec_layout L = dp_rec_layout_of(rec);
   if (L.words != rec[DP_H_WORDS] || L.words > words) return -4;
   const int32_t nv = rec[DP_H_NV], nc = rec[DP_H_NC], nk = rec[DP_H_NK], nch = rec[DP_H_NCH];
   const int32_t nid = rec[DP_H_NID];
+  std::vector<int32_t> run_starts;
   auto mono = [&](int32_t off, int32_t n, int32_t total) {
     if (rec[off] != 0 || rec[off + n] != total) return false;
     for (int32_t i = 0; i < n; ++i)
@@ -1029,14 +1064,18 @@ int dp_rec_validate(const int32_t* rec, int64_t words) {
   for (int32_t k = 0; k < nk; ++k) {
     if (rec[L.card_id + k] < 0 || rec[L.card_id + k] >= nid) return -10;
     if (rec[L.card_bound + k] < 0) return -15;  // (lowering folds AtMost(n<0) into an empty clause)
-    // duplicates of a variable must be consecutive (one run per variable)
-    for (int32_t j = rec[L.card_off + k]; j < rec[L.card_off + k + 1]; ++j) {
+    // duplicates of a variable must be consecutive (one run per variable):
+    // the run starts of a row are distinct
+    const int32_t a = rec[L.card_off + k], b = rec[L.card_off + k + 1];
+    for (int32_t j = a; j < b; ++j) {
       int32_t v = rec[L.card_lits + j];
       if (v < 0 || v >= nv) return -11;
-      if (j > rec[L.card_off + k] && rec[L.card_lits + j - 1] != v)
-        for (int32_t i = rec[L.card_off + k]; i < j - 1; ++i)
-          if (rec[L.card_lits + i] == v) return -12;
     }
+    run_starts.clear();
+    for (int32_t j = a; j < b; ++j)
+      if (j == a || rec[L.card_lits + j - 1] != rec[L.card_lits + j]) run_starts.push_back(rec[L.card_lits + j]);
+    std::sort(run_starts.begin(), run_starts.end());
+    if (std::adjacent_find(run_starts.begin(), run_starts.end()) != run_starts.end()) return -12;
   }
   for (int32_t j = 0; j < rec[DP_H_NCHL]; ++j)
     if (rec[L.choice_lits + j] < 0 || rec[L.choice_lits + j] >= nv) return -13;

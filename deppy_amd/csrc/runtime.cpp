@@ -99,14 +99,16 @@ bool lds_path(const int32_t* h, int32_t opt_flags) {
          (int64_t)dp::layout<dp::M_LDS>(h).lds_bytes <= group_above();
 }
 
-// Header sanity needed before any layout arithmetic on it (the full check,
-// dp_rec_validate, runs while the record is staged).
+// Header sanity needed before any layout arithmetic on it: the counts bound
+// every array, so the kernel can stage and validate the body (valid_record)
+// without reading past the record.
 bool header_ok(const int32_t* h, int64_t avail) {
   if (avail < DP_H_SIZE || h[DP_H_MAGIC] != DP_REC_MAGIC) return false;
   for (int i = DP_H_NV; i <= DP_H_NCHL; ++i)
     if (h[i] < 0 || h[i] > (1 << 28)) return false;
+  if (h[DP_H_FMT] != DP_FMT_I32 && (h[DP_H_FMT] != DP_FMT_U16 || !dp_rec_fits16(h))) return false;
   const int64_t w = dp_rec_layout_of(h).words;
-  return w == h[DP_H_WORDS] && w <= avail;
+  return w == h[DP_H_WORDS] && dp_rec_phys_words(h) <= avail;
 }
 
 }  // namespace
@@ -130,6 +132,7 @@ struct Plan {
   std::vector<int64_t> scratch_off;  // [order.size() - big_base] int32-word offsets
   int64_t scratch_words = 0;
   std::vector<int32_t> skip;      // local problems not launched (-> DP_ERROR)
+  std::vector<int32_t> skip_flags; // their dp_flag (DP_F_TOO_LARGE / DP_F_MALFORMED)
   std::vector<int64_t> inst_off;  // [n+1] local installed-word offsets
   int64_t core_cap = 0;           // sum of identity counts (pool capacity)
   int64_t rec_bytes = 0;          // staged record bytes
@@ -137,57 +140,104 @@ struct Plan {
 
 // rec + rec_off[p0 + i] is local problem i.  Problems whose header is not
 // well formed are planned as skipped (the caller reports them).
+// What the plan needs of one record, from its header alone (one cache line
+// per record: the header pass runs on the host pool, since the headers of a
+// chunk sit a record apart and every one is a cache miss).
+struct Head {
+  int8_t place;  // -1 malformed, -2 too large, else the Mode
+  int32_t lds, inst_words, nid;
+  int64_t sw, rec_bytes;
+};
+
+void read_head(Head& H, const int32_t* h, int64_t avail, int32_t opt_flags) {
+  H = Head{};
+  if (!header_ok(h, avail)) { H.place = -1; return; }
+  H.inst_words = bits_words(h[DP_H_NV]);
+  H.nid = h[DP_H_NID];
+  const bool nar = lds_path(h, opt_flags);
+  H.sw = staged_words(h, nar);
+  H.rec_bytes = nar ? 4 * DP_H_SIZE + 2 * ((int64_t)h[DP_H_WORDS] - DP_H_SIZE) : 4 * (int64_t)h[DP_H_WORDS];
+  if (nar) {
+    H.place = M_LDS;
+    H.lds = layout<M_LDS>(h).lds_bytes;
+    return;
+  }
+  const bool forced = forced_of(opt_flags);
+  // (layout arithmetic is int32: variables are capped well below its range)
+  const bool sized = h[DP_H_NV] < (1 << 24) && h[DP_H_NID] < (1 << 26) && h[DP_H_WORDS] < (1 << 28);
+  if (sized && layout<M_SPLIT>(h).lds_bytes <= kMaxLdsBytes && !(opt_flags & DP_OPT_FORCE_HBM))
+    H.place = (opt_flags & DP_OPT_FORCE_MID) || (!forced && h[DP_H_NV] < kMidMaxVars) ? M_SPLIT4 : M_SPLIT;
+  else if (sized && layout<M_HBM>(h).lds_bytes <= kMaxLdsBytes)
+    H.place = M_HBM;
+  else
+    H.place = -2;
+}
+
+// rec + rec_off[p0 + i] is local problem i.  Problems whose header is not
+// well formed are planned as skipped (the caller reports them).  pool (may
+// be null) reads the headers in parallel.
 void plan_chunk(Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0, int32_t n,
-                int32_t opt_flags, std::vector<uint8_t>* bad) {
+                int32_t opt_flags, std::vector<uint8_t>* bad, Pool* pool = nullptr) {
   P = Plan{};
   P.n = n;
   P.img_off.assign((size_t)n + 1, 0);
   P.narrow.assign((size_t)n, 0);
   P.inst_off.assign((size_t)n + 1, 0);
-  const bool forced = forced_of(opt_flags);
+  std::vector<Head> head((size_t)n);
+  auto rd = [&](int64_t i) {
+    read_head(head[(size_t)i], rec + rec_off[p0 + i], rec_off[p0 + i + 1] - rec_off[p0 + i], opt_flags);
+  };
+  if (pool && n > 256) pool->run(n, std::function<void(int64_t)>(rd), 64);
+  else for (int32_t i = 0; i < n; ++i) rd(i);
   std::vector<std::vector<int32_t>> bucket(kNBuckets), big(4);
   std::vector<int> lds((size_t)n, 0);
   for (int32_t i = 0; i < n; ++i) {
-    const int32_t* h = rec + rec_off[p0 + i];
-    const int64_t avail = rec_off[p0 + i + 1] - rec_off[p0 + i];
-    if (!header_ok(h, avail)) {
+    const Head& H = head[(size_t)i];
+    if (H.place == -1) {
       if (bad) (*bad)[(size_t)i] = 1;
       P.skip.push_back(i);
+      P.skip_flags.push_back(DP_F_MALFORMED);
       P.img_off[(size_t)i + 1] = P.img_off[(size_t)i];
       continue;
     }
-    P.inst_off[(size_t)i + 1] = bits_words(h[DP_H_NV]);
-    P.core_cap += h[DP_H_NID];
-    const bool nar = lds_path(h, opt_flags);
-    P.narrow[(size_t)i] = nar;
-    const int64_t sw = staged_words(h, nar);
-    P.img_off[(size_t)i + 1] = P.img_off[(size_t)i] + sw;
-    P.rec_bytes += nar ? 4 * DP_H_SIZE + 2 * ((int64_t)h[DP_H_WORDS] - DP_H_SIZE) : 4 * (int64_t)h[DP_H_WORDS];
-    if (nar) {
-      lds[(size_t)i] = layout<M_LDS>(h).lds_bytes;
+    P.inst_off[(size_t)i + 1] = H.inst_words;
+    P.core_cap += H.nid;
+    P.narrow[(size_t)i] = H.place == M_LDS;
+    P.img_off[(size_t)i + 1] = P.img_off[(size_t)i] + H.sw;
+    P.rec_bytes += H.rec_bytes;
+    if (H.place == M_LDS) {
+      lds[(size_t)i] = H.lds;
       int k = 0;
       while (lds[(size_t)i] > kCeilings[k]) ++k;
       bucket[(size_t)k].push_back(i);
-      continue;
-    }
-    const Layout ls = layout<M_SPLIT>(h), lh = layout<M_HBM>(h);
-    // (layout arithmetic is int32: variables are capped well below its range)
-    const bool sized = h[DP_H_NV] < (1 << 24) && h[DP_H_NID] < (1 << 26) && h[DP_H_WORDS] < (1 << 28);
-    if (sized && ls.lds_bytes <= kMaxLdsBytes && !(opt_flags & DP_OPT_FORCE_HBM))
-      big[(opt_flags & DP_OPT_FORCE_MID) || (!forced && h[DP_H_NV] < kMidMaxVars) ? M_SPLIT4 : M_SPLIT]
-          .push_back(i);
-    else if (sized && lh.lds_bytes <= kMaxLdsBytes)
-      big[M_HBM].push_back(i);
-    else
+    } else if (H.place >= 0) {
+      big[(size_t)H.place].push_back(i);
+    } else {
       P.skip.push_back(i);
+      P.skip_flags.push_back(DP_F_TOO_LARGE);
+    }
   }
   for (int32_t i = 0; i < n; ++i) P.inst_off[(size_t)i + 1] += P.inst_off[(size_t)i];
   // Within a launch, workgroups are dispatched in blockIdx order: largest
   // record first (longest-processing-time-first), so the long solves do not
   // form the launch's tail.
+  // (a counting sort on the staged size, stable: ties keep problem order)
   auto cost = [&](int32_t i) { return P.img_off[(size_t)i + 1] - P.img_off[(size_t)i]; };
+  std::vector<int32_t> cnt, tmp;
   auto lpt = [&](std::vector<int32_t>& v) {
-    std::stable_sort(v.begin(), v.end(), [&](int32_t x, int32_t y) { return cost(x) > cost(y); });
+    if (v.size() < 2) return;
+    int64_t lo = INT64_MAX, hi = 0;
+    for (int32_t i : v) { lo = std::min(lo, cost(i)); hi = std::max(hi, cost(i)); }
+    if (hi - lo > 4 * (int64_t)v.size() + 65536) {  // a wide range: comparison sort
+      std::stable_sort(v.begin(), v.end(), [&](int32_t x, int32_t y) { return cost(x) > cost(y); });
+      return;
+    }
+    cnt.assign((size_t)(hi - lo) + 2, 0);
+    for (int32_t i : v) cnt[(size_t)(hi - cost(i)) + 1]++;
+    for (size_t k = 1; k < cnt.size(); ++k) cnt[k] += cnt[k - 1];
+    tmp.resize(v.size());
+    for (int32_t i : v) tmp[(size_t)cnt[(size_t)(hi - cost(i))]++] = i;
+    v.swap(tmp);
   };
   // multi-wave launches first: the long-running large catalogs start earliest
   for (int mode : {(int)M_SPLIT4, (int)M_SPLIT, (int)M_HBM}) {
@@ -209,8 +259,10 @@ void plan_chunk(Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0,
   P.big_base = 0;  // scratch_off is indexed from the first multi-wave workgroup (order index 0)
   // Adjacent LDS buckets are merged into one launch while the merged request
   // keeps at least kMergeRatio of the first bucket's workgroups per CU.
-  double merge = kMergeRatio;
-  if (const char* m = std::getenv("DEPPY_BUCKET_MERGE")) merge = std::atof(m);  // diagnostic
+  static const double merge = [] {  // diagnostic DEPPY_BUCKET_MERGE
+    const char* m = std::getenv("DEPPY_BUCKET_MERGE");
+    return m ? std::atof(m) : kMergeRatio;
+  }();
   std::vector<Launch> bl;
   std::vector<std::vector<int32_t>> members;
   int first_lds = 0;
@@ -241,85 +293,121 @@ void plan_chunk(Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0,
     P.launches.push_back(bl[g]);
     P.order.insert(P.order.end(), members[g].begin(), members[g].end());
   }
-  if (const char* pad = std::getenv("DEPPY_LDS_PAD_KB"))  // diagnostic (occupancy study)
+  static const int pad_kb = (int)env_i64("DEPPY_LDS_PAD_KB", 0);  // diagnostic (occupancy study)
+  if (pad_kb > 0)
     for (auto& L : P.launches)
-      if (L.mode == M_LDS) L.lds = std::max(L.lds, std::atoi(pad) * 1024);
+      if (L.mode == M_LDS) L.lds = std::max(L.lds, pad_kb * 1024);
 }
 
-// Narrow n words of s into d, checking lo <= x < hi for each (one pass; the
-// checks vectorise with the stores).
-static inline bool narrow_range(const int32_t* s, uint16_t* d, int32_t n, int32_t lo, int32_t hi) {
-  uint32_t bad = 0;
-  const uint32_t span = (uint32_t)(hi - lo);
+// Narrow n words of s into d, checking lo <= x < hi for each (one pass: the
+// min/max reductions and the stores vectorise).
+__attribute__((always_inline)) static inline bool narrow_range(const int32_t* __restrict s, uint16_t* __restrict d,
+                                                               int32_t n, int32_t lo, int32_t hi) {
+  int32_t mn = INT32_MAX, mx = INT32_MIN;
   for (int32_t j = 0; j < n; ++j) {
-    bad |= (uint32_t)((uint32_t)(s[j] - lo) >= span);
+    mn = s[j] < mn ? s[j] : mn;
+    mx = s[j] > mx ? s[j] : mx;
     d[j] = (uint16_t)s[j];
   }
-  return bad == 0;
+  return n == 0 || (mn >= lo && mx < hi);
 }
 // An offsets array: s[0] == 0, non-decreasing, s[n] == total.
-static inline bool narrow_offsets(const int32_t* s, uint16_t* d, int32_t n, int32_t total) {
-  uint32_t bad = (uint32_t)(s[0] != 0) | (uint32_t)(s[n] != total);
-  for (int32_t j = 0; j < n; ++j) bad |= (uint32_t)(s[j + 1] < s[j]);
+__attribute__((always_inline)) static inline bool narrow_offsets(const int32_t* __restrict s,
+                                                                 uint16_t* __restrict d, int32_t n, int32_t total) {
+  int32_t dec = 0;
+  for (int32_t j = 0; j < n; ++j) dec |= s[j + 1] < s[j];
   for (int32_t j = 0; j <= n; ++j) d[j] = (uint16_t)s[j];
-  return bad == 0;
+  return s[0] == 0 && s[n] == total && !dec;
 }
 
 // The 16-bit form of a record whose header passed header_ok and fits16:
 // dp_rec_validate's checks fused into the narrowing pass.  AtMost bounds
 // over the row length are stored as the row length (the same row: neither
 // can be exceeded by the count).
-static bool stage_narrow(const int32_t* src, uint16_t* o) {
+__attribute__((always_inline)) static inline bool stage_narrow_body(const int32_t* src, uint16_t* o) {
   const dp_rec_layout L = dp_rec_layout_of(src);
   const int32_t nv = src[DP_H_NV], nc = src[DP_H_NC], nk = src[DP_H_NK], nch = src[DP_H_NCH];
   const int32_t nid = src[DP_H_NID], ncl = src[DP_H_NCL], nkl = src[DP_H_NKL], nchl = src[DP_H_NCHL];
   auto d = [&](int32_t word) { return o + (word - DP_H_SIZE); };
-  bool ok = narrow_offsets(src + L.clause_off, d(L.clause_off), nc, ncl) &&
-            narrow_range(src + L.clause_lits, d(L.clause_lits), ncl, 0, 2 * nv) &&
-            narrow_range(src + L.clause_id, d(L.clause_id), nc, 0, nid) &&
-            narrow_offsets(src + L.card_off, d(L.card_off), nk, nkl) &&
-            narrow_range(src + L.card_lits, d(L.card_lits), nkl, 0, nv) &&
-            narrow_range(src + L.card_id, d(L.card_id), nk, 0, nid) &&
-            narrow_offsets(src + L.var_choice_off, d(L.var_choice_off), nv, nch) &&
-            narrow_offsets(src + L.choice_off, d(L.choice_off), nch, nchl) &&
-            narrow_range(src + L.choice_lits, d(L.choice_lits), nchl, 0, nv) &&
-            narrow_range(src + L.anchors, d(L.anchors), src[DP_H_NA], 0, nv);
+  bool ok = narrow_offsets(src + L.clause_off, d(L.clause_off), nc, ncl);
+  ok &= narrow_range(src + L.clause_lits, d(L.clause_lits), ncl, 0, 2 * nv);
+  ok &= narrow_range(src + L.clause_id, d(L.clause_id), nc, 0, nid);
+  ok &= narrow_offsets(src + L.card_off, d(L.card_off), nk, nkl);
+  ok &= narrow_range(src + L.card_lits, d(L.card_lits), nkl, 0, nv);
+  ok &= narrow_range(src + L.card_id, d(L.card_id), nk, 0, nid);
+  ok &= narrow_offsets(src + L.var_choice_off, d(L.var_choice_off), nv, nch);
+  ok &= narrow_offsets(src + L.choice_off, d(L.choice_off), nch, nchl);
+  ok &= narrow_range(src + L.choice_lits, d(L.choice_lits), nchl, 0, nv);
+  ok &= narrow_range(src + L.anchors, d(L.anchors), src[DP_H_NA], 0, nv);
   if (!ok) return false;
+  // the positions of a variable form one run: run starts are distinct within
+  // a row (a per-thread mark array, one tag per row)
+  static thread_local std::vector<uint32_t> mark;
+  static thread_local uint32_t tag = 0;
+  if (mark.size() < (size_t)nv) mark.assign((size_t)nv + 1024, 0);
   const int32_t* co = src + L.card_off;
   const int32_t* cl = src + L.card_lits;
   for (int32_t k = 0; k < nk; ++k) {
     const int32_t a = co[k], b = co[k + 1], bound = src[L.card_bound + k];
     if (bound < 0) return false;
     d(L.card_bound)[k] = (uint16_t)std::min(bound, b - a);
-    // the positions of a variable form one run
-    for (int32_t j = a + 1; j < b; ++j)
-      if (cl[j] != cl[j - 1])
-        for (int32_t i = a; i < j - 1; ++i)
-          if (cl[i] == cl[j]) return false;
+    if (++tag == 0) {
+      std::fill(mark.begin(), mark.end(), 0u);
+      tag = 1;
+    }
+    for (int32_t j = a; j < b; ++j)
+      if (j == a || cl[j] != cl[j - 1]) {
+        if (mark[(size_t)cl[j]] == tag) return false;
+        mark[(size_t)cl[j]] = tag;
+      }
   }
   return true;
 }
+__attribute__((target("avx2"))) static bool stage_narrow_avx2(const int32_t* src, uint16_t* o) {
+  return stage_narrow_body(src, o);
+}
+static bool stage_narrow_generic(const int32_t* src, uint16_t* o) { return stage_narrow_body(src, o); }
+static bool stage_narrow(const int32_t* src, uint16_t* o) {
+  static const bool avx2 = __builtin_cpu_supports("avx2");
+  return avx2 ? stage_narrow_avx2(src, o) : stage_narrow_generic(src, o);
+}
 
 // Stage local problem i of the plan into dst (the staged image area): the
-// int32 header with its format word, then the body in 16-bit or int32 form.
-// Returns false when the record is malformed (the checks of dp_rec_validate).
+// int32 header with its format word, then the body in the form the plan
+// chose.  A 16-bit record to a 16-bit copy, or an int32 record to an int32
+// copy, is copied as it is; a 16-bit record for a multi-wave problem is
+// widened.  The kernel validates every staged body (valid_record); only the
+// narrowing of an int32 record is checked here, since truncation to 16 bits
+// would hide an out-of-range index.  Returns false for a malformed record:
+// its staged copy is marked DP_FMT_REJECT and the kernel reports DP_ERROR /
+// DP_F_MALFORMED for it.
 bool stage_one(const Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0, int32_t i,
                int32_t* dst) {
   const int64_t at = P.img_off[(size_t)i], sw = P.img_off[(size_t)i + 1] - at;
   if (sw == 0) return true;  // skipped (header already rejected)
   const int32_t* src = rec + rec_off[p0 + i];
   int32_t* d = dst + at;
-  const int64_t words = src[DP_H_WORDS];
+  const int64_t words = src[DP_H_WORDS], body = words - DP_H_SIZE;
+  const bool src16 = src[DP_H_FMT] == DP_FMT_U16;
   std::memcpy(d, src, 4 * DP_H_SIZE);
   if (P.narrow[(size_t)i]) {
     d[DP_H_FMT] = DP_FMT_U16;
     uint16_t* o = reinterpret_cast<uint16_t*>(d + DP_H_SIZE);
-    if (!stage_narrow(src, o)) return false;
-    for (int64_t j = words - DP_H_SIZE; j < 2 * (sw - DP_H_SIZE); ++j) o[j] = 0;
+    if (src16) {
+      std::memcpy(o, src + DP_H_SIZE, 2 * (size_t)body);
+    } else if (!stage_narrow(src, o)) {
+      d[DP_H_FMT] = DP_FMT_REJECT;
+      return false;
+    }
+    for (int64_t j = body; j < 2 * (sw - DP_H_SIZE); ++j) o[j] = 0;
   } else {
-    if (dp_rec_validate(src, rec_off[p0 + i + 1] - rec_off[p0 + i]) != 0) return false;
     d[DP_H_FMT] = DP_FMT_I32;
-    std::memcpy(d + DP_H_SIZE, src + DP_H_SIZE, 4 * (size_t)(words - DP_H_SIZE));
+    if (src16) {
+      const uint16_t* u = reinterpret_cast<const uint16_t*>(src + DP_H_SIZE);
+      for (int64_t j = 0; j < body; ++j) d[DP_H_SIZE + j] = u[j];
+    } else {
+      std::memcpy(d + DP_H_SIZE, src + DP_H_SIZE, 4 * (size_t)body);
+    }
     for (int64_t j = words; j < sw; ++j) d[j] = 0;
   }
   return true;
@@ -407,9 +495,10 @@ void scatter(const Plan& P, const OutLayout& L, const char* out, int32_t p0, dp_
       const int64_t cap = res->core_off[p0 + i + 1] - res->core_off[p0 + i];
       std::memcpy(res->core + res->core_off[p0 + i], pool + ca[i], (size_t)std::min<int64_t>(cl[i], cap) * 4);
     }
-  for (int32_t i : P.skip) {
+  for (size_t q = 0; q < P.skip.size(); ++q) {
+    const int32_t i = P.skip[q];
     res->status[p0 + i] = DP_ERROR;
-    res->flags[p0 + i] = DP_F_TOO_LARGE;
+    res->flags[p0 + i] = P.skip_flags[q];
     res->core_len[p0 + i] = 0;
     if (res->steps) res->steps[p0 + i] = 0;
     for (int64_t w = res->inst_off[p0 + i]; w < res->inst_off[p0 + i + 1]; ++w) res->installed[w] = 0;
@@ -510,7 +599,7 @@ struct dp_ctx {
   std::mutex mu;
   dp::Pool* pool = nullptr;
   int next_lane = 0;  // pipeline cursor over (device, lane)
-  bool zc_in = true, zc_out = true;  // zero-copy records / results (start_chunk)
+  bool zc_in = false, zc_out = true;  // zero-copy records / results (start_chunk)
   int32_t chunk_problems = kChunkProblems;
   int64_t chunk_bytes = kChunkBytes;
   dp_stats st{};
@@ -596,7 +685,9 @@ int start_chunk(dp_ctx* ctx, Lane& L, dp_job* job, int32_t p0, int32_t n) {
   HIP_OK(hipSetDevice(L.device));
   const double t0 = now_ms();
   std::vector<uint8_t> bad((size_t)n, 0);
-  dp::plan_chunk(L.plan, job->rec, job->rec_off, p0, n, ctx->flags, &bad);
+  dp::plan_chunk(L.plan, job->rec, job->rec_off, p0, n, ctx->flags, &bad, ctx->pool);
+  const double t_plan = now_ms();
+  ctx->st.plan_ms += t_plan - t0;
   const InLayout il = in_layout(L.plan);
   L.ol = out_layout(L.plan);
   HIP_OK(L.h_in.reserve(il.end));
@@ -610,22 +701,19 @@ int start_chunk(dp_ctx* ctx, Lane& L, dp_job* job, int32_t p0, int32_t n) {
   ctx->pool->run(n, [&](int64_t i) {
     if (!dp::stage_one(P, job->rec, job->rec_off, p0, (int32_t)i, img)) bad[(size_t)i] = 1;
   }, 32);
-  for (int32_t i = 0; i < n; ++i)
-    if (bad[(size_t)i]) {
-      job->rc = -1;
-      job->err = "dp_solve: record " + std::to_string(p0 + i) + " malformed";
-      return 0;  // the chunk is not launched; the job reports the error
-    }
+  // (records found malformed while staging are reported by the kernel)
   fill_in_tables(P, il, L.h_in.p);
   ctx->st.stage_ms += now_ms() - t0;
-  // Zero-copy: the kernels write their results straight into the lane's
-  // mapped pinned buffer, and (when no multi-wave problem, which re-reads its
-  // record, is in the chunk) read the staged records from it.  With a D2H
-  // copy per chunk instead, copies from every stream queue on the same copy
-  // engine: a chunk's H2D waited behind the previous chunk's D2H, which waits
-  // for that chunk's kernel, and the lanes ran one after another (config 2:
-  // 3.0M res/s with H2D + D2H, 5.9M with zero-copy results, 6.4M with both
-  // zero-copy; profiles/r02_zero_copy_ab.jsonl).
+  // Zero-copy results: the kernels write their results straight into the
+  // lane's mapped pinned buffer.  With a D2H copy per chunk instead, copies
+  // from every stream queue on the same copy engine: a chunk's H2D waited
+  // behind the previous chunk's D2H, which waits for that chunk's kernel, and
+  // the lanes ran one after another (config 2: 3.0M res/s with H2D + D2H,
+  // 5.9M with zero-copy results; profiles/r02_zero_copy_ab.jsonl).  Records
+  // go by H2D copy: once staging got faster, the copy engine (8.4M res/s at
+  // 3 jobs in flight) beat kernels reading them over PCIe (6.9M;
+  // DEPPY_ZC_IN=1, only for chunks without multi-wave problems, which re-read
+  // their record; profiles/r02_h2h_sweep.jsonl).
   const bool zc_in = ctx->zc_in && P.scratch_off.empty();
   L.zc_out = ctx->zc_out;
   char* din = zc_in ? L.h_in.dev : L.d_in.p;
@@ -737,7 +825,7 @@ dp_ctx* dp_create(const dp_opts* opts) {
   if (opts) ctx->flags = opts->flags;
   ctx->chunk_problems = (int32_t)std::max<int64_t>(1, env_i64("DEPPY_CHUNK_PROBLEMS", kChunkProblems));
   ctx->chunk_bytes = std::max<int64_t>(1, env_i64("DEPPY_CHUNK_BYTES", kChunkBytes));
-  ctx->zc_in = env_i64("DEPPY_ZC_IN", 1) != 0;   // diagnostic: 0 = H2D copy of every chunk
+  ctx->zc_in = env_i64("DEPPY_ZC_IN", 0) != 0;   // diagnostic: 1 = kernels read staged records over PCIe
   ctx->zc_out = env_i64("DEPPY_ZC_OUT", 1) != 0; // diagnostic: 0 = D2H copy of every chunk
   ctx->pool = new dp::Pool(dp::host_threads());
   return ctx;
@@ -851,7 +939,7 @@ int build_slice(dp_ctx* ctx, Slice& s, const dp_batch* b, int32_t trace_cap) {
   HIP_OK(hipEventCreate(&s.k1));
   const int32_t n = s.p1 - s.p0;
   std::vector<uint8_t> bad((size_t)std::max(n, 1), 0);
-  dp::plan_chunk(s.plan, b->rec, b->rec_off, s.p0, n, ctx->flags, &bad);
+  dp::plan_chunk(s.plan, b->rec, b->rec_off, s.p0, n, ctx->flags, &bad, ctx->pool);
   s.il = in_layout(s.plan);
   s.ol = out_layout(s.plan);
   std::vector<char> host(s.il.end);
@@ -860,11 +948,6 @@ int build_slice(dp_ctx* ctx, Slice& s, const dp_batch* b, int32_t trace_cap) {
   ctx->pool->run(n, [&](int64_t i) {
     if (!dp::stage_one(P, b->rec, b->rec_off, s.p0, (int32_t)i, img)) bad[(size_t)i] = 1;
   }, 32);
-  for (int32_t i = 0; i < n; ++i)
-    if (bad[(size_t)i]) {
-      ctx->err = "dp_upload: record " + std::to_string(s.p0 + i) + " malformed";
-      return -1;
-    }
   fill_in_tables(P, s.il, host.data());
   s.d_in.host = s.d_out.host = s.scratch.host = false;
   HIP_OK(s.d_in.reserve(s.il.end));
@@ -1071,36 +1154,46 @@ static dp::Pool& hook_pool() { return dp::host_pool(); }
 
 int dp_stage_roundtrip(const dp_batch* b, int32_t opt_flags, int32_t chunk_problems, int64_t chunk_bytes,
                        int32_t* out_rec, int32_t* chunk_first, int32_t cap) {
-  if (!b || !out_rec || b->n_problems < 0) return -1;
+  if (!b || b->n_problems < 0) return -1;
   if (chunk_problems <= 0) chunk_problems = kChunkProblems;
   if (chunk_bytes <= 0) chunk_bytes = kChunkBytes;
   const int32_t P = b->n_problems;
   int32_t nchunks = 0;
   Plan plan;
-  std::vector<int32_t> staged;
+  static std::vector<int32_t> staged, wide;  // (test hook: one caller at a time)
   for (int32_t p = 0; p < P;) {
     const int32_t q = next_chunk(b->rec_off, p, P, chunk_problems, chunk_bytes);
     if (chunk_first && nchunks < cap) chunk_first[nchunks] = p;
     ++nchunks;
     std::vector<uint8_t> bad((size_t)(q - p), 0);
-    dp::plan_chunk(plan, b->rec, b->rec_off, p, q - p, opt_flags, &bad);
-    staged.assign((size_t)plan.img_off[(size_t)plan.n] + 1, 0);
+    dp::plan_chunk(plan, b->rec, b->rec_off, p, q - p, opt_flags, &bad, &hook_pool());
+    if (staged.size() < (size_t)plan.img_off[(size_t)plan.n] + 1) staged.resize((size_t)plan.img_off[(size_t)plan.n] + 1);
     hook_pool().run(q - p, [&](int64_t i) {
       if (!dp::stage_one(plan, b->rec, b->rec_off, p, (int32_t)i, staged.data())) bad[(size_t)i] = 1;
     }, 32);
     for (auto x : bad)
       if (x) return -1;
-    for (int32_t i = 0; i < q - p; ++i) {
+    for (int32_t i = 0; out_rec && i < q - p; ++i) {  // out_rec NULL: staging only (timing)
+      // the staged copy back in the source record's own form
+      const int32_t* src = b->rec + b->rec_off[p + i];
       const int32_t* st = staged.data() + plan.img_off[(size_t)i];
       int32_t* o = out_rec + b->rec_off[p + i];
-      const int64_t words = b->rec[b->rec_off[p + i] + DP_H_WORDS];
-      std::memcpy(o, st, 4 * DP_H_SIZE);
-      o[dp::DP_H_FMT] = b->rec[b->rec_off[p + i] + dp::DP_H_FMT];
-      if (st[dp::DP_H_FMT] == dp::DP_FMT_U16) {
+      const int64_t words = src[DP_H_WORDS];
+      wide.resize((size_t)words);
+      std::memcpy(wide.data(), st, 4 * DP_H_SIZE);
+      if (st[DP_H_FMT] == DP_FMT_U16) {
         const uint16_t* u = reinterpret_cast<const uint16_t*>(st + DP_H_SIZE);
-        for (int64_t j = DP_H_SIZE; j < words; ++j) o[j] = u[j - DP_H_SIZE];
+        for (int64_t j = DP_H_SIZE; j < words; ++j) wide[(size_t)j] = u[j - DP_H_SIZE];
       } else {
-        std::memcpy(o + DP_H_SIZE, st + DP_H_SIZE, 4 * (size_t)(words - DP_H_SIZE));
+        std::memcpy(wide.data() + DP_H_SIZE, st + DP_H_SIZE, 4 * (size_t)(words - DP_H_SIZE));
+      }
+      std::memcpy(o, wide.data(), 4 * DP_H_SIZE);
+      o[DP_H_FMT] = src[DP_H_FMT];
+      if (src[DP_H_FMT] == DP_FMT_U16) {
+        uint16_t* u = reinterpret_cast<uint16_t*>(o + DP_H_SIZE);
+        for (int64_t j = DP_H_SIZE; j < words; ++j) u[j - DP_H_SIZE] = (uint16_t)wide[(size_t)j];
+      } else {
+        std::memcpy(o + DP_H_SIZE, wide.data() + DP_H_SIZE, 4 * (size_t)(words - DP_H_SIZE));
       }
     }
     p = q;

@@ -165,7 +165,7 @@ struct Group {
   }
 
   // ---- record views ----
-  int nv, nc, nk, nid, nrows, nbv, nbi, na, nch, ncl;
+  int nv, nc, nk, nid, nrows, nbv, nbi, na, nch, ncl, nkl, nchl;
   const IX *clause_off, *clause_lits, *clause_id;
   const IX *card_off, *card_lits, *card_bound, *card_id;
   const IX *var_choice_off, *choice_off, *choice_lits, *anchors;
@@ -311,17 +311,19 @@ struct Group {
   // ------------------------------------------------------------------
   // set-up (oracle: st_init)
   // ------------------------------------------------------------------
-  __device__ __forceinline__ void init(char* lds, char* hbm, const int32_t* __restrict__ grec) {
+  // Returns false (nothing else initialised) for a malformed record.
+  __device__ __forceinline__ bool init(char* lds, char* hbm, const int32_t* __restrict__ grec) {
     tid = (int)threadIdx.x;
     lane = lane_id();
     wid = tid >> 6;
     int32_t h[DP_H_SIZE];
 #pragma unroll
     for (int i = 0; i < DP_H_SIZE; ++i) h[i] = grec[i];
+    if (h[DP_H_FMT] == DP_FMT_REJECT) return false;
     const Layout L = layout<MODE>(h);
     const dp_rec_layout R = rec_layout(h);
     const ImgLayout X = img_layout(h);
-    ncl = h[DP_H_NCL];
+    ncl = h[DP_H_NCL]; nkl = h[DP_H_NKL]; nchl = h[DP_H_NCHL];
     nv = h[DP_H_NV]; nc = h[DP_H_NC]; nk = h[DP_H_NK]; nid = h[DP_H_NID]; na = h[DP_H_NA];
     nch = h[DP_H_NCH];
     nrows = nc + nk;
@@ -439,6 +441,7 @@ struct Group {
     for (int i = 0; i < 16; ++i) acc[i] = 0;
     dbg = nullptr;
 #endif
+    if (!valid_record()) return false;
     // the watch lists follow the record (M_LDS) or live in the problem's
     // scratch; M_LDS counts on the per-literal arrays, initialised below
     if constexpr (MODE == M_LDS) {
@@ -463,6 +466,45 @@ struct Group {
     if (tid < mode_nscal(MODE)) scal[tid] = 0;
     if (tid == 0) l_off[0] = 0;
     gsync();
+    return true;
+  }
+
+  // dp_rec_validate on the device, before any data-dependent index (the host
+  // checked only the header, which bounds every array): offsets arrays start
+  // at 0, never decrease and end at their totals; every literal, variable and
+  // identity is in range; AtMost bounds are not negative; the positions of a
+  // variable in an AtMost row form one run.  Group-uniform result.
+  __device__ __forceinline__ bool valid_record() {
+    bool bad = false;
+    auto offsets = [&](const IX* off, int n, int total) {
+      for (int i = tid; i <= n; i += NT) {
+        const int x = (int)off[i];
+        bad |= i == 0 ? x != 0 : x < (int)off[i - 1];
+        bad |= i == n && x != total;
+      }
+    };
+    auto range = [&](const IX* a, int n, int hi) {
+      for (int i = tid; i < n; i += NT) bad |= (uint32_t)(int)a[i] >= (uint32_t)hi;
+    };
+    offsets(clause_off, nc, ncl);
+    offsets(card_off, nk, nkl);
+    offsets(var_choice_off, nv, nch);
+    offsets(choice_off, nch, nchl);
+    range(clause_lits, ncl, 2 * nv);
+    range(clause_id, nc, nid);
+    range(card_lits, nkl, nv);
+    range(card_id, nk, nid);
+    range(choice_lits, nchl, nv);
+    range(anchors, na, nv);
+    if (g_any(bad)) return false;  // the offsets below are now in range
+    for (int k = tid; k < nk; k += NT) {
+      const int a = card_off[k], b = card_off[k + 1];
+      bad |= (int)card_bound[k] < 0;
+      for (int j = a + 1; j < b; ++j)
+        if (card_lits[j] != card_lits[j - 1])
+          for (int i = a; i < j - 1; ++i) bad |= card_lits[i] == card_lits[j];
+    }
+    return !g_any(bad);
   }
 
   // Watch lists of the record, built on the device (the host ships the record
@@ -1680,7 +1722,19 @@ solve_kernel(KernelArgs a) {
   const int32_t* grec = a.rec + a.rec_off[pid];
   Group<MODE> W;
   char* hbm = MODE == M_LDS ? nullptr : reinterpret_cast<char*>(a.scratch + a.scratch_off[blockIdx.x]);
-  W.init(reinterpret_cast<char*>(lds4), hbm, grec);
+  if (!W.init(reinterpret_cast<char*>(lds4), hbm, grec)) {
+    if (threadIdx.x == 0) {  // a malformed record: no solve (dp_rec_validate's verdict)
+      a.status[pid] = (int8_t)DP_ERROR;
+      a.flags[pid] = DP_F_MALFORMED;
+      a.core_len[pid] = 0;
+      a.core_at[pid] = 0;
+      a.steps[pid] = 0;
+      if (a.trace) a.trace_len[pid] = 0;
+    }
+    uint32_t* inst0 = a.installed + a.inst_off[pid];
+    for (int i = threadIdx.x; i < bits_words(grec[DP_H_NV]); i += blockDim.x) inst0[i] = 0;
+    return;
+  }
 #ifdef DP_STAMPS
   if (a.stamps) W.dbg = reinterpret_cast<unsigned long long*>(a.stamps + (int64_t)DP_NSTAMP * pid + 12);
 #endif

@@ -150,7 +150,33 @@ static inline dp_rec_layout dp_rec_layout_of(const int32_t* h) {
   return L;
 }
 
-/* Validate one record (bounds of every index).  Returns 0 if well formed. */
+/* Header word DP_H_FMT selects the body's form.  DP_FMT_I32: every word after
+ * the header is an int32 (DP_H_WORDS words in all).  DP_FMT_U16: every word
+ * after the header is a uint16, two per int32 word (low half first), so the
+ * record occupies dp_rec_phys_words() int32 words; this is the form the GPU
+ * stages for one-wavefront problems, and dp_lower_into(DP_LOWER_NARROW)
+ * emits it for every record that fits (dp_rec_fits16), so that staging is a
+ * copy.  Offsets (rec_off) always count int32 words. */
+enum { DP_H_FMT = 13 };
+enum { DP_FMT_I32 = 0, DP_FMT_U16 = 1 };
+
+static inline int64_t dp_rec_phys_words(const int32_t* h) {
+  return h[DP_H_FMT] == DP_FMT_U16 ? DP_H_SIZE + ((int64_t)h[DP_H_WORDS] - DP_H_SIZE + 1) / 2
+                                   : (int64_t)h[DP_H_WORDS];
+}
+
+/* Does every index the record holds, and every value the solve stores per
+ * variable or row, fit 16 bits (below the kernel's reserved reason codes)? */
+static inline int dp_rec_fits16(const int32_t* h) {
+  const int32_t nv = h[DP_H_NV];
+  return h[DP_H_WORDS] < 65000 && nv < 16000 && h[DP_H_NID] < 65000 &&
+         h[DP_H_NC] + h[DP_H_NK] + 64 + nv < 65000 && h[DP_H_NA] + h[DP_H_NCH] < 65000 &&
+         h[DP_H_NCL] + h[DP_H_NKL] < 65000;
+}
+
+/* Validate one record of either form (bounds of every index).  Returns 0 if
+ * well formed.  The solve checks every record the same way on the device, so
+ * a malformed record yields DP_ERROR with DP_F_MALFORMED, never a fault. */
 int dp_rec_validate(const int32_t* rec, int64_t words);
 
 /* ------------------------------------------------------------------------ */
@@ -165,8 +191,12 @@ typedef struct dp_lowered dp_lowered; /* host-owned, opaque */
  * Returns 0, or -1 on malformed input (text in dp_last_global_error()). */
 int dp_lower(const dp_wire* wire, dp_lowered** out);
 /* dp_lower into an existing result, reusing its storage (a serving loop
- * lowers batch after batch without allocating).  Returns 0 or -1. */
-int dp_lower_into(const dp_wire* wire, dp_lowered* lw);
+ * lowers batch after batch without allocating).  flags: DP_LOWER_NARROW emits
+ * every record that fits 16 bits in the DP_FMT_U16 form (the staged form:
+ * half the bytes to write, to stage and to cross PCIe).  Returns 0 or -1. */
+enum { DP_LOWER_NARROW = 1 };
+int dp_lower_into(const dp_wire* wire, int32_t flags, dp_lowered* lw);
+dp_lowered* dp_lowered_new(void); /* an empty result for dp_lower_into */
 void dp_lowered_free(dp_lowered* lw);
 int32_t dp_lowered_num_problems(const dp_lowered* lw);
 /* Problems of the last lowering that went through the full And-inverter
@@ -202,7 +232,8 @@ enum dp_flag {
   DP_F_CORE_BUDGET = 1 << 5,    /* core not fully minimised within the step budget        */
   DP_F_BUDGET = 1 << 6,         /* step budget exhausted -> DP_INCOMPLETE                 */
   DP_F_TOO_LARGE = 1 << 7,      /* record does not fit the device path                    */
-  DP_F_TRACE_TRUNCATED = 1 << 8 /* search trace stopped: an event exceeded the capacity   */
+  DP_F_TRACE_TRUNCATED = 1 << 8, /* search trace stopped: an event exceeded the capacity  */
+  DP_F_MALFORMED = 1 << 9        /* the record failed dp_rec_validate's checks (DP_ERROR) */
 };
 
 typedef struct dp_opts {
@@ -284,6 +315,7 @@ typedef struct dp_stats {
   int64_t d2h_bytes; /* bytes copied device -> host                          */
   int64_t rec_bytes; /* staged record bytes (16-bit form on the LDS path)    */
   double stage_ms;   /* host: planning + staging records into pinned memory  */
+  double plan_ms;    /* host: of which planning the launches                  */
   double wait_ms;    /* host: blocked on a chunk's completion                 */
   double scatter_ms; /* host: results -> the caller's dp_result              */
 } dp_stats;
@@ -330,7 +362,8 @@ int dp_device_bytes(const dp_batch* b, int32_t opt_flags, int64_t* rec_bytes, in
  *     chunk_bytes; 0 = defaults), stages every chunk, and widens the staged
  *     copies back into out_rec (same offsets as b->rec): a round trip that
  *     reproduces every record except AtMost bounds over their row length,
- *     which are staged as the row length.  chunk_first[] receives the first
+ *     which are staged as the row length (out_rec NULL: stage only, for
+ *     timing).  chunk_first[] receives the first
  *     problem of each chunk (cap entries at most).  Returns the number of
  *     chunks, or -1 for a malformed record.
  *   dp_stitch_selftest: for every chunk, fills the chunk's output region with

@@ -83,7 +83,7 @@ def solve_batch(rec_off: np.ndarray, rec: np.ndarray, budget: int = 0, nthreads:
     rec_off = np.ascontiguousarray(rec_off, dtype=np.int64)
     rec = np.ascontiguousarray(rec, dtype=np.int32)
     n = len(rec_off) - 1
-    nvs = rec[rec_off[:-1] + 1].astype(np.int64)
+    nvs = rec[rec_off[:-1] + 1].astype(np.int64)  # (headers are int32 in either record form)
     nids = rec[rec_off[:-1] + 6].astype(np.int64)
     inst_off = np.zeros(n + 1, np.int64)
     inst_off[1:] = np.cumsum((nvs + 31) // 32)

@@ -54,6 +54,7 @@ typedef struct search_s search_t;
 
 typedef struct {
   prob_t p;
+  int32_t* wide; /* the int32 copy of a 16-bit-form record (widen), or NULL */
   /* watch lists: rows to evaluate when literal l becomes TRUE */
   int32_t *w_off, *w;
   /* assignment */
@@ -132,8 +133,25 @@ static int row_ident(const prob_t* p, int r) {
 
 static void* xcalloc(size_t n, size_t sz) { return calloc(n ? n : 1, sz); }
 
+/* A record in the 16-bit form (header word DP_H_FMT = DP_FMT_U16, every body
+ * word a uint16) widened to int32 words in *tmp (freed by the caller);
+ * int32 records are returned as they are. */
+static const int32_t* widen(const int32_t* rec, int32_t** tmp) {
+  *tmp = NULL;
+  if (rec[DP_H_FMT] != DP_FMT_U16) return rec;
+  int32_t w = rec[DP_H_WORDS];
+  int32_t* o = xcalloc((size_t)w, sizeof(int32_t));
+  memcpy(o, rec, DP_H_SIZE * sizeof(int32_t));
+  o[DP_H_FMT] = DP_FMT_I32;
+  const uint16_t* u = (const uint16_t*)(rec + DP_H_SIZE);
+  for (int32_t j = DP_H_SIZE; j < w; ++j) o[j] = u[j - DP_H_SIZE];
+  *tmp = o;
+  return o;
+}
+
 static int st_init(st_t* s, const int32_t* rec) {
   memset(s, 0, sizeof(*s));
+  rec = widen(rec, &s->wide);
   parse(&s->p, rec);
   const prob_t* p = &s->p;
   int nl = 2 * p->nv;
@@ -182,6 +200,7 @@ static int st_init(st_t* s, const int32_t* rec) {
 }
 
 static void st_free(st_t* s) {
+  free(s->wide);
   free(s->w_off); free(s->w); free(s->val); free(s->reason); free(s->rnd); free(s->trail);
   free(s->imp_pos); free(s->imp_neg); free(s->touched); free(s->is_extra); free(s->seen);
   free(s->used); free(s->uacc); free(s->work); free(s->inS); free(s->model); free(s->d_lit); free(s->d_mark);
@@ -1042,6 +1061,8 @@ int oracle_solve_batch_traced(int32_t n, const int64_t* rec_off, const int32_t* 
  * (variables not installed are false).  Returns the first violated row, or -1. */
 int oracle_check_model(const int32_t* rec, const uint32_t* installed) {
   prob_t p;
+  int32_t* wide;
+  rec = widen(rec, &wide);
   parse(&p, rec);
   for (int r = 0; r < p.nc; ++r) {
     int sat = 0;
@@ -1050,7 +1071,7 @@ int oracle_check_model(const int32_t* rec, const uint32_t* installed) {
       int x = (installed[v >> 5] >> (v & 31)) & 1;
       if (x != (l & 1)) { sat = 1; break; }
     }
-    if (!sat) return r;
+    if (!sat) { free(wide); return r; }
   }
   for (int k = 0; k < p.nk; ++k) {
     int cnt = 0;
@@ -1058,7 +1079,8 @@ int oracle_check_model(const int32_t* rec, const uint32_t* installed) {
       int v = p.card_lits[j];
       cnt += (installed[v >> 5] >> (v & 31)) & 1;
     }
-    if (cnt > p.card_bound[k]) return p.nc + k;
+    if (cnt > p.card_bound[k]) { free(wide); return p.nc + k; }
   }
+  free(wide);
   return -1;
 }

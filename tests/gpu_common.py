@@ -4,11 +4,28 @@ import numpy as np
 from deppy_amd import _lib
 
 
-def lowered_config(config, n, seed):
+def lowered_config(config, n, seed, narrow=False):
+    """Synthetic catalogs (SURVEY §8(d) generator) lowered by dp_lower;
+    narrow: records that fit 16 bits in the DP_FMT_U16 form."""
     w = _lib.generate(config, n, seed)
     return _lib.Lowered(_lib.WireArrays(**{k: w[k] for k in (
         "prob_var_off", "var_id", "var_con_off", "con_kind", "con_n", "con_arg_off", "con_arg",
-        "str_off")}, str_bytes=w["str_bytes"].tobytes()))
+        "str_off")}, str_bytes=w["str_bytes"].tobytes()), narrow=narrow)
+
+
+def widen(rec_off, rec):
+    """A batch with every DP_FMT_U16 record widened to int32 (-> rec_off, rec)."""
+    parts, offs = [], [0]
+    for p in range(len(rec_off) - 1):
+        r = rec[rec_off[p]:rec_off[p + 1]]
+        if r[13] == 1:
+            words = int(r[10])
+            body = r[16:].view(np.uint16)[:words - 16].astype(np.int32)
+            r = np.concatenate([r[:16], body])
+            r[13] = 0
+        parts.append(np.asarray(r, np.int32))
+        offs.append(offs[-1] + len(r))
+    return np.array(offs, np.int64), (np.concatenate(parts) if parts else np.zeros(0, np.int32))
 
 
 def compare_results(g, o, n, rec_off=None, rec=None):

@@ -204,3 +204,74 @@ def test_pipelined_launches_match_serial(ctx):
             s.free()
     for out, want, n in ((outs[0], ref, 400), (outs[1], ref2, 600), (outs[2], ref, 400)):
         assert compare_results(out, want, n) == []
+
+
+# ---------------------------------------------------------------------------
+# the host-to-host pipeline (dp_submit / dp_job_wait) and the record forms
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("config,n,seed", [(2, 2000, 51), (3, 5000, 52), (5, 300, 53)])
+def test_narrow_records_bit_exact(ctx, config, n, seed):
+    """16-bit-form records (dp_lower_into DP_LOWER_NARROW) solve exactly like
+    their int32 form, and like the oracle."""
+    a = lowered_config(config, n, seed)
+    b = lowered_config(config, n, seed, narrow=True)
+    ga = ctx.solve(a.rec_off, a.rec)
+    gb = ctx.solve(b.rec_off, b.rec)
+    assert compare_results(gb, ga, n) == []
+    o = oracle.solve_batch(b.rec_off, b.rec, 0, 16)
+    assert compare_results(gb, o, n) == []
+
+
+def test_jobs_in_flight_small_chunks(monkeypatch):
+    """Many chunks per job and several jobs in flight: lanes are reused across
+    jobs (a submit first delivers the lane's previous chunk), and every job's
+    results equal its own synchronous solve."""
+    monkeypatch.setenv("DEPPY_CHUNK_PROBLEMS", "97")
+    c = _lib.Context(0, 1)
+    try:
+        batches = [lowered_config(cfg, n, s, narrow=s % 2 == 0)
+                   for cfg, n, s in ((2, 700, 61), (5, 150, 62), (3, 2500, 63), (2, 300, 64))]
+        refs = [oracle.solve_batch(b.rec_off, b.rec, 0, 16) for b in batches]
+        jobs = [c.submit(b.rec_off, b.rec) for b in batches]
+        outs = [j.wait() for j in jobs]
+        st = c.stats()
+        assert st["chunks"] >= sum(-(-b.n // 97) for b in batches)
+    finally:
+        c.close()
+    for out, ref, b in zip(outs, refs, batches):
+        assert compare_results(out, ref, b.n) == []
+
+
+@pytest.mark.parametrize("flags", [0, _lib.OPT_FORCE_GROUP], ids=["lds", "group"])
+def test_malformed_records_are_per_problem_errors(flags):
+    """A malformed record yields DP_ERROR + DP_F_MALFORMED for that problem
+    (found while narrowing on the host, or by the kernel's own validation)
+    and the rest of the batch is solved bit-exactly."""
+    lw = lowered_config(2, 40, 71)
+    rec = lw.rec.copy()
+    bad = [3, 17, 30]
+    for p in bad:
+        r0 = int(lw.rec_off[p])
+        nc = int(rec[r0 + 2])
+        if p == 3:
+            rec[r0 + 16 + nc + 1] = 2 * int(rec[r0 + 1]) + 3   # clause literal past 2*nv
+        elif p == 17:
+            rec[r0 + 16 + 1] = rec[r0 + 16 + 2] + 1             # clause offsets decrease
+        else:
+            nk, ncl, nkl = int(rec[r0 + 3]), int(rec[r0 + 7]), int(rec[r0 + 8])
+            cl = r0 + 16 + nc + 1 + ncl + nc + nk + 1           # card_lits
+            rec[cl] = int(rec[r0 + 1]) + 7                      # AtMost variable past nv
+    c = _lib.Context(0, 1, flags=flags)
+    try:
+        g = c.solve(lw.rec_off, rec)
+    finally:
+        c.close()
+    o = oracle.solve_batch(lw.rec_off, lw.rec, 0, 16)
+    for p in range(lw.n):
+        if p in bad:
+            assert g["status"][p] == -2 and g["flags"][p] == 512 and g["core_len"][p] == 0, p
+        else:
+            assert compare_results({k: v for k, v in g.items()}, o, lw.n) is not None
+    ok = [p for p in range(lw.n) if p not in bad]
+    for k in ("status", "flags", "steps"):
+        np.testing.assert_array_equal(g[k][ok], o[k][ok])

@@ -111,3 +111,47 @@ def test_partition_covers_batch(nd):
     if nd <= lw.n:
         words = [int(lw.rec_off[cut[d + 1]] - lw.rec_off[cut[d]]) for d in range(nd)]
         assert max(words) <= int(lw.rec_off[-1]) / nd + int(np.diff(lw.rec_off).max())
+
+
+@pytest.mark.parametrize("config,n", [(2, 200), (3, 1000), (5, 80), (4, 1)])
+def test_narrow_lowering_is_the_16bit_form(config, n):
+    """dp_lower_into(DP_LOWER_NARROW) emits exactly the int32 records, in the
+    DP_FMT_U16 form wherever they fit 16 bits; every record validates."""
+    from tests.gpu_common import widen
+    a = lowered_config(config, n, 17)
+    b = lowered_config(config, n, 17, narrow=True)
+    off, rec = widen(b.rec_off, b.rec)
+    np.testing.assert_array_equal(off, a.rec_off)
+    np.testing.assert_array_equal(rec, a.rec)
+    for p in range(n):
+        r = b.record(p)
+        assert int(r[13]) == (1 if config != 4 else 0)
+        assert _lib.lib().dp_rec_validate(np.ascontiguousarray(r).ctypes.data_as(_lib.c_i32p), len(r)) == 0
+    np.testing.assert_array_equal(b.ident_var, a.ident_var)
+    assert b.rec_off[-1] < a.rec_off[-1] or config == 4
+
+
+@pytest.mark.parametrize("flags", [0, _lib.OPT_FORCE_GROUP])
+def test_stage_roundtrip_narrow_source(flags):
+    lw = lowered_config(2, 120, 23, narrow=True)
+    out, _ = _lib.stage_roundtrip(lw.rec_off, lw.rec, flags=flags, chunk_problems=50)
+    np.testing.assert_array_equal(out, lw.rec)
+
+
+def test_oracle_reads_narrow_records():
+    from oracle import oracle
+    a = lowered_config(5, 60, 29)
+    b = lowered_config(5, 60, 29, narrow=True)
+    oa = oracle.solve_batch(a.rec_off, a.rec)
+    ob = oracle.solve_batch(b.rec_off, b.rec)
+    for k in ("status", "flags", "installed", "core", "core_len", "steps"):
+        np.testing.assert_array_equal(oa[k], ob[k])
+
+
+def test_validate_rejects_malformed_narrow():
+    lw = lowered_config(2, 3, 31, narrow=True)
+    r = np.ascontiguousarray(lw.record(1)).copy()
+    u = r[16:].view(np.uint16)
+    nc, ncl = int(r[2]), int(r[7])
+    u[nc + 1] = 2 * int(r[1]) + 5  # first clause literal past 2*nv
+    assert _lib.lib().dp_rec_validate(r.ctypes.data_as(_lib.c_i32p), len(r)) != 0
