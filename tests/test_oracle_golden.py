@@ -82,3 +82,32 @@ def test_lookup_errors():
     assert lw.msg == ('3 errors encountered: variable "x" referenced but not provided, '
                       'variable "y" referenced but not provided, '
                       'variable "z\\"q" referenced but not provided')
+
+
+def test_order_golden():
+    """TestOrder (pkg/sat/constraints_test.go:9-39): Order() per constraint
+    kind, and the lowered record's choice lists are exactly the Order() lists
+    of each variable's constraints, in constraint order (search.go:59-69)."""
+    import numpy as np
+    from deppy_amd import _lib, sat
+    from tests.test_lowering import V, sat_var
+    cases = fixtures.load("errors")["order"]
+    assert [c["name"] for c in cases] == ["mandatory", "prohibited", "dependency", "conflict"]
+    for c in cases:
+        con = sat_var({"id": "s", "constraints": [c["constraint"]]}).Constraints()[0]
+        got = con.Order()
+        assert (None if got is None else [str(i) for i in got]) == c["expected"], c["name"]
+    vs = [V("s", *[sat_var({"id": "s", "constraints": [c["constraint"]]}).Constraints()[0] for c in cases],
+            sat.Dependency("c", "a")), V("a"), V("b"), V("c")]
+    lw = _lib.Lowered(sat.encode_inputs([vs]))
+    r = lw.record(0)
+    L = {k: int(x) for k, x in zip(("nv", "nc", "nk", "nch", "na", "nid", "ncl", "nkl", "nchl"), r[1:10])}
+    o = 16 + (L["nc"] + 1) + L["ncl"] + L["nc"] + (L["nk"] + 1) + L["nkl"] + 2 * L["nk"]
+    var_choice_off = r[o:o + L["nv"] + 1]
+    choice_off = r[o + L["nv"] + 1:o + L["nv"] + 1 + L["nch"] + 1]
+    lits = r[o + L["nv"] + 1 + L["nch"] + 1:][:L["nchl"]]
+    names = ["s", "a", "b", "c"]
+    lists = [[names[int(v)] for v in lits[choice_off[k]:choice_off[k + 1]]]
+             for k in range(var_choice_off[0], var_choice_off[1])]
+    assert lists == [["a", "b", "c"], ["c", "a"]]
+    assert np.all(np.diff(var_choice_off[1:]) == 0)
