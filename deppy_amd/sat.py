@@ -19,8 +19,10 @@ launch — the data-parallel form this engine exists for.
 """
 from __future__ import annotations
 
+import contextlib
 import io
 import threading
+import warnings
 from dataclasses import dataclass, field
 from typing import Iterable, Optional, Sequence
 
@@ -270,7 +272,10 @@ class LoggingTracer(Tracer):
 # ---------------------------------------------------------------------------
 # solver (solve.go:32-163)
 # ---------------------------------------------------------------------------
-_ctx_lock = threading.Lock()
+# The process-wide context.  _ctx_lock is held for a whole solve on it, so
+# set_device() cannot close the context while a SolveBatch is using it (the
+# library serialises calls on one context anyway).
+_ctx_lock = threading.RLock()
 _ctx: Optional[_lib.Context] = None
 
 
@@ -288,7 +293,8 @@ _device = [0]
 
 
 def set_device(ordinal: int, step_budget: int = 0) -> None:
-    """Bind this process to one MI355X (one process per GPU)."""
+    """Bind this process to one MI355X (one process per GPU).  Waits for a
+    solve in progress on the previous context."""
     global _ctx
     with _ctx_lock:
         if _ctx is not None:
@@ -448,7 +454,7 @@ def SolveBatch(inputs: Sequence[Sequence[Variable]], tracer: Optional[Tracer] = 
     Returns [(installed | None, error | None)] in input order."""
     inputs = [list(v) for v in inputs]
     traced = tracer is not None and not isinstance(tracer, DefaultTracer)
-    lw = _lib.Lowered(encode_inputs(inputs))
+    lw = _lib.Lowered(encode_inputs(inputs), narrow=True)  # 16-bit records: the staged form
     out: list = [None] * len(inputs)
     ok = [p for p in range(len(inputs)) if lw.err[p] == 0]
     for p in range(len(inputs)):
@@ -465,16 +471,29 @@ def SolveBatch(inputs: Sequence[Sequence[Variable]], tracer: Optional[Tracer] = 
             parts.append(r)
             offs.append(offs[-1] + len(r))
         rec = np.concatenate(parts).astype(np.int32)
-        ctx = context or device_context()
-        res = ctx.solve(np.array(offs, np.int64), rec, TRACE_CAP if traced else 0)
+        with (contextlib.nullcontext() if context else _ctx_lock):
+            ctx = context or device_context()
+            res = ctx.solve(np.array(offs, np.int64), rec, TRACE_CAP if traced else 0)
+            retraced = {}
+            if traced:
+                for j, p in enumerate(ok):
+                    rj, jj, cap = res, j, TRACE_CAP
+                    while rj["flags"][jj] & _lib.F_TRACE_TRUNCATED and cap < TRACE_CAP_MAX:
+                        cap *= 16
+                        r1 = lw.record(p).astype(np.int32)
+                        rj, jj = ctx.solve(np.array([0, len(r1)], np.int64), r1, cap), 0
+                    if rj["flags"][jj] & _lib.F_TRACE_TRUNCATED:
+                        # the reference's tracer sees every unsatisfiable step
+                        # (search.go:173); this one would miss the steps past
+                        # the largest reservation
+                        warnings.warn("deppy_amd: search trace of problem %d truncated at %d words; "
+                                      "the tracer sees only its first steps" % (p, TRACE_CAP_MAX),
+                                      RuntimeWarning, stacklevel=2)
+                    retraced[j] = (rj, jj)
         for j, p in enumerate(ok):
             variables = inputs[p]
             if traced:
-                rj, jj, cap = res, j, TRACE_CAP
-                while rj["flags"][jj] & _lib.F_TRACE_TRUNCATED and cap < TRACE_CAP_MAX:
-                    cap *= 16
-                    r1 = lw.record(p).astype(np.int32)
-                    rj, jj = ctx.solve(np.array([0, len(r1)], np.int64), r1, cap), 0
+                rj, jj = retraced[j]
                 _replay_trace(tracer, variables, lw, p, rj, jj)
             st = int(res["status"][j])
             if st == SAT:

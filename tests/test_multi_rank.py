@@ -11,6 +11,8 @@ import torch.multiprocessing as mp
 
 from deppy_amd import _lib, shard
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 N_PER_RANK = 40
 
 
@@ -79,3 +81,26 @@ def test_two_rank_gloo(tmp_path):
     assert np.array_equal(np.concatenate([r[0]["steps"], r[1]["steps"]]), gres["steps"])
     # no two ranks solved the same catalog
     assert not np.array_equal(r[0]["rec"], r[1]["rec"])
+
+
+def test_strong_scaling_ranges_partition_the_total():
+    """bench.py --scaling strong: the ranks' contiguous shares cover the
+    config's total exactly once (config 3: 1M catalogs over 1/2/4/8 GPUs)."""
+    from deppy_amd import shard
+    for total in (1_000_000, 10_001, 7):
+        for world in (1, 2, 4, 8):
+            rs = [shard.strong_range(total, r, world) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == total
+            assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
+            assert max(h - l for l, h in rs) - min(h - l for l, h in rs) <= 1
+
+
+def test_bench_refuses_world_mismatch(monkeypatch):
+    """bench.py --gpus N must run on N ranks: under a launcher with another
+    WORLD_SIZE it stops instead of measuring something else."""
+    import subprocess
+    import sys
+    env = dict(__import__("os").environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE" in (r.stderr + r.stdout)
