@@ -159,7 +159,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--kernel-steps", type=int, default=20,
                     help="steps of the device-resident (kernel-only) secondary figure; 0: skip")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02_pmc_traffic.json"),
+    ap.add_argument("--kernel-only", action="store_true",
+                    help="skip the host-to-host leg (profiling runs of the solve kernel)")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02_pmc_traffic.jsonl"),
                     help="HBM bytes per solve kernel dispatch from separate rocprofv3 --pmc passes; "
                          "used for roofline.traffic when its config/problems match")
     args = ap.parse_args()
@@ -195,35 +197,28 @@ def main():
         for j in jobs:
             j.wait()
 
-    run_steps(max(args.warmup, 1))
-    first_res = ctx.submit(lw.rec_off, lw.rec).wait()  # cold-free single call, for the check
-    g.barrier()
-    ctx.stats(reset=True)
-    t0 = time.perf_counter()
-    run_steps(args.steps)
-    t1 = time.perf_counter()
-    g.barrier()
-    st = ctx.stats(reset=True)
-    elapsed = g.max(t1 - t0)
-    res = ctx.submit(lw.rec_off, lw.rec).wait()
-    deterministic = same_results(res, first_res) and all(
-        same_results(res, {**o, "status": o["status"][:n], "flags": o["flags"][:n],
-                           "core_len": o["core_len"][:n], "steps": o["steps"][:n]}) for o in outs)
+    if args.kernel_only:  # profiling: only the device-resident leg below
+        args.steps = 1
+        st, elapsed, res, deterministic = ctx.stats(), float("inf"), None, None
+    else:
+        run_steps(max(args.warmup, 1))
+        first_res = ctx.submit(lw.rec_off, lw.rec).wait()  # cold-free single call, for the check
+        g.barrier()
+        ctx.stats(reset=True)
+        t0 = time.perf_counter()
+        run_steps(args.steps)
+        t1 = time.perf_counter()
+        g.barrier()
+        st = ctx.stats(reset=True)
+        elapsed = g.max(t1 - t0)
+        res = ctx.submit(lw.rec_off, lw.rec).wait()
+        deterministic = same_results(res, first_res) and all(
+            same_results(res, {**o, "status": o["status"][:n], "flags": o["flags"][:n],
+                               "core_len": o["core_len"][:n], "steps": o["steps"][:n]}) for o in outs)
 
     value = world * n * args.steps / elapsed if args.scaling == "weak" else \
         (args.problems or wl[1]) * args.steps / elapsed
-    # roofline of the solve kernel, per chunk (HIP events on its stream)
     chunks = max(st["chunks"], 1)
-    kernel_ms = st["kernel_ms"] / chunks
-    out_b = output_bytes(res)
-    alg_per_chunk = (st["rec_bytes"] / max(args.steps, 1) + out_b) / (chunks / max(args.steps, 1))
-    achieved = alg_per_chunk / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
-    traffic = None
-    if args.pmc_json and os.path.exists(args.pmc_json):
-        with open(args.pmc_json) as f:
-            pmc = json.load(f)
-        if pmc.get("config") == args.config and pmc.get("chunk_problems") == int(round(n / (chunks / args.steps))):
-            traffic = pmc.get("hbm_bytes_per_dispatch")
     step_s = elapsed / args.steps
     line = {
         "metric": METRIC,
@@ -241,42 +236,69 @@ def main():
         "config": {"workload": wl[2] % n, "catalogs_per_step_per_gpu": n,
                    "parallelism": "dp%d (host partition)" % world, "seed": args.seed,
                    "path": "host memory -> host memory (dp_submit/dp_job_wait), %d jobs in flight" % depth},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
-                     "kernel_ms_per_chunk": round(kernel_ms, 4),
-                     "algorithmic_bytes_per_chunk": int(alg_per_chunk),
-                     "chunks_per_step": round(chunks / args.steps, 2),
-                     "note": "per-chunk kernel time is measured while up to 4 chunks share the GPU"},
+        "pipeline": {"chunks_per_step": round(chunks / args.steps, 2),
+                     "kernel_ms_per_chunk": round(st["kernel_ms"] / chunks, 4),
+                     "note": "chunk kernels share the GPU with the other chunks in flight"},
         "pcie": {"h2d_GBs": round(st["h2d_bytes"] / (elapsed if world == 1 else step_s * args.steps) / 1e9, 2),
                  "d2h_GBs": round(st["d2h_bytes"] / (elapsed if world == 1 else step_s * args.steps) / 1e9, 2),
                  "h2d_bytes_per_step": st["h2d_bytes"] // args.steps, "peak_GBs": PCIE_PEAK_GBS},
         "host_ms_per_step": {k: round(st[k] / args.steps, 4) for k in ("stage_ms", "plan_ms", "wait_ms", "scatter_ms")},
-        "classes": class_mix(res),
+        "classes": class_mix(res) if res is not None else None,
         "deterministic": bool(deterministic),
         "host_lowering_res_per_s": round(n / t_lower, 1),
         "host_lowering_note": "dp_lower_into (16-bit records, storage reused) on the host pool; not in value",
     }
 
     if args.kernel_steps > 0:
-        # secondary: the batch resident in HBM, relaunched (kernel-only rate)
+        # the solve kernel alone, records resident in HBM (dp_upload): serial
+        # launches give the per-launch device time the roofline uses (HIP
+        # events on the launch's stream; rocprofv3 --kernel-trace of
+        # `bench.py --kernel-only` reports the same kernels), then 4 batches
+        # in flight give the rate the kernel sustains
         slots = [ctx.upload(lw.rec_off, lw.rec) for _ in range(4)]
-        for s in slots:
-            s.run()
+        slots[0].run()
+        kms = []
+        for _ in range(args.kernel_steps):
+            slots[0].run()
+            kms.append(ctx.last_kernel_ms())
+        for s_ in slots:
+            s_.run()
         t0 = time.perf_counter()
         for i in range(args.kernel_steps):
-            s = slots[i % 4]
+            s_ = slots[i % 4]
             if i >= 4:
-                s.wait()
-            s.launch()
-        for s in slots:
-            s.wait()
+                s_.wait()
+            s_.launch()
+        for s_ in slots:
+            s_.wait()
         tk = time.perf_counter() - t0
         kres = slots[0].download()
-        for s in slots:
-            s.free()
+        for s_ in slots:
+            s_.free()
+        if res is None:
+            res = kres
+            line["classes"] = class_mix(res)
+        rec_bytes, _ = _lib.device_bytes(lw.rec_off, lw.rec)
+        alg = rec_bytes + output_bytes(kres)
+        k_ms = float(np.mean(kms))
+        achieved = alg / (k_ms * 1e-3) / 1e9
         line["kernel_only"] = {"res_per_s": round(n * args.kernel_steps / tk, 1),
                                "ms_per_step": round(tk / args.kernel_steps * 1e3, 4),
-                               "identical_to_host_path": bool(same_results(kres, res))}
+                               "serial_launch_ms": round(k_ms, 4),
+                               "identical_to_host_path": bool(same_results(kres, res)) if res is not None else None,
+                               "note": "records resident in HBM, 4 batches in flight; not value"}
+        traffic = None
+        if args.pmc_json and os.path.exists(args.pmc_json):
+            with open(args.pmc_json) as f:
+                for ln in f:
+                    pmc = json.loads(ln)
+                    if pmc.get("config") == args.config and pmc.get("problems") == n:
+                        traffic = pmc.get("hbm_bytes_per_dispatch")
+        line["roofline"] = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
+                            "kernel": "solve_kernel (one launch of the batch, serial, records in HBM)",
+                            "kernel_ms": round(k_ms, 4), "algorithmic_bytes_per_launch": int(alg),
+                            "traffic_over_algorithmic": round(traffic / alg, 3) if traffic else None}
 
     if rank == 0 and not args.no_cpu:
         from oracle import oracle  # CPU baseline + checker only
