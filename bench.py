@@ -261,17 +261,19 @@ def main():
         for _ in range(args.kernel_steps):
             slots[0].run()
             kms.append(ctx.last_kernel_ms())
-        for s_ in slots:
-            s_.run()
-        t0 = time.perf_counter()
-        for i in range(args.kernel_steps):
-            s_ = slots[i % 4]
-            if i >= 4:
+        tk = float("nan")
+        if not args.kernel_only:  # (profiling runs keep every launch serial)
+            for s_ in slots:
+                s_.run()
+            t0 = time.perf_counter()
+            for i in range(args.kernel_steps):
+                s_ = slots[i % 4]
+                if i >= 4:
+                    s_.wait()
+                s_.launch()
+            for s_ in slots:
                 s_.wait()
-            s_.launch()
-        for s_ in slots:
-            s_.wait()
-        tk = time.perf_counter() - t0
+            tk = time.perf_counter() - t0
         kres = slots[0].download()
         for s_ in slots:
             s_.free()

@@ -5,7 +5,7 @@ reads on gfx950, so it is doubled; WRITE_SIZE is taken as reported (KiB).
 
 usage: python scripts/pmc_traffic.py <fetch_dir> <write_dir> <runs> <config> <bench_json>
 
-<runs> = solve runs of the profiled bench.py --kernel-only command (2K + 5 for
+<runs> = solve runs of the profiled bench.py --kernel-only command (K + 1 for
 K kernel steps); a run is one launch of each of the batch's footprint
 buckets, so the figure is per run of the whole batch.  <bench_json>: the
 bench line of the same command (config, problems, algorithmic bytes).
