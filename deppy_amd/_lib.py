@@ -37,7 +37,7 @@ EXPORTS = [
     "dp_last_error", "dp_last_global_error", "dp_num_devices", "dp_solve", "dp_upload", "dp_run",
     "dp_launch", "dp_wait", "dp_download", "dp_resident_free", "dp_last_kernel_ms", "dp_gen_catalogs", "dp_gen_wire",
     "dp_gen_free", "dp_upload_traced", "dp_download_trace", "dp_solve_traced", "dp_lowered_errors",
-    "dp_device_bytes", "dp_lower_into", "dp_lowered_new", "dp_lowered_exact_count", "dp_submit", "dp_job_wait", "dp_get_stats", "dp_stage_roundtrip",
+    "dp_device_bytes", "dp_lower_into", "dp_lowered_new", "dp_lowered_exact_count", "dp_lowered_pinned", "dp_submit", "dp_job_wait", "dp_get_stats", "dp_stage_roundtrip",
     "dp_stitch_selftest", "dp_partition",
 ]
 
@@ -68,7 +68,7 @@ class Stats(ctypes.Structure):
     _fields_ = [("problems", ctypes.c_int64), ("chunks", ctypes.c_int64), ("launches", ctypes.c_int64),
                 ("kernel_ms", ctypes.c_double), ("h2d_bytes", ctypes.c_int64), ("d2h_bytes", ctypes.c_int64),
                 ("rec_bytes", ctypes.c_int64), ("stage_ms", ctypes.c_double), ("plan_ms", ctypes.c_double), ("wait_ms", ctypes.c_double),
-                ("scatter_ms", ctypes.c_double)]
+                ("scatter_ms", ctypes.c_double), ("direct_chunks", ctypes.c_int64)]
 
 
 class Batch(ctypes.Structure):
@@ -100,6 +100,8 @@ def lib():
     L.dp_lowered_new.restype = vp
     L.dp_lowered_exact_count.argtypes = [vp]
     L.dp_lowered_exact_count.restype = ctypes.c_int64
+    L.dp_lowered_pinned.argtypes = [vp]
+    L.dp_lowered_pinned.restype = ctypes.c_int32
     L.dp_lowered_num_problems.argtypes = [vp]
     for f in ("dp_lowered_rec_off", "dp_lowered_ident_off"):
         getattr(L, f).argtypes = [vp]
@@ -240,16 +242,20 @@ class Lowered:
     relower(wire) lowers another batch into the same storage
     (dp_lower_into), invalidating the previous views' contents."""
 
-    def __init__(self, wire: WireArrays, narrow: bool = False):
-        """narrow: records that fit 16 bits in the DP_FMT_U16 form (the staged
-        form, DP_LOWER_NARROW); default int32 records."""
+    def __init__(self, wire: WireArrays, narrow: bool = False, pinned: bool = False):
+        """narrow: records that fit 16 bits in the DP_FMT_U16 form, each on a
+        16-byte boundary (the staged form, DP_LOWER_NARROW); default int32
+        records.  pinned: the records in page-locked memory when a GPU is
+        present (DP_LOWER_PINNED; with narrow, dp_submit copies them to the
+        device without staging)."""
         L = lib()
         h = ctypes.c_void_p()
         ws = wire.struct()
         self.narrow = narrow
-        if narrow:
+        self._flags = (1 if narrow else 0) | (2 if pinned else 0)
+        if self._flags:
             h = ctypes.c_void_p(L.dp_lowered_new())
-            if L.dp_lower_into(ctypes.byref(ws), 1, h) != 0:
+            if L.dp_lower_into(ctypes.byref(ws), self._flags, h) != 0:
                 L.dp_lowered_free(h)
                 raise ValueError(L.dp_last_global_error().decode())
         elif L.dp_lower(ctypes.byref(ws), ctypes.byref(h)) != 0:
@@ -259,7 +265,7 @@ class Lowered:
 
     def relower(self, wire: WireArrays) -> "Lowered":
         ws = wire.struct()
-        if lib().dp_lower_into(ctypes.byref(ws), 1 if self.narrow else 0, self._owner.h) != 0:
+        if lib().dp_lower_into(ctypes.byref(ws), self._flags, self._owner.h) != 0:
             raise ValueError(lib().dp_last_global_error().decode())
         self._fetch()
         return self
@@ -269,6 +275,7 @@ class Lowered:
         P = L.dp_lowered_num_problems(h)
         self.n = P
         self.n_exact = int(L.dp_lowered_exact_count(h))
+        self.pinned = bool(L.dp_lowered_pinned(h))
         self.rec_off = _view(o, L.dp_lowered_rec_off(h), P + 1, ctypes.c_int64, np.int64)
         self.rec = _view(o, L.dp_lowered_rec(h), int(self.rec_off[-1]), ctypes.c_int32, np.int32)
         self.ident_off = _view(o, L.dp_lowered_ident_off(h), P + 1, ctypes.c_int64, np.int64)

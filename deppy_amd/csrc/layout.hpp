@@ -97,19 +97,25 @@ __host__ __device__ inline dp_rec_layout rec_layout(const int32_t* h) {
 // every word after it becomes a uint16), so PCIe and the LDS-DMA of init move
 // half the bytes and the kernel has nothing to convert.
 //
-// The kernel extends the record during init (Group::build_watches) with
+// The record is extended by
 //   w_off[2nv+1], w[ncl+nkl]  watch lists: rows to evaluate when literal l
 //                             becomes true (clauses holding ~l; AtMost rows
 //                             holding var(l) when l is positive, one entry
 //                             per distinct variable)
-// right after the record in LDS (M_LDS) or in the problem's HBM scratch (the
-// multi-wave modes).  Rows that can fire on the empty assignment (clauses of
-// length <= 1, AtMost rows in which some variable's multiplicity exceeds the
-// bound) are found by a sweep of the row offsets (Group::base_propagate).
+// right after it: built by the kernel in LDS during init for one-wavefront
+// problems (Group::build_watches), and by the host while staging for the
+// multi-wave ones, whose staged image is read in place from HBM
+// (runtime.cpp stage_one).  Rows that can fire on the empty assignment
+// (clauses of length <= 1, AtMost rows in which some variable's multiplicity
+// exceeds the bound) are found by a sweep of the row offsets
+// (Group::base_propagate).
 
-// Staged-copy format of a record the host rejected while narrowing it (the
-// kernel reports it as malformed without reading its body).
-enum { DP_FMT_REJECT = 2 };
+// Staged-copy formats besides the public ones: a record the host rejected
+// while staging it (the kernel reports it as malformed without reading its
+// body), and the 16-bit form of a record the host checked while narrowing it
+// (the kernel validates only the DP_FMT_U16 copies the host passed through
+// unread, Group::valid_record).
+enum { DP_FMT_REJECT = 2, DP_FMT_U16_CHECKED = 3 };
 
 struct ImgLayout {
   int32_t w_off, w, words;
@@ -125,11 +131,12 @@ __host__ __device__ inline ImgLayout img_layout(const int32_t* h) {
   return X;
 }
 
-// Words of the staged (device) copy of a record: 16-byte aligned, the body in
-// 16-bit form when narrow.
+// Words of the staged (device) copy of a record: 16-byte aligned; the body in
+// 16-bit form when narrow (one-wavefront problems), else int32 followed by the
+// host-built watch lists.
 __host__ __device__ inline int64_t staged_words(const int32_t* h, bool narrow) {
   const int64_t body = (int64_t)h[DP_H_WORDS] - DP_H_SIZE;
-  const int64_t w = DP_H_SIZE + (narrow ? (body + 1) / 2 : body);
+  const int64_t w = narrow ? DP_H_SIZE + (body + 1) / 2 : (int64_t)img_layout(h).words;
   return (w + 3) & ~3LL;
 }
 
@@ -137,10 +144,8 @@ __host__ __device__ inline int64_t staged_words(const int32_t* h, bool narrow) {
 // allocation when the mode places that array in LDS (in_lds below), else into
 // the problem's HBM scratch region.
 struct Layout {
-  int32_t body;      // M_LDS only: the extended record (header dropped), one IX per word
-  int32_t wx;        // multi-wave modes only: w_off[2nv+1] then w[ncl+nkl], int32 (HBM)
-  int32_t cnt;       // multi-wave modes only: int32[2nv+1] watch-list build counters (HBM);
-                     // M_LDS aliases them on the per-literal arrays (reason..touched)
+  int32_t body;      // M_LDS only: the extended record (header dropped), one IX per word;
+                     // the watch-list build counts on the per-literal arrays (reason..touched)
   int32_t val;       // int8[nv]: 0 unassigned, 1 true, -1 false                  [LDS unless M_HBM]
   int32_t reason;    // IX[nv] implying row; R_DEC / R_EXTRA / a Solve() decision (-3 - index)
   int32_t rs;        // IX[nv] trail position where the assigning round started
@@ -194,8 +199,6 @@ __host__ __device__ inline Layout layout(const int32_t* h) {
   L.lcap = nv + 64;
   const ImgLayout X = img_layout(h);
   L.body = MODE == M_LDS ? take((X.words - DP_H_SIZE + 8) * ix, COLD) : 0;  // +8: dwordx4 copy slack
-  L.wx = MODE == M_LDS ? 0 : take((X.words - h[DP_H_WORDS]) * 4, COLD);
-  L.cnt = MODE == M_LDS ? 0 : take((2 * nv + 1) * 4, COLD);
   L.scal = take(mode_nscal(MODE) * 4, WORK);
   L.wbuf = take(mode_wbuf(MODE) * ix, WORK);
   L.cardq = take(mode_cq(MODE) * ix, WORK);

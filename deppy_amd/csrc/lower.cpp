@@ -9,6 +9,8 @@
 // gini's logic.C is still built, only to decide which constraints share one
 // assumed literal (the reference's constraints[m] map, lit_mapping.go:69-72).
 #include <algorithm>
+#include <cstdlib>
+#include <new>
 #include <atomic>
 #include <cstring>
 #include <mutex>
@@ -19,6 +21,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "hostmem.hpp"
 #include "pool.hpp"
 
 namespace dp {
@@ -343,18 +346,28 @@ struct Lowerer {
   Lowerer(const dp_wire& wire, bool narrow16) : w(wire), narrow(narrow16) {}
 
   // The last record appended to O (int32 words from `base`) in the 16-bit
-  // form, in place (word j -> halfword j never overtakes word j).
+  // form, in place (word j -> halfword j never overtakes word j).  Every
+  // record of a DP_LOWER_NARROW batch then ends on a 16-byte boundary, so
+  // each one's 16-bit form is the staged form as it is (runtime.cpp
+  // start_chunk copies such batches to the device without staging them).
   void narrow_last(Out& O, size_t base) const {
+    if (!narrow || O.nrec == base) return;
     int32_t* r = O.rec.data() + base;
-    if (!narrow || !dp_rec_fits16(r)) return;
     const int64_t words = r[DP_H_WORDS];
-    uint16_t* u = reinterpret_cast<uint16_t*>(r + DP_H_SIZE);
-    for (int64_t j = 0; j < words - DP_H_SIZE; ++j) u[j] = (uint16_t)r[DP_H_SIZE + j];
-    if ((words - DP_H_SIZE) & 1) u[words - DP_H_SIZE] = 0;
-    r[DP_H_FMT] = DP_FMT_U16;
-    const int64_t phys = dp_rec_phys_words(r);
-    O.nrec = base + (size_t)phys;
-    O.rec_len.back() = phys;
+    int64_t phys = words;
+    if (dp_rec_fits16(r)) {
+      uint16_t* u = reinterpret_cast<uint16_t*>(r + DP_H_SIZE);
+      for (int64_t j = 0; j < words - DP_H_SIZE; ++j) u[j] = (uint16_t)r[DP_H_SIZE + j];
+      if ((words - DP_H_SIZE) & 1) u[words - DP_H_SIZE] = 0;
+      r[DP_H_FMT] = DP_FMT_U16;
+      phys = dp_rec_phys_words(r);
+    }
+    const int64_t padded = (phys + 3) & ~3LL;
+    O.nrec = base + (size_t)std::min(words, padded);
+    if (padded > words) O.extend((size_t)(padded - words));  // (may move the storage)
+    r = O.rec.data() + base;
+    for (int64_t j = phys; j < padded; ++j) r[j] = 0;
+    O.rec_len.back() = padded;
   }
 
   std::string_view str(int64_t i) const {
@@ -820,10 +833,41 @@ struct Lowerer {
 }  // namespace
 }  // namespace dp
 
+// The records of a dp_lowered: grown, never shrunk, contents not preserved
+// across a resize (every call rewrites them); page-locked when asked and a
+// HIP device is present (dp_submit then copies them to the device as they
+// are), else ordinary 64-byte aligned memory.
+struct RecStore {
+  int32_t* p = nullptr;
+  size_t n = 0, cap = 0;
+  bool pinned = false;
+  void resize(size_t m, bool want_pinned) {
+    if (m > cap || want_pinned != pinned) {
+      release();
+      const size_t c = std::max<size_t>(m + m / 8, 1024);
+      void* q = want_pinned ? dp::pinned_alloc(4 * c) : nullptr;
+      pinned = q != nullptr;
+      if (!q) q = std::aligned_alloc(64, (4 * c + 63) & ~(size_t)63);
+      if (!q) throw std::bad_alloc();
+      p = static_cast<int32_t*>(q);
+      cap = c;
+    }
+    n = m;
+  }
+  void release() {
+    if (p) pinned ? dp::pinned_free(p) : std::free(p);
+    p = nullptr;
+    cap = n = 0;
+    pinned = false;
+  }
+  ~RecStore() { release(); }
+};
+
 struct dp_lowered {
   int32_t n = 0;
   std::vector<int64_t> rec_off, ident_off;
-  std::vector<int32_t> rec, ivar, icon, err;
+  RecStore rec;
+  std::vector<int32_t> ivar, icon, err;
   std::vector<std::string> msg;
   // scratch kept across dp_lower_into calls (once grown, no allocation or
   // page fault per call): per pool thread, and chunk c's slices of outs[t]
@@ -967,7 +1011,7 @@ int dp_lower_into(const dp_wire* wire, int32_t flags, dp_lowered* lw) {
     ai[(size_t)c + 1] = ai[(size_t)c] + (pc.i1 - pc.i0);
     ap[(size_t)c + 1] = ap[(size_t)c] + (pc.q1 - pc.q0);
   }
-  lw->rec.resize(ar.back());
+  lw->rec.resize(ar.back(), (flags & DP_LOWER_PINNED) != 0);
   lw->ivar.resize(ai.back());
   lw->icon.resize(ai.back());
   lw->rec_off.resize((size_t)P + 1);
@@ -978,7 +1022,7 @@ int dp_lower_into(const dp_wire* wire, int32_t flags, dp_lowered* lw) {
   auto merge = [&](int64_t c) {
     const auto& pc = lw->pieces[(size_t)c];
     dp::Out& o = lw->outs[(size_t)pc.t];
-    std::copy(o.rec.begin() + (int64_t)pc.r0, o.rec.begin() + (int64_t)pc.r1, lw->rec.begin() + (int64_t)ar[(size_t)c]);
+    std::copy(o.rec.begin() + (int64_t)pc.r0, o.rec.begin() + (int64_t)pc.r1, lw->rec.p + ar[(size_t)c]);
     std::copy(o.ivar.begin() + (int64_t)pc.i0, o.ivar.begin() + (int64_t)pc.i1, lw->ivar.begin() + (int64_t)ai[(size_t)c]);
     std::copy(o.icon.begin() + (int64_t)pc.i0, o.icon.begin() + (int64_t)pc.i1, lw->icon.begin() + (int64_t)ai[(size_t)c]);
     int64_t r = (int64_t)ar[(size_t)c], d = (int64_t)ai[(size_t)c];
@@ -1005,7 +1049,8 @@ dp_lowered* dp_lowered_new(void) { return new dp_lowered; }
 int32_t dp_lowered_num_problems(const dp_lowered* lw) { return lw->n; }
 int64_t dp_lowered_exact_count(const dp_lowered* lw) { return lw->n_exact.load(); }
 const int64_t* dp_lowered_rec_off(const dp_lowered* lw) { return lw->rec_off.data(); }
-const int32_t* dp_lowered_rec(const dp_lowered* lw) { return lw->rec.data(); }
+const int32_t* dp_lowered_rec(const dp_lowered* lw) { return lw->rec.p; }
+int32_t dp_lowered_pinned(const dp_lowered* lw) { return lw->rec.pinned ? 1 : 0; }
 const int64_t* dp_lowered_ident_off(const dp_lowered* lw) { return lw->ident_off.data(); }
 const int32_t* dp_lowered_ident_var(const dp_lowered* lw) { return lw->ivar.data(); }
 const int32_t* dp_lowered_ident_con(const dp_lowered* lw) { return lw->icon.data(); }

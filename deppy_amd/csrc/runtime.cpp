@@ -42,6 +42,7 @@
 #include "common.hpp"
 #include "kernel_api.hpp"
 #include "layout.hpp"
+#include "hostmem.hpp"
 #include "pool.hpp"
 
 namespace {
@@ -136,6 +137,14 @@ struct Plan {
   std::vector<int64_t> inst_off;  // [n+1] local installed-word offsets
   int64_t core_cap = 0;           // sum of identity counts (pool capacity)
   int64_t rec_bytes = 0;          // staged record bytes
+  // Device image: word offset of each problem's record, and the image's
+  // length (img_off and its total unless start_chunk copies records as they
+  // lie, see there)
+  std::vector<int64_t> dev_off;
+  int64_t img_words = 0;
+  std::vector<uint8_t> direct;    // [n] the source record is its own staged form
+  int32_t n_direct = 0;
+  int64_t other_words = 0;        // source words of the other problems
 };
 
 // rec + rec_off[p0 + i] is local problem i.  Problems whose header is not
@@ -145,11 +154,12 @@ struct Plan {
 // chunk sit a record apart and every one is a cache miss).
 struct Head {
   int8_t place;  // -1 malformed, -2 too large, else the Mode
+  bool direct;   // the record is its own staged form (16-bit, 16-byte aligned)
   int32_t lds, inst_words, nid;
   int64_t sw, rec_bytes;
 };
 
-void read_head(Head& H, const int32_t* h, int64_t avail, int32_t opt_flags) {
+void read_head(Head& H, const int32_t* h, int64_t avail, int32_t opt_flags, bool aligned) {
   H = Head{};
   if (!header_ok(h, avail)) { H.place = -1; return; }
   H.inst_words = bits_words(h[DP_H_NV]);
@@ -160,6 +170,7 @@ void read_head(Head& H, const int32_t* h, int64_t avail, int32_t opt_flags) {
   if (nar) {
     H.place = M_LDS;
     H.lds = layout<M_LDS>(h).lds_bytes;
+    H.direct = aligned && h[DP_H_FMT] == DP_FMT_U16;
     return;
   }
   const bool forced = forced_of(opt_flags);
@@ -185,14 +196,23 @@ void plan_chunk(Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0,
   P.inst_off.assign((size_t)n + 1, 0);
   std::vector<Head> head((size_t)n);
   auto rd = [&](int64_t i) {
-    read_head(head[(size_t)i], rec + rec_off[p0 + i], rec_off[p0 + i + 1] - rec_off[p0 + i], opt_flags);
+    read_head(head[(size_t)i], rec + rec_off[p0 + i], rec_off[p0 + i + 1] - rec_off[p0 + i], opt_flags,
+              (rec_off[p0 + i] & 3) == 0);
   };
   if (pool && n > 256) pool->run(n, std::function<void(int64_t)>(rd), 64);
   else for (int32_t i = 0; i < n; ++i) rd(i);
   std::vector<std::vector<int32_t>> bucket(kNBuckets), big(4);
   std::vector<int> lds((size_t)n, 0);
+  const bool rec_aligned = ((uintptr_t)rec & 15) == 0;
+  P.direct.assign((size_t)n, 0);
   for (int32_t i = 0; i < n; ++i) {
     const Head& H = head[(size_t)i];
+    if (rec_aligned && H.direct) {
+      P.direct[(size_t)i] = 1;
+      P.n_direct++;
+    } else {
+      P.other_words += rec_off[p0 + i + 1] - rec_off[p0 + i];
+    }
     if (H.place == -1) {
       if (bad) (*bad)[(size_t)i] = 1;
       P.skip.push_back(i);
@@ -218,6 +238,8 @@ void plan_chunk(Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0,
     }
   }
   for (int32_t i = 0; i < n; ++i) P.inst_off[(size_t)i + 1] += P.inst_off[(size_t)i];
+  P.dev_off.assign(P.img_off.begin(), P.img_off.end() - 1);
+  P.img_words = P.img_off[(size_t)n];
   // Within a launch, workgroups are dispatched in blockIdx order: largest
   // record first (longest-processing-time-first), so the long solves do not
   // form the launch's tail.
@@ -372,18 +394,48 @@ static bool stage_narrow(const int32_t* src, uint16_t* o) {
   return avx2 ? stage_narrow_avx2(src, o) : stage_narrow_generic(src, o);
 }
 
+// The watch lists of a multi-wave problem (layout.hpp img_layout), right
+// after its int32 record r: rows in ascending order in every list.  Returns
+// the extended length in words.
+int64_t build_watches_host(int32_t* r) {
+  const dp_rec_layout R = dp_rec_layout_of(r);
+  const ImgLayout X = img_layout(r);
+  const int32_t nv = r[DP_H_NV], nc = r[DP_H_NC], nk = r[DP_H_NK];
+  const int32_t* clause_off = r + R.clause_off;
+  const int32_t* clause_lits = r + R.clause_lits;
+  const int32_t* card_off = r + R.card_off;
+  const int32_t* card_lits = r + R.card_lits;
+  int32_t* wo = r + X.w_off;
+  int32_t* w = r + X.w;
+  std::fill(wo, wo + 2 * (int64_t)nv + 1, 0);
+  for (int32_t j = 0; j < r[DP_H_NCL]; ++j) wo[(clause_lits[j] ^ 1) + 1]++;
+  for (int32_t k = 0; k < nk; ++k)
+    for (int32_t j = card_off[k]; j < card_off[k + 1]; ++j)
+      if (j == card_off[k] || card_lits[j] != card_lits[j - 1]) wo[2 * card_lits[j] + 1]++;
+  for (int64_t l = 0; l < 2 * (int64_t)nv; ++l) wo[l + 1] += wo[l];
+  static thread_local std::vector<int32_t> cur;
+  cur.assign(wo, wo + 2 * (int64_t)nv);
+  for (int32_t rr = 0; rr < nc; ++rr)
+    for (int32_t j = clause_off[rr]; j < clause_off[rr + 1]; ++j) w[cur[(size_t)(clause_lits[j] ^ 1)]++] = rr;
+  for (int32_t k = 0; k < nk; ++k)
+    for (int32_t j = card_off[k]; j < card_off[k + 1]; ++j)
+      if (j == card_off[k] || card_lits[j] != card_lits[j - 1]) w[cur[(size_t)(2 * card_lits[j])]++] = nc + k;
+  return X.words;
+}
+
 // Stage local problem i of the plan into dst (the staged image area): the
 // int32 header with its format word, then the body in the form the plan
 // chose.  A 16-bit record to a 16-bit copy, or an int32 record to an int32
 // copy, is copied as it is; a 16-bit record for a multi-wave problem is
-// widened.  The kernel validates every staged body (valid_record); only the
-// narrowing of an int32 record is checked here, since truncation to 16 bits
-// would hide an out-of-range index.  Returns false for a malformed record:
+// widened.  Every body is checked once: a 16-bit record copied as it is by
+// the kernel (valid_record, DP_FMT_U16), any other here, while narrowing it
+// (DP_FMT_U16_CHECKED) or before building its watch lists.  Returns false for
+// a malformed record:
 // its staged copy is marked DP_FMT_REJECT and the kernel reports DP_ERROR /
 // DP_F_MALFORMED for it.
 bool stage_one(const Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0, int32_t i,
                int32_t* dst) {
-  const int64_t at = P.img_off[(size_t)i], sw = P.img_off[(size_t)i + 1] - at;
+  const int64_t at = P.dev_off[(size_t)i], sw = P.img_off[(size_t)i + 1] - P.img_off[(size_t)i];
   if (sw == 0) return true;  // skipped (header already rejected)
   const int32_t* src = rec + rec_off[p0 + i];
   int32_t* d = dst + at;
@@ -391,10 +443,10 @@ bool stage_one(const Plan& P, const int32_t* rec, const int64_t* rec_off, int32_
   const bool src16 = src[DP_H_FMT] == DP_FMT_U16;
   std::memcpy(d, src, 4 * DP_H_SIZE);
   if (P.narrow[(size_t)i]) {
-    d[DP_H_FMT] = DP_FMT_U16;
+    d[DP_H_FMT] = src16 ? DP_FMT_U16 : DP_FMT_U16_CHECKED;
     uint16_t* o = reinterpret_cast<uint16_t*>(d + DP_H_SIZE);
     if (src16) {
-      std::memcpy(o, src + DP_H_SIZE, 2 * (size_t)body);
+      std::memcpy(o, src + DP_H_SIZE, 2 * (size_t)body);  // validated by the kernel
     } else if (!stage_narrow(src, o)) {
       d[DP_H_FMT] = DP_FMT_REJECT;
       return false;
@@ -408,16 +460,46 @@ bool stage_one(const Plan& P, const int32_t* rec, const int64_t* rec_off, int32_
     } else {
       std::memcpy(d + DP_H_SIZE, src + DP_H_SIZE, 4 * (size_t)body);
     }
-    for (int64_t j = words; j < sw; ++j) d[j] = 0;
+    // the watch lists are built here, from the checked int32 copy
+    if (dp_rec_validate(d, words) != 0) {
+      d[DP_H_FMT] = DP_FMT_REJECT;
+      return false;
+    }
+    const int64_t end = build_watches_host(d);
+    for (int64_t j = end; j < sw; ++j) d[j] = 0;
   }
   return true;
 }
+
+void* pinned_alloc(size_t bytes) {
+  int n = 0;
+  void* p = nullptr;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0 || hipHostMalloc(&p, bytes, hipHostMallocPortable) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return p;
+}
+void pinned_free(void* p) { (void)hipHostFree(p); }
 
 }  // namespace dp
 
 namespace {
 
 using dp::Plan;
+
+// Are the first and the last byte of [p, p + bytes) page-locked host memory?
+bool pinned_range(const void* p, size_t bytes) {
+  auto locked = [](const void* q) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    return a.type == hipMemoryTypeHost;
+  };
+  return bytes > 0 && locked(p) && locked(static_cast<const char*>(p) + bytes - 1);
+}
 
 // Byte layout of a chunk's input region (identical in pinned host memory and
 // on the device, so one copy moves it) and of its output region.
@@ -434,7 +516,7 @@ size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 InLayout in_layout(const Plan& P) {
   InLayout L;
   size_t o = 0;
-  L.img = o;         o = al(o + (size_t)P.img_off[(size_t)P.n] * 4);
+  L.img = o;         o = al(o + (size_t)P.img_words * 4);
   L.rec_off = o;     o = al(o + (size_t)P.n * 8);
   L.order = o;       o = al(o + P.order.size() * 4);
   L.inst_off = o;    o = al(o + ((size_t)P.n + 1) * 8);
@@ -463,7 +545,7 @@ OutLayout out_layout(const Plan& P) {
 // Fill the non-image parts of an input region.
 void fill_in_tables(const Plan& P, const InLayout& L, char* base) {
   int64_t* ro = reinterpret_cast<int64_t*>(base + L.rec_off);
-  for (int32_t i = 0; i < P.n; ++i) ro[i] = P.img_off[(size_t)i];
+  std::memcpy(ro, P.dev_off.data(), (size_t)P.n * 8);
   std::memcpy(base + L.order, P.order.data(), P.order.size() * 4);
   std::memcpy(base + L.inst_off, P.inst_off.data(), ((size_t)P.n + 1) * 8);
   if (!P.scratch_off.empty()) std::memcpy(base + L.scratch_off, P.scratch_off.data(), P.scratch_off.size() * 8);
@@ -584,6 +666,7 @@ struct dp_job {
   int32_t n = 0;
   const int32_t* rec = nullptr;
   const int64_t* rec_off = nullptr;
+  bool pinned = false;  // the records are page-locked (pinned_range)
   dp_result res{};
   int pending = 0;  // chunks in flight
   int rc = 0;
@@ -600,6 +683,7 @@ struct dp_ctx {
   dp::Pool* pool = nullptr;
   int next_lane = 0;  // pipeline cursor over (device, lane)
   bool zc_in = false, zc_out = true;  // zero-copy records / results (start_chunk)
+  bool direct = true;  // copy page-locked batches of staged-form records as they are
   int32_t chunk_problems = kChunkProblems;
   int64_t chunk_bytes = kChunkBytes;
   dp_stats st{};
@@ -688,6 +772,27 @@ int start_chunk(dp_ctx* ctx, Lane& L, dp_job* job, int32_t p0, int32_t n) {
   dp::plan_chunk(L.plan, job->rec, job->rec_off, p0, n, ctx->flags, &bad, ctx->pool);
   const double t_plan = now_ms();
   ctx->st.plan_ms += t_plan - t0;
+  // Direct: records already in their staged form (16-bit, on a 16-byte
+  // boundary; dp_lower_into DP_LOWER_NARROW) in page-locked memory are
+  // copied to the device from where they lie: the chunk's source range goes
+  // by one DMA to the front of the image, each such record at its own
+  // offset, and only the other problems' records are staged, after it.
+  // (Worth it while the others' source words, copied for nothing, are few.)
+  const int64_t W = job->rec_off[p0 + n] - job->rec_off[p0];
+  const bool direct = job->pinned && L.plan.n_direct > 0 && !ctx->zc_in && 4 * L.plan.other_words <= W;
+  if (direct) {
+    Plan& Q = L.plan;
+    int64_t o = W;
+    for (int32_t i = 0; i < n; ++i) {
+      if (Q.direct[(size_t)i]) {
+        Q.dev_off[(size_t)i] = job->rec_off[p0 + i] - job->rec_off[p0];
+      } else {
+        Q.dev_off[(size_t)i] = o;
+        o += Q.img_off[(size_t)i + 1] - Q.img_off[(size_t)i];
+      }
+    }
+    Q.img_words = o;
+  }
   const InLayout il = in_layout(L.plan);
   L.ol = out_layout(L.plan);
   HIP_OK(L.h_in.reserve(il.end));
@@ -695,15 +800,17 @@ int start_chunk(dp_ctx* ctx, Lane& L, dp_job* job, int32_t p0, int32_t n) {
   HIP_OK(L.h_out.reserve(L.ol.end));
   HIP_OK(L.d_out.reserve(L.ol.end));
   HIP_OK(L.scratch.reserve((size_t)std::max<int64_t>(L.plan.scratch_words, 1) * 4));
-  // stage the records (host pool), then the tables
-  int32_t* img = at<int32_t>(L.h_in.p, il.img);
   const Plan& P = L.plan;
-  ctx->pool->run(n, [&](int64_t i) {
-    if (!dp::stage_one(P, job->rec, job->rec_off, p0, (int32_t)i, img)) bad[(size_t)i] = 1;
-  }, 32);
-  // (records found malformed while staging are reported by the kernel)
+  if (!direct || P.n_direct < n) {  // stage the records (host pool)
+    int32_t* img = at<int32_t>(L.h_in.p, il.img);
+    ctx->pool->run(n, [&](int64_t i) {
+      if (direct && P.direct[(size_t)i]) return;
+      if (!dp::stage_one(P, job->rec, job->rec_off, p0, (int32_t)i, img)) bad[(size_t)i] = 1;
+    }, 32);
+    // (records found malformed while staging are reported by the kernel)
+  }
   fill_in_tables(P, il, L.h_in.p);
-  ctx->st.stage_ms += now_ms() - t0;
+  ctx->st.stage_ms += now_ms() - t_plan;
   // Zero-copy results: the kernels write their results straight into the
   // lane's mapped pinned buffer.  With a D2H copy per chunk instead, copies
   // from every stream queue on the same copy engine: a chunk's H2D waited
@@ -718,7 +825,18 @@ int start_chunk(dp_ctx* ctx, Lane& L, dp_job* job, int32_t p0, int32_t n) {
   L.zc_out = ctx->zc_out;
   char* din = zc_in ? L.h_in.dev : L.d_in.p;
   char* dout = L.zc_out ? L.h_out.dev : L.d_out.p;
-  if (!zc_in) HIP_OK(hipMemcpyAsync(L.d_in.p, L.h_in.p, il.end, hipMemcpyHostToDevice, L.s));
+  size_t h2d = 0;
+  if (direct) {
+    const size_t src_bytes = 4 * (size_t)W, rest = il.img + src_bytes;
+    if (src_bytes)
+      HIP_OK(hipMemcpyAsync(L.d_in.p + il.img, job->rec + job->rec_off[p0], src_bytes, hipMemcpyHostToDevice, L.s));
+    HIP_OK(hipMemcpyAsync(L.d_in.p + rest, L.h_in.p + rest, il.end - rest, hipMemcpyHostToDevice, L.s));
+    h2d = src_bytes + il.end - rest;
+    ctx->st.direct_chunks++;
+  } else if (!zc_in) {
+    HIP_OK(hipMemcpyAsync(L.d_in.p, L.h_in.p, il.end, hipMemcpyHostToDevice, L.s));
+    h2d = il.end;
+  }
   HIP_OK(hipMemsetAsync(L.d_out.p + L.ol.pool_len, 0, 4, L.s));
   dp::KernelArgs a = kernel_args(il, L.ol, din, dout, reinterpret_cast<int32_t*>(L.scratch.p), ctx->budget);
   a.core_pool_len = at<int32_t>(L.d_out.p, L.ol.pool_len);
@@ -733,7 +851,7 @@ int start_chunk(dp_ctx* ctx, Lane& L, dp_job* job, int32_t p0, int32_t n) {
   job->pending++;
   ctx->st.chunks++;
   ctx->st.problems += n;
-  ctx->st.h2d_bytes += zc_in ? 0 : (int64_t)il.end;
+  ctx->st.h2d_bytes += (int64_t)h2d;
   ctx->st.d2h_bytes += L.zc_out ? 0 : (int64_t)L.ol.d2h;
   ctx->st.rec_bytes += P.rec_bytes;
   return 0;
@@ -827,6 +945,7 @@ dp_ctx* dp_create(const dp_opts* opts) {
   ctx->chunk_bytes = std::max<int64_t>(1, env_i64("DEPPY_CHUNK_BYTES", kChunkBytes));
   ctx->zc_in = env_i64("DEPPY_ZC_IN", 0) != 0;   // diagnostic: 1 = kernels read staged records over PCIe
   ctx->zc_out = env_i64("DEPPY_ZC_OUT", 1) != 0; // diagnostic: 0 = D2H copy of every chunk
+  ctx->direct = env_i64("DEPPY_DIRECT", 1) != 0; // diagnostic: 0 = stage every chunk
   ctx->pool = new dp::Pool(dp::host_threads());
   return ctx;
 }
@@ -866,7 +985,7 @@ int dp_device_bytes(const dp_batch* b, int32_t opt_flags, int64_t* rec_bytes, in
   Plan P;
   dp::plan_chunk(P, b->rec, b->rec_off, 0, b->n_problems, opt_flags, nullptr);
   if (rec_bytes) *rec_bytes = P.rec_bytes;
-  if (img_bytes) *img_bytes = 4 * P.img_off[(size_t)P.n];
+  if (img_bytes) *img_bytes = 4 * P.img_words;
   return 0;
 }
 
@@ -880,6 +999,7 @@ int dp_submit(dp_ctx* ctx, const dp_batch* b, dp_result* res, dp_job** out) {
   job->n = b->n_problems;
   job->rec = b->rec;
   job->rec_off = b->rec_off;
+  job->pinned = ctx->direct && job->n > 0 && pinned_range(b->rec, 4 * (size_t)b->rec_off[job->n]);
   job->res = *res;
   if (submit_locked(ctx, job)) {
     (void)wait_job_locked(ctx, job);
@@ -1181,7 +1301,7 @@ int dp_stage_roundtrip(const dp_batch* b, int32_t opt_flags, int32_t chunk_probl
       const int64_t words = src[DP_H_WORDS];
       wide.resize((size_t)words);
       std::memcpy(wide.data(), st, 4 * DP_H_SIZE);
-      if (st[DP_H_FMT] == DP_FMT_U16) {
+      if (st[DP_H_FMT] == DP_FMT_U16 || st[DP_H_FMT] == dp::DP_FMT_U16_CHECKED) {
         const uint16_t* u = reinterpret_cast<const uint16_t*>(st + DP_H_SIZE);
         for (int64_t j = DP_H_SIZE; j < words; ++j) wide[(size_t)j] = u[j - DP_H_SIZE];
       } else {

@@ -201,6 +201,7 @@ struct Group {
   // cycles, learned-row cycles, watch entries visited, frontier literals of
   // flattened rounds, learned rows evaluated, AtMost rows flushed
   int64_t acc[16];
+  int64_t sub[3];           // init: record staging, validation, watch-list build cycles
   unsigned long long* dbg;  // [first code, value, bound, failures]
   __device__ __noinline__ int chk_fail(int x, int hi, int code) {
     if (dbg) {
@@ -320,6 +321,9 @@ struct Group {
 #pragma unroll
     for (int i = 0; i < DP_H_SIZE; ++i) h[i] = grec[i];
     if (h[DP_H_FMT] == DP_FMT_REJECT) return false;
+#ifdef DP_STAMPS
+    const int64_t ti0 = stamp();
+#endif
     const Layout L = layout<MODE>(h);
     const dp_rec_layout R = rec_layout(h);
     const ImgLayout X = img_layout(h);
@@ -335,7 +339,7 @@ struct Group {
       // records in 16-bit form (DP_FMT_U16): they are copied as they are.
       IX* b = reinterpret_cast<IX*>(lds + L.body);
       const int4* src = reinterpret_cast<const int4*>(grec + DP_H_SIZE);
-      if (h[DP_H_FMT] == DP_FMT_U16) {
+      if (h[DP_H_FMT] == DP_FMT_U16 || h[DP_H_FMT] == DP_FMT_U16_CHECKED) {
         const int groups = (h[DP_H_WORDS] - DP_H_SIZE + 7) >> 3;
         if (L.body == 0 && ((groups + 63) >> 6) * 1024 <= L.lds_bytes) {
           // LDS-DMA, every 1 KiB piece in flight at once (lanes past the
@@ -441,7 +445,16 @@ struct Group {
     for (int i = 0; i < 16; ++i) acc[i] = 0;
     dbg = nullptr;
 #endif
-    if (!valid_record()) return false;
+#ifdef DP_STAMPS
+    const int64_t ti1 = stamp();
+    sub[0] = ti1 - ti0;
+#endif
+    if constexpr (MODE == M_LDS)
+      if (h[DP_H_FMT] == DP_FMT_U16 && !valid_record()) return false;
+#ifdef DP_STAMPS
+    const int64_t ti2 = stamp();
+    sub[1] = ti2 - ti1;
+#endif
     // the watch lists follow the record (M_LDS) or live in the problem's
     // scratch; M_LDS counts on the per-literal arrays, initialised below
     if constexpr (MODE == M_LDS) {
@@ -449,10 +462,11 @@ struct Group {
                     reinterpret_cast<uint32_t*>(lds + L.reason));
       w_off = rv(X.w_off); w = rv(X.w);
     } else {
-      IX* wo = reinterpret_cast<IX*>(hbm + L.wx);
-      build_watches(wo, wo + 2 * nv + 1, reinterpret_cast<uint32_t*>(hbm + L.cnt));
-      w_off = wo; w = wo + 2 * nv + 1;
+      w_off = rv(X.w_off); w = rv(X.w);  // host-built, staged after the record
     }
+#ifdef DP_STAMPS
+    sub[2] = stamp() - ti2;
+#endif
 
     if constexpr (MODE == M_LDS) {
       for (int v = tid; v < nv; v += NT) val[v] = 0;
@@ -469,107 +483,122 @@ struct Group {
     return true;
   }
 
-  // dp_rec_validate on the device, before any data-dependent index (the host
-  // checked only the header, which bounds every array): offsets arrays start
-  // at 0, never decrease and end at their totals; every literal, variable and
-  // identity is in range; AtMost bounds are not negative; the positions of a
-  // variable in an AtMost row form one run.  Group-uniform result.
+  // dp_rec_validate on the device, for the records the host passed through
+  // without reading them (16-bit records copied as they are, DP_FMT_U16):
+  // offsets arrays start at 0, never decrease and end at their totals; every
+  // literal, variable and identity is in range; the positions of a variable
+  // in an AtMost row form one run (16-bit bounds cannot be negative).  The
+  // host checked every other staged form (DP_FMT_U16_CHECKED, DP_FMT_I32).
+  // Array by array, two 16-bit words per LDS load.  Group-uniform result.
   __device__ __forceinline__ bool valid_record() {
+    static_assert(MODE == M_LDS, "16-bit records run one wavefront per problem");
+    const IX* base = clause_off;  // the body's first array
+    const uint32_t* b32 = reinterpret_cast<const uint32_t*>(base);  // (16-byte aligned)
     bool bad = false;
-    auto offsets = [&](const IX* off, int n, int total) {
-      for (int i = tid; i <= n; i += NT) {
-        const int x = (int)off[i];
-        bad |= i == 0 ? x != 0 : x < (int)off[i - 1];
-        bad |= i == n && x != total;
+    auto range = [&](const IX* arr, int n, int hi) {
+      const int a = (int)(arr - base), e = a + n;
+      for (int q = (a >> 1) + tid; 2 * q < e; q += NT) {
+        const uint32_t x = b32[q];
+        bad |= (2 * q >= a && (int)(x & 0xffffu) >= hi) || (2 * q + 1 < e && (int)(x >> 16) >= hi);
       }
     };
-    auto range = [&](const IX* a, int n, int hi) {
-      for (int i = tid; i < n; i += NT) bad |= (uint32_t)(int)a[i] >= (uint32_t)hi;
+    auto offsets = [&](const IX* arr, int n, int total) {  // n + 1 words
+      const int a = (int)(arr - base), e = a + n + 1;
+      for (int q = (a >> 1) + tid; 2 * q < e; q += NT) {
+        const uint32_t x = b32[q];
+        const int i0 = 2 * q, x0 = (int)(x & 0xffffu), x1 = (int)(x >> 16);
+        const int prev = i0 > a ? (int)(b32[q - 1] >> 16) : 0;  // word i0 - 1
+        if (i0 >= a) bad |= i0 == a ? x0 != 0 : x0 < prev;
+        if (i0 + 1 < e) bad |= i0 + 1 == a ? x1 != 0 : x1 < x0;
+        bad |= (i0 == e - 1 && x0 != total) || (i0 + 1 == e - 1 && x1 != total);
+      }
     };
     offsets(clause_off, nc, ncl);
-    offsets(card_off, nk, nkl);
-    offsets(var_choice_off, nv, nch);
-    offsets(choice_off, nch, nchl);
     range(clause_lits, ncl, 2 * nv);
     range(clause_id, nc, nid);
+    offsets(card_off, nk, nkl);
     range(card_lits, nkl, nv);
     range(card_id, nk, nid);
-    range(choice_lits, nchl, nv);
-    range(anchors, na, nv);
+    offsets(var_choice_off, nv, nch);
+    offsets(choice_off, nch, nchl);
+    range(choice_lits, nchl + na, nv);  // choice_lits then anchors, both variables
     if (g_any(bad)) return false;  // the offsets below are now in range
     for (int k = tid; k < nk; k += NT) {
       const int a = card_off[k], b = card_off[k + 1];
-      bad |= (int)card_bound[k] < 0;
-      for (int j = a + 1; j < b; ++j)
-        if (card_lits[j] != card_lits[j - 1])
-          for (int i = a; i < j - 1; ++i) bad |= card_lits[i] == card_lits[j];
+      for (int j = a + 1; j < b; ++j) {
+        const int x = card_lits[j];
+        if (x != (int)card_lits[j - 1])
+          for (int i = a; i < j - 1; ++i) bad |= (int)card_lits[i] == x;
+      }
     }
     return !g_any(bad);
   }
 
-  // Watch lists of the record, built on the device (the host ships the record
-  // alone): per-literal counts, an inclusive scan into w_off, then a fill
-  // through per-literal cursors.  cnt[l + 1] counts the rows literal l wakes:
-  // the clauses holding ~l, and (l positive) the AtMost rows holding var(l),
-  // once per distinct variable.  Row order within a list is left to the
-  // atomics: every outcome of a round is a minimum over rows (reasons,
-  // conflicts, Solve()'s first violated row), so nothing depends on it.
-  __device__ __forceinline__ uint32_t ld_cnt(const uint32_t* p) const {
-    if constexpr (MODE == M_LDS) return *p;
-    else return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  // Watch lists of a one-wavefront problem, built in LDS from its record
+  // (the host ships the record alone): per-literal counts, an inclusive scan
+  // into w_off, then a fill through per-literal cursors.  cnt[l + 1] counts
+  // the rows literal l wakes: the clauses holding ~l, and (l positive) the
+  // AtMost rows holding var(l), once per distinct variable.  Row order within
+  // a list is left to the atomics: every outcome of a round is a minimum over
+  // rows (reasons, conflicts, Solve()'s first violated row), so nothing
+  // depends on it.  Rows are handled a lane each with their literals loaded 8
+  // at a time (independent loads and atomics, not a dependent chain).
+  // (Multi-wave problems get host-built lists in their staged image: at
+  // OLM scale the counters live in HBM and the in-kernel build was
+  // latency-bound, 4.7M cycles a catalog.)
   __device__ __forceinline__ void build_watches(IX* wo, IX* ww, uint32_t* cnt) {
+    static_assert(MODE == M_LDS, "the multi-wave modes read host-built watch lists");
     const int n2 = 2 * nv + 1;
     for (int i = tid; i < n2; i += NT) cnt[i] = 0u;
-    gsync();
-    for (int r = tid; r < nc; r += NT)
-      for (int j = clause_off[r]; j < (int)clause_off[r + 1]; ++j)
-        atomicAdd(&cnt[((int)clause_lits[j] ^ 1) + 1], 1u);
+    wsync();
+    for (int j = tid; j < ncl; j += NT) atomicAdd(&cnt[((int)clause_lits[j] ^ 1) + 1], 1u);
     for (int k = tid; k < nk; k += NT) {
       const int a = card_off[k], b = card_off[k + 1];
-      for (int j = a; j < b; ++j)
-        if (j == a || card_lits[j] != card_lits[j - 1]) atomicAdd(&cnt[2 * (int)card_lits[j] + 1], 1u);
-    }
-    gsync();
-    if constexpr (NW == 1) {
-      // lanes over 64 consecutive counters, DPP scan, carry across chunks
-      int carry = 0;
-      for (int b = 0; b < n2; b += 64) {
-        const int i = b + lane;
-        const int x = i < n2 ? (int)cnt[i] : 0;
-        const int incl = wave_incl_scan(x) + carry;
-        if (i < n2) { wo[i] = enc(incl); cnt[i] = (uint32_t)incl; }
-        carry = __builtin_amdgcn_readlane(incl, 63);
-      }
-    } else {
-      // one contiguous segment per thread, a group scan of segment sums
-      const int seg = (n2 + NT - 1) / NT;
-      const int s0 = min(tid * seg, n2), s1 = min(s0 + seg, n2);
-      int sum = 0;
-      for (int i = s0; i < s1; ++i) sum += (int)ld_cnt(&cnt[i]);
-      const int incl = wave_incl_scan(sum);
-      if (lane == 63) scal[S_SLOT + wid] = incl;
-      bar();
-      int run = incl - sum;
+      for (int j0 = a; j0 < b; j0 += 8) {
+        int v[9];
+        v[0] = j0 == a ? -1 : (int)card_lits[j0 - 1];
 #pragma unroll
-      for (int q = 0; q < NW; ++q) run += q < wid ? scal[S_SLOT + q] : 0;
-      bar();
-      for (int i = s0; i < s1; ++i) {
-        run += (int)ld_cnt(&cnt[i]);
-        wo[i] = enc(run);
-        cnt[i] = (uint32_t)run;
+        for (int i = 0; i < 8; ++i) v[i + 1] = j0 + i < b ? (int)card_lits[j0 + i] : -1;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (j0 + i < b && v[i + 1] != v[i]) atomicAdd(&cnt[2 * v[i + 1] + 1], 1u);
       }
     }
-    gsync();
-    for (int r = tid; r < nc; r += NT)
-      for (int j = clause_off[r]; j < (int)clause_off[r + 1]; ++j)
-        ww[atomicAdd(&cnt[(int)clause_lits[j] ^ 1], 1u)] = enc(r);
+    wsync();
+    // lanes over 64 consecutive counters, DPP scan, carry across chunks
+    int carry = 0;
+    for (int b = 0; b < n2; b += 64) {
+      const int i = b + lane;
+      const int x = i < n2 ? (int)cnt[i] : 0;
+      const int incl = wave_incl_scan(x) + carry;
+      if (i < n2) { wo[i] = enc(incl); cnt[i] = (uint32_t)incl; }
+      carry = __builtin_amdgcn_readlane(incl, 63);
+    }
+    wsync();
+    for (int r = tid; r < nc; r += NT) {
+      const int a = clause_off[r], b = clause_off[r + 1];
+      for (int j0 = a; j0 < b; j0 += 8) {
+        int l[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) l[i] = j0 + i < b ? (int)clause_lits[j0 + i] : -1;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (l[i] >= 0) ww[atomicAdd(&cnt[l[i] ^ 1], 1u)] = enc(r);
+      }
+    }
     for (int k = tid; k < nk; k += NT) {
       const int a = card_off[k], b = card_off[k + 1];
-      for (int j = a; j < b; ++j)
-        if (j == a || card_lits[j] != card_lits[j - 1]) ww[atomicAdd(&cnt[2 * (int)card_lits[j]], 1u)] = enc(nc + k);
+      for (int j0 = a; j0 < b; j0 += 8) {
+        int v[9];
+        v[0] = j0 == a ? -1 : (int)card_lits[j0 - 1];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i + 1] = j0 + i < b ? (int)card_lits[j0 + i] : -1;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (j0 + i < b && v[i + 1] != v[i]) ww[atomicAdd(&cnt[2 * v[i + 1]], 1u)] = enc(nc + k);
+      }
     }
-    gsync();
+    wsync();
   }
 
   // ------------------------------------------------------------------
@@ -1788,6 +1817,7 @@ solve_kernel(KernelArgs a) {
     o[10] = wall0;
     o[11] = wallclock();
     for (int i = 5; i < 16; ++i) o[11 + i] = W.acc[i];
+    for (int i = 0; i < 3; ++i) o[27 + i] = W.sub[i];
   }
 #endif
   if (W.tr_stop) flags |= DP_F_TRACE_TRUNCATED;

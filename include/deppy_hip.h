@@ -193,11 +193,17 @@ int dp_lower(const dp_wire* wire, dp_lowered** out);
 /* dp_lower into an existing result, reusing its storage (a serving loop
  * lowers batch after batch without allocating).  flags: DP_LOWER_NARROW emits
  * every record that fits 16 bits in the DP_FMT_U16 form (the staged form:
- * half the bytes to write, to stage and to cross PCIe).  Returns 0 or -1. */
-enum { DP_LOWER_NARROW = 1 };
+ * half the bytes to write, to stage and to cross PCIe) and starts every
+ * record on a 16-byte boundary (zero padding between records, counted in
+ * rec_off); DP_LOWER_PINNED keeps the records in page-locked host memory
+ * when a HIP device is present (dp_lowered_pinned).  A batch of both is
+ * copied to the device by DMA from where it lies: dp_submit stages only
+ * chunks that need another form.  Returns 0 or -1. */
+enum { DP_LOWER_NARROW = 1, DP_LOWER_PINNED = 2 };
 int dp_lower_into(const dp_wire* wire, int32_t flags, dp_lowered* lw);
 dp_lowered* dp_lowered_new(void); /* an empty result for dp_lower_into */
 void dp_lowered_free(dp_lowered* lw);
+int32_t dp_lowered_pinned(const dp_lowered* lw); /* 1: the records are page-locked */
 int32_t dp_lowered_num_problems(const dp_lowered* lw);
 /* Problems of the last lowering that went through the full And-inverter
  * graph instead of the canonical identity keys (measurement; lower.cpp). */
@@ -314,10 +320,13 @@ typedef struct dp_stats {
   int64_t h2d_bytes; /* bytes copied host -> device                          */
   int64_t d2h_bytes; /* bytes copied device -> host                          */
   int64_t rec_bytes; /* staged record bytes (16-bit form on the LDS path)    */
-  double stage_ms;   /* host: planning + staging records into pinned memory  */
-  double plan_ms;    /* host: of which planning the launches                  */
+  double stage_ms;   /* host: staging records into pinned memory and writing
+                        the chunk tables (after planning)                    */
+  double plan_ms;    /* host: planning the launches (header pass, buckets)   */
   double wait_ms;    /* host: blocked on a chunk's completion                 */
   double scatter_ms; /* host: results -> the caller's dp_result              */
+  int64_t direct_chunks; /* chunks copied from the caller's page-locked
+                            records without staging (DP_LOWER_PINNED)        */
 } dp_stats;
 int dp_get_stats(dp_ctx* ctx, dp_stats* out, int32_t reset);
 

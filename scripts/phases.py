@@ -18,7 +18,8 @@ NS = 32
 NAMES = ["init", "base", "search", "epilogue", "core", "round_eval", "round_finish", "rounds",
          "rounds_1lit", "push_guess"]
 EXTRA = {16: "search_solve", 17: "pop_guess", 18: "pushes", 19: "visit_1lit", 20: "visit_flat", 21: "flush_cards",
-         22: "learned", 23: "n_watch_1lit", 24: "n_front_flat", 25: "n_learned_rows", 26: "n_cards"}
+         22: "learned", 23: "n_watch_1lit", 24: "n_front_flat", 25: "n_learned_rows", 26: "n_cards",
+         27: "init_stage", 28: "init_validate", 29: "init_build"}
 L = _lib.lib()
 L.dp_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _lib.c_i64p]
 config = int(sys.argv[1]) if len(sys.argv) > 1 else 2

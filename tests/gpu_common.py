@@ -4,13 +4,39 @@ import numpy as np
 from deppy_amd import _lib
 
 
-def lowered_config(config, n, seed, narrow=False):
+def lowered_config(config, n, seed, narrow=False, pinned=False):
     """Synthetic catalogs (SURVEY §8(d) generator) lowered by dp_lower;
-    narrow: records that fit 16 bits in the DP_FMT_U16 form."""
+    narrow: records that fit 16 bits in the DP_FMT_U16 form; pinned: in
+    page-locked memory (with a GPU)."""
     w = _lib.generate(config, n, seed)
     return _lib.Lowered(_lib.WireArrays(**{k: w[k] for k in (
         "prob_var_off", "var_id", "var_con_off", "con_kind", "con_n", "con_arg_off", "con_arg",
-        "str_off")}, str_bytes=w["str_bytes"].tobytes()), narrow=narrow)
+        "str_off")}, str_bytes=w["str_bytes"].tobytes()), narrow=narrow, pinned=pinned)
+
+
+def corrupt16(rec_off, rec, p, kind):
+    """Make 16-bit record p malformed in place: 'lit' a clause literal past
+    2*nv, 'off' decreasing clause offsets, 'run' an AtMost row whose variable
+    positions are not one run (needs a row of >= 3 positions; returns False
+    when there is none)."""
+    r = rec[rec_off[p]:rec_off[p + 1]]
+    assert r[13] == 1
+    u = r[16:].view(np.uint16)
+    nv, nc, nk, ncl = int(r[1]), int(r[2]), int(r[3]), int(r[7])
+    if kind == "lit":
+        u[nc + 1] = 2 * nv + 3
+    elif kind == "off":
+        u[1] = int(u[2]) + 1
+    else:
+        co = nc + 1 + ncl + nc
+        cl = co + nk + 1
+        for k in range(nk):
+            a, b = int(u[co + k]), int(u[co + k + 1])
+            if b - a >= 3 and u[cl + a] != u[cl + a + 1]:
+                u[cl + a + 2] = u[cl + a]  # x y x: two runs of x
+                return True
+        return False
+    return True
 
 
 def widen(rec_off, rec):
@@ -18,11 +44,13 @@ def widen(rec_off, rec):
     parts, offs = [], [0]
     for p in range(len(rec_off) - 1):
         r = rec[rec_off[p]:rec_off[p + 1]]
-        if r[13] == 1:
+        if len(r) and r[13] == 1:
             words = int(r[10])
             body = r[16:].view(np.uint16)[:words - 16].astype(np.int32)
             r = np.concatenate([r[:16], body])
             r[13] = 0
+        elif len(r):
+            r = r[:int(r[10])]  # (DP_LOWER_NARROW pads records to 16 bytes)
         parts.append(np.asarray(r, np.int32))
         offs.append(offs[-1] + len(r))
     return np.array(offs, np.int64), (np.concatenate(parts) if parts else np.zeros(0, np.int32))

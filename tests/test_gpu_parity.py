@@ -12,7 +12,7 @@ import pytest
 from deppy_amd import _lib, sat
 from oracle import oracle
 from tests import fixtures
-from tests.gpu_common import compare_results, lowered_config
+from tests.gpu_common import compare_results, corrupt16, lowered_config
 from tests.test_lowering import V, sat_var
 
 pytestmark = pytest.mark.gpu
@@ -287,3 +287,55 @@ def test_malformed_records_are_per_problem_errors(flags):
     ok = [p for p in range(lw.n) if p not in bad]
     for k in ("status", "flags", "steps"):
         np.testing.assert_array_equal(g[k][ok], o[k][ok])
+
+
+@pytest.mark.parametrize("config,n,seed", [(2, 3000, 81), (3, 9000, 82), (5, 400, 83)])
+def test_pinned_records_copied_directly(config, n, seed, monkeypatch):
+    """A DP_LOWER_NARROW | DP_LOWER_PINNED batch goes to the device by DMA
+    from where it lies (no staging): every chunk of an all-16-bit batch is
+    direct, and the results equal the staged path's and the oracle's."""
+    monkeypatch.setenv("DEPPY_CHUNK_PROBLEMS", "700")
+    lw = lowered_config(config, n, seed, narrow=True, pinned=True)
+    assert lw.pinned and np.all(lw.rec_off % 4 == 0)
+    c = _lib.Context(0, 1)
+    try:
+        g = c.submit(lw.rec_off, lw.rec).wait()
+        st = c.stats(reset=True)
+        assert st["chunks"] == -(-n // 700)
+        if config != 5:  # every record on the one-wavefront path: no staging at all
+            assert st["direct_chunks"] == st["chunks"]
+        # (config 5: chunks whose multi-wave records are a small part of them
+        # go direct, those records staged after the copied range)
+        staged = c.submit(lw.rec_off, lw.rec.copy()).wait()  # pageable copy: staged
+        assert c.stats()["direct_chunks"] == 0
+    finally:
+        c.close()
+    assert compare_results(g, staged, n) == []
+    o = oracle.solve_batch(lw.rec_off, lw.rec, 0, 16)
+    assert compare_results(g, o, n) == []
+
+
+@pytest.mark.parametrize("pinned", [False, True], ids=["staged", "direct"])
+def test_malformed_16bit_records_found_by_the_kernel(pinned):
+    """16-bit records the host passes through unread are validated by the
+    kernel (Group::valid_record): each malformed one is DP_ERROR +
+    DP_F_MALFORMED, the rest of the batch is solved bit-exactly."""
+    lw = lowered_config(2, 60, 91, narrow=True, pinned=pinned)
+    ref = oracle.solve_batch(lw.rec_off, lw.rec, 0, 16)
+    rec = lw.rec if pinned else lw.rec.copy()
+    bad = []
+    for p, kind in ((4, "lit"), (19, "off"), (33, "run"), (47, "run")):
+        if corrupt16(lw.rec_off, rec, p, kind):
+            bad.append(p)
+    assert len(bad) >= 3
+    c = _lib.Context(0, 1)
+    try:
+        g = c.solve(lw.rec_off, rec)
+        assert (c.stats()["direct_chunks"] > 0) == pinned
+    finally:
+        c.close()
+    ok = [p for p in range(lw.n) if p not in bad]
+    for p in bad:
+        assert g["status"][p] == -2 and g["flags"][p] == 512 and g["core_len"][p] == 0, p
+    for k in ("status", "flags", "steps"):
+        np.testing.assert_array_equal(g[k][ok], ref[k][ok])

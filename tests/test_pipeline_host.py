@@ -155,3 +155,21 @@ def test_validate_rejects_malformed_narrow():
     nc, ncl = int(r[2]), int(r[7])
     u[nc + 1] = 2 * int(r[1]) + 5  # first clause literal past 2*nv
     assert _lib.lib().dp_rec_validate(r.ctypes.data_as(_lib.c_i32p), len(r)) != 0
+
+
+@pytest.mark.parametrize("config,n", [(2, 150), (4, 1), (5, 90)])
+def test_narrow_records_on_16_byte_boundaries(config, n):
+    """DP_LOWER_NARROW starts every record on a 16-byte boundary (the staged
+    form as it is, so a page-locked batch needs no staging); the padding is
+    zero and outside the record.  Without a GPU, DP_LOWER_PINNED falls back
+    to ordinary memory."""
+    b = lowered_config(config, n, 37, narrow=True, pinned=True)
+    assert np.all(b.rec_off % 4 == 0)
+    assert b.rec.ctypes.data % 16 == 0
+    for p in range(n):
+        r = b.record(p)
+        phys = 16 + (int(r[10]) - 15) // 2 if r[13] == 1 else int(r[10])
+        assert len(r) == (phys + 3) // 4 * 4 and not np.any(r[phys:])
+    import torch
+    if not torch.cuda.is_available():
+        assert not b.pinned
