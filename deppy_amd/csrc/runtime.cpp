@@ -65,9 +65,15 @@ constexpr int64_t kGroupAbove = 64 << 10;
 // Routed-off catalogs under kMidMaxVars variables run in 4-wave groups
 // (M_SPLIT4), larger ones in 8-wave groups (profiles/r01_group_waves_ab.jsonl).
 constexpr int32_t kMidMaxVars = 8192;
-// Pipeline chunks: at most this many problems or staged bytes each.
-constexpr int32_t kChunkProblems = 4096;
-constexpr int64_t kChunkBytes = 24ll << 20;
+// Pipeline chunks: at most this many problems or record bytes each.  A
+// chunk's kernels last as long as its slowest problem, and at most one chunk
+// per lane is in flight, so chunks are large (config 3 host to host: 11.0M
+// res/s with 4096-problem / 24 MiB chunks, 45.1M with 65536 / 64 MiB;
+// config 2: 10.0M -> 12.4M, one chunk per 10,000-catalog batch,
+// profiles/r02_h2h_sweep_b.jsonl; config 5: 363k at 64 MiB, 456k at 256 MiB;
+// config 4: 1.6k -> 3.0k, profiles/r02_h2h_sweep_c.jsonl).
+constexpr int32_t kChunkProblems = 65536;
+constexpr int64_t kChunkBytes = 256ll << 20;
 // D2H of the explanation pool per chunk: this many words per problem are
 // copied with the fixed outputs; a chunk whose cores need more fetches the
 // rest with a second copy.
@@ -94,12 +100,6 @@ bool forced_of(int32_t opt_flags) {
   return opt_flags & (DP_OPT_FORCE_GROUP | DP_OPT_FORCE_HBM | DP_OPT_FORCE_MID);
 }
 
-// Does a record (its header) run on the one-wavefront LDS path?
-bool lds_path(const int32_t* h, int32_t opt_flags) {
-  return !forced_of(opt_flags) && dp::fits16(h) &&
-         (int64_t)dp::layout<dp::M_LDS>(h).lds_bytes <= group_above();
-}
-
 // Header sanity needed before any layout arithmetic on it: the counts bound
 // every array, so the kernel can stage and validate the body (valid_record)
 // without reading past the record.
@@ -121,6 +121,17 @@ namespace dp {
 // ---------------------------------------------------------------------------
 struct Launch {
   int first, count, mode, lds;
+};
+
+// What the plan needs of one record, from its header alone (one cache line
+// per record: the header pass runs on the host pool, since the headers of a
+// chunk sit a record apart and every one is a cache miss).
+struct Head {
+  int8_t place;   // -1 malformed, -2 too large, else the Mode
+  int8_t bucket;  // M_LDS: the LDS bucket (kCeilings)
+  bool direct;    // the record is its own staged form (16-bit, 16-byte aligned)
+  int32_t lds, inst_words, nid;
+  int64_t sw, rec_bytes;
 };
 
 struct Plan {
@@ -145,18 +156,10 @@ struct Plan {
   std::vector<uint8_t> direct;    // [n] the source record is its own staged form
   int32_t n_direct = 0;
   int64_t other_words = 0;        // source words of the other problems
-};
-
-// rec + rec_off[p0 + i] is local problem i.  Problems whose header is not
-// well formed are planned as skipped (the caller reports them).
-// What the plan needs of one record, from its header alone (one cache line
-// per record: the header pass runs on the host pool, since the headers of a
-// chunk sit a record apart and every one is a cache miss).
-struct Head {
-  int8_t place;  // -1 malformed, -2 too large, else the Mode
-  bool direct;   // the record is its own staged form (16-bit, 16-byte aligned)
-  int32_t lds, inst_words, nid;
-  int64_t sw, rec_bytes;
+  // planning scratch, kept across chunks (no allocation or page fault per
+  // chunk once grown)
+  std::vector<Head> head;
+  std::vector<int32_t> big[4], cnt, tmp, grp;
 };
 
 void read_head(Head& H, const int32_t* h, int64_t avail, int32_t opt_flags, bool aligned) {
@@ -164,12 +167,19 @@ void read_head(Head& H, const int32_t* h, int64_t avail, int32_t opt_flags, bool
   if (!header_ok(h, avail)) { H.place = -1; return; }
   H.inst_words = bits_words(h[DP_H_NV]);
   H.nid = h[DP_H_NID];
-  const bool nar = lds_path(h, opt_flags);
+  // lds_path, with the one-wavefront layout computed once
+  bool nar = false;
+  if (!forced_of(opt_flags) && dp::fits16(h)) {
+    H.lds = layout<M_LDS>(h).lds_bytes;
+    nar = H.lds <= group_above();
+  }
   H.sw = staged_words(h, nar);
   H.rec_bytes = nar ? 4 * DP_H_SIZE + 2 * ((int64_t)h[DP_H_WORDS] - DP_H_SIZE) : 4 * (int64_t)h[DP_H_WORDS];
   if (nar) {
     H.place = M_LDS;
-    H.lds = layout<M_LDS>(h).lds_bytes;
+    int k = 0;
+    while (H.lds > kCeilings[k]) ++k;
+    H.bucket = (int8_t)k;
     H.direct = aligned && h[DP_H_FMT] == DP_FMT_U16;
     return;
   }
@@ -189,85 +199,95 @@ void read_head(Head& H, const int32_t* h, int64_t avail, int32_t opt_flags, bool
 // be null) reads the headers in parallel.
 void plan_chunk(Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0, int32_t n,
                 int32_t opt_flags, std::vector<uint8_t>* bad, Pool* pool = nullptr) {
-  P = Plan{};
   P.n = n;
-  P.img_off.assign((size_t)n + 1, 0);
-  P.narrow.assign((size_t)n, 0);
-  P.inst_off.assign((size_t)n + 1, 0);
-  std::vector<Head> head((size_t)n);
+  P.img_off.resize((size_t)n + 1);
+  P.inst_off.resize((size_t)n + 1);
+  P.narrow.resize((size_t)n);
+  P.direct.resize((size_t)n);
+  P.head.resize((size_t)n);
+  P.order.clear();
+  P.launches.clear();
+  P.scratch_off.clear();
+  P.skip.clear();
+  P.skip_flags.clear();
+  P.scratch_words = P.core_cap = P.rec_bytes = P.other_words = 0;
+  P.n_direct = 0;
+  P.big_base = 0;
+  Head* head = P.head.data();
   auto rd = [&](int64_t i) {
-    read_head(head[(size_t)i], rec + rec_off[p0 + i], rec_off[p0 + i + 1] - rec_off[p0 + i], opt_flags,
+    // every header is a cache miss: keep the next ones in flight
+    if (i + 8 < n) {
+      const int32_t* h8 = rec + rec_off[p0 + i + 8];
+      __builtin_prefetch(h8);
+      __builtin_prefetch(h8 + 15);
+    }
+    read_head(head[i], rec + rec_off[p0 + i], rec_off[p0 + i + 1] - rec_off[p0 + i], opt_flags,
               (rec_off[p0 + i] & 3) == 0);
   };
   if (pool && n > 256) pool->run(n, std::function<void(int64_t)>(rd), 64);
   else for (int32_t i = 0; i < n; ++i) rd(i);
-  std::vector<std::vector<int32_t>> bucket(kNBuckets), big(4);
-  std::vector<int> lds((size_t)n, 0);
+  // one pass: offsets, totals and per-bucket counts / LDS maxima
+  for (auto& v : P.big) v.clear();
+  int32_t bcount[kNBuckets] = {}, bmax[kNBuckets] = {};
   const bool rec_aligned = ((uintptr_t)rec & 15) == 0;
-  P.direct.assign((size_t)n, 0);
+  int64_t img = 0, inst = 0;
+  P.img_off[0] = P.inst_off[0] = 0;
   for (int32_t i = 0; i < n; ++i) {
-    const Head& H = head[(size_t)i];
-    if (rec_aligned && H.direct) {
-      P.direct[(size_t)i] = 1;
-      P.n_direct++;
-    } else {
-      P.other_words += rec_off[p0 + i + 1] - rec_off[p0 + i];
-    }
-    if (H.place == -1) {
-      if (bad) (*bad)[(size_t)i] = 1;
-      P.skip.push_back(i);
-      P.skip_flags.push_back(DP_F_MALFORMED);
-      P.img_off[(size_t)i + 1] = P.img_off[(size_t)i];
-      continue;
-    }
-    P.inst_off[(size_t)i + 1] = H.inst_words;
-    P.core_cap += H.nid;
+    const Head& H = head[i];
+    const bool d = rec_aligned && H.direct;
+    P.direct[(size_t)i] = d;
+    P.n_direct += d;
+    P.other_words += d ? 0 : rec_off[p0 + i + 1] - rec_off[p0 + i];
     P.narrow[(size_t)i] = H.place == M_LDS;
-    P.img_off[(size_t)i + 1] = P.img_off[(size_t)i] + H.sw;
-    P.rec_bytes += H.rec_bytes;
     if (H.place == M_LDS) {
-      lds[(size_t)i] = H.lds;
-      int k = 0;
-      while (lds[(size_t)i] > kCeilings[k]) ++k;
-      bucket[(size_t)k].push_back(i);
+      bcount[H.bucket]++;
+      bmax[H.bucket] = std::max(bmax[H.bucket], H.lds);
     } else if (H.place >= 0) {
-      big[(size_t)H.place].push_back(i);
+      P.big[(size_t)H.place].push_back(i);
     } else {
+      if (H.place == -1 && bad) (*bad)[(size_t)i] = 1;
       P.skip.push_back(i);
-      P.skip_flags.push_back(DP_F_TOO_LARGE);
+      P.skip_flags.push_back(H.place == -1 ? DP_F_MALFORMED : DP_F_TOO_LARGE);
     }
+    if (H.place != -1) {
+      img += H.sw;
+      inst += H.inst_words;
+      P.core_cap += H.nid;
+      P.rec_bytes += H.rec_bytes;
+    }
+    P.img_off[(size_t)i + 1] = img;
+    P.inst_off[(size_t)i + 1] = inst;
   }
-  for (int32_t i = 0; i < n; ++i) P.inst_off[(size_t)i + 1] += P.inst_off[(size_t)i];
   P.dev_off.assign(P.img_off.begin(), P.img_off.end() - 1);
-  P.img_words = P.img_off[(size_t)n];
+  P.img_words = img;
   // Within a launch, workgroups are dispatched in blockIdx order: largest
   // record first (longest-processing-time-first), so the long solves do not
   // form the launch's tail.
   // (a counting sort on the staged size, stable: ties keep problem order)
   auto cost = [&](int32_t i) { return P.img_off[(size_t)i + 1] - P.img_off[(size_t)i]; };
-  std::vector<int32_t> cnt, tmp;
-  auto lpt = [&](std::vector<int32_t>& v) {
-    if (v.size() < 2) return;
+  auto lpt = [&](int32_t* v, size_t m) {
+    if (m < 2) return;
     int64_t lo = INT64_MAX, hi = 0;
-    for (int32_t i : v) { lo = std::min(lo, cost(i)); hi = std::max(hi, cost(i)); }
-    if (hi - lo > 4 * (int64_t)v.size() + 65536) {  // a wide range: comparison sort
-      std::stable_sort(v.begin(), v.end(), [&](int32_t x, int32_t y) { return cost(x) > cost(y); });
+    for (size_t j = 0; j < m; ++j) { lo = std::min(lo, cost(v[j])); hi = std::max(hi, cost(v[j])); }
+    if (hi - lo > 4 * (int64_t)m + 65536) {  // a wide range: comparison sort
+      std::stable_sort(v, v + m, [&](int32_t x, int32_t y) { return cost(x) > cost(y); });
       return;
     }
-    cnt.assign((size_t)(hi - lo) + 2, 0);
-    for (int32_t i : v) cnt[(size_t)(hi - cost(i)) + 1]++;
-    for (size_t k = 1; k < cnt.size(); ++k) cnt[k] += cnt[k - 1];
-    tmp.resize(v.size());
-    for (int32_t i : v) tmp[(size_t)cnt[(size_t)(hi - cost(i))]++] = i;
-    v.swap(tmp);
+    P.cnt.assign((size_t)(hi - lo) + 2, 0);
+    for (size_t j = 0; j < m; ++j) P.cnt[(size_t)(hi - cost(v[j])) + 1]++;
+    for (size_t k = 1; k < P.cnt.size(); ++k) P.cnt[k] += P.cnt[k - 1];
+    P.tmp.resize(m);
+    for (size_t j = 0; j < m; ++j) P.tmp[(size_t)P.cnt[(size_t)(hi - cost(v[j]))]++] = v[j];
+    std::copy(P.tmp.begin(), P.tmp.begin() + (int64_t)m, v);
   };
   // multi-wave launches first: the long-running large catalogs start earliest
   for (int mode : {(int)M_SPLIT4, (int)M_SPLIT, (int)M_HBM}) {
-    if (big[(size_t)mode].empty()) continue;
-    lpt(big[(size_t)mode]);
+    auto& bg = P.big[(size_t)mode];
+    if (bg.empty()) continue;
+    lpt(bg.data(), bg.size());
     int mx = 0;
-    Launch L{(int)P.order.size(), (int)big[(size_t)mode].size(), mode, 0};
-    for (int32_t i : big[(size_t)mode]) {
+    Launch L{(int)P.order.size(), (int)bg.size(), mode, 0};
+    for (int32_t i : bg) {
       const int32_t* h = rec + rec_off[p0 + i];
       const Layout Y = mode == M_SPLIT ? layout<M_SPLIT>(h) : mode == M_SPLIT4 ? layout<M_SPLIT4>(h) : layout<M_HBM>(h);
       mx = std::max(mx, Y.lds_bytes);
@@ -276,7 +296,7 @@ void plan_chunk(Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0,
     }
     L.lds = mx;
     P.launches.push_back(L);
-    P.order.insert(P.order.end(), big[(size_t)mode].begin(), big[(size_t)mode].end());
+    P.order.insert(P.order.end(), bg.begin(), bg.end());
   }
   P.big_base = 0;  // scratch_off is indexed from the first multi-wave workgroup (order index 0)
   // Adjacent LDS buckets are merged into one launch while the merged request
@@ -285,35 +305,45 @@ void plan_chunk(Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0,
     const char* m = std::getenv("DEPPY_BUCKET_MERGE");
     return m ? std::atof(m) : kMergeRatio;
   }();
-  std::vector<Launch> bl;
-  std::vector<std::vector<int32_t>> members;
-  int first_lds = 0;
+  int group_of[kNBuckets];
+  Launch bl[kNBuckets];
+  int64_t gsize[kNBuckets] = {};
+  int ng = 0, first_lds = 0;
   for (int k = 0; k < kNBuckets; ++k) {
-    if (bucket[(size_t)k].empty()) continue;
-    int mx = 0;
-    for (int32_t i : bucket[(size_t)k]) mx = std::max(mx, lds[(size_t)i]);
-    const bool join = !bl.empty() && merge > 0 &&
-                      (double)(kMaxLdsBytes / std::max(mx, bl.back().lds)) >=
+    if (!bcount[k]) continue;
+    const bool join = ng > 0 && merge > 0 &&
+                      (double)(kMaxLdsBytes / std::max(bmax[k], bl[ng - 1].lds)) >=
                           merge * (double)(kMaxLdsBytes / first_lds);
     if (join) {
-      bl.back().lds = std::max(bl.back().lds, mx);
-      members.back().insert(members.back().end(), bucket[(size_t)k].begin(), bucket[(size_t)k].end());
+      bl[ng - 1].lds = std::max(bl[ng - 1].lds, bmax[k]);
     } else {
-      first_lds = mx;
-      bl.push_back(Launch{0, 0, M_LDS, mx});
-      members.push_back(bucket[(size_t)k]);
+      first_lds = bmax[k];
+      bl[ng++] = Launch{0, 0, M_LDS, bmax[k]};
     }
+    group_of[k] = ng - 1;
+    gsize[ng - 1] += bcount[k];
   }
-  // the bucket launches, the most problems first
-  std::vector<size_t> ix(bl.size());
-  for (size_t g = 0; g < ix.size(); ++g) ix[g] = g;
-  std::stable_sort(ix.begin(), ix.end(), [&](size_t x, size_t y) { return members[x].size() > members[y].size(); });
-  for (size_t g : ix) {
-    lpt(members[g]);
-    bl[g].first = (int)P.order.size();
-    bl[g].count = (int)members[g].size();
+  // the bucket launches, the most problems first; members in problem order,
+  // then each launch's members by LPT
+  int ix[kNBuckets];
+  for (int g = 0; g < ng; ++g) ix[g] = g;
+  std::stable_sort(ix, ix + ng, [&](int x, int y) { return gsize[x] > gsize[y]; });
+  int64_t at[kNBuckets];
+  int64_t o = (int64_t)P.order.size();
+  for (int r = 0; r < ng; ++r) {
+    const int g = ix[r];
+    bl[g].first = (int)o;
+    bl[g].count = (int)gsize[g];
+    at[g] = o;
+    o += gsize[g];
+  }
+  P.order.resize((size_t)o);
+  for (int32_t i = 0; i < n; ++i)
+    if (head[i].place == M_LDS) P.order[(size_t)at[group_of[head[i].bucket]]++] = i;
+  for (int r = 0; r < ng; ++r) {
+    const int g = ix[r];
+    lpt(P.order.data() + bl[g].first, (size_t)bl[g].count);
     P.launches.push_back(bl[g]);
-    P.order.insert(P.order.end(), members[g].begin(), members[g].end());
   }
   static const int pad_kb = (int)env_i64("DEPPY_LDS_PAD_KB", 0);  // diagnostic (occupancy study)
   if (pad_kb > 0)
@@ -321,58 +351,66 @@ void plan_chunk(Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0,
       if (L.mode == M_LDS) L.lds = std::max(L.lds, pad_kb * 1024);
 }
 
-// Narrow n words of s into d, checking lo <= x < hi for each (one pass: the
-// min/max reductions and the stores vectorise).
-__attribute__((always_inline)) static inline bool narrow_range(const int32_t* __restrict s, uint16_t* __restrict d,
-                                                               int32_t n, int32_t lo, int32_t hi) {
+// Copy n words of s into d (narrowing or widening), checking lo <= x < hi
+// for each (one pass: the min/max reductions and the stores vectorise).
+template <class S, class D>
+__attribute__((always_inline)) static inline bool copy_range(const S* __restrict s, D* __restrict d, int32_t n,
+                                                             int32_t lo, int32_t hi) {
   int32_t mn = INT32_MAX, mx = INT32_MIN;
   for (int32_t j = 0; j < n; ++j) {
-    mn = s[j] < mn ? s[j] : mn;
-    mx = s[j] > mx ? s[j] : mx;
-    d[j] = (uint16_t)s[j];
+    const int32_t x = (int32_t)s[j];
+    mn = x < mn ? x : mn;
+    mx = x > mx ? x : mx;
+    d[j] = (D)x;
   }
   return n == 0 || (mn >= lo && mx < hi);
 }
 // An offsets array: s[0] == 0, non-decreasing, s[n] == total.
-__attribute__((always_inline)) static inline bool narrow_offsets(const int32_t* __restrict s,
-                                                                 uint16_t* __restrict d, int32_t n, int32_t total) {
+template <class S, class D>
+__attribute__((always_inline)) static inline bool copy_offsets(const S* __restrict s, D* __restrict d, int32_t n,
+                                                               int32_t total) {
   int32_t dec = 0;
-  for (int32_t j = 0; j < n; ++j) dec |= s[j + 1] < s[j];
-  for (int32_t j = 0; j <= n; ++j) d[j] = (uint16_t)s[j];
-  return s[0] == 0 && s[n] == total && !dec;
+  for (int32_t j = 0; j < n; ++j) dec |= (int32_t)s[j + 1] < (int32_t)s[j];
+  for (int32_t j = 0; j <= n; ++j) d[j] = (D)s[j];
+  return (int32_t)s[0] == 0 && (int32_t)s[n] == total && !dec;
 }
 
-// The 16-bit form of a record whose header passed header_ok and fits16:
-// dp_rec_validate's checks fused into the narrowing pass.  AtMost bounds
-// over the row length are stored as the row length (the same row: neither
-// can be exceeded by the count).
-__attribute__((always_inline)) static inline bool stage_narrow_body(const int32_t* src, uint16_t* o) {
-  const dp_rec_layout L = dp_rec_layout_of(src);
-  const int32_t nv = src[DP_H_NV], nc = src[DP_H_NC], nk = src[DP_H_NK], nch = src[DP_H_NCH];
-  const int32_t nid = src[DP_H_NID], ncl = src[DP_H_NCL], nkl = src[DP_H_NKL], nchl = src[DP_H_NCHL];
-  auto d = [&](int32_t word) { return o + (word - DP_H_SIZE); };
-  bool ok = narrow_offsets(src + L.clause_off, d(L.clause_off), nc, ncl);
-  ok &= narrow_range(src + L.clause_lits, d(L.clause_lits), ncl, 0, 2 * nv);
-  ok &= narrow_range(src + L.clause_id, d(L.clause_id), nc, 0, nid);
-  ok &= narrow_offsets(src + L.card_off, d(L.card_off), nk, nkl);
-  ok &= narrow_range(src + L.card_lits, d(L.card_lits), nkl, 0, nv);
-  ok &= narrow_range(src + L.card_id, d(L.card_id), nk, 0, nid);
-  ok &= narrow_offsets(src + L.var_choice_off, d(L.var_choice_off), nv, nch);
-  ok &= narrow_offsets(src + L.choice_off, d(L.choice_off), nch, nchl);
-  ok &= narrow_range(src + L.choice_lits, d(L.choice_lits), nchl, 0, nv);
-  ok &= narrow_range(src + L.anchors, d(L.anchors), src[DP_H_NA], 0, nv);
+// The checked copy of a record's body (header h, which passed header_ok;
+// source body in S words, destination body in D words): dp_rec_validate's
+// checks fused into the copy.  Into 16 bits, AtMost bounds over the row
+// length are stored as the row length (the same row: neither can be
+// exceeded by the count).
+template <class S, class D>
+__attribute__((always_inline)) static inline bool convert_body(const int32_t* h, const S* sb, D* db) {
+  const dp_rec_layout L = dp_rec_layout_of(h);
+  const int32_t nv = h[DP_H_NV], nc = h[DP_H_NC], nk = h[DP_H_NK], nch = h[DP_H_NCH];
+  const int32_t nid = h[DP_H_NID], ncl = h[DP_H_NCL], nkl = h[DP_H_NKL], nchl = h[DP_H_NCHL];
+  auto s = [&](int32_t word) { return sb + (word - DP_H_SIZE); };
+  auto d = [&](int32_t word) { return db + (word - DP_H_SIZE); };
+  bool ok = copy_offsets(s(L.clause_off), d(L.clause_off), nc, ncl);
+  ok &= copy_range(s(L.clause_lits), d(L.clause_lits), ncl, 0, 2 * nv);
+  ok &= copy_range(s(L.clause_id), d(L.clause_id), nc, 0, nid);
+  ok &= copy_offsets(s(L.card_off), d(L.card_off), nk, nkl);
+  ok &= copy_range(s(L.card_lits), d(L.card_lits), nkl, 0, nv);
+  ok &= copy_range(s(L.card_id), d(L.card_id), nk, 0, nid);
+  ok &= copy_offsets(s(L.var_choice_off), d(L.var_choice_off), nv, nch);
+  ok &= copy_offsets(s(L.choice_off), d(L.choice_off), nch, nchl);
+  ok &= copy_range(s(L.choice_lits), d(L.choice_lits), nchl, 0, nv);
+  ok &= copy_range(s(L.anchors), d(L.anchors), h[DP_H_NA], 0, nv);
   if (!ok) return false;
   // the positions of a variable form one run: run starts are distinct within
   // a row (a per-thread mark array, one tag per row)
   static thread_local std::vector<uint32_t> mark;
   static thread_local uint32_t tag = 0;
   if (mark.size() < (size_t)nv) mark.assign((size_t)nv + 1024, 0);
-  const int32_t* co = src + L.card_off;
-  const int32_t* cl = src + L.card_lits;
+  const S* co = s(L.card_off);
+  const S* cl = s(L.card_lits);
+  const S* cb = s(L.card_bound);
+  D* ob = d(L.card_bound);
   for (int32_t k = 0; k < nk; ++k) {
-    const int32_t a = co[k], b = co[k + 1], bound = src[L.card_bound + k];
+    const int32_t a = (int32_t)co[k], b = (int32_t)co[k + 1], bound = (int32_t)cb[k];
     if (bound < 0) return false;
-    d(L.card_bound)[k] = (uint16_t)std::min(bound, b - a);
+    ob[k] = (D)(sizeof(D) == 2 ? std::min(bound, b - a) : bound);
     if (++tag == 0) {
       std::fill(mark.begin(), mark.end(), 0u);
       tag = 1;
@@ -385,13 +423,17 @@ __attribute__((always_inline)) static inline bool stage_narrow_body(const int32_
   }
   return true;
 }
-__attribute__((target("avx2"))) static bool stage_narrow_avx2(const int32_t* src, uint16_t* o) {
-  return stage_narrow_body(src, o);
+// (AVX2 clones of the three checked copies, picked at run time)
+template <class S, class D>
+__attribute__((target("avx2"))) static bool convert_avx2(const int32_t* h, const S* sb, D* db) {
+  return convert_body(h, sb, db);
 }
-static bool stage_narrow_generic(const int32_t* src, uint16_t* o) { return stage_narrow_body(src, o); }
-static bool stage_narrow(const int32_t* src, uint16_t* o) {
+template <class S, class D>
+static bool convert_generic(const int32_t* h, const S* sb, D* db) { return convert_body(h, sb, db); }
+template <class S, class D>
+static bool convert(const int32_t* h, const S* sb, D* db) {
   static const bool avx2 = __builtin_cpu_supports("avx2");
-  return avx2 ? stage_narrow_avx2(src, o) : stage_narrow_generic(src, o);
+  return avx2 ? convert_avx2(h, sb, db) : convert_generic(h, sb, db);
 }
 
 // The watch lists of a multi-wave problem (layout.hpp img_layout), right
@@ -423,6 +465,12 @@ int64_t build_watches_host(int32_t* r) {
   return X.words;
 }
 
+// Problems per pool work item when staging n records: a few items per
+// thread at least (a chunk of 28 OLM-scale records must not go to one thread).
+int64_t stage_block(int64_t n, const Pool& pool) {
+  return std::max<int64_t>(1, std::min<int64_t>(32, n / (8 * (int64_t)std::max(1, pool.size()))));
+}
+
 // Stage local problem i of the plan into dst (the staged image area): the
 // int32 header with its format word, then the body in the form the plan
 // chose.  A 16-bit record to a 16-bit copy, or an int32 record to an int32
@@ -447,21 +495,17 @@ bool stage_one(const Plan& P, const int32_t* rec, const int64_t* rec_off, int32_
     uint16_t* o = reinterpret_cast<uint16_t*>(d + DP_H_SIZE);
     if (src16) {
       std::memcpy(o, src + DP_H_SIZE, 2 * (size_t)body);  // validated by the kernel
-    } else if (!stage_narrow(src, o)) {
+    } else if (!convert(src, src + DP_H_SIZE, o)) {
       d[DP_H_FMT] = DP_FMT_REJECT;
       return false;
     }
     for (int64_t j = body; j < 2 * (sw - DP_H_SIZE); ++j) o[j] = 0;
   } else {
     d[DP_H_FMT] = DP_FMT_I32;
-    if (src16) {
-      const uint16_t* u = reinterpret_cast<const uint16_t*>(src + DP_H_SIZE);
-      for (int64_t j = 0; j < body; ++j) d[DP_H_SIZE + j] = u[j];
-    } else {
-      std::memcpy(d + DP_H_SIZE, src + DP_H_SIZE, 4 * (size_t)body);
-    }
+    const bool ok = src16 ? convert(src, reinterpret_cast<const uint16_t*>(src + DP_H_SIZE), d + DP_H_SIZE)
+                          : convert(src, src + DP_H_SIZE, d + DP_H_SIZE);
     // the watch lists are built here, from the checked int32 copy
-    if (dp_rec_validate(d, words) != 0) {
+    if (!ok) {
       d[DP_H_FMT] = DP_FMT_REJECT;
       return false;
     }
@@ -777,9 +821,10 @@ int start_chunk(dp_ctx* ctx, Lane& L, dp_job* job, int32_t p0, int32_t n) {
   // copied to the device from where they lie: the chunk's source range goes
   // by one DMA to the front of the image, each such record at its own
   // offset, and only the other problems' records are staged, after it.
-  // (Worth it while the others' source words, copied for nothing, are few.)
+  // (Worth it while the others' source words, copied for nothing, are not
+  // the larger part.)
   const int64_t W = job->rec_off[p0 + n] - job->rec_off[p0];
-  const bool direct = job->pinned && L.plan.n_direct > 0 && !ctx->zc_in && 4 * L.plan.other_words <= W;
+  const bool direct = job->pinned && L.plan.n_direct > 0 && !ctx->zc_in && 2 * L.plan.other_words <= W;
   if (direct) {
     Plan& Q = L.plan;
     int64_t o = W;
@@ -806,7 +851,7 @@ int start_chunk(dp_ctx* ctx, Lane& L, dp_job* job, int32_t p0, int32_t n) {
     ctx->pool->run(n, [&](int64_t i) {
       if (direct && P.direct[(size_t)i]) return;
       if (!dp::stage_one(P, job->rec, job->rec_off, p0, (int32_t)i, img)) bad[(size_t)i] = 1;
-    }, 32);
+    }, dp::stage_block(n, *ctx->pool));
     // (records found malformed while staging are reported by the kernel)
   }
   fill_in_tables(P, il, L.h_in.p);
@@ -1067,7 +1112,7 @@ int build_slice(dp_ctx* ctx, Slice& s, const dp_batch* b, int32_t trace_cap) {
   const Plan& P = s.plan;
   ctx->pool->run(n, [&](int64_t i) {
     if (!dp::stage_one(P, b->rec, b->rec_off, s.p0, (int32_t)i, img)) bad[(size_t)i] = 1;
-  }, 32);
+  }, dp::stage_block(n, *ctx->pool));
   fill_in_tables(P, s.il, host.data());
   s.d_in.host = s.d_out.host = s.scratch.host = false;
   HIP_OK(s.d_in.reserve(s.il.end));
@@ -1290,7 +1335,7 @@ int dp_stage_roundtrip(const dp_batch* b, int32_t opt_flags, int32_t chunk_probl
     if (staged.size() < (size_t)plan.img_off[(size_t)plan.n] + 1) staged.resize((size_t)plan.img_off[(size_t)plan.n] + 1);
     hook_pool().run(q - p, [&](int64_t i) {
       if (!dp::stage_one(plan, b->rec, b->rec_off, p, (int32_t)i, staged.data())) bad[(size_t)i] = 1;
-    }, 32);
+    }, dp::stage_block(q - p, hook_pool()));
     for (auto x : bad)
       if (x) return -1;
     for (int32_t i = 0; out_rec && i < q - p; ++i) {  // out_rec NULL: staging only (timing)
