@@ -94,10 +94,10 @@ def maybe_relaunch(args) -> None:
 
 
 def lowered_config(config, n, seed):
-    """The batch lowered twice: in the 16-bit staged form into page-locked
-    memory (dp_lower_into DP_LOWER_NARROW | DP_LOWER_PINNED, as a serving
-    loop keeps its lowering storage; what the GPU path is given) and as int32
-    records (what the CPU baseline is given).  Also the steady-state lowering rate
+    """The batch lowered twice: in the packed 16-bit form into page-locked
+    memory (dp_lower_into DP_LOWER_NARROW | DP_LOWER_PACKED | DP_LOWER_PINNED,
+    as a serving loop keeps its lowering storage; what the GPU path is given)
+    and as int32 records (what the CPU baseline is given).  Also the steady-state lowering rate
     (dp_lower_into reusing its storage, the wire format -> records)."""
     from deppy_amd import _lib
     w = _lib.generate(config, n, seed)
@@ -105,7 +105,7 @@ def lowered_config(config, n, seed):
         "prob_var_off", "var_id", "var_con_off", "con_kind", "con_n", "con_arg_off", "con_arg",
         "str_off")}, str_bytes=w["str_bytes"].tobytes())
     lw32 = _lib.Lowered(wa)
-    lw = _lib.Lowered(wa, narrow=True, pinned=True)
+    lw = _lib.Lowered(wa, narrow=True, pinned=True, packed=True)
     reps, t0 = 0, time.perf_counter()
     while reps < 3 or time.perf_counter() - t0 < 1.0:
         lw.relower(wa)
@@ -249,7 +249,7 @@ def main():
         "classes": class_mix(res) if res is not None else None,
         "deterministic": bool(deterministic),
         "host_lowering_res_per_s": round(n / t_lower, 1),
-        "host_lowering_note": "dp_lower_into (16-bit records, storage reused) on the host pool; not in value",
+        "host_lowering_note": "dp_lower_into (packed 16-bit records, storage reused) on the host pool; not in value",
     }
 
     if args.kernel_steps > 0:
@@ -345,7 +345,7 @@ def main():
                                           % (n, reps, cpu_t, share["nproc"], share["affinity"],
                                              share["cgroup_quota"])}
         line["verified_bit_exact_vs_oracle"] = bool(ok)
-        line["verified_note"] = "GPU on the 16-bit records vs oracle on the int32 records, every field incl. cores"
+        line["verified_note"] = "GPU on the packed 16-bit records vs oracle on the int32 records, every field incl. cores"
     if rank == 0:
         print(json.dumps(line), flush=True)
     g.close()

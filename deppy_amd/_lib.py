@@ -37,7 +37,7 @@ EXPORTS = [
     "dp_last_error", "dp_last_global_error", "dp_num_devices", "dp_solve", "dp_upload", "dp_run",
     "dp_launch", "dp_wait", "dp_download", "dp_resident_free", "dp_last_kernel_ms", "dp_gen_catalogs", "dp_gen_wire",
     "dp_gen_free", "dp_upload_traced", "dp_download_trace", "dp_solve_traced", "dp_lowered_errors",
-    "dp_device_bytes", "dp_lower_into", "dp_lowered_new", "dp_lowered_exact_count", "dp_lowered_pinned", "dp_submit", "dp_job_wait", "dp_get_stats", "dp_stage_roundtrip",
+    "dp_device_bytes", "dp_lower_into", "dp_lowered_new", "dp_lowered_exact_count", "dp_lowered_pinned", "dp_rec_widen", "dp_submit", "dp_job_wait", "dp_get_stats", "dp_stage_roundtrip",
     "dp_stitch_selftest", "dp_partition",
 ]
 
@@ -94,6 +94,7 @@ def lib():
     L = ctypes.CDLL(LIB_PATH)
     vp = ctypes.c_void_p
     L.dp_rec_validate.argtypes = [c_i32p, ctypes.c_int64]
+    L.dp_rec_widen.argtypes = [c_i32p, ctypes.c_int64, c_i32p]
     L.dp_lower.argtypes = [ctypes.POINTER(Wire), ctypes.POINTER(vp)]
     L.dp_lowered_free.argtypes = [vp]
     L.dp_lower_into.argtypes = [ctypes.POINTER(Wire), ctypes.c_int32, vp]
@@ -242,17 +243,18 @@ class Lowered:
     relower(wire) lowers another batch into the same storage
     (dp_lower_into), invalidating the previous views' contents."""
 
-    def __init__(self, wire: WireArrays, narrow: bool = False, pinned: bool = False):
+    def __init__(self, wire: WireArrays, narrow: bool = False, pinned: bool = False, packed: bool = False):
         """narrow: records that fit 16 bits in the DP_FMT_U16 form, each on a
         16-byte boundary (the staged form, DP_LOWER_NARROW); default int32
         records.  pinned: the records in page-locked memory when a GPU is
         present (DP_LOWER_PINNED; with narrow, dp_submit copies them to the
-        device without staging)."""
+        device without staging).  packed (with narrow): the DP_FMT_P16 form
+        where it applies (DP_LOWER_PACKED; a fifth fewer bytes)."""
         L = lib()
         h = ctypes.c_void_p()
         ws = wire.struct()
         self.narrow = narrow
-        self._flags = (1 if narrow else 0) | (2 if pinned else 0)
+        self._flags = (1 if narrow else 0) | (2 if pinned else 0) | (4 if packed else 0)
         if self._flags:
             h = ctypes.c_void_p(L.dp_lowered_new())
             if L.dp_lower_into(ctypes.byref(ws), self._flags, h) != 0:

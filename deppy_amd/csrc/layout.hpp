@@ -71,6 +71,14 @@ constexpr bool IMP16_LDS = DP_IMP16;
 constexpr int32_t NSCAL = 64;
 __host__ __device__ constexpr int32_t mode_nscal(int mode) { return mode == M_LDS ? 8 : NSCAL; }
 
+// dp_p16_tail_at / dp_p16_tail_bytes (include/deppy_hip.h) for device code.
+__host__ __device__ inline int64_t p16_tail_at(const int32_t* h) {
+  return (2 * ((int64_t)h[DP_H_NCL] + h[DP_H_NKL] + h[DP_H_NK] + h[DP_H_NCHL] + h[DP_H_NA]) + 15) & ~(int64_t)15;
+}
+__host__ __device__ inline int64_t p16_tail_bytes(const int32_t* h) {
+  return (int64_t)h[DP_H_NC] + h[DP_H_NK] + h[DP_H_NV] + h[DP_H_NCH] + ((int64_t)h[DP_H_NID] + 7) / 8;
+}
+
 // dp_rec_layout_of (include/deppy_hip.h) for host and device code.
 __host__ __device__ inline dp_rec_layout rec_layout(const int32_t* h) {
   dp_rec_layout L;
@@ -115,7 +123,7 @@ __host__ __device__ inline dp_rec_layout rec_layout(const int32_t* h) {
 // body), and the 16-bit form of a record the host checked while narrowing it
 // (the kernel validates only the DP_FMT_U16 copies the host passed through
 // unread, Group::valid_record).
-enum { DP_FMT_REJECT = 2, DP_FMT_U16_CHECKED = 3 };
+enum { DP_FMT_REJECT = 2, DP_FMT_U16_CHECKED = 16 };
 
 struct ImgLayout {
   int32_t w_off, w, words;

@@ -343,7 +343,8 @@ inline uint64_t keyh(uint64_t tag, uint64_t h) { return tag << 60 | (h & ((1ULL 
 struct Lowerer {
   const dp_wire& w;
   const bool narrow;  // DP_LOWER_NARROW: records that fit 16 bits in the DP_FMT_U16 form
-  Lowerer(const dp_wire& wire, bool narrow16) : w(wire), narrow(narrow16) {}
+  const bool packed;  // DP_LOWER_PACKED: ... in the DP_FMT_P16 form where they allow it
+  Lowerer(const dp_wire& wire, bool narrow16, bool packed16) : w(wire), narrow(narrow16), packed(packed16) {}
 
   // The last record appended to O (int32 words from `base`) in the 16-bit
   // form, in place (word j -> halfword j never overtakes word j).  Every
@@ -355,7 +356,9 @@ struct Lowerer {
     int32_t* r = O.rec.data() + base;
     const int64_t words = r[DP_H_WORDS];
     int64_t phys = words;
-    if (dp_rec_fits16(r)) {
+    if (packed && pack16(r)) {
+      phys = dp_rec_phys_words(r);
+    } else if (dp_rec_fits16(r)) {
       uint16_t* u = reinterpret_cast<uint16_t*>(r + DP_H_SIZE);
       for (int64_t j = 0; j < words - DP_H_SIZE; ++j) u[j] = (uint16_t)r[DP_H_SIZE + j];
       if ((words - DP_H_SIZE) & 1) u[words - DP_H_SIZE] = 0;
@@ -368,6 +371,57 @@ struct Lowerer {
     r = O.rec.data() + base;
     for (int64_t j = phys; j < padded; ++j) r[j] = 0;
     O.rec_len.back() = padded;
+  }
+
+  // The int32 record r (fits16) in the DP_FMT_P16 form, in place, if it
+  // allows it (every identity one row, each row kind's identities
+  // ascending, lengths below 256, DP_P16_TAIL_MAX); false leaves r as it is.
+  static bool pack16(int32_t* r) {
+    if (!dp_rec_fits16(r) || r[DP_H_NID] != r[DP_H_NC] + r[DP_H_NK] ||
+        dp_p16_tail_bytes(r) > DP_P16_TAIL_MAX)
+      return false;
+    const dp_rec_layout L = dp_rec_layout_of(r);
+    const int32_t nc = r[DP_H_NC], nk = r[DP_H_NK], nv = r[DP_H_NV], nch = r[DP_H_NCH], nid = r[DP_H_NID];
+    for (int32_t i = 1; i < nc; ++i)
+      if (r[L.clause_id + i] <= r[L.clause_id + i - 1]) return false;
+    for (int32_t i = 1; i < nk; ++i)
+      if (r[L.card_id + i] <= r[L.card_id + i - 1]) return false;
+    auto short_lens = [&](int32_t off, int32_t n) {
+      for (int32_t j = 0; j < n; ++j)
+        if (r[off + j + 1] - r[off + j] > 255) return false;
+      return true;
+    };
+    if (!short_lens(L.clause_off, nc) || !short_lens(L.card_off, nk) || !short_lens(L.var_choice_off, nv) ||
+        !short_lens(L.choice_off, nch))
+      return false;
+    static thread_local std::vector<uint8_t> buf;
+    const int64_t at = dp_p16_tail_at(r), tb = dp_p16_tail_bytes(r);
+    buf.assign((size_t)(at + tb), 0);
+    uint16_t* u = reinterpret_cast<uint16_t*>(buf.data());
+    auto put16 = [&](int32_t off, int32_t n) {
+      for (int32_t j = 0; j < n; ++j) *u++ = (uint16_t)r[off + j];
+    };
+    put16(L.clause_lits, r[DP_H_NCL]);
+    put16(L.card_lits, r[DP_H_NKL]);
+    put16(L.card_bound, nk);
+    put16(L.choice_lits, r[DP_H_NCHL]);
+    put16(L.anchors, r[DP_H_NA]);
+    uint8_t* t = buf.data() + at;
+    auto put_lens = [&](int32_t off, int32_t n) {
+      for (int32_t j = 0; j < n; ++j) *t++ = (uint8_t)(r[off + j + 1] - r[off + j]);
+    };
+    put_lens(L.clause_off, nc);
+    put_lens(L.card_off, nk);
+    put_lens(L.var_choice_off, nv);
+    put_lens(L.choice_off, nch);
+    for (int32_t k = 0; k < nk; ++k) {
+      const int32_t id = r[L.card_id + k];
+      if (id < 0 || id >= nid) return false;
+      t[id >> 3] |= (uint8_t)(1u << (id & 7));
+    }
+    std::memcpy(r + DP_H_SIZE, buf.data(), buf.size());
+    r[DP_H_FMT] = DP_FMT_P16;
+    return true;
   }
 
   std::string_view str(int64_t i) const {
@@ -966,7 +1020,8 @@ int dp_lower_into(const dp_wire* wire, int32_t flags, dp_lowered* lw) {
   }
   lw->pieces.resize((size_t)nchunks);
   lw->n_exact.store(0);
-  dp::Lowerer L(*wire, (flags & DP_LOWER_NARROW) != 0);
+  dp::Lowerer L(*wire, (flags & DP_LOWER_NARROW) != 0, (flags & (DP_LOWER_NARROW | DP_LOWER_PACKED)) ==
+                                                          (DP_LOWER_NARROW | DP_LOWER_PACKED));
   std::atomic<bool> bad{false};
   auto lower_chunk = [&](int64_t c, int t) {
     dp::Work& W = lw->work[(size_t)t];
@@ -1069,19 +1124,69 @@ int32_t dp_lowered_errors(const dp_lowered* lw, int32_t* err) {
   return bad;
 }
 
+int dp_rec_widen(const int32_t* rec, int64_t avail, int32_t* out) {
+  if (!rec || !out || avail < DP_H_SIZE) return -1;
+  if (rec[DP_H_MAGIC] != DP_REC_MAGIC) return -2;
+  for (int i = DP_H_NV; i <= DP_H_NCHL; ++i)
+    if (rec[i] < 0 || rec[i] > (1 << 28)) return -3;
+  const int32_t fmt = rec[DP_H_FMT];
+  if (fmt != DP_FMT_I32 && fmt != DP_FMT_U16 && fmt != DP_FMT_P16) return -16;
+  const dp_rec_layout L = dp_rec_layout_of(rec);
+  if (L.words != rec[DP_H_WORDS] || (fmt != DP_FMT_I32 && !dp_rec_fits16(rec))) return -4;
+  if (fmt == DP_FMT_P16 && dp_p16_tail_bytes(rec) > DP_P16_TAIL_MAX) return -17;
+  if (dp_rec_phys_words(rec) > avail) return -4;
+  const int64_t words = rec[DP_H_WORDS];
+  std::memcpy(out, rec, 4 * DP_H_SIZE);
+  out[DP_H_FMT] = DP_FMT_I32;
+  if (fmt == DP_FMT_I32) {
+    std::memcpy(out + DP_H_SIZE, rec + DP_H_SIZE, 4 * (size_t)(words - DP_H_SIZE));
+  } else if (fmt == DP_FMT_U16) {
+    const uint16_t* u = reinterpret_cast<const uint16_t*>(rec + DP_H_SIZE);
+    for (int64_t j = DP_H_SIZE; j < words; ++j) out[j] = u[j - DP_H_SIZE];
+  } else {
+    const uint16_t* u = reinterpret_cast<const uint16_t*>(rec + DP_H_SIZE);
+    auto get16 = [&](int32_t off, int32_t n) {
+      for (int32_t j = 0; j < n; ++j) out[off + j] = *u++;
+    };
+    get16(L.clause_lits, rec[DP_H_NCL]);
+    get16(L.card_lits, rec[DP_H_NKL]);
+    get16(L.card_bound, rec[DP_H_NK]);
+    get16(L.choice_lits, rec[DP_H_NCHL]);
+    get16(L.anchors, rec[DP_H_NA]);
+    const uint8_t* t = reinterpret_cast<const uint8_t*>(rec + DP_H_SIZE) + dp_p16_tail_at(rec);
+    auto get_lens = [&](int32_t off, int32_t n) {
+      out[off] = 0;
+      for (int32_t j = 0; j < n; ++j) out[off + j + 1] = out[off + j] + *t++;
+    };
+    get_lens(L.clause_off, rec[DP_H_NC]);
+    get_lens(L.card_off, rec[DP_H_NK]);
+    get_lens(L.var_choice_off, rec[DP_H_NV]);
+    get_lens(L.choice_off, rec[DP_H_NCH]);
+    int32_t c0 = 0, c1 = 0;
+    const int32_t nc = rec[DP_H_NC], nk = rec[DP_H_NK];
+    for (int32_t i = 0; i < rec[DP_H_NID]; ++i) {
+      if ((t[i >> 3] >> (i & 7)) & 1) {
+        if (c1 == nk) return -18;
+        out[L.card_id + c1++] = i;
+      } else {
+        if (c0 == nc) return -18;
+        out[L.clause_id + c0++] = i;
+      }
+    }
+    if (c0 != nc || c1 != nk) return -18;
+  }
+  return 0;
+}
+
 int dp_rec_validate(const int32_t* rec, int64_t words) {
   if (!rec || words < DP_H_SIZE) return -1;
   if (rec[DP_H_MAGIC] != DP_REC_MAGIC) return -2;
-  if (rec[DP_H_FMT] == DP_FMT_U16) {  // widen, then the int32 checks
+  if (rec[DP_H_FMT] == DP_FMT_U16 || rec[DP_H_FMT] == DP_FMT_P16) {  // widen, then the int32 checks
     for (int i = DP_H_NV; i <= DP_H_NCHL; ++i)
-      if (rec[i] < 0) return -3;
-    if (!dp_rec_fits16(rec) || dp_rec_layout_of(rec).words != rec[DP_H_WORDS]) return -4;
-    if (dp_rec_phys_words(rec) > words) return -4;
-    std::vector<int32_t> w((size_t)rec[DP_H_WORDS]);
-    std::memcpy(w.data(), rec, 4 * DP_H_SIZE);
-    w[DP_H_FMT] = DP_FMT_I32;
-    const uint16_t* u = reinterpret_cast<const uint16_t*>(rec + DP_H_SIZE);
-    for (size_t j = DP_H_SIZE; j < w.size(); ++j) w[j] = u[j - DP_H_SIZE];
+      if (rec[i] < 0 || rec[i] > (1 << 28)) return -3;
+    std::vector<int32_t> w((size_t)std::max<int32_t>(rec[DP_H_WORDS], DP_H_SIZE));
+    const int e = dp_rec_widen(rec, words, w.data());
+    if (e) return e;
     return dp_rec_validate(w.data(), (int64_t)w.size());
   }
   if (rec[DP_H_FMT] != DP_FMT_I32) return -16;

@@ -107,7 +107,9 @@ bool header_ok(const int32_t* h, int64_t avail) {
   if (avail < DP_H_SIZE || h[DP_H_MAGIC] != DP_REC_MAGIC) return false;
   for (int i = DP_H_NV; i <= DP_H_NCHL; ++i)
     if (h[i] < 0 || h[i] > (1 << 28)) return false;
-  if (h[DP_H_FMT] != DP_FMT_I32 && (h[DP_H_FMT] != DP_FMT_U16 || !dp_rec_fits16(h))) return false;
+  const int32_t fmt = h[DP_H_FMT];
+  if (fmt != DP_FMT_I32 && ((fmt != DP_FMT_U16 && fmt != DP_FMT_P16) || !dp_rec_fits16(h))) return false;
+  if (fmt == DP_FMT_P16 && dp_p16_tail_bytes(h) > DP_P16_TAIL_MAX) return false;
   const int64_t w = dp_rec_layout_of(h).words;
   return w == h[DP_H_WORDS] && dp_rec_phys_words(h) <= avail;
 }
@@ -180,7 +182,7 @@ void read_head(Head& H, const int32_t* h, int64_t avail, int32_t opt_flags, bool
     int k = 0;
     while (H.lds > kCeilings[k]) ++k;
     H.bucket = (int8_t)k;
-    H.direct = aligned && h[DP_H_FMT] == DP_FMT_U16;
+    H.direct = aligned && (h[DP_H_FMT] == DP_FMT_U16 || h[DP_H_FMT] == DP_FMT_P16);
     return;
   }
   const bool forced = forced_of(opt_flags);
@@ -488,22 +490,34 @@ bool stage_one(const Plan& P, const int32_t* rec, const int64_t* rec_off, int32_
   const int32_t* src = rec + rec_off[p0 + i];
   int32_t* d = dst + at;
   const int64_t words = src[DP_H_WORDS], body = words - DP_H_SIZE;
-  const bool src16 = src[DP_H_FMT] == DP_FMT_U16;
+  const int32_t fmt = src[DP_H_FMT];
   std::memcpy(d, src, 4 * DP_H_SIZE);
   if (P.narrow[(size_t)i]) {
-    d[DP_H_FMT] = src16 ? DP_FMT_U16 : DP_FMT_U16_CHECKED;
-    uint16_t* o = reinterpret_cast<uint16_t*>(d + DP_H_SIZE);
-    if (src16) {
-      std::memcpy(o, src + DP_H_SIZE, 2 * (size_t)body);  // validated by the kernel
-    } else if (!convert(src, src + DP_H_SIZE, o)) {
-      d[DP_H_FMT] = DP_FMT_REJECT;
-      return false;
+    if (fmt == DP_FMT_I32) {
+      d[DP_H_FMT] = DP_FMT_U16_CHECKED;
+      uint16_t* o = reinterpret_cast<uint16_t*>(d + DP_H_SIZE);
+      if (!convert(src, src + DP_H_SIZE, o)) {
+        d[DP_H_FMT] = DP_FMT_REJECT;
+        return false;
+      }
+      for (int64_t j = body; j < 2 * (sw - DP_H_SIZE); ++j) o[j] = 0;
+    } else {  // a 16-bit form, copied as it is (validated by the kernel)
+      const int64_t phys = dp_rec_phys_words(src);
+      std::memcpy(d + DP_H_SIZE, src + DP_H_SIZE, 4 * (size_t)(phys - DP_H_SIZE));
+      for (int64_t j = phys; j < sw; ++j) d[j] = 0;
     }
-    for (int64_t j = body; j < 2 * (sw - DP_H_SIZE); ++j) o[j] = 0;
   } else {
     d[DP_H_FMT] = DP_FMT_I32;
-    const bool ok = src16 ? convert(src, reinterpret_cast<const uint16_t*>(src + DP_H_SIZE), d + DP_H_SIZE)
-                          : convert(src, src + DP_H_SIZE, d + DP_H_SIZE);
+    bool ok;
+    if (fmt == DP_FMT_P16) {  // its int32 form, then the checked copy
+      static thread_local std::vector<int32_t> wide;
+      wide.resize((size_t)words);
+      ok = dp_rec_widen(src, rec_off[p0 + i + 1] - rec_off[p0 + i], wide.data()) == 0 &&
+           convert(src, wide.data() + DP_H_SIZE, d + DP_H_SIZE);
+    } else {
+      ok = fmt == DP_FMT_U16 ? convert(src, reinterpret_cast<const uint16_t*>(src + DP_H_SIZE), d + DP_H_SIZE)
+                             : convert(src, src + DP_H_SIZE, d + DP_H_SIZE);
+    }
     // the watch lists are built here, from the checked int32 copy
     if (!ok) {
       d[DP_H_FMT] = DP_FMT_REJECT;
@@ -1346,6 +1360,10 @@ int dp_stage_roundtrip(const dp_batch* b, int32_t opt_flags, int32_t chunk_probl
       const int64_t words = src[DP_H_WORDS];
       wide.resize((size_t)words);
       std::memcpy(wide.data(), st, 4 * DP_H_SIZE);
+      if (src[DP_H_FMT] == DP_FMT_P16) {  // staged as it is (one-wavefront), else not shown
+        if (st[DP_H_FMT] == DP_FMT_P16) std::memcpy(o, st, 4 * (size_t)dp_rec_phys_words(src));
+        continue;
+      }
       if (st[DP_H_FMT] == DP_FMT_U16 || st[DP_H_FMT] == dp::DP_FMT_U16_CHECKED) {
         const uint16_t* u = reinterpret_cast<const uint16_t*>(st + DP_H_SIZE);
         for (int64_t j = DP_H_SIZE; j < words; ++j) wide[(size_t)j] = u[j - DP_H_SIZE];

@@ -333,37 +333,22 @@ struct Group {
     nrows = nc + nk;
     nbv = bits_words(nv); nbi = bits_words(nid);
     const IX* body;
+    bool packed = false;
     if constexpr (MODE == M_LDS) {
-      // the record -> LDS uint16 with dwordx4 loads (staged records are
-      // 16-byte aligned and padded to 4 words).  The host stages LDS-path
-      // records in 16-bit form (DP_FMT_U16): they are copied as they are.
+      // The record -> LDS, as it is: the host stages one-wavefront records in
+      // a 16-bit form (DP_FMT_U16, or DP_FMT_P16 whose tail is decoded below),
+      // 16-byte aligned and padded to 4 words.
       IX* b = reinterpret_cast<IX*>(lds + L.body);
       const int4* src = reinterpret_cast<const int4*>(grec + DP_H_SIZE);
-      if (h[DP_H_FMT] == DP_FMT_U16 || h[DP_H_FMT] == DP_FMT_U16_CHECKED) {
-        const int groups = (h[DP_H_WORDS] - DP_H_SIZE + 7) >> 3;
-        if (L.body == 0 && ((groups + 63) >> 6) * 1024 <= L.lds_bytes) {
-          // LDS-DMA, every 1 KiB piece in flight at once (lanes past the
-          // image re-read its last piece into LDS the later arrays own; they
-          // are initialised after this)
-          for (int c = 0; c < groups; c += 64) {
-            const int i = min(c + lane, groups - 1);
-            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src + i),
-                                             (__attribute__((address_space(3))) void*)(lds + 16 * c), 16, 0, 0);
-          }
-          __builtin_amdgcn_s_waitcnt(0);
-          wsync();
-        } else {
-          for (int i = tid; i < groups; i += NT) reinterpret_cast<int4*>(b)[i] = src[i];
-          wsync();
-        }
-      } else {
-      const int groups = (h[DP_H_WORDS] - DP_H_SIZE + 3) >> 2;
+      const int fmt = h[DP_H_FMT];
+      packed = fmt == DP_FMT_P16;
+      if (!packed && fmt != DP_FMT_U16 && fmt != DP_FMT_U16_CHECKED) return false;
+      const int groups = packed ? (int)((p16_tail_at(h) + p16_tail_bytes(h) + 15) >> 4)
+                                : (h[DP_H_WORDS] - DP_H_SIZE + 7) >> 3;
       if (L.body == 0 && ((groups + 63) >> 6) * 1024 <= L.lds_bytes) {
-        // Stage the int32 image into the allocation with LDS-DMA (every
-        // 1 KiB piece in flight at once: one memory latency), then narrow it
-        // in place: piece c is read from [1024c, +1024) and written to
-        // [512c, +512), below every piece not yet read.  The arrays the
-        // staging overwrites are initialised after this.
+        // LDS-DMA, every 1 KiB piece in flight at once (lanes past the image
+        // re-read its last piece into LDS the later arrays own; they are
+        // initialised after this)
         for (int c = 0; c < groups; c += 64) {
           const int i = min(c + lane, groups - 1);
           __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src + i),
@@ -371,34 +356,39 @@ struct Group {
         }
         __builtin_amdgcn_s_waitcnt(0);
         wsync();
-        for (int c = 0; c < groups; c += 64) {
-          const int i = c + lane;
-          const int4 x = reinterpret_cast<const int4*>(lds)[min(i, groups - 1)];
-          if (i < groups) {  // the store depends on the load: this piece is read first
-            uint2 y;
-            y.x = (uint32_t)(x.x & 0xffff) | ((uint32_t)x.y << 16);
-            y.y = (uint32_t)(x.z & 0xffff) | ((uint32_t)x.w << 16);
-            reinterpret_cast<uint2*>(b)[i] = y;
-          }
-        }
-      } else
-      for (int i = tid; i < groups; i += NT) {
-        const int4 x = src[i];
-        uint2 y;
-        y.x = (uint32_t)(x.x & 0xffff) | ((uint32_t)x.y << 16);
-        y.y = (uint32_t)(x.z & 0xffff) | ((uint32_t)x.w << 16);
-        reinterpret_cast<uint2*>(b)[i] = y;
-      }
+      } else {
+        for (int i = tid; i < groups; i += NT) reinterpret_cast<int4*>(b)[i] = src[i];
+        wsync();
       }
       body = b;
+      if (packed) {
+        // DP_FMT_P16 in LDS: the uint16 arrays where they landed, then the
+        // offsets arrays and the identities decoded from the tail
+        IX* q = b;
+        clause_lits = q; q += ncl;
+        card_lits = q;   q += nkl;
+        card_bound = q;  q += nk;
+        choice_lits = q; q += nchl;
+        anchors = q;     q += na;
+        clause_off = q;  q += nc + 1;
+        card_off = q;    q += nk + 1;
+        var_choice_off = q; q += nv + 1;
+        choice_off = q;  q += nch + 1;
+        clause_id = q;   q += nc;
+        card_id = q;
+        if (!unpack16(reinterpret_cast<const char*>(b) + p16_tail_at(h), (int)p16_tail_bytes(h)))
+          return false;
+      }
     } else {
       body = reinterpret_cast<const IX*>(grec + DP_H_SIZE);  // read in place (read-only)
     }
     auto rv = [&](int32_t word_off) { return body + (word_off - DP_H_SIZE); };
-    clause_off = rv(R.clause_off); clause_lits = rv(R.clause_lits); clause_id = rv(R.clause_id);
-    card_off = rv(R.card_off); card_lits = rv(R.card_lits); card_bound = rv(R.card_bound);
-    card_id = rv(R.card_id); var_choice_off = rv(R.var_choice_off); choice_off = rv(R.choice_off);
-    choice_lits = rv(R.choice_lits); anchors = rv(R.anchors);
+    if (!packed) {
+      clause_off = rv(R.clause_off); clause_lits = rv(R.clause_lits); clause_id = rv(R.clause_id);
+      card_off = rv(R.card_off); card_lits = rv(R.card_lits); card_bound = rv(R.card_bound);
+      card_id = rv(R.card_id); var_choice_off = rv(R.var_choice_off); choice_off = rv(R.choice_off);
+      choice_lits = rv(R.choice_lits); anchors = rv(R.anchors);
+    }
     nwatch = h[DP_H_NCL] + h[DP_H_NKL];
     dthr = nrows + L_MAX;
     char* hot = MODE == M_HBM ? hbm : lds;   // val and the bitsets
@@ -450,7 +440,7 @@ struct Group {
     sub[0] = ti1 - ti0;
 #endif
     if constexpr (MODE == M_LDS)
-      if (h[DP_H_FMT] == DP_FMT_U16 && !valid_record()) return false;
+      if ((h[DP_H_FMT] == DP_FMT_U16 || packed) && !valid_record(body)) return false;
 #ifdef DP_STAMPS
     const int64_t ti2 = stamp();
     sub[1] = ti2 - ti1;
@@ -490,10 +480,10 @@ struct Group {
   // in an AtMost row form one run (16-bit bounds cannot be negative).  The
   // host checked every other staged form (DP_FMT_U16_CHECKED, DP_FMT_I32).
   // Array by array, two 16-bit words per LDS load.  Group-uniform result.
-  __device__ __forceinline__ bool valid_record() {
+  __device__ __forceinline__ bool valid_record(const IX* base) {
     static_assert(MODE == M_LDS, "16-bit records run one wavefront per problem");
-    const IX* base = clause_off;  // the body's first array
-    const uint32_t* b32 = reinterpret_cast<const uint32_t*>(base);  // (16-byte aligned)
+    // (base: the body's start, 16-byte aligned; arrays anywhere after it)
+    const uint32_t* b32 = reinterpret_cast<const uint32_t*>(base);
     bool bad = false;
     auto range = [&](const IX* arr, int n, int hi) {
       const int a = (int)(arr - base), e = a + n;
@@ -532,6 +522,69 @@ struct Group {
       }
     }
     return !g_any(bad);
+  }
+
+  // DP_FMT_P16 tail (include/deppy_hip.h) -> the offsets arrays and the row
+  // identities, in place after the uint16 arrays.  The tail (at most
+  // DP_P16_TAIL_MAX bytes) is first read into registers, 16 bytes a lane,
+  // since the decoded arrays overwrite it; a byte of it is then fetched from
+  // its lane by ds_bpermute.  Lengths become offsets by a DPP scan, the mask
+  // becomes clause / AtMost identities by ballot ranks.  False when the mask
+  // does not have nc clear and nk set bits (a malformed record).
+  __device__ __forceinline__ bool unpack16(const char* tail, int tb) {
+    static_assert(MODE == M_LDS, "16-bit records run one wavefront per problem");
+    uint4 r = make_uint4(0u, 0u, 0u, 0u);
+    if (16 * lane < tb) r = *reinterpret_cast<const uint4*>(tail + 16 * lane);
+    wsync();
+    auto tbyte = [&](int i) -> int {  // wave-converged; i in [0, DP_P16_TAIL_MAX)
+      const int q = (i >> 4) & 63, sel = (i >> 2) & 3;
+      const uint32_t d0 = (uint32_t)__shfl((int)r.x, q), d1 = (uint32_t)__shfl((int)r.y, q);
+      const uint32_t d2 = (uint32_t)__shfl((int)r.z, q), d3 = (uint32_t)__shfl((int)r.w, q);
+      const uint32_t d = sel == 0 ? d0 : sel == 1 ? d1 : sel == 2 ? d2 : d3;
+      return (int)((d >> ((i & 3) * 8)) & 0xffu);
+    };
+    int at = 0;
+    auto lens = [&](const IX* off_c, int n) {
+      IX* off = const_cast<IX*>(off_c);
+      int carry = 0;
+      for (int c = 0; c < n; c += 64) {
+        const int j = c + lane;
+        const int x = tbyte(at + min(j, n - 1));
+        const int incl = wave_incl_scan(j < n ? x : 0) + carry;
+        if (j < n) off[j + 1] = enc(incl);
+        carry = __builtin_amdgcn_readlane(incl, 63);
+      }
+      if (lane == 0) off[0] = enc(0);
+      at += n;
+    };
+    lens(clause_off, nc);
+    lens(card_off, nk);
+    lens(var_choice_off, nv);
+    lens(choice_off, nch);
+    IX* cid = const_cast<IX*>(clause_id);
+    IX* kid = const_cast<IX*>(card_id);
+    int c0 = 0, c1 = 0;
+    const uint64_t lt = lanemask_lt();
+    for (int c = 0; c < nid; c += 64) {
+      const int i = c + lane;
+      const bool valid = i < nid;
+      const int byte = tbyte(at + (min(i, nid - 1) >> 3));
+      const bool bit = valid && ((byte >> (i & 7)) & 1);
+      const uint64_t mb = __ballot(bit), mv = __ballot(valid);
+      if (valid) {
+        if (bit) {
+          const int k = c1 + __popcll(mb & lt);
+          if (k < nk) kid[k] = enc(i);
+        } else {
+          const int k = c0 + __popcll(~mb & mv & lt);
+          if (k < nc) cid[k] = enc(i);
+        }
+      }
+      c1 += __popcll(mb);
+      c0 += __popcll(~mb & mv);
+    }
+    wsync();
+    return c0 == nc && c1 == nk;
   }
 
   // Watch lists of a one-wavefront problem, built in LDS from its record

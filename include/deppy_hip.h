@@ -156,13 +156,41 @@ static inline dp_rec_layout dp_rec_layout_of(const int32_t* h) {
  * record occupies dp_rec_phys_words() int32 words; this is the form the GPU
  * stages for one-wavefront problems, and dp_lower_into(DP_LOWER_NARROW)
  * emits it for every record that fits (dp_rec_fits16), so that staging is a
- * copy.  Offsets (rec_off) always count int32 words. */
+ * copy.  Offsets (rec_off) always count int32 words.
+ *
+ * DP_FMT_P16 (dp_lower_into DP_LOWER_PACKED): the 16-bit form with every
+ * offsets array sent as byte lengths and the row identities as a bit mask,
+ * about a fifth fewer bytes to cross PCIe than DP_FMT_U16.  After the header:
+ *   uint16 clause_lits[ncl], card_lits[nkl], card_bound[nk], choice_lits[nchl],
+ *          anchors[na]
+ *   zero padding to a 16-byte boundary (from the body's start)
+ *   uint8  clause_len[nc], card_len[nk], var_choice_len[nv], choice_len[nch]
+ *          (the differences of the offsets arrays, each below 256)
+ *   uint8  card_mask[(nid+7)/8]: bit i (LSB first) set iff identity i is an
+ *          AtMost row's.  Every identity has exactly one row (nid == nc + nk)
+ *          and each row kind lists its identities in ascending order, so
+ *          clause_id is the clear bits in order and card_id the set ones.
+ * The lengths and the mask together are at most DP_P16_TAIL_MAX bytes (the
+ * kernel decodes them from one 16-byte load per lane).  DP_H_WORDS stays the
+ * int32 form's length.  dp_rec_widen gives the int32 form of any record. */
 enum { DP_H_FMT = 13 };
-enum { DP_FMT_I32 = 0, DP_FMT_U16 = 1 };
+enum { DP_FMT_I32 = 0, DP_FMT_U16 = 1, DP_FMT_P16 = 3 };
+enum { DP_P16_TAIL_MAX = 1024 };
+
+/* DP_FMT_P16: uint16 words before the padding, byte offset of the lengths
+ * (from the body's start), and bytes of lengths plus mask. */
+static inline int64_t dp_p16_nu16(const int32_t* h) {
+  return (int64_t)h[DP_H_NCL] + h[DP_H_NKL] + h[DP_H_NK] + h[DP_H_NCHL] + h[DP_H_NA];
+}
+static inline int64_t dp_p16_tail_at(const int32_t* h) { return (2 * dp_p16_nu16(h) + 15) & ~(int64_t)15; }
+static inline int64_t dp_p16_tail_bytes(const int32_t* h) {
+  return (int64_t)h[DP_H_NC] + h[DP_H_NK] + h[DP_H_NV] + h[DP_H_NCH] + ((int64_t)h[DP_H_NID] + 7) / 8;
+}
 
 static inline int64_t dp_rec_phys_words(const int32_t* h) {
-  return h[DP_H_FMT] == DP_FMT_U16 ? DP_H_SIZE + ((int64_t)h[DP_H_WORDS] - DP_H_SIZE + 1) / 2
-                                   : (int64_t)h[DP_H_WORDS];
+  if (h[DP_H_FMT] == DP_FMT_U16) return DP_H_SIZE + ((int64_t)h[DP_H_WORDS] - DP_H_SIZE + 1) / 2;
+  if (h[DP_H_FMT] == DP_FMT_P16) return DP_H_SIZE + (dp_p16_tail_at(h) + dp_p16_tail_bytes(h) + 3) / 4;
+  return (int64_t)h[DP_H_WORDS];
 }
 
 /* Does every index the record holds, and every value the solve stores per
@@ -174,10 +202,14 @@ static inline int dp_rec_fits16(const int32_t* h) {
          h[DP_H_NCL] + h[DP_H_NKL] < 65000;
 }
 
-/* Validate one record of either form (bounds of every index).  Returns 0 if
+/* Validate one record of any form (bounds of every index).  Returns 0 if
  * well formed.  The solve checks every record the same way on the device, so
  * a malformed record yields DP_ERROR with DP_F_MALFORMED, never a fault. */
 int dp_rec_validate(const int32_t* rec, int64_t words);
+/* The int32 form (DP_FMT_I32, DP_H_WORDS words into out) of a record of any
+ * form that occupies at most `avail` words.  Returns 0, or < 0 when the
+ * header or a DP_FMT_P16 length / mask is inconsistent. */
+int dp_rec_widen(const int32_t* rec, int64_t avail, int32_t* out);
 
 /* ------------------------------------------------------------------------ */
 /* Lowering: wire -> records                                                  */
@@ -198,8 +230,10 @@ int dp_lower(const dp_wire* wire, dp_lowered** out);
  * rec_off); DP_LOWER_PINNED keeps the records in page-locked host memory
  * when a HIP device is present (dp_lowered_pinned).  A batch of both is
  * copied to the device by DMA from where it lies: dp_submit stages only
- * chunks that need another form.  Returns 0 or -1. */
-enum { DP_LOWER_NARROW = 1, DP_LOWER_PINNED = 2 };
+ * chunks that need another form.  DP_LOWER_PACKED (with DP_LOWER_NARROW)
+ * emits the DP_FMT_P16 form for the records that allow it, the DP_FMT_U16
+ * form for the other 16-bit ones.  Returns 0 or -1. */
+enum { DP_LOWER_NARROW = 1, DP_LOWER_PINNED = 2, DP_LOWER_PACKED = 4 };
 int dp_lower_into(const dp_wire* wire, int32_t flags, dp_lowered* lw);
 dp_lowered* dp_lowered_new(void); /* an empty result for dp_lower_into */
 void dp_lowered_free(dp_lowered* lw);

@@ -133,18 +133,45 @@ static int row_ident(const prob_t* p, int r) {
 
 static void* xcalloc(size_t n, size_t sz) { return calloc(n ? n : 1, sz); }
 
-/* A record in the 16-bit form (header word DP_H_FMT = DP_FMT_U16, every body
- * word a uint16) widened to int32 words in *tmp (freed by the caller);
- * int32 records are returned as they are. */
+/* A record in a 16-bit form widened to int32 words in *tmp (freed by the
+ * caller); int32 records are returned as they are.  DP_FMT_U16: every body
+ * word a uint16.  DP_FMT_P16 (include/deppy_hip.h): the uint16 arrays, then
+ * byte lengths of the offsets arrays and the AtMost-identity bit mask (a
+ * mask with the wrong number of set bits leaves the ids it cannot place 0;
+ * records are validated before the oracle sees them). */
 static const int32_t* widen(const int32_t* rec, int32_t** tmp) {
   *tmp = NULL;
-  if (rec[DP_H_FMT] != DP_FMT_U16) return rec;
+  if (rec[DP_H_FMT] != DP_FMT_U16 && rec[DP_H_FMT] != DP_FMT_P16) return rec;
   int32_t w = rec[DP_H_WORDS];
   int32_t* o = xcalloc((size_t)w, sizeof(int32_t));
   memcpy(o, rec, DP_H_SIZE * sizeof(int32_t));
   o[DP_H_FMT] = DP_FMT_I32;
   const uint16_t* u = (const uint16_t*)(rec + DP_H_SIZE);
-  for (int32_t j = DP_H_SIZE; j < w; ++j) o[j] = u[j - DP_H_SIZE];
+  if (rec[DP_H_FMT] == DP_FMT_U16) {
+    for (int32_t j = DP_H_SIZE; j < w; ++j) o[j] = u[j - DP_H_SIZE];
+  } else {
+    const dp_rec_layout L = dp_rec_layout_of(rec);
+    const int32_t nc = rec[DP_H_NC], nk = rec[DP_H_NK];
+    const int32_t n16[5] = {rec[DP_H_NCL], rec[DP_H_NKL], nk, rec[DP_H_NCHL], rec[DP_H_NA]};
+    const int32_t at16[5] = {L.clause_lits, L.card_lits, L.card_bound, L.choice_lits, L.anchors};
+    for (int a = 0; a < 5; ++a)
+      for (int32_t j = 0; j < n16[a]; ++j) o[at16[a] + j] = *u++;
+    const uint8_t* t = (const uint8_t*)(rec + DP_H_SIZE) + dp_p16_tail_at(rec);
+    const int32_t nl[4] = {nc, nk, rec[DP_H_NV], rec[DP_H_NCH]};
+    const int32_t atl[4] = {L.clause_off, L.card_off, L.var_choice_off, L.choice_off};
+    for (int a = 0; a < 4; ++a) {
+      o[atl[a]] = 0;
+      for (int32_t j = 0; j < nl[a]; ++j) o[atl[a] + j + 1] = o[atl[a] + j] + *t++;
+    }
+    int32_t c0 = 0, c1 = 0;
+    for (int32_t i = 0; i < rec[DP_H_NID]; ++i) {
+      if ((t[i >> 3] >> (i & 7)) & 1) {
+        if (c1 < nk) o[L.card_id + c1++] = i;
+      } else if (c0 < nc) {
+        o[L.clause_id + c0++] = i;
+      }
+    }
+  }
   *tmp = o;
   return o;
 }

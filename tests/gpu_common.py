@@ -4,14 +4,16 @@ import numpy as np
 from deppy_amd import _lib
 
 
-def lowered_config(config, n, seed, narrow=False, pinned=False):
+def lowered_config(config, n, seed, narrow=False, pinned=False, packed=False):
     """Synthetic catalogs (SURVEY §8(d) generator) lowered by dp_lower;
-    narrow: records that fit 16 bits in the DP_FMT_U16 form; pinned: in
-    page-locked memory (with a GPU)."""
+    narrow: records that fit 16 bits in the DP_FMT_U16 form (packed: the
+    DP_FMT_P16 form where it applies); pinned: in page-locked memory (with a
+    GPU)."""
     w = _lib.generate(config, n, seed)
     return _lib.Lowered(_lib.WireArrays(**{k: w[k] for k in (
         "prob_var_off", "var_id", "var_con_off", "con_kind", "con_n", "con_arg_off", "con_arg",
-        "str_off")}, str_bytes=w["str_bytes"].tobytes()), narrow=narrow, pinned=pinned)
+        "str_off")}, str_bytes=w["str_bytes"].tobytes()), narrow=narrow or packed, pinned=pinned,
+        packed=packed)
 
 
 def corrupt16(rec_off, rec, p, kind):
@@ -39,12 +41,39 @@ def corrupt16(rec_off, rec, p, kind):
     return True
 
 
+def unpack_p16(r):
+    """The int32 form of one DP_FMT_P16 record (include/deppy_hip.h), restated
+    here independently of the library's dp_rec_widen."""
+    nv, nc, nk, nch, na, nid, ncl, nkl, nchl, words = (int(r[i]) for i in range(1, 11))
+    u = r[16:].view(np.uint16)
+    o, parts16 = 0, []
+    for n in (ncl, nkl, nk, nchl, na):
+        parts16.append(u[o:o + n].astype(np.int32))
+        o += n
+    cl, kl, kb, chl, anc = parts16
+    tail_at = (2 * o + 15) // 16 * 16
+    t = r[16:].view(np.uint8)[tail_at:]
+    offs, o = [], 0
+    for n in (nc, nk, nv, nch):
+        offs.append(np.concatenate([[0], np.cumsum(t[o:o + n].astype(np.int32))]).astype(np.int32))
+        o += n
+    bits = np.unpackbits(t[o:o + (nid + 7) // 8], bitorder="little")[:nid].astype(bool)
+    ids = np.arange(nid, dtype=np.int32)
+    cid, kid = ids[~bits], ids[bits]
+    out = np.concatenate([r[:16], offs[0], cl, cid, offs[1], kl, kb, kid, offs[2], offs[3], chl, anc]).astype(np.int32)
+    out[13] = 0
+    assert len(out) == words
+    return out
+
+
 def widen(rec_off, rec):
-    """A batch with every DP_FMT_U16 record widened to int32 (-> rec_off, rec)."""
+    """A batch with every 16-bit-form record widened to int32 (-> rec_off, rec)."""
     parts, offs = [], [0]
     for p in range(len(rec_off) - 1):
         r = rec[rec_off[p]:rec_off[p + 1]]
-        if len(r) and r[13] == 1:
+        if len(r) and r[13] == 3:
+            r = unpack_p16(r)
+        elif len(r) and r[13] == 1:
             words = int(r[10])
             body = r[16:].view(np.uint16)[:words - 16].astype(np.int32)
             r = np.concatenate([r[:16], body])

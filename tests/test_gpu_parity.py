@@ -339,3 +339,57 @@ def test_malformed_16bit_records_found_by_the_kernel(pinned):
         assert g["status"][p] == -2 and g["flags"][p] == 512 and g["core_len"][p] == 0, p
     for k in ("status", "flags", "steps"):
         np.testing.assert_array_equal(g[k][ok], ref[k][ok])
+
+
+@pytest.mark.parametrize("config,n,seed,flags", [(2, 3000, 101, 0), (3, 9000, 102, 0), (5, 300, 103, 0),
+                                                 (2, 200, 104, _lib.OPT_FORCE_GROUP)],
+                         ids=["c2", "c3", "c5", "c2-group"])
+def test_packed_records_bit_exact(config, n, seed, flags):
+    """DP_FMT_P16 records (dp_lower_into DP_LOWER_PACKED), copied to the device
+    as they lie and decoded by the kernel (or widened on the host for a
+    multi-wave placement), solve exactly like their int32 form and the oracle."""
+    a = lowered_config(config, n, seed)
+    b = lowered_config(config, n, seed, packed=True, pinned=True)
+    c = _lib.Context(0, 1, flags=flags)
+    try:
+        gb = c.submit(b.rec_off, b.rec).wait()
+        direct = c.stats()["direct_chunks"]
+        ga = c.solve(a.rec_off, a.rec)
+    finally:
+        c.close()
+    if flags == 0 and config != 5:
+        assert direct > 0
+    assert compare_results(gb, ga, n) == []
+    o = oracle.solve_batch(a.rec_off, a.rec, 0, 16)
+    assert compare_results(gb, o, n) == []
+
+
+def test_malformed_packed_records_found_by_the_kernel():
+    """Packed records are validated on the device: a wrong identity mask, row
+    lengths that do not sum to the total, an out-of-range literal -> DP_ERROR
+    + DP_F_MALFORMED for that problem only."""
+    lw = lowered_config(2, 40, 111, packed=True, pinned=True)
+    ref = oracle.solve_batch(lw.rec_off, lw.rec, 0, 16)
+    rec = lw.rec
+    bad = [5, 12, 27]
+    for p, kind in zip(bad, ("mask", "len", "lit")):
+        r = rec[lw.rec_off[p]:lw.rec_off[p + 1]]
+        nv, nc, nk, nch, na, nid, ncl, nkl, nchl = (int(r[i]) for i in range(1, 10))
+        tail = (2 * (ncl + nkl + nk + nchl + na) + 15) // 16 * 16
+        t = r[16:].view(np.uint8)
+        if kind == "mask":
+            t[tail + nc + nk + nv + nch] ^= 1
+        elif kind == "len":
+            t[tail] += 1
+        else:
+            r[16:].view(np.uint16)[0] = 2 * nv + 1
+    c = _lib.Context(0, 1)
+    try:
+        g = c.solve(lw.rec_off, rec)
+    finally:
+        c.close()
+    ok = [p for p in range(lw.n) if p not in bad]
+    for p in bad:
+        assert g["status"][p] == -2 and g["flags"][p] == 512 and g["core_len"][p] == 0, p
+    for k in ("status", "flags", "steps"):
+        np.testing.assert_array_equal(g[k][ok], ref[k][ok])

@@ -173,3 +173,71 @@ def test_narrow_records_on_16_byte_boundaries(config, n):
     import torch
     if not torch.cuda.is_available():
         assert not b.pinned
+
+
+# ---------------------------------------------------------------------------
+# DP_FMT_P16: the packed 16-bit form (byte lengths + identity mask)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("config,n", [(2, 200), (3, 800), (5, 60), (4, 1)])
+def test_packed_lowering_is_the_int32_record(config, n):
+    """dp_lower_into(DP_LOWER_PACKED) emits exactly the int32 records (widened
+    by an independent restatement of the format), in the DP_FMT_P16 form
+    wherever it applies; dp_rec_widen and dp_rec_validate agree."""
+    from tests.gpu_common import unpack_p16, widen
+    a = lowered_config(config, n, 17)
+    b = lowered_config(config, n, 17, packed=True)
+    off, rec = widen(b.rec_off, b.rec)
+    np.testing.assert_array_equal(off, a.rec_off)
+    np.testing.assert_array_equal(rec, a.rec)
+    fmt = b.rec[b.rec_off[:-1] + 13]
+    if config in (2, 3):
+        assert np.all(fmt == 3)
+        assert b.rec_off[-1] < 0.8 * lowered_config(config, n, 17, narrow=True).rec_off[-1]
+    assert np.all(b.rec_off % 4 == 0)
+    L = _lib.lib()
+    for p in range(n):
+        r = np.ascontiguousarray(b.record(p))
+        out = np.zeros(int(r[10]), np.int32)
+        assert L.dp_rec_widen(r.ctypes.data_as(_lib.c_i32p), len(r), out.ctypes.data_as(_lib.c_i32p)) == 0
+        np.testing.assert_array_equal(out, a.record(p))
+        assert L.dp_rec_validate(r.ctypes.data_as(_lib.c_i32p), len(r)) == 0
+        if r[13] == 3:
+            np.testing.assert_array_equal(unpack_p16(r), a.record(p))
+
+
+def test_packed_malformed_is_rejected():
+    """A mask with the wrong number of AtMost identities, lengths that do not
+    sum to the row total, an out-of-range literal: dp_rec_validate rejects
+    each (the kernel checks the same, tests/test_gpu_parity.py)."""
+    b = lowered_config(2, 4, 41, packed=True)
+    L = _lib.lib()
+    r0 = np.ascontiguousarray(b.record(1)).copy()
+    assert r0[13] == 3
+    nv, nc, nk, nch, na, nid, ncl, nkl, nchl = (int(r0[i]) for i in range(1, 10))
+    nu16 = ncl + nkl + nk + nchl + na
+    tail = (2 * nu16 + 15) // 16 * 16
+    def bad(r):
+        return L.dp_rec_validate(np.ascontiguousarray(r).ctypes.data_as(_lib.c_i32p), len(r)) != 0
+    r = r0.copy(); t = r[16:].view(np.uint8); t[tail + nc + nk + nv + nch] ^= 1      # mask: one bit flipped
+    assert bad(r)
+    r = r0.copy(); t = r[16:].view(np.uint8); t[tail] += 1                           # clause lengths: sum != ncl
+    assert bad(r)
+    r = r0.copy(); r[16:].view(np.uint16)[0] = 2 * nv + 1                             # clause literal past 2nv
+    assert bad(r)
+    assert not bad(r0)
+
+
+def test_oracle_reads_packed_records():
+    from oracle import oracle
+    a = lowered_config(5, 60, 29)
+    b = lowered_config(5, 60, 29, packed=True)
+    oa = oracle.solve_batch(a.rec_off, a.rec)
+    ob = oracle.solve_batch(b.rec_off, b.rec)
+    for k in ("status", "flags", "installed", "core", "core_len", "steps"):
+        np.testing.assert_array_equal(oa[k], ob[k])
+
+
+def test_stage_roundtrip_packed_source():
+    lw = lowered_config(2, 120, 23, packed=True)
+    out, _ = _lib.stage_roundtrip(lw.rec_off, lw.rec, chunk_problems=50)
+    np.testing.assert_array_equal(out, lw.rec)
