@@ -22,6 +22,7 @@
 
 #include "common.hpp"
 #include "hostmem.hpp"
+#include "placement.hpp"
 #include "pool.hpp"
 
 namespace dp {
@@ -356,7 +357,14 @@ struct Lowerer {
     int32_t* r = O.rec.data() + base;
     const int64_t words = r[DP_H_WORDS];
     int64_t phys = words;
-    if (packed && pack16(r)) {
+    if (!one_wave(r)) {  // a multi-wave problem: its staged form, with watch lists
+      const int64_t ext = 2 * (int64_t)r[DP_H_NV] + 1 + r[DP_H_NCL] + r[DP_H_NKL];
+      O.extend((size_t)ext);  // (may move the storage)
+      r = O.rec.data() + base;
+      build_watches_host(r);
+      r[DP_H_FMT] = DP_FMT_I32W;
+      phys = words + ext;
+    } else if (packed && pack16(r)) {
       phys = dp_rec_phys_words(r);
     } else if (dp_rec_fits16(r)) {
       uint16_t* u = reinterpret_cast<uint16_t*>(r + DP_H_SIZE);
@@ -366,8 +374,9 @@ struct Lowerer {
       phys = dp_rec_phys_words(r);
     }
     const int64_t padded = (phys + 3) & ~3LL;
-    O.nrec = base + (size_t)std::min(words, padded);
-    if (padded > words) O.extend((size_t)(padded - words));  // (may move the storage)
+    const int64_t have = (int64_t)(O.nrec - base);  // words appended for the record so far
+    O.nrec = base + (size_t)std::min(have, padded);
+    if (padded > have) O.extend((size_t)(padded - have));  // (may move the storage)
     r = O.rec.data() + base;
     for (int64_t j = phys; j < padded; ++j) r[j] = 0;
     O.rec_len.back() = padded;
@@ -1130,15 +1139,15 @@ int dp_rec_widen(const int32_t* rec, int64_t avail, int32_t* out) {
   for (int i = DP_H_NV; i <= DP_H_NCHL; ++i)
     if (rec[i] < 0 || rec[i] > (1 << 28)) return -3;
   const int32_t fmt = rec[DP_H_FMT];
-  if (fmt != DP_FMT_I32 && fmt != DP_FMT_U16 && fmt != DP_FMT_P16) return -16;
+  if (fmt != DP_FMT_I32 && fmt != DP_FMT_U16 && fmt != DP_FMT_P16 && fmt != DP_FMT_I32W) return -16;
   const dp_rec_layout L = dp_rec_layout_of(rec);
-  if (L.words != rec[DP_H_WORDS] || (fmt != DP_FMT_I32 && !dp_rec_fits16(rec))) return -4;
+  if (L.words != rec[DP_H_WORDS] || ((fmt == DP_FMT_U16 || fmt == DP_FMT_P16) && !dp_rec_fits16(rec))) return -4;
   if (fmt == DP_FMT_P16 && dp_p16_tail_bytes(rec) > DP_P16_TAIL_MAX) return -17;
   if (dp_rec_phys_words(rec) > avail) return -4;
   const int64_t words = rec[DP_H_WORDS];
   std::memcpy(out, rec, 4 * DP_H_SIZE);
   out[DP_H_FMT] = DP_FMT_I32;
-  if (fmt == DP_FMT_I32) {
+  if (fmt == DP_FMT_I32 || fmt == DP_FMT_I32W) {
     std::memcpy(out + DP_H_SIZE, rec + DP_H_SIZE, 4 * (size_t)(words - DP_H_SIZE));
   } else if (fmt == DP_FMT_U16) {
     const uint16_t* u = reinterpret_cast<const uint16_t*>(rec + DP_H_SIZE);
@@ -1181,6 +1190,23 @@ int dp_rec_widen(const int32_t* rec, int64_t avail, int32_t* out) {
 int dp_rec_validate(const int32_t* rec, int64_t words) {
   if (!rec || words < DP_H_SIZE) return -1;
   if (rec[DP_H_MAGIC] != DP_REC_MAGIC) return -2;
+  if (rec[DP_H_FMT] == DP_FMT_I32W) {  // the watch lists' bounds, then the record's checks
+    for (int i = DP_H_NV; i <= DP_H_NCHL; ++i)
+      if (rec[i] < 0 || rec[i] > (1 << 28)) return -3;
+    if (dp_rec_layout_of(rec).words != rec[DP_H_WORDS] || dp_rec_phys_words(rec) > words) return -4;
+    const int64_t n2 = 2 * (int64_t)rec[DP_H_NV], cap = (int64_t)rec[DP_H_NCL] + rec[DP_H_NKL];
+    const int32_t* wo = rec + rec[DP_H_WORDS];
+    const int32_t* w = wo + n2 + 1;
+    if (wo[0] != 0 || wo[n2] > cap) return -19;
+    for (int64_t l = 0; l < n2; ++l)
+      if (wo[l + 1] < wo[l]) return -19;
+    const int64_t nrows = (int64_t)rec[DP_H_NC] + rec[DP_H_NK];
+    for (int64_t j = 0; j < wo[n2]; ++j)
+      if (w[j] < 0 || w[j] >= nrows) return -19;
+    std::vector<int32_t> t(rec, rec + rec[DP_H_WORDS]);
+    t[DP_H_FMT] = DP_FMT_I32;
+    return dp_rec_validate(t.data(), (int64_t)t.size());
+  }
   if (rec[DP_H_FMT] == DP_FMT_U16 || rec[DP_H_FMT] == DP_FMT_P16) {  // widen, then the int32 checks
     for (int i = DP_H_NV; i <= DP_H_NCHL; ++i)
       if (rec[i] < 0 || rec[i] > (1 << 28)) return -3;

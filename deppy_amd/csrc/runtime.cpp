@@ -43,11 +43,12 @@
 #include "kernel_api.hpp"
 #include "layout.hpp"
 #include "hostmem.hpp"
+#include "placement.hpp"
 #include "pool.hpp"
 
 namespace {
 
-constexpr int kMaxLdsBytes = 160 * 1024;          // LDS per CU on gfx950
+using dp::kMaxLdsBytes;  // (placement.hpp)
 constexpr int64_t kDefaultBudget = 1 << 16;        // BCP invocations per problem
 // LDS bucket ceilings (bytes); one launch per non-empty bucket after merging.
 // (160 KiB / 10, / 5, / 3, / 2, / 1.  Config 5, 30 steps: 588k res/s with
@@ -57,11 +58,6 @@ constexpr int kCeilings[] = {16 << 10, 32 << 10, 53 << 10, 80 << 10, 160 << 10};
 constexpr int kNBuckets = (int)(sizeof(kCeilings) / sizeof(kCeilings[0]));
 constexpr int kLanes = 4;            // streams per device, one per hardware queue
 constexpr double kMergeRatio = 0.5;  // bucket merging (plan_chunk)
-// Problems whose one-wavefront LDS footprint exceeds kGroupAbove run as
-// multi-wave workgroups: at two or one per CU a lone wavefront per problem
-// leaves SIMDs idle.  Tuned on config 5 (profiles/r01_group_above_ab.jsonl):
-// a tuning point of that workload's footprint buckets, not a derived constant.
-constexpr int64_t kGroupAbove = 64 << 10;
 // Routed-off catalogs under kMidMaxVars variables run in 4-wave groups
 // (M_SPLIT4), larger ones in 8-wave groups (profiles/r01_group_waves_ab.jsonl).
 constexpr int32_t kMidMaxVars = 8192;
@@ -71,9 +67,10 @@ constexpr int32_t kMidMaxVars = 8192;
 // res/s with 4096-problem / 24 MiB chunks, 45.1M with 65536 / 64 MiB;
 // config 2: 10.0M -> 12.4M, one chunk per 10,000-catalog batch,
 // profiles/r02_h2h_sweep_b.jsonl; config 5: 363k at 64 MiB, 456k at 256 MiB;
-// config 4: 1.6k -> 3.0k, profiles/r02_h2h_sweep_c.jsonl).
+// config 4: 1.6k -> 3.0k, profiles/r02_h2h_sweep_c.jsonl; a directly copied
+// batch needs no pinned staging room, so the cap is the device image).
 constexpr int32_t kChunkProblems = 65536;
-constexpr int64_t kChunkBytes = 256ll << 20;
+constexpr int64_t kChunkBytes = 1ll << 30;
 // D2H of the explanation pool per chunk: this many words per problem are
 // copied with the fixed outputs; a chunk whose cores need more fetches the
 // rest with a second copy.
@@ -88,14 +85,6 @@ int64_t env_i64(const char* name, int64_t dflt) {
   return e && *e ? std::atoll(e) : dflt;
 }
 
-int64_t group_above() {
-  static const int64_t v = [] {
-    const int64_t x = env_i64("DEPPY_GROUP_ABOVE", 0);  // diagnostic
-    return x > 0 ? std::min<int64_t>(x, kMaxLdsBytes) : kGroupAbove;
-  }();
-  return v;
-}
-
 bool forced_of(int32_t opt_flags) {
   return opt_flags & (DP_OPT_FORCE_GROUP | DP_OPT_FORCE_HBM | DP_OPT_FORCE_MID);
 }
@@ -108,7 +97,8 @@ bool header_ok(const int32_t* h, int64_t avail) {
   for (int i = DP_H_NV; i <= DP_H_NCHL; ++i)
     if (h[i] < 0 || h[i] > (1 << 28)) return false;
   const int32_t fmt = h[DP_H_FMT];
-  if (fmt != DP_FMT_I32 && ((fmt != DP_FMT_U16 && fmt != DP_FMT_P16) || !dp_rec_fits16(h))) return false;
+  if (fmt != DP_FMT_I32 && fmt != DP_FMT_I32W && ((fmt != DP_FMT_U16 && fmt != DP_FMT_P16) || !dp_rec_fits16(h)))
+    return false;
   if (fmt == DP_FMT_P16 && dp_p16_tail_bytes(h) > DP_P16_TAIL_MAX) return false;
   const int64_t w = dp_rec_layout_of(h).words;
   return w == h[DP_H_WORDS] && dp_rec_phys_words(h) <= avail;
@@ -173,7 +163,7 @@ void read_head(Head& H, const int32_t* h, int64_t avail, int32_t opt_flags, bool
   bool nar = false;
   if (!forced_of(opt_flags) && dp::fits16(h)) {
     H.lds = layout<M_LDS>(h).lds_bytes;
-    nar = H.lds <= group_above();
+    nar = H.lds <= dp::group_above();
   }
   H.sw = staged_words(h, nar);
   H.rec_bytes = nar ? 4 * DP_H_SIZE + 2 * ((int64_t)h[DP_H_WORDS] - DP_H_SIZE) : 4 * (int64_t)h[DP_H_WORDS];
@@ -185,6 +175,7 @@ void read_head(Head& H, const int32_t* h, int64_t avail, int32_t opt_flags, bool
     H.direct = aligned && (h[DP_H_FMT] == DP_FMT_U16 || h[DP_H_FMT] == DP_FMT_P16);
     return;
   }
+  H.direct = aligned && h[DP_H_FMT] == DP_FMT_I32W;  // the multi-wave staged form
   const bool forced = forced_of(opt_flags);
   // (layout arithmetic is int32: variables are capped well below its range)
   const bool sized = h[DP_H_NV] < (1 << 24) && h[DP_H_NID] < (1 << 26) && h[DP_H_WORDS] < (1 << 28);
@@ -438,35 +429,6 @@ static bool convert(const int32_t* h, const S* sb, D* db) {
   return avx2 ? convert_avx2(h, sb, db) : convert_generic(h, sb, db);
 }
 
-// The watch lists of a multi-wave problem (layout.hpp img_layout), right
-// after its int32 record r: rows in ascending order in every list.  Returns
-// the extended length in words.
-int64_t build_watches_host(int32_t* r) {
-  const dp_rec_layout R = dp_rec_layout_of(r);
-  const ImgLayout X = img_layout(r);
-  const int32_t nv = r[DP_H_NV], nc = r[DP_H_NC], nk = r[DP_H_NK];
-  const int32_t* clause_off = r + R.clause_off;
-  const int32_t* clause_lits = r + R.clause_lits;
-  const int32_t* card_off = r + R.card_off;
-  const int32_t* card_lits = r + R.card_lits;
-  int32_t* wo = r + X.w_off;
-  int32_t* w = r + X.w;
-  std::fill(wo, wo + 2 * (int64_t)nv + 1, 0);
-  for (int32_t j = 0; j < r[DP_H_NCL]; ++j) wo[(clause_lits[j] ^ 1) + 1]++;
-  for (int32_t k = 0; k < nk; ++k)
-    for (int32_t j = card_off[k]; j < card_off[k + 1]; ++j)
-      if (j == card_off[k] || card_lits[j] != card_lits[j - 1]) wo[2 * card_lits[j] + 1]++;
-  for (int64_t l = 0; l < 2 * (int64_t)nv; ++l) wo[l + 1] += wo[l];
-  static thread_local std::vector<int32_t> cur;
-  cur.assign(wo, wo + 2 * (int64_t)nv);
-  for (int32_t rr = 0; rr < nc; ++rr)
-    for (int32_t j = clause_off[rr]; j < clause_off[rr + 1]; ++j) w[cur[(size_t)(clause_lits[j] ^ 1)]++] = rr;
-  for (int32_t k = 0; k < nk; ++k)
-    for (int32_t j = card_off[k]; j < card_off[k + 1]; ++j)
-      if (j == card_off[k] || card_lits[j] != card_lits[j - 1]) w[cur[(size_t)(2 * card_lits[j])]++] = nc + k;
-  return X.words;
-}
-
 // Problems per pool work item when staging n records: a few items per
 // thread at least (a chunk of 28 OLM-scale records must not go to one thread).
 int64_t stage_block(int64_t n, const Pool& pool) {
@@ -493,7 +455,7 @@ bool stage_one(const Plan& P, const int32_t* rec, const int64_t* rec_off, int32_
   const int32_t fmt = src[DP_H_FMT];
   std::memcpy(d, src, 4 * DP_H_SIZE);
   if (P.narrow[(size_t)i]) {
-    if (fmt == DP_FMT_I32) {
+    if (fmt == DP_FMT_I32 || fmt == DP_FMT_I32W) {
       d[DP_H_FMT] = DP_FMT_U16_CHECKED;
       uint16_t* o = reinterpret_cast<uint16_t*>(d + DP_H_SIZE);
       if (!convert(src, src + DP_H_SIZE, o)) {
@@ -854,21 +816,26 @@ int start_chunk(dp_ctx* ctx, Lane& L, dp_job* job, int32_t p0, int32_t n) {
   }
   const InLayout il = in_layout(L.plan);
   L.ol = out_layout(L.plan);
-  HIP_OK(L.h_in.reserve(il.end));
+  // The host side of the input region: all of it, or (direct) only what
+  // follows the copied source range -- the staged records and the tables --
+  // with `hin` the address the region's offset 0 would have.
+  const size_t rest = direct ? il.img + 4 * (size_t)W : 0;
+  HIP_OK(L.h_in.reserve(il.end - rest));
+  char* const hin = L.h_in.p - rest;  // (only offsets >= rest are used)
   HIP_OK(L.d_in.reserve(il.end));
   HIP_OK(L.h_out.reserve(L.ol.end));
   HIP_OK(L.d_out.reserve(L.ol.end));
   HIP_OK(L.scratch.reserve((size_t)std::max<int64_t>(L.plan.scratch_words, 1) * 4));
   const Plan& P = L.plan;
   if (!direct || P.n_direct < n) {  // stage the records (host pool)
-    int32_t* img = at<int32_t>(L.h_in.p, il.img);
+    int32_t* img = at<int32_t>(hin, il.img);
     ctx->pool->run(n, [&](int64_t i) {
       if (direct && P.direct[(size_t)i]) return;
       if (!dp::stage_one(P, job->rec, job->rec_off, p0, (int32_t)i, img)) bad[(size_t)i] = 1;
     }, dp::stage_block(n, *ctx->pool));
     // (records found malformed while staging are reported by the kernel)
   }
-  fill_in_tables(P, il, L.h_in.p);
+  fill_in_tables(P, il, hin);
   ctx->st.stage_ms += now_ms() - t_plan;
   // Zero-copy results: the kernels write their results straight into the
   // lane's mapped pinned buffer.  With a D2H copy per chunk instead, copies
@@ -880,16 +847,16 @@ int start_chunk(dp_ctx* ctx, Lane& L, dp_job* job, int32_t p0, int32_t n) {
   // 3 jobs in flight) beat kernels reading them over PCIe (6.9M;
   // DEPPY_ZC_IN=1, only for chunks without multi-wave problems, which re-read
   // their record; profiles/r02_h2h_sweep.jsonl).
-  const bool zc_in = ctx->zc_in && P.scratch_off.empty();
+  const bool zc_in = ctx->zc_in && !direct && P.scratch_off.empty();
   L.zc_out = ctx->zc_out;
   char* din = zc_in ? L.h_in.dev : L.d_in.p;
   char* dout = L.zc_out ? L.h_out.dev : L.d_out.p;
   size_t h2d = 0;
   if (direct) {
-    const size_t src_bytes = 4 * (size_t)W, rest = il.img + src_bytes;
+    const size_t src_bytes = 4 * (size_t)W;
     if (src_bytes)
       HIP_OK(hipMemcpyAsync(L.d_in.p + il.img, job->rec + job->rec_off[p0], src_bytes, hipMemcpyHostToDevice, L.s));
-    HIP_OK(hipMemcpyAsync(L.d_in.p + rest, L.h_in.p + rest, il.end - rest, hipMemcpyHostToDevice, L.s));
+    HIP_OK(hipMemcpyAsync(L.d_in.p + rest, L.h_in.p, il.end - rest, hipMemcpyHostToDevice, L.s));
     h2d = src_bytes + il.end - rest;
     ctx->st.direct_chunks++;
   } else if (!zc_in) {

@@ -441,6 +441,8 @@ struct Group {
 #endif
     if constexpr (MODE == M_LDS)
       if ((h[DP_H_FMT] == DP_FMT_U16 || packed) && !valid_record(body)) return false;
+    if constexpr (MODE != M_LDS)
+      if (h[DP_H_FMT] == DP_FMT_I32W && !valid_wide(R, X)) return false;
 #ifdef DP_STAMPS
     const int64_t ti2 = stamp();
     sub[1] = ti2 - ti1;
@@ -520,6 +522,52 @@ struct Group {
         if (x != (int)card_lits[j - 1])
           for (int i = a; i < j - 1; ++i) bad |= (int)card_lits[i] == x;
       }
+    }
+    return !g_any(bad);
+  }
+
+  // dp_rec_validate for an int32 record the host passed through unread
+  // (DP_FMT_I32W, read in place from HBM by a multi-wave group), with its
+  // watch lists' bounds: offsets arrays from 0, non-decreasing, to their
+  // totals; indices in range; AtMost bounds not negative and each variable's
+  // positions one run; w_off from 0, non-decreasing, within w; every listed
+  // row a row.  Group-uniform result.
+  __device__ __noinline__ bool valid_wide(const dp_rec_layout& R, const ImgLayout& X) {
+    static_assert(MODE != M_LDS, "the int32 form runs on multi-wave groups");
+    const int32_t* r = reinterpret_cast<const int32_t*>(clause_off) - R.clause_off;  // the record
+    bool bad = false;
+    auto offsets = [&](int at, int n, int total, bool exact) {
+      for (int i = tid; i <= n; i += NT) {
+        const int x = r[at + i];
+        bad |= i == 0 ? x != 0 : x < r[at + i - 1];
+        bad |= i == n && (exact ? x != total : x > total);
+      }
+    };
+    auto range = [&](int at, int n, int lo, int hi) {
+      for (int i = tid; i < n; i += NT) {
+        const int x = r[at + i];
+        bad |= x < lo || x >= hi;
+      }
+    };
+    offsets(R.clause_off, nc, ncl, true);
+    offsets(R.card_off, nk, nkl, true);
+    offsets(R.var_choice_off, nv, nch, true);
+    offsets(R.choice_off, nch, nchl, true);
+    offsets(X.w_off, 2 * nv, ncl + nkl, false);
+    range(R.clause_lits, ncl, 0, 2 * nv);
+    range(R.clause_id, nc, 0, nid);
+    range(R.card_lits, nkl, 0, nv);
+    range(R.card_bound, nk, 0, 1 << 30);
+    range(R.card_id, nk, 0, nid);
+    range(R.choice_lits, nchl + na, 0, nv);  // choice_lits then anchors
+    if (g_any(bad)) return false;  // the offsets below are now in range
+    range(X.w, r[X.w_off + 2 * nv], 0, nrows);
+    for (int k = tid; k < nk; k += NT) {
+      const int a = r[R.card_off + k], b = r[R.card_off + k + 1];
+      const int32_t* cl = r + R.card_lits;
+      for (int j = a + 1; j < b; ++j)
+        if (cl[j] != cl[j - 1])
+          for (int i = a; i < j - 1; ++i) bad |= cl[i] == cl[j];
     }
     return !g_any(bad);
   }

@@ -172,9 +172,21 @@ static inline dp_rec_layout dp_rec_layout_of(const int32_t* h) {
  *          clause_id is the clear bits in order and card_id the set ones.
  * The lengths and the mask together are at most DP_P16_TAIL_MAX bytes (the
  * kernel decodes them from one 16-byte load per lane).  DP_H_WORDS stays the
- * int32 form's length.  dp_rec_widen gives the int32 form of any record. */
+ * int32 form's length.  dp_rec_widen gives the int32 form of any record.
+ *
+ * DP_FMT_I32W: the int32 form followed by its watch lists, the form a
+ * problem solved by a multi-wave workgroup is staged in (dp_lower_into
+ * DP_LOWER_NARROW emits it for the records that do not run one wavefront
+ * per problem, so that they too go to the device as they lie):
+ *   int32 w_off[2nv+1]  rows literal l wakes: w[w_off[l] .. w_off[l+1]) (the
+ *                       clauses holding ~l; when l = 2v is positive, the
+ *                       AtMost rows holding v, once each)
+ *   int32 w[ncl+nkl]    row ids, ascending within a list (entries past
+ *                       w_off[2nv] unused)
+ * The kernel checks their bounds; that they list exactly those rows is the
+ * producer's contract (dp_lower_into builds them). */
 enum { DP_H_FMT = 13 };
-enum { DP_FMT_I32 = 0, DP_FMT_U16 = 1, DP_FMT_P16 = 3 };
+enum { DP_FMT_I32 = 0, DP_FMT_U16 = 1, DP_FMT_P16 = 3, DP_FMT_I32W = 4 };
 enum { DP_P16_TAIL_MAX = 1024 };
 
 /* DP_FMT_P16: uint16 words before the padding, byte offset of the lengths
@@ -190,6 +202,8 @@ static inline int64_t dp_p16_tail_bytes(const int32_t* h) {
 static inline int64_t dp_rec_phys_words(const int32_t* h) {
   if (h[DP_H_FMT] == DP_FMT_U16) return DP_H_SIZE + ((int64_t)h[DP_H_WORDS] - DP_H_SIZE + 1) / 2;
   if (h[DP_H_FMT] == DP_FMT_P16) return DP_H_SIZE + (dp_p16_tail_at(h) + dp_p16_tail_bytes(h) + 3) / 4;
+  if (h[DP_H_FMT] == DP_FMT_I32W)
+    return (int64_t)h[DP_H_WORDS] + 2 * (int64_t)h[DP_H_NV] + 1 + h[DP_H_NCL] + h[DP_H_NKL];
   return (int64_t)h[DP_H_WORDS];
 }
 
@@ -232,7 +246,9 @@ int dp_lower(const dp_wire* wire, dp_lowered** out);
  * copied to the device by DMA from where it lies: dp_submit stages only
  * chunks that need another form.  DP_LOWER_PACKED (with DP_LOWER_NARROW)
  * emits the DP_FMT_P16 form for the records that allow it, the DP_FMT_U16
- * form for the other 16-bit ones.  Returns 0 or -1. */
+ * form for the other 16-bit ones.  With DP_LOWER_NARROW, records of problems
+ * solved by multi-wave workgroups (too large for one wavefront's LDS image,
+ * or beyond 16 bits) take the DP_FMT_I32W form.  Returns 0 or -1. */
 enum { DP_LOWER_NARROW = 1, DP_LOWER_PINNED = 2, DP_LOWER_PACKED = 4 };
 int dp_lower_into(const dp_wire* wire, int32_t flags, dp_lowered* lw);
 dp_lowered* dp_lowered_new(void); /* an empty result for dp_lower_into */

@@ -79,7 +79,8 @@ def widen(rec_off, rec):
             r = np.concatenate([r[:16], body])
             r[13] = 0
         elif len(r):
-            r = r[:int(r[10])]  # (DP_LOWER_NARROW pads records to 16 bytes)
+            r = r[:int(r[10])].copy()  # (DP_LOWER_NARROW pads records to 16 bytes)
+            r[13] = 0  # (DP_FMT_I32W: the watch lists dropped)
         parts.append(np.asarray(r, np.int32))
         offs.append(offs[-1] + len(r))
     return np.array(offs, np.int64), (np.concatenate(parts) if parts else np.zeros(0, np.int32))

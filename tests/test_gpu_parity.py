@@ -393,3 +393,47 @@ def test_malformed_packed_records_found_by_the_kernel():
         assert g["status"][p] == -2 and g["flags"][p] == 512 and g["core_len"][p] == 0, p
     for k in ("status", "flags", "steps"):
         np.testing.assert_array_equal(g[k][ok], ref[k][ok])
+
+
+def test_wide_records_direct_and_validated():
+    """Multi-wave records in the DP_FMT_I32W form (record + watch lists, as
+    dp_lower_into DP_LOWER_NARROW emits them) go to the device as they lie;
+    the kernel checks their bounds: a watch entry past the rows, a clause
+    literal past 2nv -> DP_F_MALFORMED for that problem, the rest exact."""
+    a = lowered_config(5, 120, 121)
+    b = lowered_config(5, 120, 121, packed=True, pinned=True)
+    wide = [p for p in range(b.n) if b.rec[b.rec_off[p] + 13] == 4]
+    assert len(wide) >= 3
+    ref = oracle.solve_batch(a.rec_off, a.rec, 0, 16)
+    c = _lib.Context(0, 1)
+    try:
+        g = c.submit(b.rec_off, b.rec).wait()
+        assert c.stats(reset=True)["direct_chunks"] > 0
+        assert compare_results(g, ref, b.n) == []
+        bad = wide[:2]
+        r0 = b.rec[b.rec_off[bad[0]]:b.rec_off[bad[0] + 1]]
+        words, nv = int(r0[10]), int(r0[1])
+        r0[words + 2 * nv + 1] = int(r0[2]) + int(r0[3]) + 5      # first watch entry past the rows
+        r1 = b.rec[b.rec_off[bad[1]]:b.rec_off[bad[1] + 1]]
+        r1[16 + int(r1[2]) + 1] = 2 * int(r1[1]) + 1                # first clause literal past 2nv
+        g = c.submit(b.rec_off, b.rec).wait()
+    finally:
+        c.close()
+    ok = [p for p in range(b.n) if p not in bad]
+    for p in bad:
+        assert g["status"][p] == -2 and g["flags"][p] == 512, p
+    for k in ("status", "flags", "steps"):
+        np.testing.assert_array_equal(g[k][ok], ref[k][ok])
+
+
+def test_olm_scale_direct_bit_exact(ctx):
+    """One OLM-scale catalog (config 4) lowered to DP_FMT_I32W and copied
+    directly: the same result as its int32 form and the oracle."""
+    a = lowered_config(4, 2, 131)
+    b = lowered_config(4, 2, 131, narrow=True, pinned=True)
+    assert np.all(b.rec[b.rec_off[:-1] + 13] == 4)
+    gb = ctx.submit(b.rec_off, b.rec).wait()
+    ga = ctx.solve(a.rec_off, a.rec)
+    assert compare_results(gb, ga, 2) == []
+    o = oracle.solve_batch(a.rec_off, a.rec, 0, 2)
+    assert compare_results(gb, o, 2) == []
