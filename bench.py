@@ -10,8 +10,8 @@ lowered records in host memory -> dp_submit (stage, H2D, solve, D2H) ->
 results in host memory (dp_job_wait), for one batch of BASELINE config 2 by
 default: 10,000 synthetic operator catalogs (~200 bundle entities,
 Dependency + Conflict + AtMost; SURVEY.md §8(d) generator).  `--depth` jobs
-are in flight, as a serving loop keeps them (default 3): step i is submitted
-before step i-3 is collected.  Every step resolves its whole batch, and every
+are in flight, as a serving loop keeps them (default 4, one per pipeline lane): step i is submitted
+before step i-4 is collected.  Every step resolves its whole batch, and every
 result lands in host memory.
 
 `value` = resolutions/s over all ranks, host to host.  Secondary figures:
@@ -155,7 +155,7 @@ def main():
     ap.add_argument("--problems", type=int, default=0,
                     help="catalogs per step and rank (weak) or in total (strong); 0: WORKLOADS")
     ap.add_argument("--seed", type=int, default=1000)
-    ap.add_argument("--depth", type=int, default=3, help="host-to-host jobs in flight")
+    ap.add_argument("--depth", type=int, default=4, help="host-to-host jobs in flight (one per pipeline lane)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--kernel-steps", type=int, default=20,
