@@ -245,6 +245,10 @@ def main():
                  "h2d_bytes_per_step": st["h2d_bytes"] // args.steps, "peak_GBs": PCIE_PEAK_GBS},
         "host_ms_per_step": {k: round(st[k] / args.steps, 4) for k in ("stage_ms", "plan_ms", "wait_ms", "scatter_ms")},
         "direct_chunks_per_step": round(st["direct_chunks"] / args.steps, 2),
+        "bcp": {"visited_bytes_per_resolution": round(st["bcp_bytes"] / max(st["problems"], 1), 1),
+                "GBs": round(st["bcp_bytes"] / elapsed / 1e9, 2) if elapsed != float("inf") else None,
+                "note": "bytes unit propagation reads (watch entries, row offsets, literals, values; in LDS "
+                        "for one-wavefront problems, HBM for multi-wave), counted in the kernel (dp_stats)"},
         "records_pinned": bool(lw.pinned),
         "classes": class_mix(res) if res is not None else None,
         "deterministic": bool(deterministic),

@@ -68,7 +68,8 @@ class Stats(ctypes.Structure):
     _fields_ = [("problems", ctypes.c_int64), ("chunks", ctypes.c_int64), ("launches", ctypes.c_int64),
                 ("kernel_ms", ctypes.c_double), ("h2d_bytes", ctypes.c_int64), ("d2h_bytes", ctypes.c_int64),
                 ("rec_bytes", ctypes.c_int64), ("stage_ms", ctypes.c_double), ("plan_ms", ctypes.c_double), ("wait_ms", ctypes.c_double),
-                ("scatter_ms", ctypes.c_double), ("direct_chunks", ctypes.c_int64)]
+                ("scatter_ms", ctypes.c_double), ("direct_chunks", ctypes.c_int64),
+                ("bcp_bytes", ctypes.c_int64)]
 
 
 class Batch(ctypes.Structure):

@@ -27,6 +27,7 @@ struct KernelArgs {
   int32_t* core_pool_len;
   int32_t* core_len;
   int64_t* steps;
+  uint64_t* bcp;  // [problems] BCP-visited bytes (may be null)
   int64_t budget;
   // HBM scratch of the multi-wave modes (M_SPLIT / M_HBM, problems over the
   // LDS limit): workgroup b works in scratch + scratch_off[b] (and in LDS)

@@ -527,7 +527,7 @@ struct InLayout {
   size_t img, rec_off, order, inst_off, scratch_off, end;
 };
 struct OutLayout {
-  size_t status, flags, core_len, core_at, steps, installed, pool_len, pool, end;
+  size_t status, flags, core_len, core_at, steps, bcp, installed, pool_len, pool, end;
   size_t d2h;  // bytes copied back by the pipelined D2H
 };
 
@@ -554,6 +554,7 @@ OutLayout out_layout(const Plan& P) {
   L.core_len = o;  o = al(o + n * 4);
   L.core_at = o;   o = al(o + n * 4);
   L.steps = o;     o = al(o + n * 8);
+  L.bcp = o;       o = al(o + n * 8);
   L.installed = o; o = al(o + (size_t)P.inst_off[n] * 4);
   L.pool_len = o;  o = al(o + 4);
   L.pool = o;      o = al(o + (size_t)std::max<int64_t>(P.core_cap, 1) * 4);
@@ -626,6 +627,7 @@ dp::KernelArgs kernel_args(const InLayout& I, const OutLayout& O, char* din, cha
   a.core_pool_len = at<int32_t>(dout, O.pool_len);
   a.core_len = at<int32_t>(dout, O.core_len);
   a.steps = at<int64_t>(dout, O.steps);
+  a.bcp = at<uint64_t>(dout, O.bcp);
   a.budget = budget;
   a.scratch = scratch;
   a.scratch_off = at<int64_t>(din, I.scratch_off);
@@ -780,6 +782,8 @@ int finish_lane(dp_ctx* ctx, Lane& L) {
     ctx->st.d2h_bytes += (int64_t)(need - L.ol.d2h);
   }
   scatter(L.plan, L.ol, L.h_out.p, L.p0, &job->res);
+  const uint64_t* bcp = at<uint64_t>(L.h_out.p, L.ol.bcp);
+  for (int32_t i = 0; i < L.plan.n; ++i) ctx->st.bcp_bytes += (int64_t)bcp[i];
   ctx->st.scatter_ms += now_ms() - t1;
   return 0;
 }

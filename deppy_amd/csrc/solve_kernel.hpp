@@ -171,6 +171,9 @@ struct Group {
   const IX *var_choice_off, *choice_off, *choice_lits, *anchors;
   const IX *w_off, *w;  // watch lists, built by build_watches
   int nwatch, dthr;
+  // BCP-visited bytes (this thread): the watch entries, row offsets, row
+  // literals and their values that propagation reads
+  uint32_t vis;
   // ---- working set ----
   int8_t* val;
   IX *reason, *rs, *trail, *touched, *d_mark, *l_off, *l_lits, *dq, *stk;
@@ -420,6 +423,7 @@ struct Group {
     cap = L.cap; lcap = L.lcap;
     tlen = qhead = 0;
     steps = 0;
+    vis = 0;
     budget_hit = false;
     ck = CK_NONE; c_row = c_var = c_rp = c_rn = 0;
     collect_guess = false;
@@ -532,7 +536,7 @@ struct Group {
   // totals; indices in range; AtMost bounds not negative and each variable's
   // positions one run; w_off from 0, non-decreasing, within w; every listed
   // row a row.  Group-uniform result.
-  __device__ __noinline__ bool valid_wide(const dp_rec_layout& R, const ImgLayout& X) {
+  __device__ __forceinline__ bool valid_wide(const dp_rec_layout& R, const ImgLayout& X) {
     static_assert(MODE != M_LDS, "the int32 form runs on multi-wave groups");
     const int32_t* r = reinterpret_cast<const int32_t*>(clause_off) - R.clause_off;  // the record
     bool bad = false;
@@ -757,6 +761,7 @@ struct Group {
   // Returns the row's one unassigned literal when it is unit, else -1.
   __device__ __forceinline__ int eval_clause(int r, const IX* lits, int a, int b, int& crow) {
     int nun = 0, ul = -1;
+    vis += 2 * sizeof(IX) + (uint32_t)(b - a) * (sizeof(IX) + 1);  // offsets, literals, their values
     for (int j = a; j < b; j += 4) {
       int l[4];
 #pragma unroll
@@ -784,6 +789,7 @@ struct Group {
   __device__ __forceinline__ void card_serial(int r, int& crow) {
     const int k = r - nc, a = card_off[k], b = card_off[k + 1];
     int cnt = 0, nun = 0;
+    vis += 3 * sizeof(IX) + (uint32_t)(b - a) * (sizeof(IX) + 1);
     for (int j = a; j < b; ++j) {
       const int x = val[card_lits[j]];
       cnt += (x > 0);
@@ -821,6 +827,7 @@ struct Group {
   // ncq counts the queue in the one-wavefront mode (a register); with several
   // wavefronts the queue length is the LDS counter S_NK.
   __device__ __forceinline__ void visit(int r, int& crow, int& ncq) {
+    vis += r >= 0 ? sizeof(IX) : 0;  // the watch entry
     const bool ok = r >= 0 && row_on(r);
     const bool card = ok && r >= nc && r < nrows;
     const uint64_t m = __ballot(card);
@@ -876,6 +883,7 @@ struct Group {
       }
       const int v = lane < len ? (int)card_lits[a + lane] : -1;
       const int x = v >= 0 ? val[v] : 0;
+      vis += (v >= 0 ? sizeof(IX) + 1 : 0) + (lane == 0 ? 3 * sizeof(IX) : 0);  // positions, values; offsets, bound
       const int cnt = __popcll(__ballot(v >= 0 && x > 0));
       if (cnt > bound) { crow = min(crow, r); continue; }
       if (!__ballot(v >= 0 && x == 0)) continue;
@@ -893,6 +901,7 @@ struct Group {
       const int j = j0 + lane;
       const int v = j < len ? (int)card_lits[a + j] : -1;
       const int x = v >= 0 ? val[v] : 0;
+      vis += v >= 0 ? sizeof(IX) + 1 : 0;
       cnt += __popcll(__ballot(v >= 0 && x > 0));
       any |= __ballot(v >= 0 && x == 0) != 0ull;
     }
@@ -1922,7 +1931,9 @@ solve_kernel(KernelArgs a) {
   }
 #endif
   if (W.tr_stop) flags |= DP_F_TRACE_TRUNCATED;
+  const uint64_t bcp = (uint32_t)W.g_sum((int)W.vis);  // (a problem reads well under 2 GB)
   if (W.tid == 0) {
+    if (a.bcp) a.bcp[pid] = bcp;
     if (a.trace) a.trace_len[pid] = W.tr_len;
     a.status[pid] = (int8_t)status;
     a.flags[pid] = flags;

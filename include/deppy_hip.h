@@ -377,6 +377,9 @@ typedef struct dp_stats {
   double scatter_ms; /* host: results -> the caller's dp_result              */
   int64_t direct_chunks; /* chunks copied from the caller's page-locked
                             records without staging (DP_LOWER_PINNED)        */
+  int64_t bcp_bytes; /* bytes unit propagation read (watch entries, row
+                        offsets, row literals and their values), summed over
+                        the problems (SURVEY.md 8(d) "BCP-visited bytes")    */
 } dp_stats;
 int dp_get_stats(dp_ctx* ctx, dp_stats* out, int32_t reset);
 
