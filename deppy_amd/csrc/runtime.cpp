@@ -166,7 +166,11 @@ void read_head(Head& H, const int32_t* h, int64_t avail, int32_t opt_flags, bool
     nar = H.lds <= dp::group_above();
   }
   H.sw = staged_words(h, nar);
-  H.rec_bytes = nar ? 4 * DP_H_SIZE + 2 * ((int64_t)h[DP_H_WORDS] - DP_H_SIZE) : 4 * (int64_t)h[DP_H_WORDS];
+  // the record image the kernel reads: the packed form as it is, else the
+  // 16-bit form (LDS path) or the int32 form with its watch lists
+  H.rec_bytes = nar ? (h[DP_H_FMT] == DP_FMT_P16 ? 4 * dp_rec_phys_words(h)
+                                                 : 4 * DP_H_SIZE + 2 * ((int64_t)h[DP_H_WORDS] - DP_H_SIZE))
+                    : 4 * (int64_t)img_layout(h).words;
   if (nar) {
     H.place = M_LDS;
     int k = 0;

@@ -369,7 +369,7 @@ typedef struct dp_stats {
                         events on the chunk's stream, around its launches)   */
   int64_t h2d_bytes; /* bytes copied host -> device                          */
   int64_t d2h_bytes; /* bytes copied device -> host                          */
-  int64_t rec_bytes; /* staged record bytes (16-bit form on the LDS path)    */
+  int64_t rec_bytes; /* record image bytes the kernels read (dp_device_bytes) */
   double stage_ms;   /* host: staging records into pinned memory and writing
                         the chunk tables (after planning)                    */
   double plan_ms;    /* host: planning the launches (header pass, buckets)   */
@@ -411,11 +411,13 @@ int dp_solve_traced(dp_ctx* ctx, const dp_batch* b, int32_t trace_cap, dp_result
                     int32_t* trace, int32_t* trace_len);
 
 /* Measurement helper (no reference counterpart): bytes of the batch as the
- * device stores it.  rec_bytes = the records (the compulsory input of SURVEY
- * §8(d)): 4 bytes per word, or for problems on the LDS path, whose records
- * are staged in 16-bit form, 64 header bytes + 2 per word.  img_bytes = the
- * staged copies as they cross PCIe (16-byte aligned; the kernel builds the
- * watch lists itself).  opt_flags as dp_opts.flags.  Returns 0 or -1. */
+ * device stores it.  rec_bytes = the record images the kernels read (the
+ * compulsory input of SURVEY §8(d)): on the LDS path the 16-bit form (a
+ * DP_FMT_P16 record as it is, else 64 header bytes + 2 per word; the kernel
+ * builds the watch lists itself), on the multi-wave paths the int32 form
+ * with its watch lists (DP_FMT_I32W).  img_bytes = the staged copies as
+ * they cross PCIe when staged (16-byte aligned).  opt_flags as
+ * dp_opts.flags.  Returns 0 or -1. */
 int dp_device_bytes(const dp_batch* b, int32_t opt_flags, int64_t* rec_bytes, int64_t* img_bytes);
 
 /* Host-only test hooks (no device, no reference counterpart): the chunking,
