@@ -1,4 +1,6 @@
 // Mode dispatch of the solve kernel launches (kernel_api.hpp).
+#include <cstdlib>
+
 #include "kernel_api.hpp"
 #include "layout.hpp"
 
@@ -24,7 +26,11 @@ constexpr int kLdsPerCU = 160 * 1024;
 
 hipError_t launch_solve(const KernelArgs& a, int mode, int n_blocks, int lds_bytes, hipStream_t stream) {
   if (mode == M_LDS) {
-    const bool dense = lds_bytes > 0 && kLdsPerCU / lds_bytes > kUnboundedWavesPerCU;
+    static const bool no_dense = [] {  // diagnostic DEPPY_NO_DENSE=1: the unbounded build only
+      const char* e = std::getenv("DEPPY_NO_DENSE");
+      return e && *e && *e != '0';
+    }();
+    const bool dense = !no_dense && lds_bytes > 0 && kLdsPerCU / lds_bytes > kUnboundedWavesPerCU;
     return dense ? launch_lds_dense(a, n_blocks, lds_bytes, stream) : launch_lds(a, n_blocks, lds_bytes, stream);
   }
   if (mode == M_SPLIT) return launch_split(a, n_blocks, lds_bytes, stream);
