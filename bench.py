@@ -115,9 +115,11 @@ def lowered_config(config, n, seed):
 
 
 def output_bytes(res) -> int:
-    """Every output word the kernel writes."""
+    """Every output word the kernel writes: a 32-byte result
+    record per problem (status, flags, core length and offset, steps, BCP
+    bytes), the installed bitmaps, the core identities."""
     n = len(res["status"])
-    return n * (1 + 4 + 4 + 4 + 8) + 4 * int(res["inst_off"][-1]) + 4 * int(res["core_len"].sum())
+    return n * 32 + 4 * int(res["inst_off"][-1]) + 4 * int(res["core_len"].sum())
 
 
 def class_mix(res) -> dict:
@@ -162,6 +164,8 @@ def main():
                     help="steps of the device-resident (kernel-only) secondary figure; 0: skip")
     ap.add_argument("--kernel-only", action="store_true",
                     help="skip the host-to-host leg (profiling runs of the solve kernel)")
+    ap.add_argument("--flags", type=int, default=0,
+                    help="dp_opts.flags (diagnostic placements: 1 group, 2 HBM, 4 mid groups)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02_pmc_traffic.jsonl"),
                     help="HBM bytes per solve kernel dispatch from separate rocprofv3 --pmc passes; "
                          "used for roofline.traffic when its config/problems match")
@@ -183,7 +187,7 @@ def main():
         lo, hi = shard.strong_range(total, rank, world)
         n, first = hi - lo, args.seed + lo
     lw, lw32, t_lower = lowered_config(args.config, n, first)
-    ctx = _lib.Context(local, 1)
+    ctx = _lib.Context(local, 1, flags=args.flags)
 
     # host-to-host: depth jobs in flight, each the whole batch
     depth = max(1, args.depth)

@@ -11,23 +11,39 @@ namespace dp {
 // number of failed checks, then 3 more counters (Solve, pop_guess, pushes)
 constexpr int DP_NSTAMP = 32;
 
+// A problem's fixed-size results, written by one lane as two 16-byte stores:
+// one transaction per problem whether the output region is device memory or
+// mapped host memory (zero-copy results cross PCIe as written).
+struct alignas(32) ProblemOut {
+  int8_t status;
+  int8_t pad[3];
+  int32_t flags;
+  int32_t core_len;  // identities at core[core_at ...]
+  int32_t core_at;
+  int64_t steps;
+  uint64_t bcp;      // BCP-visited bytes
+};
+static_assert(sizeof(ProblemOut) == 32, "two 16-byte stores");
+
+// What one workgroup needs to find its problem: one 16-byte read, in launch
+// order, so consecutive workgroups read consecutive items.
+struct alignas(16) WorkItem {
+  int64_t rec_off;   // word offset of the record in the image
+  int32_t inst_off;  // word offset of its installed bitmap
+  int32_t pid;       // local problem index (results, traces)
+};
+static_assert(sizeof(WorkItem) == 16, "one 16-byte read");
+
 struct KernelArgs {
   const int32_t* rec;      // staged records (layout.hpp), each 16-byte aligned
-  const int64_t* rec_off;  // [n] word offset of each record
-  const int32_t* order;    // [grid] problem index of each workgroup
-  int8_t* status;
-  int32_t* flags;
+  const WorkItem* items;   // [grid] the workgroup's problem (launch order)
+  ProblemOut* out;         // [n] per-problem results (one 32-byte store each)
   uint32_t* installed;
-  const int64_t* inst_off;
   // NotSatisfiable explanations: problem p's core_len[p] identities are at
   // core[core_at[p]...], claimed from *core_pool_len (the pool holds the sum
   // of the problems' identity counts, so it cannot overflow)
   int32_t* core;
-  int32_t* core_at;
   int32_t* core_pool_len;
-  int32_t* core_len;
-  int64_t* steps;
-  uint64_t* bcp;  // [problems] BCP-visited bytes (may be null)
   int64_t budget;
   // HBM scratch of the multi-wave modes (M_SPLIT / M_HBM, problems over the
   // LDS limit): workgroup b works in scratch + scratch_off[b] (and in LDS)

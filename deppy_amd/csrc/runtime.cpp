@@ -528,10 +528,10 @@ bool pinned_range(const void* p, size_t bytes) {
 // Byte layout of a chunk's input region (identical in pinned host memory and
 // on the device, so one copy moves it) and of its output region.
 struct InLayout {
-  size_t img, rec_off, order, inst_off, scratch_off, end;
+  size_t img, items, scratch_off, end;
 };
 struct OutLayout {
-  size_t status, flags, core_len, core_at, steps, bcp, installed, pool_len, pool, end;
+  size_t prob, installed, pool_len, pool, end;
   size_t d2h;  // bytes copied back by the pipelined D2H
 };
 
@@ -541,9 +541,7 @@ InLayout in_layout(const Plan& P) {
   InLayout L;
   size_t o = 0;
   L.img = o;         o = al(o + (size_t)P.img_words * 4);
-  L.rec_off = o;     o = al(o + (size_t)P.n * 8);
-  L.order = o;       o = al(o + P.order.size() * 4);
-  L.inst_off = o;    o = al(o + ((size_t)P.n + 1) * 8);
+  L.items = o;       o = al(o + P.order.size() * sizeof(dp::WorkItem));
   L.scratch_off = o; o = al(o + P.scratch_off.size() * 8);
   L.end = o;
   return L;
@@ -553,12 +551,7 @@ OutLayout out_layout(const Plan& P) {
   OutLayout L;
   const size_t n = (size_t)P.n;
   size_t o = 0;
-  L.status = o;    o = al(o + n);
-  L.flags = o;     o = al(o + n * 4);
-  L.core_len = o;  o = al(o + n * 4);
-  L.core_at = o;   o = al(o + n * 4);
-  L.steps = o;     o = al(o + n * 8);
-  L.bcp = o;       o = al(o + n * 8);
+  L.prob = o;      o = al(o + n * sizeof(dp::ProblemOut));
   L.installed = o; o = al(o + (size_t)P.inst_off[n] * 4);
   L.pool_len = o;  o = al(o + 4);
   L.pool = o;      o = al(o + (size_t)std::max<int64_t>(P.core_cap, 1) * 4);
@@ -569,10 +562,11 @@ OutLayout out_layout(const Plan& P) {
 
 // Fill the non-image parts of an input region.
 void fill_in_tables(const Plan& P, const InLayout& L, char* base) {
-  int64_t* ro = reinterpret_cast<int64_t*>(base + L.rec_off);
-  std::memcpy(ro, P.dev_off.data(), (size_t)P.n * 8);
-  std::memcpy(base + L.order, P.order.data(), P.order.size() * 4);
-  std::memcpy(base + L.inst_off, P.inst_off.data(), ((size_t)P.n + 1) * 8);
+  dp::WorkItem* it = reinterpret_cast<dp::WorkItem*>(base + L.items);
+  for (size_t k = 0; k < P.order.size(); ++k) {
+    const int32_t i = P.order[k];
+    it[k] = dp::WorkItem{P.dev_off[(size_t)i], (int32_t)P.inst_off[(size_t)i], i};
+  }
   if (!P.scratch_off.empty()) std::memcpy(base + L.scratch_off, P.scratch_off.data(), P.scratch_off.size() * 8);
 }
 
@@ -580,10 +574,14 @@ void fill_in_tables(const Plan& P, const InLayout& L, char* base) {
 // dp_result at global problems p0...  Cores come from the pool.
 void scatter(const Plan& P, const OutLayout& L, const char* out, int32_t p0, dp_result* res) {
   const int32_t n = P.n;
-  std::memcpy(res->status + p0, out + L.status, (size_t)n);
-  std::memcpy(res->flags + p0, out + L.flags, (size_t)n * 4);
-  std::memcpy(res->core_len + p0, out + L.core_len, (size_t)n * 4);
-  if (res->steps) std::memcpy(res->steps + p0, out + L.steps, (size_t)n * 8);
+  const dp::ProblemOut* po = reinterpret_cast<const dp::ProblemOut*>(out + L.prob);
+  for (int32_t i = 0; i < n; ++i) {
+    res->status[p0 + i] = po[i].status;
+    res->flags[p0 + i] = po[i].flags;
+    res->core_len[p0 + i] = po[i].core_len;
+  }
+  if (res->steps)
+    for (int32_t i = 0; i < n; ++i) res->steps[p0 + i] = po[i].steps;
   const uint32_t* inst = reinterpret_cast<const uint32_t*>(out + L.installed);
   if (res->inst_off[p0 + n] - res->inst_off[p0] == P.inst_off[(size_t)n]) {
     std::memcpy(res->installed + res->inst_off[p0], inst, (size_t)P.inst_off[(size_t)n] * 4);
@@ -594,13 +592,12 @@ void scatter(const Plan& P, const OutLayout& L, const char* out, int32_t p0, dp_
       std::memcpy(res->installed + res->inst_off[p0 + i], inst + P.inst_off[(size_t)i], (size_t)w * 4);
     }
   }
-  const int32_t* cl = reinterpret_cast<const int32_t*>(out + L.core_len);
-  const int32_t* ca = reinterpret_cast<const int32_t*>(out + L.core_at);
   const int32_t* pool = reinterpret_cast<const int32_t*>(out + L.pool);
   for (int32_t i = 0; i < n; ++i)
-    if (cl[i] > 0) {
+    if (po[i].core_len > 0) {
       const int64_t cap = res->core_off[p0 + i + 1] - res->core_off[p0 + i];
-      std::memcpy(res->core + res->core_off[p0 + i], pool + ca[i], (size_t)std::min<int64_t>(cl[i], cap) * 4);
+      std::memcpy(res->core + res->core_off[p0 + i], pool + po[i].core_at,
+                  (size_t)std::min<int64_t>(po[i].core_len, cap) * 4);
     }
   for (size_t q = 0; q < P.skip.size(); ++q) {
     const int32_t i = P.skip[q];
@@ -621,17 +618,11 @@ dp::KernelArgs kernel_args(const InLayout& I, const OutLayout& O, char* din, cha
                            int64_t budget) {
   dp::KernelArgs a{};
   a.rec = at<int32_t>(din, I.img);
-  a.rec_off = at<int64_t>(din, I.rec_off);
-  a.inst_off = at<int64_t>(din, I.inst_off);
-  a.status = at<int8_t>(dout, O.status);
-  a.flags = at<int32_t>(dout, O.flags);
+  a.items = at<dp::WorkItem>(din, I.items);
+  a.out = at<dp::ProblemOut>(dout, O.prob);
   a.installed = at<uint32_t>(dout, O.installed);
   a.core = at<int32_t>(dout, O.pool);
-  a.core_at = at<int32_t>(dout, O.core_at);
   a.core_pool_len = at<int32_t>(dout, O.pool_len);
-  a.core_len = at<int32_t>(dout, O.core_len);
-  a.steps = at<int64_t>(dout, O.steps);
-  a.bcp = at<uint64_t>(dout, O.bcp);
   a.budget = budget;
   a.scratch = scratch;
   a.scratch_off = at<int64_t>(din, I.scratch_off);
@@ -754,7 +745,7 @@ namespace {
 int enqueue_launches(dp_ctx* ctx, const Plan& P, const dp::KernelArgs& base, hipStream_t s) {
   for (const auto& L : P.launches) {
     dp::KernelArgs a = base;
-    a.order = base.order + L.first;
+    a.items = base.items + L.first;
     if (L.mode != dp::M_LDS) a.scratch_off = base.scratch_off + (L.first - P.big_base);
     HIP_OK(dp::launch_solve(a, L.mode, L.count, L.lds, s));
     ctx->st.launches++;
@@ -786,8 +777,8 @@ int finish_lane(dp_ctx* ctx, Lane& L) {
     ctx->st.d2h_bytes += (int64_t)(need - L.ol.d2h);
   }
   scatter(L.plan, L.ol, L.h_out.p, L.p0, &job->res);
-  const uint64_t* bcp = at<uint64_t>(L.h_out.p, L.ol.bcp);
-  for (int32_t i = 0; i < L.plan.n; ++i) ctx->st.bcp_bytes += (int64_t)bcp[i];
+  const dp::ProblemOut* po = at<dp::ProblemOut>(L.h_out.p, L.ol.prob);
+  for (int32_t i = 0; i < L.plan.n; ++i) ctx->st.bcp_bytes += (int64_t)po[i].bcp;
   ctx->st.scatter_ms += now_ms() - t1;
   return 0;
 }
@@ -874,7 +865,7 @@ int start_chunk(dp_ctx* ctx, Lane& L, dp_job* job, int32_t p0, int32_t n) {
   HIP_OK(hipMemsetAsync(L.d_out.p + L.ol.pool_len, 0, 4, L.s));
   dp::KernelArgs a = kernel_args(il, L.ol, din, dout, reinterpret_cast<int32_t*>(L.scratch.p), ctx->budget);
   a.core_pool_len = at<int32_t>(L.d_out.p, L.ol.pool_len);
-  a.order = at<int32_t>(din, il.order);
+  a.items = at<dp::WorkItem>(din, il.items);
   HIP_OK(hipEventRecord(L.k0, L.s));
   if (enqueue_launches(ctx, P, a, L.s)) return -1;
   HIP_OK(hipEventRecord(L.k1, L.s));
@@ -1128,7 +1119,7 @@ int launch_slice(dp_ctx* ctx, Slice& s, int32_t trace_cap) {
   HIP_OK(hipMemsetAsync(s.d_out.p + s.ol.pool_len, 0, 4, s.stream));
   dp::KernelArgs a = kernel_args(s.il, s.ol, s.d_in.p, s.d_out.p, reinterpret_cast<int32_t*>(s.scratch.p),
                                  ctx->budget);
-  a.order = at<int32_t>(s.d_in.p, s.il.order);
+  a.items = at<dp::WorkItem>(s.d_in.p, s.il.items);
   a.stamps = s.stamps;
   a.trace = s.trace;
   a.trace_len = s.trace_len;
@@ -1377,15 +1368,16 @@ int dp_stitch_selftest(const dp_batch* b, int32_t chunk_problems, dp_result* res
       const int32_t* h = b->rec + b->rec_off[g];
       const int32_t nid = h[DP_H_NID];
       const bool unsat = g % 3 == 0 && nid > 0;
-      at<int8_t>(out.data(), ol.status)[i] = (int8_t)(unsat ? DP_UNSAT : DP_SAT);
-      at<int32_t>(out.data(), ol.flags)[i] = (int32_t)(g & 0xff);
-      at<int64_t>(out.data(), ol.steps)[i] = 7 * g;
+      dp::ProblemOut& po = at<dp::ProblemOut>(out.data(), ol.prob)[i];
+      po.status = (int8_t)(unsat ? DP_UNSAT : DP_SAT);
+      po.flags = (int32_t)(g & 0xff);
+      po.steps = 7 * g;
       uint32_t* inst = at<uint32_t>(out.data(), ol.installed) + plan.inst_off[(size_t)i];
       for (int64_t w = 0; w < plan.inst_off[(size_t)i + 1] - plan.inst_off[(size_t)i]; ++w)
         inst[w] = (uint32_t)(g * 2654435761u) ^ (uint32_t)w;
       const int32_t len = unsat ? std::min<int32_t>(nid, 1 + (int32_t)(g % 4)) : 0;
-      at<int32_t>(out.data(), ol.core_len)[i] = len;
-      at<int32_t>(out.data(), ol.core_at)[i] = pool_len;
+      po.core_len = len;
+      po.core_at = pool_len;
       for (int32_t j = 0; j < len; ++j) at<int32_t>(out.data(), ol.pool)[pool_len + j] = (int32_t)((g + j) % nid);
       pool_len += len;
     }

@@ -320,9 +320,18 @@ struct Group {
     tid = (int)threadIdx.x;
     lane = lane_id();
     wid = tid >> 6;
+    // the header by a 16-byte vector load on lanes 0..3 (one 64-byte read,
+    // like the body's), broadcast by readlane
+    int4 hv = make_int4(0, 0, 0, 0);
+    if (lane < 4) hv = reinterpret_cast<const int4*>(grec)[lane];
     int32_t h[DP_H_SIZE];
 #pragma unroll
-    for (int i = 0; i < DP_H_SIZE; ++i) h[i] = grec[i];
+    for (int q = 0; q < 4; ++q) {
+      h[4 * q + 0] = __builtin_amdgcn_readlane(hv.x, q);
+      h[4 * q + 1] = __builtin_amdgcn_readlane(hv.y, q);
+      h[4 * q + 2] = __builtin_amdgcn_readlane(hv.z, q);
+      h[4 * q + 3] = __builtin_amdgcn_readlane(hv.w, q);
+    }
     if (h[DP_H_FMT] == DP_FMT_REJECT) return false;
 #ifdef DP_STAMPS
     const int64_t ti0 = stamp();
@@ -1848,6 +1857,23 @@ struct Group {
 // problems share a CU (small catalogs: config 3 70.8M -> 86.0M res/s); at 9
 // per CU (config 2) its spills are ~40 MB of extra scratch writes per run for
 // no throughput.  launch_solve picks the build per launch by footprint.)
+// One problem's results as two 16-byte vector stores (kernel_api.hpp).
+__device__ __forceinline__ void put_out(ProblemOut* o, int status, int32_t flags, int32_t clen, int32_t cat,
+                                        int64_t steps, uint64_t bcp) {
+  uint4 x, y;
+  x.x = (uint32_t)(uint8_t)(int8_t)status;
+  x.y = (uint32_t)flags;
+  x.z = (uint32_t)clen;
+  x.w = (uint32_t)cat;
+  y.x = (uint32_t)(uint64_t)steps;
+  y.y = (uint32_t)((uint64_t)steps >> 32);
+  y.z = (uint32_t)bcp;
+  y.w = (uint32_t)(bcp >> 32);
+  uint4* p = reinterpret_cast<uint4*>(o);
+  p[0] = x;
+  p[1] = y;
+}
+
 template <int MODE, int MINW>
 __global__ void __launch_bounds__(64 * mode_waves(MODE), MINW)
 solve_kernel(KernelArgs a) {
@@ -1857,20 +1883,17 @@ solve_kernel(KernelArgs a) {
   const int64_t wall0 = wallclock();
 #endif
   DP_STAMP(0);
-  const int pid = a.order[blockIdx.x];
-  const int32_t* grec = a.rec + a.rec_off[pid];
+  const WorkItem it = a.items[blockIdx.x];
+  const int pid = it.pid;
+  const int32_t* grec = a.rec + it.rec_off;
   Group<MODE> W;
   char* hbm = MODE == M_LDS ? nullptr : reinterpret_cast<char*>(a.scratch + a.scratch_off[blockIdx.x]);
   if (!W.init(reinterpret_cast<char*>(lds4), hbm, grec)) {
     if (threadIdx.x == 0) {  // a malformed record: no solve (dp_rec_validate's verdict)
-      a.status[pid] = (int8_t)DP_ERROR;
-      a.flags[pid] = DP_F_MALFORMED;
-      a.core_len[pid] = 0;
-      a.core_at[pid] = 0;
-      a.steps[pid] = 0;
+      put_out(a.out + pid, DP_ERROR, DP_F_MALFORMED, 0, 0, 0, 0);
       if (a.trace) a.trace_len[pid] = 0;
     }
-    uint32_t* inst0 = a.installed + a.inst_off[pid];
+    uint32_t* inst0 = a.installed + it.inst_off;
     for (int i = threadIdx.x; i < bits_words(grec[DP_H_NV]); i += blockDim.x) inst0[i] = 0;
     return;
   }
@@ -1882,7 +1905,7 @@ solve_kernel(KernelArgs a) {
     W.tr = a.trace + (int64_t)a.trace_cap * pid;
     W.tr_cap = a.trace_cap;
   }
-  uint32_t* inst = a.installed + a.inst_off[pid];
+  uint32_t* inst = a.installed + it.inst_off;
   int32_t flags = 0;
   int status;
   for (int i = W.tid; i < W.nbv; i += Group<MODE>::NT) inst[i] = 0;
@@ -1933,13 +1956,8 @@ solve_kernel(KernelArgs a) {
   if (W.tr_stop) flags |= DP_F_TRACE_TRUNCATED;
   const uint64_t bcp = (uint32_t)W.g_sum((int)W.vis);  // (a problem reads well under 2 GB)
   if (W.tid == 0) {
-    if (a.bcp) a.bcp[pid] = bcp;
     if (a.trace) a.trace_len[pid] = W.tr_len;
-    a.status[pid] = (int8_t)status;
-    a.flags[pid] = flags;
-    a.core_len[pid] = clen;
-    a.core_at[pid] = cat;
-    a.steps[pid] = W.steps;
+    put_out(a.out + pid, status, flags, clen, cat, W.steps, bcp);
   }
 }
 
