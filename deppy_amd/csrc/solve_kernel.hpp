@@ -243,17 +243,30 @@ struct Group {
     if constexpr (NW == 1) wsync();
     else bar();
   }
+  // Several wavefronts: publish one value per wavefront (from the lanes with
+  // `writer`) and return the slots after one barrier.  Exchanges alternate
+  // between two banks of slots: a wavefront writes bank b for exchange k+2
+  // only after passing exchange k+1's barrier, which every wavefront reaches
+  // after its reads of exchange k (bar() drains them first) -- so no
+  // trailing barrier is needed.  Every exchange is group-uniform.
+  int sbank;
+  static_assert(NW == 1 || S_SLOT + 2 * NW <= NSCAL, "two banks of per-wave slots");
+  __device__ __forceinline__ const int32_t* exchange(int v, bool writer) {
+    int32_t* sl = scal + S_SLOT + sbank * NW;
+    if (writer) sl[wid] = v;
+    bar();
+    sbank ^= 1;
+    return sl;
+  }
   __device__ __forceinline__ bool g_any(bool b) {
     const bool w = __ballot(b) != 0;
     if constexpr (NW == 1) {
       return w;
     } else {
-      if (lane == 0) scal[S_SLOT + wid] = w;
-      bar();
+      const int32_t* sl = exchange(w, lane == 0);
       int r = 0;
 #pragma unroll
-      for (int i = 0; i < NW; ++i) r |= scal[S_SLOT + i];
-      bar();
+      for (int i = 0; i < NW; ++i) r |= sl[i];
       return r != 0;
     }
   }
@@ -262,12 +275,10 @@ struct Group {
     if constexpr (NW == 1) {
       return x;
     } else {
-      if (lane == 0) scal[S_SLOT + wid] = x;
-      bar();
+      const int32_t* sl = exchange(x, lane == 0);
       int r = INF;
 #pragma unroll
-      for (int i = 0; i < NW; ++i) r = min(r, scal[S_SLOT + i]);
-      bar();
+      for (int i = 0; i < NW; ++i) r = min(r, sl[i]);
       return r;
     }
   }
@@ -276,12 +287,10 @@ struct Group {
     if constexpr (NW == 1) {
       return x;
     } else {
-      if (lane == 0) scal[S_SLOT + wid] = x;
-      bar();
+      const int32_t* sl = exchange(x, lane == 0);
       int r = 0;
 #pragma unroll
-      for (int i = 0; i < NW; ++i) r += scal[S_SLOT + i];
-      bar();
+      for (int i = 0; i < NW; ++i) r += sl[i];
       return r;
     }
   }
@@ -433,6 +442,7 @@ struct Group {
     tlen = qhead = 0;
     steps = 0;
     vis = 0;
+    sbank = 0;
     budget_hit = false;
     ck = CK_NONE; c_row = c_var = c_rp = c_rn = 0;
     collect_guess = false;
@@ -1080,16 +1090,14 @@ struct Group {
           const int incl = wave_incl_scan(cnt);
           int total = __builtin_amdgcn_readlane(incl, 63), before = 0;
           if constexpr (NW > 1) {
-            if (lane == 63) scal[S_SLOT + wid] = incl;
-            bar();
+            const int32_t* sl = exchange(incl, lane == 63);
             total = 0;
 #pragma unroll
             for (int q = 0; q < NW; ++q) {
-              const int c = scal[S_SLOT + q];
+              const int c = sl[q];
               before += q < wid ? c : 0;
               total += c;
             }
-            bar();
           }
           if (total <= WBUF) {
             // every frontier literal writes its watch range into the list
@@ -1637,16 +1645,14 @@ struct Group {
       const int incl = wave_incl_scan(c);
       int before = incl - c, total = __builtin_amdgcn_readlane(incl, 63);
       if constexpr (NW > 1) {
-        if (lane == 63) scal[S_SLOT + wid] = incl;
-        bar();
+        const int32_t* sl = exchange(incl, lane == 63);
         total = 0;
 #pragma unroll
         for (int q = 0; q < NW; ++q) {
-          const int s = scal[S_SLOT + q];
+          const int s = sl[q];
           before += q < wid ? s : 0;
           total += s;
         }
-        bar();
       }
       for (uint32_t y = x; y; y &= y - 1) out[len + before++] = 32 * i + __ffs(y) - 1;
       len += total;
@@ -1732,11 +1738,7 @@ struct Group {
     if constexpr (NW == 1) {
       return __shfl(x, 0);
     } else {
-      if (tid == 0) scal[S_SLOT] = x;
-      bar();
-      x = scal[S_SLOT];
-      bar();
-      return x;
+      return exchange(x, tid == 0)[0];
     }
   }
 
