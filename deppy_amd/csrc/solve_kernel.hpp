@@ -463,7 +463,7 @@ struct Group {
     sub[0] = ti1 - ti0;
 #endif
     if constexpr (MODE == M_LDS)
-      if ((h[DP_H_FMT] == DP_FMT_U16 || packed) && !valid_record(body)) return false;
+      if ((h[DP_H_FMT] == DP_FMT_U16 || packed) && !valid_record(body, packed)) return false;
     if constexpr (MODE != M_LDS)
       if (h[DP_H_FMT] == DP_FMT_I32W && !valid_wide(R, X)) return false;
 #ifdef DP_STAMPS
@@ -505,7 +505,7 @@ struct Group {
   // in an AtMost row form one run (16-bit bounds cannot be negative).  The
   // host checked every other staged form (DP_FMT_U16_CHECKED, DP_FMT_I32).
   // Array by array, two 16-bit words per LDS load.  Group-uniform result.
-  __device__ __forceinline__ bool valid_record(const IX* base) {
+  __device__ __forceinline__ bool valid_record(const IX* base, bool packed) {
     static_assert(MODE == M_LDS, "16-bit records run one wavefront per problem");
     // (base: the body's start, 16-byte aligned; arrays anywhere after it)
     const uint32_t* b32 = reinterpret_cast<const uint32_t*>(base);
@@ -528,22 +528,46 @@ struct Group {
         bad |= (i0 == e - 1 && x0 != total) || (i0 + 1 == e - 1 && x1 != total);
       }
     };
-    offsets(clause_off, nc, ncl);
+    if (packed) {
+      // decoded (unpack16): offsets are prefix sums of byte lengths (from 0,
+      // non-decreasing), identities come from the mask (in range); only the
+      // totals remain to check
+      if (tid == 0)
+        bad = (int)clause_off[nc] != ncl || (int)card_off[nk] != nkl || (int)var_choice_off[nv] != nch ||
+              (int)choice_off[nch] != nchl;
+    } else {
+      offsets(clause_off, nc, ncl);
+      range(clause_id, nc, nid);
+      offsets(card_off, nk, nkl);
+      range(card_id, nk, nid);
+      offsets(var_choice_off, nv, nch);
+      offsets(choice_off, nch, nchl);
+    }
     range(clause_lits, ncl, 2 * nv);
-    range(clause_id, nc, nid);
-    offsets(card_off, nk, nkl);
     range(card_lits, nkl, nv);
-    range(card_id, nk, nid);
-    offsets(var_choice_off, nv, nch);
-    offsets(choice_off, nch, nchl);
     range(choice_lits, nchl + na, nv);  // choice_lits then anchors, both variables
     if (g_any(bad)) return false;  // the offsets below are now in range
+    // a lane per AtMost row: its positions in registers (rows of up to 16:
+    // independent loads, then register compares), longer rows in a loop
     for (int k = tid; k < nk; k += NT) {
-      const int a = card_off[k], b = card_off[k + 1];
-      for (int j = a + 1; j < b; ++j) {
-        const int x = card_lits[j];
-        if (x != (int)card_lits[j - 1])
-          for (int i = a; i < j - 1; ++i) bad |= (int)card_lits[i] == x;
+      const int a = card_off[k], len = (int)card_off[k + 1] - a;
+      if (len <= 16) {
+        int v[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = i < len ? (int)card_lits[a + i] : -1 - i;
+#pragma unroll
+        for (int j = 2; j < 16; ++j) {
+          bool dup = false;
+#pragma unroll
+          for (int i = 0; i < j - 1; ++i) dup |= v[i] == v[j];
+          bad |= dup && v[j] != v[j - 1];
+        }
+      } else {
+        for (int j = a + 1; j < a + len; ++j) {
+          const int x = card_lits[j];
+          if (x != (int)card_lits[j - 1])
+            for (int i = a; i < j - 1; ++i) bad |= (int)card_lits[i] == x;
+        }
       }
     }
     return !g_any(bad);

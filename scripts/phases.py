@@ -26,7 +26,7 @@ config = int(sys.argv[1]) if len(sys.argv) > 1 else 2
 sizes = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [64, 10000]
 ctx = _lib.Context(0, 1)
 for n in sizes:
-    lw = lowered_config(config, n, 1000)
+    lw = lowered_config(config, n, 1000, packed=os.environ.get("DEPPY_PHASES_FORM") == "packed")
     r = ctx.upload(lw.rec_off, lw.rec)
     r.run()
     r.run()
