@@ -9,7 +9,7 @@ namespace dp {
 // diagnostic stamps per problem: 5 phase cycles, 5 counters, wall-clock
 // start/end, then the first failed index check (code, value, bound) and the
 // number of failed checks, then 3 more counters (Solve, pop_guess, pushes)
-constexpr int DP_NSTAMP = 32;
+constexpr int DP_NSTAMP = 56;
 
 // A problem's fixed-size results, written by one lane as two 16-byte stores:
 // one transaction per problem whether the output region is device memory or

@@ -69,14 +69,22 @@ constexpr bool IMP16_LDS = DP_IMP16;
 
 // wave-shared scalars (S_*), then (multi-wave modes) per-wave reduction slots
 constexpr int32_t NSCAL = 64;
-__host__ __device__ constexpr int32_t mode_nscal(int mode) { return mode == M_LDS ? 8 : NSCAL; }
+__host__ __device__ constexpr int32_t mode_nscal(int mode) {
+#ifdef DP_STAMPS
+  return (mode == M_LDS ? 8 : NSCAL) + 64;  // diagnostic build: 32 int64 phase accumulators after the scalars
+#else
+  return mode == M_LDS ? 8 : NSCAL;
+#endif
+}
 
 // dp_p16_tail_at / dp_p16_tail_bytes (include/deppy_hip.h) for device code.
 __host__ __device__ inline int64_t p16_tail_at(const int32_t* h) {
-  return (2 * ((int64_t)h[DP_H_NCL] + h[DP_H_NKL] + h[DP_H_NK] + h[DP_H_NCHL] + h[DP_H_NA]) + 15) & ~(int64_t)15;
+  const int64_t ch = h[DP_H_FMT] == DP_FMT_P16D ? 0 : h[DP_H_NCHL];
+  return (2 * ((int64_t)h[DP_H_NCL] + h[DP_H_NKL] + h[DP_H_NK] + ch + h[DP_H_NA]) + 15) & ~(int64_t)15;
 }
 __host__ __device__ inline int64_t p16_tail_bytes(const int32_t* h) {
-  return (int64_t)h[DP_H_NC] + h[DP_H_NK] + h[DP_H_NV] + h[DP_H_NCH] + ((int64_t)h[DP_H_NID] + 7) / 8;
+  const int64_t vc = h[DP_H_FMT] == DP_FMT_P16D ? 0 : (int64_t)h[DP_H_NV];
+  return (int64_t)h[DP_H_NC] + h[DP_H_NK] + h[DP_H_NCH] + vc + ((int64_t)h[DP_H_NID] + 7) / 8;
 }
 
 // dp_rec_layout_of (include/deppy_hip.h) for host and device code.
@@ -178,12 +186,35 @@ struct Layout {
   int32_t wbuf;      // IX[wbuf] flattened work list (watch-list positions)       [LDS]
   int32_t cardq;     // IX[cq] AtMost rows queued this round                      [LDS]
   int32_t scal;      // i32[nscal] wave-shared scalars and reduction slots        [LDS]
+  // M_SPLIT / M_SPLIT4 round state in LDS (mode_lds_rounds): a round's
+  // implications in an open-addressing table keyed by variable, the list of
+  // first implications, and a ring of the latest trail entries (the next
+  // round's frontier), so a round touches HBM only for the record
+  int32_t hkey;      // i32[hc] variable of the slot (-1 empty)                    [LDS]
+  int32_t hrp, hrn;  // u32[hc] lowest row implying +v / -v this round (INF none)  [LDS]
+  int32_t tl;        // u16[2hc] first implications, (slot << 1) | negative       [LDS]
+  int32_t fr;        // i32[hc] trail ring: trail[i] at fr[i & (hc - 1)]          [LDS]
+  int32_t hc;        // slots (a power of two; 0 when the mode keeps rounds in HBM)
   int32_t bytes;     // HBM scratch bytes (0 for M_LDS)
   int32_t lds_bytes; // LDS bytes
   int32_t cap, lcap;
 };
 
-enum Scalar { S_NTOUCHED = 0, S_NWORK = 1, S_NK = 2, S_APP = 3, S_SLOT = 32 };
+// S_NTB / S_CVB / S_OVB: two banks each (alternate LDS-table rounds) of the
+// round's first-implication count, lowest variable implied both ways (stored
+// as INF - v, 0 none) and table-overflow flag.
+enum Scalar { S_NTOUCHED = 0, S_NWORK = 1, S_NK = 2, S_APP = 3, S_NTB = 4, S_CVB = 6, S_OVB = 8, S_SLOT = 32 };
+
+// Multi-wave modes whose per-variable state is in LDS keep a round's state
+// there too (Layout::hkey..fr); M_HBM keeps it in HBM.
+__host__ __device__ constexpr bool mode_lds_rounds(int mode) { return mode == M_SPLIT || mode == M_SPLIT4; }
+// Implication-table slots: about one per 8 variables, 64..1024 (a round that
+// implies more than the table holds is redone on the HBM arrays).
+__host__ __device__ inline int32_t round_slots(int32_t nv) {
+  int32_t c = 64;
+  while (c < 1024 && c < nv / 8) c <<= 1;
+  return c;
+}
 
 template <int MODE>
 __host__ __device__ inline Layout layout(const int32_t* h) {
@@ -210,6 +241,12 @@ __host__ __device__ inline Layout layout(const int32_t* h) {
   L.scal = take(mode_nscal(MODE) * 4, WORK);
   L.wbuf = take(mode_wbuf(MODE) * ix, WORK);
   L.cardq = take(mode_cq(MODE) * ix, WORK);
+  L.hc = mode_lds_rounds(MODE) ? round_slots(nv) : 0;
+  L.hkey = take(L.hc * 4, WORK);
+  L.hrp = take(L.hc * 4, WORK);
+  L.hrn = take(L.hc * 4, WORK);
+  L.tl = take(L.hc * 4, WORK);
+  L.fr = take(L.hc * 4, WORK);
   L.val = take(nv, HOT);
   L.d_flip = take(nbv * 4, HOT);
   L.inS = take(nbv * 4, HOT);

@@ -341,6 +341,107 @@ inline uint64_t hmix(uint64_t h, uint64_t x) {
 }
 inline uint64_t keyh(uint64_t tag, uint64_t h) { return tag << 60 | (h & ((1ULL << 60) - 1)); }
 
+// DP_FMT_P16D (include/deppy_hip.h): the choice lists a record's dependency
+// rows imply.  Dependency rows are clause rows of two or more literals, the
+// first negative and the others positive, in row order.  src[k] == 0: list k
+// is the next dependency row's variables after its first literal; src[k] = d
+// > 0: list k repeats list k - d (which took a row).  var_choice_off counts
+// the lists per subject (the first literal's variable; subjects never
+// decrease).  Writes vco[nv+1], co[nch+1], cl[nchl]; false unless every
+// dependency row is taken once and the lists hold exactly nchl variables,
+// every index in range.
+bool implied_choices(const int32_t* clause_off, const int32_t* clause_lits, int32_t nc, int32_t nv, int32_t nch,
+                     int32_t nchl, const uint8_t* src, int32_t* vco, int32_t* co, int32_t* cl) {
+  static thread_local std::vector<int32_t> dep, rowk;
+  dep.clear();
+  for (int32_t r = 0; r < nc; ++r) {
+    const int32_t a = clause_off[r], b = clause_off[r + 1];
+    if (b - a < 2 || !(clause_lits[a] & 1)) continue;
+    bool d = true;
+    for (int32_t j = a + 1; j < b && d; ++j) d = !(clause_lits[j] & 1);
+    if (d) dep.push_back(r);
+  }
+  rowk.assign((size_t)nch, -1);
+  size_t j = 0;
+  int32_t n = 0, filled = 0, last = 0;
+  vco[0] = 0;
+  co[0] = 0;
+  for (int32_t k = 0; k < nch; ++k) {
+    int32_t row;
+    if (src[k] == 0) {
+      if (j == dep.size()) return false;
+      row = dep[j++];
+    } else {
+      if (src[k] > k || src[k - src[k]] != 0) return false;
+      row = rowk[(size_t)(k - src[k])];
+    }
+    rowk[(size_t)k] = row;
+    const int32_t a = clause_off[row], b = clause_off[row + 1];
+    const int32_t s = clause_lits[a] >> 1;
+    if (s < last || s >= nv || n + (b - a - 1) > nchl) return false;
+    last = s;
+    while (filled < s) vco[++filled] = k;
+    for (int32_t q = a + 1; q < b; ++q) {
+      if ((clause_lits[q] >> 1) >= nv) return false;
+      cl[n++] = clause_lits[q] >> 1;
+    }
+    co[k + 1] = n;
+  }
+  while (filled < nv) vco[++filled] = nch;
+  return j == dep.size() && n == nchl;
+}
+
+// The DP_FMT_P16D sources of an int32 record's choice lists (src[nch]), or
+// false when its dependency rows do not imply them (a list whose row was
+// folded away, a repeat more than 255 lists back, ...).  Matched greedily:
+// list k takes the next dependency row when that row is (~subject, list k),
+// else repeats an earlier list of the same subject and content.
+bool choice_sources(const int32_t* r, const dp_rec_layout& L, uint8_t* src) {
+  const int32_t nc = r[DP_H_NC], nv = r[DP_H_NV], nch = r[DP_H_NCH];
+  const int32_t* clause_off = r + L.clause_off;
+  const int32_t* clause_lits = r + L.clause_lits;
+  const int32_t* vco = r + L.var_choice_off;
+  const int32_t* co = r + L.choice_off;
+  const int32_t* cl = r + L.choice_lits;
+  int32_t row = 0, v = 0;
+  auto next_dep = [&]() {
+    for (; row < nc; ++row) {
+      const int32_t a = clause_off[row], b = clause_off[row + 1];
+      if (b - a < 2 || !(clause_lits[a] & 1)) continue;
+      bool d = true;
+      for (int32_t j = a + 1; j < b && d; ++j) d = !(clause_lits[j] & 1);
+      if (d) return;
+    }
+  };
+  auto same = [&](int32_t k, int32_t k2) {
+    return co[k + 1] - co[k] == co[k2 + 1] - co[k2] && std::equal(cl + co[k], cl + co[k + 1], cl + co[k2]);
+  };
+  next_dep();
+  for (int32_t k = 0; k < nch; ++k) {
+    while (v < nv && vco[v + 1] <= k) ++v;
+    bool took = false;
+    if (row < nc) {
+      const int32_t a = clause_off[row], b = clause_off[row + 1];
+      if (clause_lits[a] == 2 * v + 1 && b - a - 1 == co[k + 1] - co[k]) {
+        took = true;
+        for (int32_t q = 0; q < b - a - 1 && took; ++q) took = clause_lits[a + 1 + q] == 2 * cl[co[k] + q];
+      }
+    }
+    if (took) {
+      src[k] = 0;
+      ++row;
+      next_dep();
+      continue;
+    }
+    int32_t d = 1;
+    for (; d <= 255 && d <= k && vco[v] <= k - d; ++d)
+      if (src[k - d] == 0 && same(k, k - d)) break;
+    if (d > 255 || d > k || vco[v] > k - d) return false;
+    src[k] = (uint8_t)d;
+  }
+  return true;
+}
+
 struct Lowerer {
   const dp_wire& w;
   const bool narrow;  // DP_LOWER_NARROW: records that fit 16 bits in the DP_FMT_U16 form
@@ -382,27 +483,47 @@ struct Lowerer {
     O.rec_len.back() = padded;
   }
 
-  // The int32 record r (fits16) in the DP_FMT_P16 form, in place, if it
-  // allows it (every identity one row, each row kind's identities
-  // ascending, lengths below 256, DP_P16_TAIL_MAX); false leaves r as it is.
+  // The int32 record r (fits16) in a packed form, in place, if it allows it
+  // (every identity one row, each row kind's identities ascending, lengths
+  // below 256, DP_P16_TAIL_MAX): DP_FMT_P16D when its dependency rows imply
+  // its choice lists, else DP_FMT_P16.  False leaves r as it is.
   static bool pack16(int32_t* r) {
-    if (!dp_rec_fits16(r) || r[DP_H_NID] != r[DP_H_NC] + r[DP_H_NK] ||
-        dp_p16_tail_bytes(r) > DP_P16_TAIL_MAX)
-      return false;
+    if (!dp_rec_fits16(r) || r[DP_H_NID] != r[DP_H_NC] + r[DP_H_NK]) return false;
     const dp_rec_layout L = dp_rec_layout_of(r);
     const int32_t nc = r[DP_H_NC], nk = r[DP_H_NK], nv = r[DP_H_NV], nch = r[DP_H_NCH], nid = r[DP_H_NID];
+    // DP_FMT_P16D when the dependency rows imply the choice lists exactly
+    static thread_local std::vector<int32_t> ch;
+    static thread_local std::vector<uint8_t> srcs;
+    ch.resize((size_t)nv + 1 + nch + 1 + r[DP_H_NCHL]);
+    srcs.assign((size_t)nch + 1, 0);
+    int32_t* vco = ch.data();
+    int32_t* co = vco + nv + 1;
+    int32_t* cl = co + nch + 1;
+    const bool derived =
+        choice_sources(r, L, srcs.data()) &&
+        implied_choices(r + L.clause_off, r + L.clause_lits, nc, nv, nch, r[DP_H_NCHL], srcs.data(), vco, co, cl) &&
+        std::equal(vco, vco + nv + 1, r + L.var_choice_off) && std::equal(co, co + nch + 1, r + L.choice_off) &&
+        std::equal(cl, cl + r[DP_H_NCHL], r + L.choice_lits);
     for (int32_t i = 1; i < nc; ++i)
       if (r[L.clause_id + i] <= r[L.clause_id + i - 1]) return false;
     for (int32_t i = 1; i < nk; ++i)
       if (r[L.card_id + i] <= r[L.card_id + i - 1]) return false;
+    for (int32_t k = 0; k < nk; ++k)
+      if (r[L.card_id + k] < 0 || r[L.card_id + k] >= nid) return false;
     auto short_lens = [&](int32_t off, int32_t n) {
       for (int32_t j = 0; j < n; ++j)
         if (r[off + j + 1] - r[off + j] > 255) return false;
       return true;
     };
-    if (!short_lens(L.clause_off, nc) || !short_lens(L.card_off, nk) || !short_lens(L.var_choice_off, nv) ||
-        !short_lens(L.choice_off, nch))
+    if (!short_lens(L.clause_off, nc) || !short_lens(L.card_off, nk) ||
+        (!derived && (!short_lens(L.var_choice_off, nv) || !short_lens(L.choice_off, nch))))
       return false;
+    const int32_t fmt0 = r[DP_H_FMT];
+    r[DP_H_FMT] = derived ? DP_FMT_P16D : DP_FMT_P16;  // (the tail's size depends on the form)
+    if (dp_p16_tail_bytes(r) > DP_P16_TAIL_MAX) {
+      r[DP_H_FMT] = fmt0;
+      return false;
+    }
     static thread_local std::vector<uint8_t> buf;
     const int64_t at = dp_p16_tail_at(r), tb = dp_p16_tail_bytes(r);
     buf.assign((size_t)(at + tb), 0);
@@ -413,7 +534,7 @@ struct Lowerer {
     put16(L.clause_lits, r[DP_H_NCL]);
     put16(L.card_lits, r[DP_H_NKL]);
     put16(L.card_bound, nk);
-    put16(L.choice_lits, r[DP_H_NCHL]);
+    if (!derived) put16(L.choice_lits, r[DP_H_NCHL]);
     put16(L.anchors, r[DP_H_NA]);
     uint8_t* t = buf.data() + at;
     auto put_lens = [&](int32_t off, int32_t n) {
@@ -421,15 +542,15 @@ struct Lowerer {
     };
     put_lens(L.clause_off, nc);
     put_lens(L.card_off, nk);
-    put_lens(L.var_choice_off, nv);
-    put_lens(L.choice_off, nch);
-    for (int32_t k = 0; k < nk; ++k) {
-      const int32_t id = r[L.card_id + k];
-      if (id < 0 || id >= nid) return false;
-      t[id >> 3] |= (uint8_t)(1u << (id & 7));
+    if (!derived) {
+      put_lens(L.var_choice_off, nv);
+      put_lens(L.choice_off, nch);
+    } else {
+      std::memcpy(t, srcs.data(), (size_t)nch);
+      t += nch;
     }
+    for (int32_t k = 0; k < nk; ++k) t[r[L.card_id + k] >> 3] |= (uint8_t)(1u << (r[L.card_id + k] & 7));
     std::memcpy(r + DP_H_SIZE, buf.data(), buf.size());
-    r[DP_H_FMT] = DP_FMT_P16;
     return true;
   }
 
@@ -1139,10 +1260,10 @@ int dp_rec_widen(const int32_t* rec, int64_t avail, int32_t* out) {
   for (int i = DP_H_NV; i <= DP_H_NCHL; ++i)
     if (rec[i] < 0 || rec[i] > (1 << 28)) return -3;
   const int32_t fmt = rec[DP_H_FMT];
-  if (fmt != DP_FMT_I32 && fmt != DP_FMT_U16 && fmt != DP_FMT_P16 && fmt != DP_FMT_I32W) return -16;
+  if (fmt != DP_FMT_I32 && fmt != DP_FMT_U16 && !dp_fmt_packed(fmt) && fmt != DP_FMT_I32W) return -16;
   const dp_rec_layout L = dp_rec_layout_of(rec);
-  if (L.words != rec[DP_H_WORDS] || ((fmt == DP_FMT_U16 || fmt == DP_FMT_P16) && !dp_rec_fits16(rec))) return -4;
-  if (fmt == DP_FMT_P16 && dp_p16_tail_bytes(rec) > DP_P16_TAIL_MAX) return -17;
+  if (L.words != rec[DP_H_WORDS] || ((fmt == DP_FMT_U16 || dp_fmt_packed(fmt)) && !dp_rec_fits16(rec))) return -4;
+  if (dp_fmt_packed(fmt) && dp_p16_tail_bytes(rec) > DP_P16_TAIL_MAX) return -17;
   if (dp_rec_phys_words(rec) > avail) return -4;
   const int64_t words = rec[DP_H_WORDS];
   std::memcpy(out, rec, 4 * DP_H_SIZE);
@@ -1160,7 +1281,7 @@ int dp_rec_widen(const int32_t* rec, int64_t avail, int32_t* out) {
     get16(L.clause_lits, rec[DP_H_NCL]);
     get16(L.card_lits, rec[DP_H_NKL]);
     get16(L.card_bound, rec[DP_H_NK]);
-    get16(L.choice_lits, rec[DP_H_NCHL]);
+    if (fmt == DP_FMT_P16) get16(L.choice_lits, rec[DP_H_NCHL]);
     get16(L.anchors, rec[DP_H_NA]);
     const uint8_t* t = reinterpret_cast<const uint8_t*>(rec + DP_H_SIZE) + dp_p16_tail_at(rec);
     auto get_lens = [&](int32_t off, int32_t n) {
@@ -1169,8 +1290,13 @@ int dp_rec_widen(const int32_t* rec, int64_t avail, int32_t* out) {
     };
     get_lens(L.clause_off, rec[DP_H_NC]);
     get_lens(L.card_off, rec[DP_H_NK]);
-    get_lens(L.var_choice_off, rec[DP_H_NV]);
-    get_lens(L.choice_off, rec[DP_H_NCH]);
+    const uint8_t* srcs = t;
+    if (fmt == DP_FMT_P16) {
+      get_lens(L.var_choice_off, rec[DP_H_NV]);
+      get_lens(L.choice_off, rec[DP_H_NCH]);
+    } else {
+      t += rec[DP_H_NCH];  // the lists' sources; the lists follow the identities
+    }
     int32_t c0 = 0, c1 = 0;
     const int32_t nc = rec[DP_H_NC], nk = rec[DP_H_NK];
     for (int32_t i = 0; i < rec[DP_H_NID]; ++i) {
@@ -1183,6 +1309,13 @@ int dp_rec_widen(const int32_t* rec, int64_t avail, int32_t* out) {
       }
     }
     if (c0 != nc || c1 != nk) return -18;
+    // DP_FMT_P16D: the lists from the rows (the clause literals are not
+    // range-checked yet: implied_choices checks every index it derives)
+    if (fmt == DP_FMT_P16D &&
+        (out[L.clause_off + nc] != rec[DP_H_NCL] ||
+         !dp::implied_choices(out + L.clause_off, out + L.clause_lits, nc, rec[DP_H_NV], rec[DP_H_NCH], rec[DP_H_NCHL],
+                              srcs, out + L.var_choice_off, out + L.choice_off, out + L.choice_lits)))
+      return -20;
   }
   return 0;
 }
@@ -1207,7 +1340,7 @@ int dp_rec_validate(const int32_t* rec, int64_t words) {
     t[DP_H_FMT] = DP_FMT_I32;
     return dp_rec_validate(t.data(), (int64_t)t.size());
   }
-  if (rec[DP_H_FMT] == DP_FMT_U16 || rec[DP_H_FMT] == DP_FMT_P16) {  // widen, then the int32 checks
+  if (rec[DP_H_FMT] == DP_FMT_U16 || dp_fmt_packed(rec[DP_H_FMT])) {  // widen, then the int32 checks
     for (int i = DP_H_NV; i <= DP_H_NCHL; ++i)
       if (rec[i] < 0 || rec[i] > (1 << 28)) return -3;
     std::vector<int32_t> w((size_t)std::max<int32_t>(rec[DP_H_WORDS], DP_H_SIZE));

@@ -97,9 +97,9 @@ bool header_ok(const int32_t* h, int64_t avail) {
   for (int i = DP_H_NV; i <= DP_H_NCHL; ++i)
     if (h[i] < 0 || h[i] > (1 << 28)) return false;
   const int32_t fmt = h[DP_H_FMT];
-  if (fmt != DP_FMT_I32 && fmt != DP_FMT_I32W && ((fmt != DP_FMT_U16 && fmt != DP_FMT_P16) || !dp_rec_fits16(h)))
+  if (fmt != DP_FMT_I32 && fmt != DP_FMT_I32W && ((fmt != DP_FMT_U16 && !dp_fmt_packed(fmt)) || !dp_rec_fits16(h)))
     return false;
-  if (fmt == DP_FMT_P16 && dp_p16_tail_bytes(h) > DP_P16_TAIL_MAX) return false;
+  if (dp_fmt_packed(fmt) && dp_p16_tail_bytes(h) > DP_P16_TAIL_MAX) return false;
   const int64_t w = dp_rec_layout_of(h).words;
   return w == h[DP_H_WORDS] && dp_rec_phys_words(h) <= avail;
 }
@@ -168,7 +168,7 @@ void read_head(Head& H, const int32_t* h, int64_t avail, int32_t opt_flags, bool
   H.sw = staged_words(h, nar);
   // the record image the kernel reads: the packed form as it is, else the
   // 16-bit form (LDS path) or the int32 form with its watch lists
-  H.rec_bytes = nar ? (h[DP_H_FMT] == DP_FMT_P16 ? 4 * dp_rec_phys_words(h)
+  H.rec_bytes = nar ? (dp_fmt_packed(h[DP_H_FMT]) ? 4 * dp_rec_phys_words(h)
                                                  : 4 * DP_H_SIZE + 2 * ((int64_t)h[DP_H_WORDS] - DP_H_SIZE))
                     : 4 * (int64_t)img_layout(h).words;
   if (nar) {
@@ -176,7 +176,7 @@ void read_head(Head& H, const int32_t* h, int64_t avail, int32_t opt_flags, bool
     int k = 0;
     while (H.lds > kCeilings[k]) ++k;
     H.bucket = (int8_t)k;
-    H.direct = aligned && (h[DP_H_FMT] == DP_FMT_U16 || h[DP_H_FMT] == DP_FMT_P16);
+    H.direct = aligned && (h[DP_H_FMT] == DP_FMT_U16 || dp_fmt_packed(h[DP_H_FMT]));
     return;
   }
   H.direct = aligned && h[DP_H_FMT] == DP_FMT_I32W;  // the multi-wave staged form
@@ -475,7 +475,7 @@ bool stage_one(const Plan& P, const int32_t* rec, const int64_t* rec_off, int32_
   } else {
     d[DP_H_FMT] = DP_FMT_I32;
     bool ok;
-    if (fmt == DP_FMT_P16) {  // its int32 form, then the checked copy
+    if (dp_fmt_packed(fmt)) {  // its int32 form, then the checked copy
       static thread_local std::vector<int32_t> wide;
       wide.resize((size_t)words);
       ok = dp_rec_widen(src, rec_off[p0 + i + 1] - rec_off[p0 + i], wide.data()) == 0 &&
@@ -1326,8 +1326,8 @@ int dp_stage_roundtrip(const dp_batch* b, int32_t opt_flags, int32_t chunk_probl
       const int64_t words = src[DP_H_WORDS];
       wide.resize((size_t)words);
       std::memcpy(wide.data(), st, 4 * DP_H_SIZE);
-      if (src[DP_H_FMT] == DP_FMT_P16) {  // staged as it is (one-wavefront), else not shown
-        if (st[DP_H_FMT] == DP_FMT_P16) std::memcpy(o, st, 4 * (size_t)dp_rec_phys_words(src));
+      if (dp_fmt_packed(src[DP_H_FMT])) {  // staged as it is (one-wavefront), else not shown
+        if (dp_fmt_packed(st[DP_H_FMT])) std::memcpy(o, st, 4 * (size_t)dp_rec_phys_words(src));
         continue;
       }
       if (st[DP_H_FMT] == DP_FMT_U16 || st[DP_H_FMT] == dp::DP_FMT_U16_CHECKED) {

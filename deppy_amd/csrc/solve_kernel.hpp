@@ -115,10 +115,11 @@ __device__ __forceinline__ int64_t wallclock() {
 #else
 #define DP_STAMP(i) (void)0
 #endif
-// Index checks of the diagnostic build: a data-derived index outside its
+// Index checks of the diagnostic build (-DDP_STAMPS -DDP_CHECKS; the calls
+// cost registers, so plain phase builds leave them out): a data-derived index outside its
 // range is recorded (first failure per problem) and clamped to `lo`, so a
 // broken invariant shows up as a report instead of a memory fault.
-#ifdef DP_STAMPS
+#if defined(DP_STAMPS) && defined(DP_CHECKS)
 #define DP_CHK(x, lo, hi, code) chk((x), (lo), (hi), (code))
 #else
 #define DP_CHK(x, lo, hi, code) (x)
@@ -181,6 +182,14 @@ struct Group {
   uint32_t *d_flip, *inS, *extra, *seen, *model, *used, *en, *en2, *dset, *fg;
   IX *wbuf, *cardq;
   int32_t* scal;
+  // LDS round state (mode_lds_rounds; layout.hpp Layout::hkey..fr)
+  static constexpr bool LR = mode_lds_rounds(MODE);
+  int32_t *hkey, *fr;
+  uint32_t *hrp, *hrn;
+  uint16_t* tl;
+  int hmask;   // hc - 1
+  bool hmode;  // this round's implications go to the LDS table (else imp/touched in HBM)
+  int rb;      // the LDS-table round's counter bank (S_NTB / S_CVB / S_OVB)
   int cap, lcap;
   int tid, lane, wid;
   // ---- group-uniform state (registers, identical in every thread) ----
@@ -203,7 +212,7 @@ struct Group {
   // round: 1-literal visit cycles, flattened-frontier cycles, AtMost flush
   // cycles, learned-row cycles, watch entries visited, frontier literals of
   // flattened rounds, learned rows evaluated, AtMost rows flushed
-  int64_t acc[16];
+  unsigned long long* lacc;  // LDS phase accumulators (thread 0 adds; no registers held)
   int64_t sub[3];           // init: record staging, validation, watch-list build cycles
   unsigned long long* dbg;  // [first code, value, bound, failures]
   __device__ __noinline__ int chk_fail(int x, int hi, int code) {
@@ -219,7 +228,7 @@ struct Group {
   __device__ __forceinline__ int chk(int x, int lo, int hi, int code) {
     return (x < lo || x >= hi) ? (chk_fail(x, hi, code), lo) : x;
   }
-#define DP_ACC(i, x) acc[i] += (x)
+#define DP_ACC(i, x) do { if (tid == 0) atomicAdd(&lacc[i], (unsigned long long)(x)); } while (0)
 #else
 #define DP_ACC(i, x) (void)0
 #endif
@@ -232,7 +241,17 @@ struct Group {
   // in HBM and __syncthreads() only drains LDS traffic (lgkmcnt) before
   // s_barrier: a wavefront could pass it with global stores still in flight
   // and another wavefront read the old words.  Drain every counter first.
-  __device__ __forceinline__ static void bar() {
+  // Within an LDS-table round (lds_sync) the wavefronts hand each other only
+  // LDS words: the round's global stores (reason, rs, trail) are read by no
+  // other wavefront before propagate() returns, which drains them.
+  bool lds_sync;
+  __device__ __forceinline__ void bar() const {
+    if constexpr (mode_lds_rounds(MODE)) {
+      if (lds_sync) {
+        __syncthreads();
+        return;
+      }
+    }
     __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0)
     __syncthreads();
 #ifdef DP_BAR_INV
@@ -362,7 +381,7 @@ struct Group {
       IX* b = reinterpret_cast<IX*>(lds + L.body);
       const int4* src = reinterpret_cast<const int4*>(grec + DP_H_SIZE);
       const int fmt = h[DP_H_FMT];
-      packed = fmt == DP_FMT_P16;
+      packed = fmt == DP_FMT_P16 || fmt == DP_FMT_P16D;
       if (!packed && fmt != DP_FMT_U16 && fmt != DP_FMT_U16_CHECKED) return false;
       const int groups = packed ? (int)((p16_tail_at(h) + p16_tail_bytes(h) + 15) >> 4)
                                 : (h[DP_H_WORDS] - DP_H_SIZE + 7) >> 3;
@@ -383,21 +402,25 @@ struct Group {
       }
       body = b;
       if (packed) {
-        // DP_FMT_P16 in LDS: the uint16 arrays where they landed, then the
-        // offsets arrays and the identities decoded from the tail
+        // DP_FMT_P16 / DP_FMT_P16D in LDS: the uint16 arrays where they
+        // landed, then the offsets arrays and the identities decoded from the
+        // tail (and, DP_FMT_P16D, the choice lists derived after them)
+        const bool derived = fmt == DP_FMT_P16D;
         IX* q = b;
         clause_lits = q; q += ncl;
         card_lits = q;   q += nkl;
         card_bound = q;  q += nk;
-        choice_lits = q; q += nchl;
+        if (!derived) { choice_lits = q; q += nchl; }
         anchors = q;     q += na;
         clause_off = q;  q += nc + 1;
         card_off = q;    q += nk + 1;
         var_choice_off = q; q += nv + 1;
         choice_off = q;  q += nch + 1;
         clause_id = q;   q += nc;
-        card_id = q;
-        if (!unpack16(reinterpret_cast<const char*>(b) + p16_tail_at(h), (int)p16_tail_bytes(h)))
+        card_id = q;     q += nk;
+        if (derived) choice_lits = q;
+        if (!unpack16(reinterpret_cast<const char*>(b) + p16_tail_at(h), (int)p16_tail_bytes(h), derived,
+                      lds + L.reason))
           return false;
       }
     } else {
@@ -438,6 +461,18 @@ struct Group {
     wbuf = reinterpret_cast<IX*>(lds + L.wbuf);
     cardq = reinterpret_cast<IX*>(lds + L.cardq);
     scal = reinterpret_cast<int32_t*>(lds + L.scal);
+    hkey = reinterpret_cast<int32_t*>(lds + L.hkey);
+    hrp = reinterpret_cast<uint32_t*>(lds + L.hrp);
+    hrn = reinterpret_cast<uint32_t*>(lds + L.hrn);
+    tl = reinterpret_cast<uint16_t*>(lds + L.tl);
+    fr = reinterpret_cast<int32_t*>(lds + L.fr);
+    hmask = L.hc - 1;
+    hmode = LR;
+    lds_sync = false;
+    rb = 0;
+#ifdef DP_STAMPS
+    lacc = reinterpret_cast<unsigned long long*>(scal + (MODE == M_LDS ? 8 : NSCAL));
+#endif
     cap = L.cap; lcap = L.lcap;
     tlen = qhead = 0;
     steps = 0;
@@ -455,7 +490,6 @@ struct Group {
     tr_cap = tr_len = 0;
     tr_stop = false;
 #ifdef DP_STAMPS
-    for (int i = 0; i < 16; ++i) acc[i] = 0;
     dbg = nullptr;
 #endif
 #ifdef DP_STAMPS
@@ -489,10 +523,12 @@ struct Group {
       for (int v = tid; v < (nv + 3) / 4; v += NT) reinterpret_cast<uint32_t*>(val)[v] = 0;
     }
     for (int l = tid; l < 2 * nv; l += NT) imp[l] = (IMP)IMP_NONE;
+    if constexpr (LR)
+      for (int i = tid; i <= hmask; i += NT) { hkey[i] = -1; hrp[i] = (uint32_t)INF; hrn[i] = (uint32_t)INF; }
     for (int i = tid; i < nbv; i += NT) {
       d_flip[i] = 0; inS[i] = 0; extra[i] = 0; seen[i] = 0; model[i] = 0; dset[i] = 0; fg[i] = 0;
     }
-    if (tid < mode_nscal(MODE)) scal[tid] = 0;
+    for (int i = tid; i < mode_nscal(MODE); i += NT) scal[i] = 0;
     if (tid == 0) l_off[0] = 0;
     gsync();
     return true;
@@ -545,7 +581,8 @@ struct Group {
     }
     range(clause_lits, ncl, 2 * nv);
     range(card_lits, nkl, nv);
-    range(choice_lits, nchl + na, nv);  // choice_lits then anchors, both variables
+    range(choice_lits, nchl, nv);
+    range(anchors, na, nv);
     if (g_any(bad)) return false;  // the offsets below are now in range
     // a lane per AtMost row: its positions in registers (rows of up to 16:
     // independent loads, then register compares), longer rows in a loop
@@ -626,7 +663,11 @@ struct Group {
   // its lane by ds_bpermute.  Lengths become offsets by a DPP scan, the mask
   // becomes clause / AtMost identities by ballot ranks.  False when the mask
   // does not have nc clear and nk set bits (a malformed record).
-  __device__ __forceinline__ bool unpack16(const char* tail, int tb) {
+  // DP_FMT_P16D (derived): the choice lists from the dependency rows and the
+  // lists' sources (include/deppy_hip.h; lower.cpp implied_choices), with
+  // `scratch` (the per-literal arrays' LDS, not yet in use) for the
+  // dependency rows by rank, each list's row and the per-subject counts.
+  __device__ __forceinline__ bool unpack16(const char* tail, int tb, bool derived, char* scratch) {
     static_assert(MODE == M_LDS, "16-bit records run one wavefront per problem");
     uint4 r = make_uint4(0u, 0u, 0u, 0u);
     if (16 * lane < tb) r = *reinterpret_cast<const uint4*>(tail + 16 * lane);
@@ -654,8 +695,13 @@ struct Group {
     };
     lens(clause_off, nc);
     lens(card_off, nk);
-    lens(var_choice_off, nv);
-    lens(choice_off, nch);
+    const int src_at = at;
+    if (!derived) {
+      lens(var_choice_off, nv);
+      lens(choice_off, nch);
+    } else {
+      at += nch;
+    }
     IX* cid = const_cast<IX*>(clause_id);
     IX* kid = const_cast<IX*>(card_id);
     int c0 = 0, c1 = 0;
@@ -679,7 +725,104 @@ struct Group {
       c0 += __popcll(~mb & mv);
     }
     wsync();
-    return c0 == nc && c1 == nk;
+    if (c0 != nc || c1 != nk) return false;
+    if (!derived) return true;
+    // -- DP_FMT_P16D: the choice lists --
+    if ((int)clause_off[nc] != ncl) return false;  // (rows read below stay in clause_lits)
+    uint16_t* depr = reinterpret_cast<uint16_t*>(scratch);  // [nch] dependency rows by rank
+    uint16_t* rowk = depr + nch;                             // [nch] each list's row
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(scratch + ((4 * nch + 15) & ~15));  // [nv + 1]
+    IX* co = const_cast<IX*>(choice_off);
+    IX* cl = const_cast<IX*>(choice_lits);
+    IX* vco = const_cast<IX*>(var_choice_off);
+    for (int i = tid; i <= nv; i += NT) cnt[i] = 0u;
+    bool bad = false;
+    int nd = 0;  // dependency rows
+    for (int c = 0; c < nc; c += 64) {
+      const int r = c + lane;
+      bool dep = false;
+      if (r < nc) {
+        const int a = clause_off[r], e = clause_off[r + 1];
+        dep = e - a >= 2 && ((int)clause_lits[a] & 1);
+        for (int j = a + 1; j < e && dep; ++j) dep = !((int)clause_lits[j] & 1);
+      }
+      const uint64_t m = __ballot(dep);
+      const int j = nd + __popcll(m & lt);
+      if (dep && j < nch) depr[j] = (uint16_t)r;
+      nd += __popcll(m);
+    }
+    bad |= nd > nch;
+    wsync();
+    int taken = 0, n0 = 0, smax = -1;
+    for (int c = 0; c < nch; c += 64) {
+      const int k = c + lane;
+      const int sv = tbyte(src_at + min(k, nch - 1));
+      const bool zero = k < nch && sv == 0;
+      const uint64_t mz = __ballot(zero);
+      const int j = taken + __popcll(mz & lt);
+      taken += __popcll(mz);
+      if (zero) {
+        bad |= j >= nd;
+        rowk[k] = j < nd ? depr[j] : (uint16_t)0;
+      }
+      // a repeat names an earlier list that took a row (written above or
+      // in an earlier chunk)
+      const int ks = k - sv;
+      const int ss = tbyte(src_at + max(0, min(ks, nch - 1)));
+      wsync();
+      if (k < nch && !zero) {
+        bad |= ks < 0 || ss != 0;
+        rowk[k] = ks >= 0 ? rowk[ks] : (uint16_t)0;
+      }
+      wsync();
+      int x = 0, s = -1, a = 0;
+      if (k < nch) {
+        const int row = rowk[k];
+        a = clause_off[row];
+        x = (int)clause_off[row + 1] - a - 1;
+        s = (int)clause_lits[a] >> 1;
+      }
+      const int incl = wave_incl_scan(x);
+      const int n = n0 + incl - x;
+      int pm = s;  // the highest subject of the lists up to this one
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(pm, d);
+        if (lane >= d) pm = max(pm, y);
+      }
+      const int up = __shfl_up(pm, 1);
+      const int before = max(smax, lane > 0 ? up : -1);
+      if (k < nch) {
+        if (s >= nv || s < before || n + x > nchl) {
+          bad = true;
+        } else {
+          for (int q = 0; q < x; ++q) {
+            const int l = clause_lits[a + 1 + q];
+            bad |= (l >> 1) >= nv;
+            cl[n + q] = enc(l >> 1);
+          }
+          co[k + 1] = enc(n + x);
+          atomicAdd(&cnt[s], 1u);
+        }
+      }
+      n0 += __builtin_amdgcn_readlane(incl, 63);
+      smax = max(smax, __builtin_amdgcn_readlane(pm, 63));
+    }
+    if (lane == 0) co[0] = enc(0);
+    bad |= taken != nd || n0 != nchl;
+    wsync();
+    if (__ballot(bad)) return false;
+    int carry = 0;
+    for (int c = 0; c <= nv; c += 64) {
+      const int v = c + lane;
+      const int y = v < nv ? (int)cnt[v] : 0;
+      const int incl = wave_incl_scan(y) + carry;
+      if (v < nv) vco[v + 1] = enc(incl);
+      carry = __builtin_amdgcn_readlane(incl, 63);
+    }
+    if (lane == 0) vco[0] = enc(0);
+    wsync();
+    return true;
   }
 
   // Watch lists of a one-wavefront problem, built in LDS from its record
@@ -787,8 +930,54 @@ struct Group {
   }
   // record "row r implies literal l" (lowest row wins, oracle: note); the
   // first implication of a literal in the round lists it
+  // LDS table: probe for variable l >> 1 (claiming an empty slot), keep the
+  // lowest row per polarity, list the slot on the round's first implication
+  // of l.  A full table flags the round for a redo on the HBM arrays.
+  __device__ __forceinline__ void note_lds(int l, int r) {
+    const int v = l >> 1;
+    int h = (int)(((uint32_t)v * 2654435761u) >> 16) & hmask;
+    for (int probe = 0;; ++probe) {
+      const int k = hkey[h];
+      if (k == v) break;
+      if (k < 0) {
+        const int old = atomicCAS(&hkey[h], -1, v);
+        if (old < 0 || old == v) break;
+      }
+      if (probe == 32 || probe == hmask) {
+        scal[S_OVB + rb] = 1;
+        return;
+      }
+      h = (h + 1) & hmask;
+    }
+    uint32_t* rr = (l & 1) ? hrn : hrp;
+    if (atomicMin(&rr[h], (uint32_t)r) == (uint32_t)INF) {
+      tl[atomicAdd(&scal[S_NTB + rb], 1)] = (uint16_t)((h << 1) | (l & 1));
+      // implied both ways?  Of the two first implications of v, the later
+      // one (in the LDS's order of these atomics) sees the other's row.
+      const uint32_t* ro = (l & 1) ? hrp : hrn;
+      if (ro[h] != (uint32_t)INF) atomicMax(&scal[S_CVB + rb], INF - v);
+    }
+  }
+  // the slot of variable v (listed this round)
+  __device__ __forceinline__ int slot_of(int v) const {
+    int h = (int)(((uint32_t)v * 2654435761u) >> 16) & hmask;
+    while (hkey[h] != v) h = (h + 1) & hmask;
+    return h;
+  }
+  // trail position i holds literal l (and the ring, for the next round's frontier)
+  __device__ __forceinline__ void put_trail(int i, int l) {
+    trail[DP_CHK(i, 0, nv, 9)] = enc(l);
+    if constexpr (LR) fr[i & hmask] = l;
+  }
+
   __device__ __forceinline__ void note(int l, int r) {
     l = DP_CHK(l, 0, 2 * nv, 1);
+    if constexpr (LR) {
+      if (hmode) {
+        note_lds(l, r);
+        return;
+      }
+    }
     if (imp_min(l, r))
       touched[DP_CHK(atomicAdd(&scal[S_NTOUCHED], 1), 0, 2 * nv, 2)] = enc(l);
   }
@@ -983,13 +1172,72 @@ struct Group {
     val[v] = (l & 1) ? -1 : 1;
     reason[v] = enc(r);
     rs[v] = enc(start);
-    trail[DP_CHK(start + i, 0, nv, 9)] = enc(l);
+    put_trail(start + i, l);
     imp[l] = (IMP)IMP_NONE;
+  }
+
+  // The round's table slots back to empty (every thread has read them).
+  __device__ __forceinline__ void clear_slots(int nt) {
+    gsync();
+    for (int i = tid; i < nt; i += NT) {
+      const int h = tl[i] >> 1;
+      hkey[h] = -1; hrp[h] = (uint32_t)INF; hrn[h] = (uint32_t)INF;
+    }
+    gsync();
+  }
+
+  // finish_round on the LDS table (hmode): one exchange, then the commit.
+  // Returns 2 when the table overflowed: nothing was committed and the caller
+  // redoes the round on the HBM arrays (the outcome does not depend on where
+  // the round is kept).  The bank's counters are read here and reset at the
+  // start of the round after next (run_round), past this round's last barrier.
+  __device__ __forceinline__ int finish_round_lds(int crow) {
+    const int cr = g_min(crow);  // the notes, the AtMost flush and the counters are complete
+    const int nt = DP_CHK(scal[S_NTB + rb], 0, 2 * (hmask + 1) + 1, 4);
+    const bool ovf = scal[S_OVB + rb] != 0;
+    const int cvx = scal[S_CVB + rb];
+    if (tid == 0) scal[S_NK] = 0;  // the AtMost queue was flushed (read before the exchange)
+    if (ovf) {
+      clear_slots(nt);
+      return 2;
+    }
+    if (cr != INF) {
+      c_row = cr;
+      clear_slots(nt);
+      ck = CK_ROW;
+      return -1;
+    }
+    if (cvx != 0) {
+      c_var = INF - cvx;
+      const int h = slot_of(c_var);
+      c_rp = (int)hrp[h]; c_rn = (int)hrn[h];
+      ck = CK_VAR; c_row = tlen;  // bound: every variable assigned so far
+      clear_slots(nt);
+      return -1;
+    }
+    // no variable is listed twice: each thread reads and empties its own slots
+    const int start = tlen;
+    for (int i = tid; i < nt; i += NT) {
+      const int e = tl[i], h = e >> 1, v = hkey[h];
+      const int l = 2 * v + (e & 1);
+      const int r = (int)((e & 1) ? hrn[h] : hrp[h]);
+      val[v] = (l & 1) ? -1 : 1;
+      reason[v] = enc(r);
+      rs[v] = enc(start);
+      put_trail(start + i, l);
+      hkey[h] = -1; hrp[h] = (uint32_t)INF; hrn[h] = (uint32_t)INF;
+    }
+    tlen += nt;
+    gsync();
+    return 0;
   }
 
   // Commit the implications of the round, or report its conflict: the lowest
   // conflicting row, else the lowest variable implied both ways.
   __device__ __forceinline__ int finish_round(int crow) {
+    if constexpr (LR) {
+      if (hmode) return finish_round_lds(crow);
+    }
     gsync();
     const int nt = DP_CHK(scal[S_NTOUCHED], 0, 2 * nv + 1, 4);
     if constexpr (NW > 1) {
@@ -1060,7 +1308,7 @@ struct Group {
         const int at = claim(f, run);
         if (f) {
           val[v] = -1; reason[v] = enc(R_EXTRA); rs[v] = enc(start);
-          trail[DP_CHK(at, 0, nv, 28)] = enc(2 * v + 1);
+          put_trail(at, 2 * v + 1);
         }
       }
       claim_end(run);
@@ -1072,6 +1320,11 @@ struct Group {
   }
 
   __device__ __forceinline__ int propagate() {
+    const int r = propagate_rounds();
+    if constexpr (LR) bar();  // the rounds' global stores, for every wavefront
+    return r;
+  }
+  __device__ __forceinline__ int propagate_rounds() {
     for (;;) {
       if (qhead == tlen) {
         if (extra_mode) {
@@ -1083,15 +1336,63 @@ struct Group {
       }
       const int lo = qhead, hi = tlen;
       qhead = hi;
-      int crow = INF;
 #ifdef DP_STAMPS
       const int64_t t0 = stamp();
       DP_ACC(2, 1);
       DP_ACC(3, hi - lo == 1);
 #endif
+      // the frontier from the trail ring (LDS) unless the ring has wrapped
+      // over it; then from the trail in HBM, whose stores bar() drains
+      const bool ring = LR && hi - lo <= hmask + 1;
+      if constexpr (LR)
+        if (!ring) bar();
+      auto front = [&](int i) { return LR && ring ? (int)fr[i & hmask] : (int)trail[i]; };
+      if (run_round([&](int& crow) { visit_frontier(lo, hi, crow, front); }) < 0) return -1;
+#ifdef DP_STAMPS
+      DP_ACC(0, stamp() - t0);
+#endif
+    }
+  }
+
+  // One round: `visit` evaluates the rows the round reaches (into crow and
+  // the implication table), then the round is finished.  With the LDS table
+  // full the round is redone on the HBM arrays (returns finish_round's value).
+  template <class F>
+  __device__ __forceinline__ int run_round(F&& visit) {
+    int crow = INF;
+    const uint32_t vis0 = vis;
+    if constexpr (LR) {
+      lds_sync = true;
+      rb ^= 1;  // this round's bank; the other one was read before the last round's final barrier
+      if (tid == 0) { scal[S_NTB + (rb ^ 1)] = 0; scal[S_CVB + (rb ^ 1)] = 0; scal[S_OVB + (rb ^ 1)] = 0; }
+    }
+    visit(crow);
+    int r = finish_round(crow);
+    if constexpr (LR) {
+      lds_sync = false;
+      if (r == 2) {
+        vis = vis0;
+        hmode = false;
+        crow = INF;
+        visit(crow);
+        r = finish_round(crow);
+        hmode = true;
+      }
+      if (r < 0) bar();  // the callers' conflict analysis reads the trail
+    }
+    return r;
+  }
+
+  // The rows watched by the frontier trail[lo..hi) (front(i) = trail[i]),
+  // then the AtMost queue and the learned rows.
+  template <class FR>
+  __device__ __forceinline__ void visit_frontier(int lo, int hi, int& crow, FR&& front) {
+#ifdef DP_STAMPS
+      const int64_t t0 = stamp();
+#endif
       int ncq = 0;
       if (hi - lo == 1) {  // one new literal: threads over its watch list
-        const int l = DP_CHK((int)trail[lo], 0, 2 * nv, 10);
+        const int l = DP_CHK(front(lo), 0, 2 * nv, 10);
         const int a = w_off[l], e = w_off[l + 1];
         for (int k0 = a; k0 < e; k0 += NT) {
           make_room(crow, ncq);
@@ -1106,7 +1407,7 @@ struct Group {
           const int i = b + tid;
           int cnt = 0, a = 0;
           if (i < hi) {
-            const int l = DP_CHK((int)trail[i], 0, 2 * nv, 11);
+            const int l = DP_CHK(front(i), 0, 2 * nv, 11);
             a = w_off[l];
             cnt = (int)w_off[l + 1] - a;
           }
@@ -1132,12 +1433,14 @@ struct Group {
               visit(t0 + tid < total ? DP_CHK((int)w[DP_CHK((int)wbuf[t0 + tid], 0, nwatch, 12)], 0, nrows, 13) : -1,
                     crow, ncq);
             }
-            gsync();
+            // wbuf is reused by the next chunk; after the last one the
+            // AtMost flush's barrier (several wavefronts) comes first
+            if (NW == 1 || b + NT < hi) gsync();
           } else {
             // a very large chunk: one frontier literal at a time
             const int n = min(NT, hi - b);
             for (int e = 0; e < n; ++e) {
-              const int l = trail[b + e];
+              const int l = front(b + e);
               const int a2 = w_off[l], e2 = w_off[l + 1];
               for (int k0 = a2; k0 < e2; k0 += NT) {
                 make_room(crow, ncq);
@@ -1155,26 +1458,16 @@ struct Group {
       const int64_t tf = stamp();
       DP_ACC(15, NW == 1 ? ncq : min(scal[S_NK], CQ));
       flush_cards(crow, ncq);
-      const int64_t tl = stamp();
-      DP_ACC(10, tl - tf);
+      const int64_t tq = stamp();
+      DP_ACC(10, tq - tf);
       DP_ACC(14, nl - learn_lo);
       eval_learned(crow);
-      DP_ACC(11, stamp() - tl);
+      DP_ACC(11, stamp() - tq);
+      DP_ACC(1, stamp() - t0);
 #else
       flush_cards(crow, ncq);
       eval_learned(crow);
 #endif
-#ifdef DP_STAMPS
-      const int64_t t1 = stamp();
-      const int fr = finish_round(crow);
-      const int64_t t2 = stamp();
-      DP_ACC(0, t1 - t0);
-      DP_ACC(1, t2 - t1);
-      if (fr < 0) return -1;
-#else
-      if (finish_round(crow) < 0) return -1;
-#endif
-    }
   }
 
   // Can AtMost row k fire on the empty assignment (a variable listed more
@@ -1195,20 +1488,30 @@ struct Group {
   // on the empty assignment only clauses of length <= 1 and AtMost rows with
   // a multiplicity over the bound can fire, so a sweep visits just those.
   __device__ __forceinline__ int base_propagate() {
-    int crow = INF, ncq = 0;
-    for (int i0 = 0; i0 < nrows; i0 += NT) {
-      const int r = i0 + tid;
-      const bool f = r < nc ? (int)clause_off[r + 1] - (int)clause_off[r] <= 1 : r < nrows && card_fires(r - nc);
-      make_room(crow, ncq);
-      visit(f ? r : -1, crow, ncq);
-    }
-    flush_cards(crow, ncq);
-    eval_learned(crow);
-    if (finish_round(crow) < 0) return -1;
+    const int r = run_round([&](int& crow) {
+      int ncq = 0;
+      for (int i0 = 0; i0 < nrows; i0 += NT) {
+        const int row = i0 + tid;
+        const bool f = row < nc ? (int)clause_off[row + 1] - (int)clause_off[row] <= 1
+                                : row < nrows && card_fires(row - nc);
+        make_room(crow, ncq);
+        visit(f ? row : -1, crow, ncq);
+      }
+      flush_cards(crow, ncq);
+      eval_learned(crow);
+    });
+    if (r < 0) return -1;
     return propagate();
   }
 
   __device__ __forceinline__ void truncate_to(int mark) {
+#ifdef DP_STAMPS
+    const int64_t t0 = stamp();
+    truncate_to_(mark);
+    DP_ACC(19, stamp() - t0);
+  }
+  __device__ __forceinline__ void truncate_to_(int mark) {
+#endif
     gsync();
     for (int i = mark + tid; i < tlen; i += NT) val[DP_CHK((int)trail[i], 0, 2 * nv, 14) >> 1] = 0;
     tlen = qhead = mark;
@@ -1219,9 +1522,7 @@ struct Group {
   __device__ __forceinline__ int untest_to(int mark) {
     truncate_to(mark);
     if (nl > learn_lo) {
-      int crow = INF;
-      eval_learned(crow);
-      if (finish_round(crow) < 0) return -1;
+      if (run_round([&](int& crow) { eval_learned(crow); }) < 0) return -1;
       return propagate();
     }
     return tlen == nv ? 1 : 0;
@@ -1236,7 +1537,7 @@ struct Group {
     if (tid == 0) {
       const int v = DP_CHK(l, 0, 2 * nv, 30) >> 1;
       val[v] = (l & 1) ? -1 : 1; reason[v] = enc(decision >= 0 ? -3 - decision : why);
-      rs[v] = enc(tlen); trail[DP_CHK(tlen, 0, nv, 31)] = enc(l);
+      rs[v] = enc(tlen); put_trail(tlen, l);
     }
     ++tlen;
     gsync();
@@ -1295,6 +1596,14 @@ struct Group {
   }
 
   __device__ __forceinline__ void analyze() {
+#ifdef DP_STAMPS
+    const int64_t t0 = stamp();
+    analyze_();
+    DP_ACC(17, stamp() - t0);
+    DP_ACC(22, 1);
+  }
+  __device__ __forceinline__ void analyze_() {
+#endif
     gsync();
     if (tid == 0) {
       scal[S_NWORK] = 0;
@@ -1356,6 +1665,15 @@ struct Group {
   // threads scan the watch lists of the variables assigned true instead of
   // every clause row (same answer as the oracle's full scan).
   __device__ __forceinline__ int first_violated() {
+#ifdef DP_STAMPS
+    const int64_t t0 = stamp();
+    const int r = first_violated_();
+    DP_ACC(16, stamp() - t0);
+    DP_ACC(18, 1);
+    return r;
+  }
+  __device__ __forceinline__ int first_violated_() {
+#endif
     int best = INF;
     if (nc <= 4 * NT) {
       // few rows: every thread scans its rows in ascending order (the
@@ -1387,6 +1705,13 @@ struct Group {
   }
 
   __device__ __forceinline__ void save_model() {
+#ifdef DP_STAMPS
+    const int64_t t0 = stamp();
+    save_model_();
+    DP_ACC(20, stamp() - t0);
+  }
+  __device__ __forceinline__ void save_model_() {
+#endif
     for (int b = 0; b < nv; b += NT) {
       const int v = b + tid;
       const uint64_t m = __ballot(v < nv && val[v] > 0);
@@ -1510,6 +1835,9 @@ struct Group {
 
   // PushGuess, search.go:34-77
   __device__ __forceinline__ void push_guess() {
+#ifdef DP_STAMPS
+    const int64_t tpg = stamp();
+#endif
     gsync();
     const int list = DP_CHK((int)dq[2 * dq_head], 0, nch + nv, 17), idx = DP_CHK((int)dq[2 * dq_head + 1], 0, nv + 1, 18);
     dq_head = dq_head + 1 == cap ? 0 : dq_head + 1;
@@ -1532,6 +1860,9 @@ struct Group {
     gsync();
     if (m < 0) return;
     if (steps >= budget) { budget_hit = true; result = 0; return; }
+#ifdef DP_STAMPS
+    DP_ACC(21, stamp() - tpg);
+#endif
     result = test_assume(2 * m);
     last_solve = false;
   }
@@ -1601,7 +1932,14 @@ struct Group {
     fill_bits(used, nid, false);
     fill_bits(en, nid, false);
     bool from_solve = false;
+#ifdef DP_STAMPS
+    const int64_t tloop = stamp();
+    int64_t tgap = tloop;
+#endif
     for (;;) {
+#ifdef DP_STAMPS
+      DP_ACC(24, stamp() - tgap);
+#endif
       if (dq_n == 0 && result == 0) {
         if (tr) {
           or_bits(en, used, nid);
@@ -1637,7 +1975,8 @@ struct Group {
 #ifdef DP_STAMPS
       const int64_t tp = stamp();
       push_guess();
-      DP_ACC(4, stamp() - tp);
+      tgap = stamp();
+      DP_ACC(4, tgap - tp);
       DP_ACC(7, 1);
 #else
       push_guess();
@@ -1645,6 +1984,9 @@ struct Group {
       from_solve = false;
       if (budget_hit) { result = RS_BUDGET; break; }
     }
+#ifdef DP_STAMPS
+    DP_ACC(23, stamp() - tloop);
+#endif
     final_from_solve = from_solve;
     or_bits(used, en, nid);
     // Value() after an ending on Test()==1 reads that scope's full assignment
@@ -1838,7 +2180,7 @@ struct Group {
       const int at = claim(f, run);
       if (f) {
         val[v] = (l & 1) ? -1 : 1; reason[v] = enc(R_DEC); rs[v] = enc(start);
-        trail[DP_CHK(at, 0, nv, 29)] = enc(l);
+        put_trail(at, l);
       }
     }
     claim_end(run);
@@ -1972,11 +2314,12 @@ solve_kernel(KernelArgs a) {
   if (W.tid == 0 && a.stamps) {
     int64_t* o = a.stamps + (int64_t)DP_NSTAMP * pid;
     for (int i = 0; i < 5; ++i) o[i] = t[i + 1] - t[i];
-    for (int i = 0; i < 5; ++i) o[5 + i] = W.acc[i];
+    for (int i = 0; i < 5; ++i) o[5 + i] = (int64_t)W.lacc[i];
     o[10] = wall0;
     o[11] = wallclock();
-    for (int i = 5; i < 16; ++i) o[11 + i] = W.acc[i];
+    for (int i = 5; i < 16; ++i) o[11 + i] = (int64_t)W.lacc[i];
     for (int i = 0; i < 3; ++i) o[27 + i] = W.sub[i];
+    for (int i = 16; i < 32; ++i) o[16 + i] = (int64_t)W.lacc[i];
   }
 #endif
   if (W.tr_stop) flags |= DP_F_TRACE_TRUNCATED;

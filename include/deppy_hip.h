@@ -174,6 +174,22 @@ static inline dp_rec_layout dp_rec_layout_of(const int32_t* h) {
  * kernel decodes them from one 16-byte load per lane).  DP_H_WORDS stays the
  * int32 form's length.  dp_rec_widen gives the int32 form of any record.
  *
+ * DP_FMT_P16D: DP_FMT_P16 with the choice lists implied by the record's
+ * dependency rows (dp_lower_into DP_LOWER_PACKED emits it when they are;
+ * config 2's catalogs cross PCIe in about a third fewer bytes).  A
+ * dependency row is a clause row of two or more literals whose first literal
+ * is negative and every other one positive: Dependency(s; d1..dn) lowers to
+ * (~s d1 .. dn), and no other constraint gives that shape.  src[k] == 0:
+ * choice list k is the variables of the next dependency row (in row order)
+ * after its first literal; src[k] = d > 0: list k repeats list k - d, which
+ * took a row (a Dependency whose gate an earlier one of the same subject
+ * already emitted).  Every dependency row is taken once; the lists'
+ * subjects (first literal's variable) never decrease and var_choice_off
+ * counts them per subject; nch and nchl are the header's.  After the header:
+ *   uint16 clause_lits[ncl], card_lits[nkl], card_bound[nk], anchors[na]
+ *   zero padding to a 16-byte boundary (from the body's start)
+ *   uint8  clause_len[nc], card_len[nk], src[nch], card_mask[(nid+7)/8]
+ *
  * DP_FMT_I32W: the int32 form followed by its watch lists, the form a
  * problem solved by a multi-wave workgroup is staged in (dp_lower_into
  * DP_LOWER_NARROW emits it for the records that do not run one wavefront
@@ -186,22 +202,26 @@ static inline dp_rec_layout dp_rec_layout_of(const int32_t* h) {
  * The kernel checks their bounds; that they list exactly those rows is the
  * producer's contract (dp_lower_into builds them). */
 enum { DP_H_FMT = 13 };
-enum { DP_FMT_I32 = 0, DP_FMT_U16 = 1, DP_FMT_P16 = 3, DP_FMT_I32W = 4 };
+enum { DP_FMT_I32 = 0, DP_FMT_U16 = 1, DP_FMT_P16 = 3, DP_FMT_I32W = 4, DP_FMT_P16D = 5 };
 enum { DP_P16_TAIL_MAX = 1024 };
 
-/* DP_FMT_P16: uint16 words before the padding, byte offset of the lengths
- * (from the body's start), and bytes of lengths plus mask. */
+/* DP_FMT_P16 / DP_FMT_P16D (the packed forms): uint16 words before the
+ * padding, byte offset of the lengths (from the body's start), and bytes of
+ * lengths plus mask. */
+static inline int dp_fmt_packed(int32_t fmt) { return fmt == DP_FMT_P16 || fmt == DP_FMT_P16D; }
 static inline int64_t dp_p16_nu16(const int32_t* h) {
-  return (int64_t)h[DP_H_NCL] + h[DP_H_NKL] + h[DP_H_NK] + h[DP_H_NCHL] + h[DP_H_NA];
+  return (int64_t)h[DP_H_NCL] + h[DP_H_NKL] + h[DP_H_NK] + h[DP_H_NA] +
+         (h[DP_H_FMT] == DP_FMT_P16D ? 0 : h[DP_H_NCHL]);
 }
 static inline int64_t dp_p16_tail_at(const int32_t* h) { return (2 * dp_p16_nu16(h) + 15) & ~(int64_t)15; }
 static inline int64_t dp_p16_tail_bytes(const int32_t* h) {
-  return (int64_t)h[DP_H_NC] + h[DP_H_NK] + h[DP_H_NV] + h[DP_H_NCH] + ((int64_t)h[DP_H_NID] + 7) / 8;
+  return (int64_t)h[DP_H_NC] + h[DP_H_NK] + h[DP_H_NCH] + ((int64_t)h[DP_H_NID] + 7) / 8 +
+         (h[DP_H_FMT] == DP_FMT_P16D ? 0 : (int64_t)h[DP_H_NV]);
 }
 
 static inline int64_t dp_rec_phys_words(const int32_t* h) {
   if (h[DP_H_FMT] == DP_FMT_U16) return DP_H_SIZE + ((int64_t)h[DP_H_WORDS] - DP_H_SIZE + 1) / 2;
-  if (h[DP_H_FMT] == DP_FMT_P16) return DP_H_SIZE + (dp_p16_tail_at(h) + dp_p16_tail_bytes(h) + 3) / 4;
+  if (dp_fmt_packed(h[DP_H_FMT])) return DP_H_SIZE + (dp_p16_tail_at(h) + dp_p16_tail_bytes(h) + 3) / 4;
   if (h[DP_H_FMT] == DP_FMT_I32W)
     return (int64_t)h[DP_H_WORDS] + 2 * (int64_t)h[DP_H_NV] + 1 + h[DP_H_NCL] + h[DP_H_NKL];
   return (int64_t)h[DP_H_WORDS];
@@ -222,7 +242,8 @@ static inline int dp_rec_fits16(const int32_t* h) {
 int dp_rec_validate(const int32_t* rec, int64_t words);
 /* The int32 form (DP_FMT_I32, DP_H_WORDS words into out) of a record of any
  * form that occupies at most `avail` words.  Returns 0, or < 0 when the
- * header or a DP_FMT_P16 length / mask is inconsistent. */
+ * header or a packed form's length / mask (or DP_FMT_P16D's implied choice
+ * lists) is inconsistent. */
 int dp_rec_widen(const int32_t* rec, int64_t avail, int32_t* out);
 
 /* ------------------------------------------------------------------------ */

@@ -138,10 +138,49 @@ static void* xcalloc(size_t n, size_t sz) { return calloc(n ? n : 1, sz); }
  * word a uint16.  DP_FMT_P16 (include/deppy_hip.h): the uint16 arrays, then
  * byte lengths of the offsets arrays and the AtMost-identity bit mask (a
  * mask with the wrong number of set bits leaves the ids it cannot place 0;
- * records are validated before the oracle sees them). */
+ * records are validated before the oracle sees them).  DP_FMT_P16D: the same
+ * without the choice lists, restated from the dependency rows by
+ * implied_choices below. */
+/* DP_FMT_P16D's choice lists (include/deppy_hip.h): dependency rows -- two
+ * or more literals, the first negative, the rest positive -- in row order;
+ * src[k] == 0: list k is the next one's variables after its first literal,
+ * src[k] = d: list k repeats list k - d; var_choice_off counts the lists per
+ * subject (the first literal's variable).  Records are validated before the
+ * oracle sees them. */
+static void implied_choices(const dp_rec_layout* L, const uint8_t* src, int32_t* o) {
+  const int32_t nc = o[DP_H_NC], nv = o[DP_H_NV], nch = o[DP_H_NCH];
+  int32_t* rowk = xcalloc((size_t)nch + 1, sizeof(int32_t));
+  int32_t r = 0, n = 0, filled = 0;
+  o[L->var_choice_off] = 0;
+  o[L->choice_off] = 0;
+  for (int32_t k = 0; k < nch; ++k) {
+    int32_t row = -1;
+    if (src[k] == 0) {
+      for (; r < nc && row < 0; ++r) {
+        const int32_t a = o[L->clause_off + r], b = o[L->clause_off + r + 1];
+        int dep = b - a >= 2 && (o[L->clause_lits + a] & 1);
+        for (int32_t j = a + 1; j < b && dep; ++j) dep = !(o[L->clause_lits + j] & 1);
+        if (dep) row = r;
+      }
+    } else if (src[k] <= k) {
+      row = rowk[k - src[k]];
+    }
+    rowk[k] = row;
+    if (row < 0) break;
+    const int32_t a = o[L->clause_off + row], b = o[L->clause_off + row + 1];
+    const int32_t subj = o[L->clause_lits + a] >> 1;
+    while (filled < subj && filled < nv) o[L->var_choice_off + ++filled] = k;
+    for (int32_t j = a + 1; j < b && n < o[DP_H_NCHL]; ++j) o[L->choice_lits + n++] = o[L->clause_lits + j] >> 1;
+    o[L->choice_off + k + 1] = n;
+  }
+  while (filled < nv) o[L->var_choice_off + ++filled] = nch;
+  free(rowk);
+}
+
 static const int32_t* widen(const int32_t* rec, int32_t** tmp) {
   *tmp = NULL;
-  if (rec[DP_H_FMT] != DP_FMT_U16 && rec[DP_H_FMT] != DP_FMT_P16) return rec;
+  const int32_t fmt = rec[DP_H_FMT];
+  if (fmt != DP_FMT_U16 && fmt != DP_FMT_P16 && fmt != DP_FMT_P16D) return rec;
   int32_t w = rec[DP_H_WORDS];
   int32_t* o = xcalloc((size_t)w, sizeof(int32_t));
   memcpy(o, rec, DP_H_SIZE * sizeof(int32_t));
@@ -152,17 +191,20 @@ static const int32_t* widen(const int32_t* rec, int32_t** tmp) {
   } else {
     const dp_rec_layout L = dp_rec_layout_of(rec);
     const int32_t nc = rec[DP_H_NC], nk = rec[DP_H_NK];
-    const int32_t n16[5] = {rec[DP_H_NCL], rec[DP_H_NKL], nk, rec[DP_H_NCHL], rec[DP_H_NA]};
+    const int derived = fmt == DP_FMT_P16D;
+    const int32_t n16[5] = {rec[DP_H_NCL], rec[DP_H_NKL], nk, derived ? 0 : rec[DP_H_NCHL], rec[DP_H_NA]};
     const int32_t at16[5] = {L.clause_lits, L.card_lits, L.card_bound, L.choice_lits, L.anchors};
     for (int a = 0; a < 5; ++a)
       for (int32_t j = 0; j < n16[a]; ++j) o[at16[a] + j] = *u++;
     const uint8_t* t = (const uint8_t*)(rec + DP_H_SIZE) + dp_p16_tail_at(rec);
     const int32_t nl[4] = {nc, nk, rec[DP_H_NV], rec[DP_H_NCH]};
     const int32_t atl[4] = {L.clause_off, L.card_off, L.var_choice_off, L.choice_off};
-    for (int a = 0; a < 4; ++a) {
+    for (int a = 0; a < (derived ? 2 : 4); ++a) {
       o[atl[a]] = 0;
       for (int32_t j = 0; j < nl[a]; ++j) o[atl[a] + j + 1] = o[atl[a] + j] + *t++;
     }
+    const uint8_t* src = t;
+    if (derived) t += rec[DP_H_NCH];
     int32_t c0 = 0, c1 = 0;
     for (int32_t i = 0; i < rec[DP_H_NID]; ++i) {
       if ((t[i >> 3] >> (i & 7)) & 1) {
@@ -171,6 +213,7 @@ static const int32_t* widen(const int32_t* rec, int32_t** tmp) {
         o[L.clause_id + c0++] = i;
       }
     }
+    if (derived) implied_choices(&L, src, o);
   }
   *tmp = o;
   return o;

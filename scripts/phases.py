@@ -14,12 +14,14 @@ import numpy as np  # noqa: E402
 from deppy_amd import _lib  # noqa: E402
 from tests.gpu_common import lowered_config  # noqa: E402
 
-NS = 32
-NAMES = ["init", "base", "search", "epilogue", "core", "round_eval", "round_finish", "rounds",
+NS = 56
+NAMES = ["init", "base", "search", "epilogue", "core", "round_total", "round_visit", "rounds",
          "rounds_1lit", "push_guess"]
 EXTRA = {16: "search_solve", 17: "pop_guess", 18: "pushes", 19: "visit_1lit", 20: "visit_flat", 21: "flush_cards",
          22: "learned", 23: "n_watch_1lit", 24: "n_front_flat", 25: "n_learned_rows", 26: "n_cards",
-         27: "init_stage", 28: "init_validate", 29: "init_build"}
+         27: "init_stage", 28: "init_validate", 29: "init_build",
+         32: "first_violated", 33: "analyze", 34: "n_first_violated", 35: "truncate", 36: "save_model",
+         37: "push_pre", 38: "n_analyze", 39: "search_loop", 40: "loop_gap"}
 L = _lib.lib()
 L.dp_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _lib.c_i64p]
 config = int(sys.argv[1]) if len(sys.argv) > 1 else 2

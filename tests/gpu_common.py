@@ -7,7 +7,7 @@ from deppy_amd import _lib
 def lowered_config(config, n, seed, narrow=False, pinned=False, packed=False):
     """Synthetic catalogs (SURVEY §8(d) generator) lowered by dp_lower;
     narrow: records that fit 16 bits in the DP_FMT_U16 form (packed: the
-    DP_FMT_P16 form where it applies); pinned: in page-locked memory (with a
+    DP_FMT_P16D / DP_FMT_P16 forms where they apply); pinned: in page-locked memory (with a
     GPU)."""
     w = _lib.generate(config, n, seed)
     return _lib.Lowered(_lib.WireArrays(**{k: w[k] for k in (
@@ -41,29 +41,91 @@ def corrupt16(rec_off, rec, p, kind):
     return True
 
 
+def implied_choices(nv, clause_off, clause_lits, src):
+    """DP_FMT_P16D's choice lists (include/deppy_hip.h), restated: dependency
+    rows (two or more literals, the first negative, the rest positive) in row
+    order; src[k] == 0: list k = the variables after the first literal of the
+    next one; src[k] = d: list k repeats list k - d; var_choice_off counts the
+    lists per subject (the first literal's variable)."""
+    dep = [r for r in range(len(clause_off) - 1)
+           if clause_off[r + 1] - clause_off[r] >= 2 and clause_lits[clause_off[r]] & 1
+           and not np.any(clause_lits[clause_off[r] + 1:clause_off[r + 1]] & 1)]
+    per_var = np.zeros(nv, np.int64)
+    co, chl, rows, j = [0], [], [], 0
+    for s in src:
+        row = dep[j] if s == 0 else rows[len(rows) - int(s)]
+        j += s == 0
+        rows.append(row)
+        lits = clause_lits[clause_off[row]:clause_off[row + 1]]
+        per_var[lits[0] >> 1] += 1
+        chl.extend(int(x) >> 1 for x in lits[1:])
+        co.append(len(chl))
+    assert j == len(dep)
+    vco = np.concatenate([[0], np.cumsum(per_var)])
+    return vco.astype(np.int32), np.array(co, np.int32), np.array(chl, np.int32)
+
+
 def unpack_p16(r):
-    """The int32 form of one DP_FMT_P16 record (include/deppy_hip.h), restated
-    here independently of the library's dp_rec_widen."""
+    """The int32 form of one DP_FMT_P16 / DP_FMT_P16D record
+    (include/deppy_hip.h), restated here independently of the library's
+    dp_rec_widen."""
     nv, nc, nk, nch, na, nid, ncl, nkl, nchl, words = (int(r[i]) for i in range(1, 11))
+    derived = int(r[13]) == 5
     u = r[16:].view(np.uint16)
     o, parts16 = 0, []
-    for n in (ncl, nkl, nk, nchl, na):
+    for n in (ncl, nkl, nk, 0 if derived else nchl, na):
         parts16.append(u[o:o + n].astype(np.int32))
         o += n
     cl, kl, kb, chl, anc = parts16
     tail_at = (2 * o + 15) // 16 * 16
     t = r[16:].view(np.uint8)[tail_at:]
     offs, o = [], 0
-    for n in (nc, nk, nv, nch):
+    for n in ((nc, nk) if derived else (nc, nk, nv, nch)):
         offs.append(np.concatenate([[0], np.cumsum(t[o:o + n].astype(np.int32))]).astype(np.int32))
         o += n
+    src = t[o:o + nch] if derived else None
+    o += nch if derived else 0
     bits = np.unpackbits(t[o:o + (nid + 7) // 8], bitorder="little")[:nid].astype(bool)
     ids = np.arange(nid, dtype=np.int32)
     cid, kid = ids[~bits], ids[bits]
+    if derived:
+        vco, co, chl = implied_choices(nv, offs[0], cl, src)
+        offs += [vco, co]
     out = np.concatenate([r[:16], offs[0], cl, cid, offs[1], kl, kb, kid, offs[2], offs[3], chl, anc]).astype(np.int32)
     out[13] = 0
     assert len(out) == words
     return out
+
+
+def pack_p16(r32):
+    """The DP_FMT_P16 form (explicit choice lists) of an int32 record that
+    allows it, padded to 16 bytes -- how a producer that does not derive
+    choice lists packs a record (the library's lowering emits DP_FMT_P16D when
+    it can)."""
+    nv, nc, nk, nch, na, nid, ncl, nkl, nchl, words = (int(r32[i]) for i in range(1, 11))
+    o = 16
+    clause_off = r32[o:o + nc + 1]; o += nc + 1
+    clause_lits = r32[o:o + ncl]; o += ncl
+    o += nc  # clause_id (ascending, the mask's clear bits)
+    card_off = r32[o:o + nk + 1]; o += nk + 1
+    card_lits = r32[o:o + nkl]; o += nkl
+    card_bound = r32[o:o + nk]; o += nk
+    card_id = r32[o:o + nk]; o += nk
+    vco = r32[o:o + nv + 1]; o += nv + 1
+    co = r32[o:o + nch + 1]; o += nch + 1
+    chl = r32[o:o + nchl]; o += nchl
+    anc = r32[o:o + na]
+    u16 = np.concatenate([clause_lits, card_lits, card_bound, chl, anc]).astype(np.uint16).tobytes()
+    u16 += bytes((-len(u16)) % 16)
+    mask = np.zeros(nid, bool)
+    mask[card_id] = True
+    tail = np.concatenate([np.diff(x) for x in (clause_off, card_off, vco, co)]).astype(np.uint8).tobytes()
+    tail += np.packbits(mask, bitorder="little").tobytes()
+    body = u16 + tail
+    body += bytes((-(64 + len(body))) % 16)
+    head = np.asarray(r32[:16], np.int32).copy()
+    head[13] = 3
+    return np.concatenate([head, np.frombuffer(body, np.int32)])
 
 
 def widen(rec_off, rec):
@@ -71,7 +133,7 @@ def widen(rec_off, rec):
     parts, offs = [], [0]
     for p in range(len(rec_off) - 1):
         r = rec[rec_off[p]:rec_off[p + 1]]
-        if len(r) and r[13] == 3:
+        if len(r) and r[13] in (3, 5):
             r = unpack_p16(r)
         elif len(r) and r[13] == 1:
             words = int(r[10])

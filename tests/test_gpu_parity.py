@@ -345,7 +345,7 @@ def test_malformed_16bit_records_found_by_the_kernel(pinned):
                                                  (2, 200, 104, _lib.OPT_FORCE_GROUP)],
                          ids=["c2", "c3", "c5", "c2-group"])
 def test_packed_records_bit_exact(config, n, seed, flags):
-    """DP_FMT_P16 records (dp_lower_into DP_LOWER_PACKED), copied to the device
+    """Packed records (dp_lower_into DP_LOWER_PACKED: DP_FMT_P16D), copied to the device
     as they lie and decoded by the kernel (or widened on the host for a
     multi-wave placement), solve exactly like their int32 form and the oracle."""
     a = lowered_config(config, n, seed)
@@ -366,23 +366,30 @@ def test_packed_records_bit_exact(config, n, seed, flags):
 
 def test_malformed_packed_records_found_by_the_kernel():
     """Packed records are validated on the device: a wrong identity mask, row
-    lengths that do not sum to the total, an out-of-range literal -> DP_ERROR
-    + DP_F_MALFORMED for that problem only."""
+    lengths that do not sum to the total, an out-of-range literal, dependency
+    rows that no longer imply the header's choice lists (DP_FMT_P16D) ->
+    DP_ERROR + DP_F_MALFORMED for that problem only."""
     lw = lowered_config(2, 40, 111, packed=True, pinned=True)
     ref = oracle.solve_batch(lw.rec_off, lw.rec, 0, 16)
     rec = lw.rec
-    bad = [5, 12, 27]
-    for p, kind in zip(bad, ("mask", "len", "lit")):
+    bad = [5, 12, 27, 33]
+    for p, kind in zip(bad, ("mask", "len", "lit", "dep")):
         r = rec[lw.rec_off[p]:lw.rec_off[p + 1]]
+        assert r[13] == 5
         nv, nc, nk, nch, na, nid, ncl, nkl, nchl = (int(r[i]) for i in range(1, 10))
-        tail = (2 * (ncl + nkl + nk + nchl + na) + 15) // 16 * 16
+        tail = (2 * (ncl + nkl + nk + na) + 15) // 16 * 16
         t = r[16:].view(np.uint8)
+        u = r[16:].view(np.uint16)
         if kind == "mask":
-            t[tail + nc + nk + nv + nch] ^= 1
+            t[tail + nc + nk + nch] ^= 1
         elif kind == "len":
             t[tail] += 1
-        else:
-            r[16:].view(np.uint16)[0] = 2 * nv + 1
+        elif kind == "lit":
+            u[0] = 2 * nv + 1
+        else:  # a dependency row's first literal made positive: one list short
+            offs = np.concatenate([[0], np.cumsum(t[tail:tail + nc].astype(np.int64))])
+            a = next(a for a, e in zip(offs[:-1], offs[1:]) if e - a >= 2 and u[a] & 1 and not np.any(u[a + 1:e] & 1))
+            u[a] ^= 1
     c = _lib.Context(0, 1)
     try:
         g = c.solve(lw.rec_off, rec)
@@ -393,6 +400,23 @@ def test_malformed_packed_records_found_by_the_kernel():
         assert g["status"][p] == -2 and g["flags"][p] == 512 and g["core_len"][p] == 0, p
     for k in ("status", "flags", "steps"):
         np.testing.assert_array_equal(g[k][ok], ref[k][ok])
+
+
+def test_explicit_choice_packed_records_bit_exact():
+    """DP_FMT_P16 records (explicit choice lists, as a producer that does not
+    derive them packs them) are decoded by the kernel like DP_FMT_P16D."""
+    from tests.gpu_common import pack_p16
+    a = lowered_config(2, 500, 131)
+    parts = [pack_p16(a.record(p)) for p in range(a.n)]
+    off = np.concatenate([[0], np.cumsum([len(x) for x in parts])]).astype(np.int64)
+    rec = np.concatenate(parts).astype(np.int32)
+    assert np.all(rec[off[:-1] + 13] == 3)
+    c = _lib.Context(0, 1)
+    try:
+        g = c.solve(off, rec)
+    finally:
+        c.close()
+    assert compare_results(g, oracle.solve_batch(a.rec_off, a.rec, 0, 16), a.n) == []
 
 
 def test_wide_records_direct_and_validated():

@@ -192,8 +192,9 @@ def test_packed_lowering_is_the_int32_record(config, n):
     np.testing.assert_array_equal(rec, a.rec)
     fmt = b.rec[b.rec_off[:-1] + 13]
     if config in (2, 3):
-        assert np.all(fmt == 3)
-        assert b.rec_off[-1] < 0.8 * lowered_config(config, n, 17, narrow=True).rec_off[-1]
+        # the generated catalogs' dependency rows imply their choice lists
+        assert np.all(fmt == 5)
+        assert b.rec_off[-1] < 0.65 * lowered_config(config, n, 17, narrow=True).rec_off[-1]
     assert np.all(b.rec_off % 4 == 0)
     L = _lib.lib()
     for p in range(n):
@@ -202,30 +203,65 @@ def test_packed_lowering_is_the_int32_record(config, n):
         assert L.dp_rec_widen(r.ctypes.data_as(_lib.c_i32p), len(r), out.ctypes.data_as(_lib.c_i32p)) == 0
         np.testing.assert_array_equal(out, a.record(p))
         assert L.dp_rec_validate(r.ctypes.data_as(_lib.c_i32p), len(r)) == 0
-        if r[13] == 3:
+        if r[13] in (3, 5):
             np.testing.assert_array_equal(unpack_p16(r), a.record(p))
 
 
 def test_packed_malformed_is_rejected():
     """A mask with the wrong number of AtMost identities, lengths that do not
-    sum to the row total, an out-of-range literal: dp_rec_validate rejects
-    each (the kernel checks the same, tests/test_gpu_parity.py)."""
+    sum to the row total, an out-of-range literal, dependency rows that no
+    longer imply the header's choice lists (DP_FMT_P16D): dp_rec_validate
+    rejects each (the kernel checks the same, tests/test_gpu_parity.py)."""
     b = lowered_config(2, 4, 41, packed=True)
     L = _lib.lib()
     r0 = np.ascontiguousarray(b.record(1)).copy()
-    assert r0[13] == 3
+    assert r0[13] == 5
     nv, nc, nk, nch, na, nid, ncl, nkl, nchl = (int(r0[i]) for i in range(1, 10))
-    nu16 = ncl + nkl + nk + nchl + na
+    nu16 = ncl + nkl + nk + na
     tail = (2 * nu16 + 15) // 16 * 16
     def bad(r):
         return L.dp_rec_validate(np.ascontiguousarray(r).ctypes.data_as(_lib.c_i32p), len(r)) != 0
-    r = r0.copy(); t = r[16:].view(np.uint8); t[tail + nc + nk + nv + nch] ^= 1      # mask: one bit flipped
+    r = r0.copy(); t = r[16:].view(np.uint8); t[tail + nc + nk + nch] ^= 1            # mask: one bit flipped
     assert bad(r)
     r = r0.copy(); t = r[16:].view(np.uint8); t[tail] += 1                           # clause lengths: sum != ncl
     assert bad(r)
     r = r0.copy(); r[16:].view(np.uint16)[0] = 2 * nv + 1                             # clause literal past 2nv
     assert bad(r)
+    r = r0.copy(); r[9] -= 1                                                          # nchl: one choice short
+    assert bad(r)
+    # a dependency row's first literal made positive: one list fewer than nch
+    u = r0[16:].view(np.uint16)
+    lens = r0[16:].view(np.uint8)[tail:tail + nc].astype(np.int64)
+    offs = np.concatenate([[0], np.cumsum(lens)])
+    dep = [a for a, e in zip(offs[:-1], offs[1:]) if e - a >= 2 and u[a] & 1 and not np.any(u[a + 1:e] & 1)]
+    r = r0.copy(); r[16:].view(np.uint16)[dep[0]] ^= 1
+    assert bad(r)
     assert not bad(r0)
+
+
+def test_explicit_choice_packed_form():
+    """DP_FMT_P16 (explicit choice lists, tests/gpu_common.pack_p16) widens to
+    the int32 record through dp_rec_widen and the independent restatement,
+    validates, and the oracle solves it like the int32 form."""
+    from oracle import oracle
+    from tests.gpu_common import pack_p16, unpack_p16
+    a = lowered_config(2, 40, 23)
+    L = _lib.lib()
+    parts = []
+    for p in range(a.n):
+        r = pack_p16(a.record(p))
+        assert r[13] == 3 and len(r) % 4 == 0
+        out = np.zeros(int(r[10]), np.int32)
+        assert L.dp_rec_widen(r.ctypes.data_as(_lib.c_i32p), len(r), out.ctypes.data_as(_lib.c_i32p)) == 0
+        np.testing.assert_array_equal(out, a.record(p))
+        np.testing.assert_array_equal(unpack_p16(r), a.record(p))
+        assert L.dp_rec_validate(r.ctypes.data_as(_lib.c_i32p), len(r)) == 0
+        parts.append(r)
+    off = np.concatenate([[0], np.cumsum([len(x) for x in parts])]).astype(np.int64)
+    ob = oracle.solve_batch(off, np.concatenate(parts))
+    oa = oracle.solve_batch(a.rec_off, a.rec)
+    for k in ("status", "flags", "installed", "core", "core_len", "steps"):
+        np.testing.assert_array_equal(oa[k], ob[k])
 
 
 def test_oracle_reads_packed_records():
