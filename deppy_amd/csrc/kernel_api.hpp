@@ -56,7 +56,16 @@ struct KernelArgs {
   int32_t* trace;
   int32_t* trace_len;
   int32_t trace_cap;
+  // Multi-wave launches run a persistent grid (as many workgroups as the
+  // device holds at once): each workgroup takes the next item from *queue
+  // (zeroed before the launch) until n_items are taken, so the longest
+  // catalogs (first, in LPT order) never wait behind a dispatch order.
+  // nullptr: one workgroup per item.
+  int32_t* queue;
+  int32_t n_items;
 };
+// Words at the front of the multi-wave scratch holding the launches' queues.
+constexpr int kQueueWords = 64;
 
 // Launch one workgroup per problem of order[0..n_blocks) with lds_bytes of
 // LDS: one wavefront (mode M_LDS) or BIG_WAVES wavefronts (M_SPLIT, M_HBM).

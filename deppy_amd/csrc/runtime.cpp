@@ -288,6 +288,7 @@ void plan_chunk(Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0,
       const int32_t* h = rec + rec_off[p0 + i];
       const Layout Y = mode == M_SPLIT ? layout<M_SPLIT>(h) : mode == M_SPLIT4 ? layout<M_SPLIT4>(h) : layout<M_HBM>(h);
       mx = std::max(mx, Y.lds_bytes);
+      if (P.scratch_words == 0) P.scratch_words = dp::kQueueWords;  // the launches' queues first
       P.scratch_off.push_back(P.scratch_words);
       P.scratch_words += ((int64_t)Y.bytes + 15) / 16 * 4;  // int32 words, 16-byte aligned
     }
@@ -742,11 +743,24 @@ namespace {
   } while (0)
 
 // Enqueue a planned chunk's launches on stream s.
+// Multi-wave launches take their items from a queue (kernel_api.hpp
+// KernelArgs::queue) in the scratch's first words, zeroed here.
 int enqueue_launches(dp_ctx* ctx, const Plan& P, const dp::KernelArgs& base, hipStream_t s) {
+  static const bool no_queue = [] {  // diagnostic DEPPY_NO_QUEUE=1: one workgroup per item
+    const char* e = std::getenv("DEPPY_NO_QUEUE");
+    return e && *e && *e != '0';
+  }();
+  if (!P.scratch_off.empty()) HIP_OK(hipMemsetAsync(base.scratch, 0, 4 * dp::kQueueWords, s));
+  int q = 0;
   for (const auto& L : P.launches) {
     dp::KernelArgs a = base;
     a.items = base.items + L.first;
-    if (L.mode != dp::M_LDS) a.scratch_off = base.scratch_off + (L.first - P.big_base);
+    if (L.mode != dp::M_LDS) {
+      a.scratch_off = base.scratch_off + (L.first - P.big_base);
+      a.queue = no_queue ? nullptr : base.scratch + q;
+      a.n_items = L.count;
+      ++q;
+    }
     HIP_OK(dp::launch_solve(a, L.mode, L.count, L.lds, s));
     ctx->st.launches++;
   }

@@ -29,6 +29,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
 #include <type_traits>
 
 #include "kernel_api.hpp"
@@ -2242,20 +2244,19 @@ __device__ __forceinline__ void put_out(ProblemOut* o, int status, int32_t flags
   p[1] = y;
 }
 
-template <int MODE, int MINW>
-__global__ void __launch_bounds__(64 * mode_waves(MODE), MINW)
-solve_kernel(KernelArgs a) {
-  extern __shared__ int4 lds4[];
+// Item k of the launch: one problem, start to finish.
+template <int MODE>
+__device__ __forceinline__ void solve_item(const KernelArgs& a, int k, int4* lds4) {
 #ifdef DP_STAMPS
   int64_t t[6];
   const int64_t wall0 = wallclock();
 #endif
   DP_STAMP(0);
-  const WorkItem it = a.items[blockIdx.x];
+  const WorkItem it = a.items[k];
   const int pid = it.pid;
   const int32_t* grec = a.rec + it.rec_off;
   Group<MODE> W;
-  char* hbm = MODE == M_LDS ? nullptr : reinterpret_cast<char*>(a.scratch + a.scratch_off[blockIdx.x]);
+  char* hbm = MODE == M_LDS ? nullptr : reinterpret_cast<char*>(a.scratch + a.scratch_off[k]);
   if (!W.init(reinterpret_cast<char*>(lds4), hbm, grec)) {
     if (threadIdx.x == 0) {  // a malformed record: no solve (dp_rec_validate's verdict)
       put_out(a.out + pid, DP_ERROR, DP_F_MALFORMED, 0, 0, 0, 0);
@@ -2330,11 +2331,50 @@ solve_kernel(KernelArgs a) {
   }
 }
 
+template <int MODE, int MINW>
+__global__ void __launch_bounds__(64 * mode_waves(MODE), MINW)
+solve_kernel(KernelArgs a) {
+  extern __shared__ int4 lds4[];
+  if constexpr (MODE != M_LDS) {
+    if (a.queue) {
+      // persistent workgroup: items in queue order until the queue is
+      // drained (every workgroup reaches the exit).  The item number is
+      // handed over in LDS word 0, the scalars' first word, which init
+      // rewrites only after the third barrier.
+      int32_t* slot = reinterpret_cast<int32_t*>(lds4);
+      for (;;) {
+        __syncthreads();
+        if (threadIdx.x == 0) *slot = atomicAdd(a.queue, 1);
+        __syncthreads();
+        const int k = *slot;
+        __syncthreads();
+        if (k >= a.n_items) return;
+        solve_item<MODE>(a, k, lds4);
+      }
+    }
+  }
+  solve_item<MODE>(a, (int)blockIdx.x, lds4);
+}
+
 // Instantiate and launch one mode (included once per translation unit).
+// A queued (persistent) launch gets as many workgroups as the device holds
+// at once, at most one per item.
 #define DP_DEFINE_MODE(MODE, MINW, NAME)                                                    \
   hipError_t NAME(const KernelArgs& a, int n_blocks, int lds_bytes, hipStream_t stream) {   \
     if (n_blocks <= 0) return hipSuccess;                                                   \
-    hipLaunchKernelGGL((solve_kernel<MODE, MINW>), dim3((unsigned)n_blocks), dim3(64 * mode_waves(MODE)), \
+    int grid = n_blocks;                                                                    \
+    if (a.queue) {                                                                          \
+      int dev = 0, cus = 0, per = 0;                                                        \
+      if (hipGetDevice(&dev) == hipSuccess &&                                               \
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && \
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (solve_kernel<MODE, MINW>),    \
+                                                       64 * mode_waves(MODE), lds_bytes) == hipSuccess && \
+          per > 0 && cus > 0)                                                               \
+        grid = per * cus < n_blocks ? per * cus : n_blocks;                                 \
+      if (std::getenv("DEPPY_DEBUG_GRID"))  /* diagnostic */                                \
+        fprintf(stderr, "solve launch mode %d: %d items, %d cus x %d per cu -> grid %d\n", MODE, n_blocks, cus, per, grid); \
+    }                                                                                       \
+    hipLaunchKernelGGL((solve_kernel<MODE, MINW>), dim3((unsigned)grid), dim3(64 * mode_waves(MODE)), \
                        (size_t)lds_bytes, stream, a);                                       \
     return hipGetLastError();                                                               \
   }                                                                                         \
