@@ -393,9 +393,11 @@ bool implied_choices(const int32_t* clause_off, const int32_t* clause_lits, int3
 
 // The DP_FMT_P16D sources of an int32 record's choice lists (src[nch]), or
 // false when its dependency rows do not imply them (a list whose row was
-// folded away, a repeat more than 255 lists back, ...).  Matched greedily:
-// list k takes the next dependency row when that row is (~subject, list k),
-// else repeats an earlier list of the same subject and content.
+// folded away, a repeat more than 255 lists back, a row no list takes, ...).
+// Matched greedily: list k takes the next dependency row when that row is
+// (~subject, list k), else repeats an earlier list of the same subject and
+// content.  Every list is checked against what it derives from, so true
+// means implied_choices(src) gives back exactly the record's arrays.
 bool choice_sources(const int32_t* r, const dp_rec_layout& L, uint8_t* src) {
   const int32_t nc = r[DP_H_NC], nv = r[DP_H_NV], nch = r[DP_H_NCH];
   const int32_t* clause_off = r + L.clause_off;
@@ -439,7 +441,7 @@ bool choice_sources(const int32_t* r, const dp_rec_layout& L, uint8_t* src) {
     if (d > 255 || d > k || vco[v] > k - d) return false;
     src[k] = (uint8_t)d;
   }
-  return true;
+  return row >= nc;  // every dependency row taken
 }
 
 struct Lowerer {
@@ -492,18 +494,9 @@ struct Lowerer {
     const dp_rec_layout L = dp_rec_layout_of(r);
     const int32_t nc = r[DP_H_NC], nk = r[DP_H_NK], nv = r[DP_H_NV], nch = r[DP_H_NCH], nid = r[DP_H_NID];
     // DP_FMT_P16D when the dependency rows imply the choice lists exactly
-    static thread_local std::vector<int32_t> ch;
     static thread_local std::vector<uint8_t> srcs;
-    ch.resize((size_t)nv + 1 + nch + 1 + r[DP_H_NCHL]);
-    srcs.assign((size_t)nch + 1, 0);
-    int32_t* vco = ch.data();
-    int32_t* co = vco + nv + 1;
-    int32_t* cl = co + nch + 1;
-    const bool derived =
-        choice_sources(r, L, srcs.data()) &&
-        implied_choices(r + L.clause_off, r + L.clause_lits, nc, nv, nch, r[DP_H_NCHL], srcs.data(), vco, co, cl) &&
-        std::equal(vco, vco + nv + 1, r + L.var_choice_off) && std::equal(co, co + nch + 1, r + L.choice_off) &&
-        std::equal(cl, cl + r[DP_H_NCHL], r + L.choice_lits);
+    if (srcs.size() < (size_t)nch + 1) srcs.resize((size_t)nch + 1);
+    const bool derived = choice_sources(r, L, srcs.data());
     for (int32_t i = 1; i < nc; ++i)
       if (r[L.clause_id + i] <= r[L.clause_id + i - 1]) return false;
     for (int32_t i = 1; i < nk; ++i)

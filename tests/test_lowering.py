@@ -230,3 +230,37 @@ def test_relower_reuses_storage():
     assert lw.msg == fresh_b.msg
     lw.relower(sat.encode_inputs(a))
     np.testing.assert_array_equal(lw.rec, keep)
+
+
+@pytest.mark.parametrize("seed", [11, 12])
+def test_packed_forms_of_colliding_problems(seed):
+    """Random small problems with repeated and folded Dependencies, lowered
+    in the packed forms: every DP_FMT_P16D / DP_FMT_P16 record widens back to
+    its int32 record (dp_rec_widen and the independent restatement), and
+    choice lists that repeat an earlier one (a Dependency whose gate an
+    earlier one of the same subject emitted) are encoded as repeats."""
+    from tests.gpu_common import unpack_p16
+    probs = _random_problems(seed, 400) + [
+        [V("a", sat.Dependency("b", "c"), sat.Dependency("c"), sat.Dependency("b", "c")), V("b", sat.Dependency("c")),
+         V("c")]]
+    wire = sat.encode_inputs(probs)
+    a = _lib.Lowered(wire)
+    b = _lib.Lowered(wire, narrow=True, packed=True)
+    L = _lib.lib()
+    fmts = {}
+    repeats = 0
+    for p in range(a.n):
+        r = np.ascontiguousarray(b.record(p))
+        fmt = int(r[13])
+        fmts[fmt] = fmts.get(fmt, 0) + 1
+        out = np.zeros(int(r[10]), np.int32)
+        assert L.dp_rec_widen(r.ctypes.data_as(_lib.c_i32p), len(r), out.ctypes.data_as(_lib.c_i32p)) == 0
+        np.testing.assert_array_equal(out, a.record(p))
+        if fmt in (3, 5):
+            np.testing.assert_array_equal(unpack_p16(r), a.record(p))
+        if fmt == 5:
+            nc, nk, nch, ncl, nkl, na = (int(r[i]) for i in (2, 3, 4, 7, 8, 5))
+            tail = (2 * (ncl + nkl + nk + na) + 15) // 16 * 16
+            repeats += int(np.count_nonzero(r[16:].view(np.uint8)[tail + nc + nk:tail + nc + nk + nch]))
+    assert fmts.get(5, 0) > 0.3 * a.n, fmts
+    assert repeats > 0
