@@ -496,7 +496,11 @@ struct Lowerer {
     // DP_FMT_P16D when the dependency rows imply the choice lists exactly
     static thread_local std::vector<uint8_t> srcs;
     if (srcs.size() < (size_t)nch + 1) srcs.resize((size_t)nch + 1);
-    const bool derived = choice_sources(r, L, srcs.data());
+    static const bool no_p16d = [] {  // diagnostic DEPPY_NO_P16D=1: explicit choice lists (DP_FMT_P16)
+      const char* e = std::getenv("DEPPY_NO_P16D");
+      return e && *e && *e != '0';
+    }();
+    const bool derived = !no_p16d && choice_sources(r, L, srcs.data());
     for (int32_t i = 1; i < nc; ++i)
       if (r[L.clause_id + i] <= r[L.clause_id + i - 1]) return false;
     for (int32_t i = 1; i < nk; ++i)
@@ -517,19 +521,13 @@ struct Lowerer {
       r[DP_H_FMT] = fmt0;
       return false;
     }
-    static thread_local std::vector<uint8_t> buf;
+    // the tail first (it reads the offsets arrays and the AtMost identities,
+    // which the 16-bit arrays then overwrite in place: each lands at half its
+    // int32 position or less, so no word is written before it is read)
+    static thread_local std::vector<uint8_t> tail;
     const int64_t at = dp_p16_tail_at(r), tb = dp_p16_tail_bytes(r);
-    buf.assign((size_t)(at + tb), 0);
-    uint16_t* u = reinterpret_cast<uint16_t*>(buf.data());
-    auto put16 = [&](int32_t off, int32_t n) {
-      for (int32_t j = 0; j < n; ++j) *u++ = (uint16_t)r[off + j];
-    };
-    put16(L.clause_lits, r[DP_H_NCL]);
-    put16(L.card_lits, r[DP_H_NKL]);
-    put16(L.card_bound, nk);
-    if (!derived) put16(L.choice_lits, r[DP_H_NCHL]);
-    put16(L.anchors, r[DP_H_NA]);
-    uint8_t* t = buf.data() + at;
+    tail.assign((size_t)tb, 0);
+    uint8_t* t = tail.data();
     auto put_lens = [&](int32_t off, int32_t n) {
       for (int32_t j = 0; j < n; ++j) *t++ = (uint8_t)(r[off + j + 1] - r[off + j]);
     };
@@ -543,7 +541,18 @@ struct Lowerer {
       t += nch;
     }
     for (int32_t k = 0; k < nk; ++k) t[r[L.card_id + k] >> 3] |= (uint8_t)(1u << (r[L.card_id + k] & 7));
-    std::memcpy(r + DP_H_SIZE, buf.data(), buf.size());
+    uint16_t* u = reinterpret_cast<uint16_t*>(r + DP_H_SIZE);
+    auto put16 = [&](int32_t off, int32_t n) {
+      for (int32_t j = 0; j < n; ++j) *u++ = (uint16_t)r[off + j];
+    };
+    put16(L.clause_lits, r[DP_H_NCL]);
+    put16(L.card_lits, r[DP_H_NKL]);
+    put16(L.card_bound, nk);
+    if (!derived) put16(L.choice_lits, r[DP_H_NCHL]);
+    put16(L.anchors, r[DP_H_NA]);
+    uint8_t* b = reinterpret_cast<uint8_t*>(r + DP_H_SIZE);
+    std::memset(reinterpret_cast<uint8_t*>(u), 0, (size_t)(b + at - reinterpret_cast<uint8_t*>(u)));
+    std::memcpy(b + at, tail.data(), (size_t)tb);
     return true;
   }
 
