@@ -10,8 +10,9 @@ lowered records in host memory -> dp_submit (stage, H2D, solve, D2H) ->
 results in host memory (dp_job_wait), for one batch of BASELINE config 2 by
 default: 10,000 synthetic operator catalogs (~200 bundle entities,
 Dependency + Conflict + AtMost; SURVEY.md §8(d) generator).  `--depth` jobs
-are in flight, as a serving loop keeps them (default 4, one per pipeline lane): step i is submitted
-before step i-4 is collected.  Every step resolves its whole batch, and every
+are in flight, as a serving loop keeps them (default: enough to give each of the
+pipeline's 8 chunk slots a chunk, 8 for a one-chunk batch): step i is submitted
+before step i-depth is collected.  Every step resolves its whole batch, and every
 result lands in host memory.
 
 `value` = resolutions/s over all ranks, host to host.  Secondary figures:
@@ -51,6 +52,7 @@ sys.path.insert(0, ROOT)
 METRIC = "resolutions/sec (node) on synthetic catalogs at 1/2/4/8 GPUs; BCP HBM GB/s"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 PCIE_PEAK_GBS = 64.0   # PCIe Gen5 x16, one direction
+LANES = 8              # chunk slots per device (deppy_amd/csrc/runtime.cpp kLanes)
 
 # BASELINE.json configs as bench workloads: (catalogs per GPU, strong-scaling
 # total, description)
@@ -157,7 +159,8 @@ def main():
     ap.add_argument("--problems", type=int, default=0,
                     help="catalogs per step and rank (weak) or in total (strong); 0: WORKLOADS")
     ap.add_argument("--seed", type=int, default=1000)
-    ap.add_argument("--depth", type=int, default=4, help="host-to-host jobs in flight (one per pipeline lane)")
+    ap.add_argument("--depth", type=int, default=0,
+                    help="host-to-host jobs in flight; 0: enough to give every pipeline lane a chunk")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--kernel-steps", type=int, default=20,
@@ -189,8 +192,14 @@ def main():
     lw, lw32, t_lower = lowered_config(args.config, n, first)
     ctx = _lib.Context(local, 1, flags=args.flags)
 
-    # host-to-host: depth jobs in flight, each the whole batch
-    depth = max(1, args.depth)
+    # host-to-host: depth jobs in flight, each the whole batch.  The pipeline
+    # has LANES chunk slots per device (runtime.cpp kLanes, two per stream);
+    # by default as many jobs are in flight as fill them.
+    depth = args.depth
+    if depth <= 0:
+        ctx.stats(reset=True)
+        ctx.submit(lw.rec_off, lw.rec).wait()
+        depth = max(1, LANES // max(1, ctx.stats(reset=True)["chunks"]))
     outs = [_lib.result_arrays(lw.rec_off, lw.rec) for _ in range(depth)]
 
     def run_steps(k):

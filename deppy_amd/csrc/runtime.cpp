@@ -56,7 +56,9 @@ constexpr int64_t kDefaultBudget = 1 << 16;        // BCP invocations per proble
 // one launch either way.)
 constexpr int kCeilings[] = {16 << 10, 32 << 10, 53 << 10, 80 << 10, 160 << 10};
 constexpr int kNBuckets = (int)(sizeof(kCeilings) / sizeof(kCeilings[0]));
-constexpr int kLanes = 4;            // streams per device, one per hardware queue
+constexpr int kStreams = 4;          // streams per device, one per hardware queue
+constexpr int kLanes = 8;            // chunk slots per device, two per stream: a stream always has
+                                     // the next chunk queued behind the running one (no host gap)
 constexpr double kMergeRatio = 0.5;  // bucket merging (plan_chunk)
 // Routed-off catalogs under kMidMaxVars variables run in 4-wave groups
 // (M_SPLIT4), larger ones in 8-wave groups (profiles/r01_group_waves_ab.jsonl).
@@ -967,9 +969,11 @@ dp_ctx* dp_create(const dp_opts* opts) {
     }
     Device& D = ctx->dev[(size_t)i];
     D.ordinal = d;
-    for (auto& L : D.lanes) {
+    for (int li = 0; li < kLanes; ++li) {
+      Lane& L = D.lanes[li];
       L.device = d;
-      if (hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking) != hipSuccess ||
+      if (li >= kStreams) L.s = D.lanes[li % kStreams].s;  // lane li shares stream li % kStreams
+      if ((li < kStreams && hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking) != hipSuccess) ||
           hipEventCreate(&L.k0) != hipSuccess || hipEventCreate(&L.k1) != hipSuccess ||
           hipEventCreateWithFlags(&L.done, hipEventDisableTiming) != hipSuccess) {
         dp::set_global_error("dp_create: cannot create streams");
@@ -993,14 +997,17 @@ void dp_destroy(dp_ctx* ctx) {
   if (!ctx) return;
   for (auto& D : ctx->dev) {
     (void)hipSetDevice(D.ordinal);
-    for (auto& L : D.lanes) {
-      if (L.s) (void)hipStreamSynchronize(L.s);
+    for (int li = 0; li < kStreams; ++li)
+      if (D.lanes[li].s) (void)hipStreamSynchronize(D.lanes[li].s);
+    for (int li = 0; li < kLanes; ++li) {
+      Lane& L = D.lanes[li];
       for (Buf* b : {&L.h_in, &L.d_in, &L.h_out, &L.d_out, &L.scratch}) b->release();
       if (L.k0) (void)hipEventDestroy(L.k0);
       if (L.k1) (void)hipEventDestroy(L.k1);
       if (L.done) (void)hipEventDestroy(L.done);
-      if (L.s) (void)hipStreamDestroy(L.s);
     }
+    for (int li = 0; li < kStreams; ++li)  // (lanes li + kStreams... share these)
+      if (D.lanes[li].s) (void)hipStreamDestroy(D.lanes[li].s);
   }
   delete ctx;
 }

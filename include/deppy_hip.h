@@ -411,8 +411,9 @@ int dp_upload(dp_ctx* ctx, const dp_batch* b, dp_resident** out);
 int dp_run(dp_ctx* ctx, dp_resident* r);           /* launch + wait; results stay in HBM */
 /* Asynchronous form of dp_run for pipelines: dp_launch enqueues the solve and
  * returns; dp_wait blocks until it finished.  Launches of different residents
- * in flight run concurrently (each takes the next of four per-device streams,
- * one per hardware queue).  dp_launch on a resident still in flight waits for
+ * in flight run concurrently (each takes the next of eight per-device chunk
+ * slots, two on each of four streams, one stream per hardware queue).
+ * dp_launch on a resident still in flight waits for
  * it first; dp_download and dp_resident_free wait as well. */
 int dp_launch(dp_ctx* ctx, dp_resident* r);
 int dp_wait(dp_ctx* ctx, dp_resident* r);
