@@ -273,9 +273,9 @@ def main():
         # the solve kernel alone, records resident in HBM (dp_upload): serial
         # launches give the per-launch device time the roofline uses (HIP
         # events on the launch's stream; rocprofv3 --kernel-trace of
-        # `bench.py --kernel-only` reports the same kernels), then 4 batches
-        # in flight give the rate the kernel sustains
-        slots = [ctx.upload(lw.rec_off, lw.rec) for _ in range(4)]
+        # `bench.py --kernel-only` reports the same kernels), then one batch
+        # per pipeline lane in flight gives the rate the kernel sustains
+        slots = [ctx.upload(lw.rec_off, lw.rec) for _ in range(LANES)]
         slots[0].run()
         kms = []
         for _ in range(args.kernel_steps):
@@ -287,8 +287,8 @@ def main():
                 s_.run()
             t0 = time.perf_counter()
             for i in range(args.kernel_steps):
-                s_ = slots[i % 4]
-                if i >= 4:
+                s_ = slots[i % LANES]
+                if i >= LANES:
                     s_.wait()
                 s_.launch()
             for s_ in slots:
@@ -308,7 +308,7 @@ def main():
                                "ms_per_step": round(tk / args.kernel_steps * 1e3, 4),
                                "serial_launch_ms": round(k_ms, 4),
                                "identical_to_host_path": bool(same_results(kres, res)) if res is not None else None,
-                               "note": "records resident in HBM, 4 batches in flight; not value"}
+                               "note": "records resident in HBM, %d batches in flight; not value" % LANES}
         traffic = None
         if args.pmc_json and os.path.exists(args.pmc_json):
             with open(args.pmc_json) as f:
