@@ -275,7 +275,7 @@ def main():
         # events on the launch's stream; rocprofv3 --kernel-trace of
         # `bench.py --kernel-only` reports the same kernels), then one batch
         # per pipeline lane in flight gives the rate the kernel sustains
-        slots = [ctx.upload(lw.rec_off, lw.rec) for _ in range(LANES)]
+        slots = [ctx.upload(lw.rec_off, lw.rec) for _ in range(1 if args.kernel_only else LANES)]
         slots[0].run()
         kms = []
         for _ in range(args.kernel_steps):
