@@ -196,7 +196,7 @@ def main():
     # has LANES chunk slots per device (runtime.cpp kLanes, two per stream);
     # by default as many jobs are in flight as fill them.
     depth = args.depth
-    if depth <= 0:
+    if depth <= 0 and not args.kernel_only:  # (profiling runs count solve dispatches: none extra)
         ctx.stats(reset=True)
         ctx.submit(lw.rec_off, lw.rec).wait()
         depth = max(1, LANES // max(1, ctx.stats(reset=True)["chunks"]))
