@@ -241,7 +241,14 @@ __host__ __device__ inline Layout layout(const int32_t* h) {
   L.scal = take(mode_nscal(MODE) * 4, WORK);
   L.wbuf = take(mode_wbuf(MODE) * ix, WORK);
   L.cardq = take(mode_cq(MODE) * ix, WORK);
+  // the table shrinks (to 64 slots at least) when the catalog's per-variable
+  // state leaves less LDS, so it never moves a catalog off this placement
   L.hc = mode_lds_rounds(MODE) ? round_slots(nv) : 0;
+  if (mode_lds_rounds(MODE)) {
+    auto a16 = [](int32_t x) { return (x + 15) & ~15; };
+    const int32_t rest = ol + a16(nv) + 7 * a16(nbv * 4) + 3 * a16(nbi * 4);  // work lists so far + val + bitsets
+    while (L.hc > 64 && rest + 20 * L.hc > 160 * 1024) L.hc >>= 1;
+  }
   L.hkey = take(L.hc * 4, WORK);
   L.hrp = take(L.hc * 4, WORK);
   L.hrn = take(L.hc * 4, WORK);
