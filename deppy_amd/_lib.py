@@ -17,6 +17,7 @@ LIB_PATH = os.path.join(HERE, "libdeppy_hip.so")
 OPT_FORCE_GROUP = 1 << 0
 OPT_FORCE_HBM = 1 << 1
 OPT_FORCE_MID = 1 << 2
+OPT_TINY_TABLE = 1 << 3
 # dp_flag bits used on the host
 F_TRACE_TRUNCATED = 1 << 8
 if os.environ.get("DEPPY_STAMPS") == "1":  # diagnostic phase-stamp build (scripts/ only)

@@ -63,6 +63,8 @@ struct KernelArgs {
   // nullptr: one workgroup per item.
   int32_t* queue;
   int32_t n_items;
+  // test (DP_OPT_TINY_TABLE): round tables of this many slots (0: the layout's)
+  int32_t table_cap;
 };
 // Words at the front of the multi-wave scratch holding the launches' queues.
 constexpr int kQueueWords = 64;

@@ -761,6 +761,7 @@ int enqueue_launches(dp_ctx* ctx, const Plan& P, const dp::KernelArgs& base, hip
       a.scratch_off = base.scratch_off + (L.first - P.big_base);
       a.queue = no_queue ? nullptr : base.scratch + q;
       a.n_items = L.count;
+      if (ctx->flags & DP_OPT_TINY_TABLE) a.table_cap = 4;
       ++q;
     }
     HIP_OK(dp::launch_solve(a, L.mode, L.count, L.lds, s));

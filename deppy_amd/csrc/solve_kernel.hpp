@@ -1373,6 +1373,7 @@ struct Group {
     if constexpr (LR) {
       lds_sync = false;
       if (r == 2) {
+        DP_ACC(25, 1);  // diagnostic: rounds redone on the HBM arrays
         vis = vis0;
         hmode = false;
         crow = INF;
@@ -2270,6 +2271,8 @@ __device__ __forceinline__ void solve_item(const KernelArgs& a, int k, int4* lds
   if (a.stamps) W.dbg = reinterpret_cast<unsigned long long*>(a.stamps + (int64_t)DP_NSTAMP * pid + 12);
 #endif
   W.budget = a.budget;
+  if constexpr (Group<MODE>::LR)
+    if (a.table_cap > 0 && a.table_cap - 1 < W.hmask) W.hmask = a.table_cap - 1;  // (a power of two)
   if (a.trace) {
     W.tr = a.trace + (int64_t)a.trace_cap * pid;
     W.tr_cap = a.trace_cap;

@@ -327,7 +327,9 @@ typedef struct dp_opts {
 enum dp_opt_flag {
   DP_OPT_FORCE_GROUP = 1 << 0, /* every problem: multi-wave workgroup */
   DP_OPT_FORCE_HBM = 1 << 1,   /* every problem: multi-wave workgroup, state in HBM */
-  DP_OPT_FORCE_MID = 1 << 2    /* every problem: 4-wave workgroup (the mid-size path) */
+  DP_OPT_FORCE_MID = 1 << 2,   /* every problem: 4-wave workgroup (the mid-size path) */
+  DP_OPT_TINY_TABLE = 1 << 3   /* test: 4-slot round tables in the multi-wave modes, so rounds
+                                  overflow them and are redone on the HBM arrays */
 };
 
 typedef struct dp_ctx dp_ctx;

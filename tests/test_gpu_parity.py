@@ -150,6 +150,24 @@ def test_multiwave_paths_bit_exact(config, n, seed, flags):
     assert bad == [], bad[:10]
 
 
+@pytest.mark.parametrize("flags", [_lib.OPT_FORCE_MID, _lib.OPT_FORCE_GROUP], ids=["split4", "split"])
+@pytest.mark.parametrize("config,n,seed", [(2, 200, 44), (5, 80, 45)])
+def test_round_table_overflow_bit_exact(config, n, seed, flags):
+    """Multi-wave rounds whose implications overflow the LDS round table are
+    redone on the HBM arrays (solve_kernel.hpp run_round); with 4-slot tables
+    (DP_OPT_TINY_TABLE) nearly every round takes that path, and the trail
+    ring wraps, so the frontier comes from HBM: results stay bit-exact."""
+    c = _lib.Context(0, 1, flags=flags | _lib.OPT_TINY_TABLE)
+    try:
+        lw = lowered_config(config, n, seed)
+        g = c.solve(lw.rec_off, lw.rec)
+    finally:
+        c.close()
+    o = oracle.solve_batch(lw.rec_off, lw.rec, 0, 16)
+    bad = compare_results(g, o, n)
+    assert bad == [], bad[:10]
+
+
 @pytest.mark.parametrize("config,n,seed", [(2, 400, 21), (5, 60, 22)])
 def test_models_and_cores_verified(ctx, config, n, seed):
     """Every SAT answer satisfies every row; every core is UNSAT on its own and
