@@ -667,6 +667,10 @@ struct Lane {
   int device = 0;
   hipStream_t s = nullptr;
   hipEvent_t k0 = nullptr, k1 = nullptr, done = nullptr;
+  // copy stream of the lane's records (shared like s): the next chunk's H2D
+  // runs while the stream's current kernel does; `copied` orders the launch
+  hipStream_t cs = nullptr;
+  hipEvent_t copied = nullptr;
   Buf h_in{nullptr, 0, true}, d_in, h_out{nullptr, 0, true}, d_out, scratch;
   bool zc_out = false;  // the chunk's kernels wrote their results straight into h_out
   // the chunk in flight
@@ -703,6 +707,7 @@ struct dp_ctx {
   dp::Pool* pool = nullptr;
   int next_lane = 0;  // pipeline cursor over (device, lane)
   bool zc_in = false, zc_out = true;  // zero-copy records / results (start_chunk)
+  bool copy_streams = false;          // records' H2D on a stream of its own (DEPPY_COPY_STREAM=1)
   bool direct = true;  // copy page-locked batches of staged-form records as they are
   int32_t chunk_problems = kChunkProblems;
   int64_t chunk_bytes = kChunkBytes;
@@ -868,16 +873,22 @@ int start_chunk(dp_ctx* ctx, Lane& L, dp_job* job, int32_t p0, int32_t n) {
   char* din = zc_in ? L.h_in.dev : L.d_in.p;
   char* dout = L.zc_out ? L.h_out.dev : L.d_out.p;
   size_t h2d = 0;
+  // (lane buffers are free: finish_lane waited for the lane's last chunk)
+  hipStream_t cs = L.cs ? L.cs : L.s;
   if (direct) {
     const size_t src_bytes = 4 * (size_t)W;
     if (src_bytes)
-      HIP_OK(hipMemcpyAsync(L.d_in.p + il.img, job->rec + job->rec_off[p0], src_bytes, hipMemcpyHostToDevice, L.s));
-    HIP_OK(hipMemcpyAsync(L.d_in.p + rest, L.h_in.p, il.end - rest, hipMemcpyHostToDevice, L.s));
+      HIP_OK(hipMemcpyAsync(L.d_in.p + il.img, job->rec + job->rec_off[p0], src_bytes, hipMemcpyHostToDevice, cs));
+    HIP_OK(hipMemcpyAsync(L.d_in.p + rest, L.h_in.p, il.end - rest, hipMemcpyHostToDevice, cs));
     h2d = src_bytes + il.end - rest;
     ctx->st.direct_chunks++;
   } else if (!zc_in) {
-    HIP_OK(hipMemcpyAsync(L.d_in.p, L.h_in.p, il.end, hipMemcpyHostToDevice, L.s));
+    HIP_OK(hipMemcpyAsync(L.d_in.p, L.h_in.p, il.end, hipMemcpyHostToDevice, cs));
     h2d = il.end;
+  }
+  if (cs != L.s) {
+    HIP_OK(hipEventRecord(L.copied, cs));
+    HIP_OK(hipStreamWaitEvent(L.s, L.copied, 0));
   }
   HIP_OK(hipMemsetAsync(L.d_out.p + L.ol.pool_len, 0, 4, L.s));
   dp::KernelArgs a = kernel_args(il, L.ol, din, dout, reinterpret_cast<int32_t*>(L.scratch.p), ctx->budget);
@@ -970,11 +981,17 @@ dp_ctx* dp_create(const dp_opts* opts) {
     }
     Device& D = ctx->dev[(size_t)i];
     D.ordinal = d;
+    ctx->copy_streams = env_i64("DEPPY_COPY_STREAM", 0) != 0;
     for (int li = 0; li < kLanes; ++li) {
       Lane& L = D.lanes[li];
       L.device = d;
-      if (li >= kStreams) L.s = D.lanes[li % kStreams].s;  // lane li shares stream li % kStreams
-      if ((li < kStreams && hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking) != hipSuccess) ||
+      if (li >= kStreams) {  // lane li shares the streams of lane li % kStreams
+        L.s = D.lanes[li % kStreams].s;
+        L.cs = D.lanes[li % kStreams].cs;
+      }
+      if ((li < kStreams && (hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking) != hipSuccess ||
+                             (ctx->copy_streams && hipStreamCreateWithFlags(&L.cs, hipStreamNonBlocking) != hipSuccess))) ||
+          hipEventCreateWithFlags(&L.copied, hipEventDisableTiming) != hipSuccess ||
           hipEventCreate(&L.k0) != hipSuccess || hipEventCreate(&L.k1) != hipSuccess ||
           hipEventCreateWithFlags(&L.done, hipEventDisableTiming) != hipSuccess) {
         dp::set_global_error("dp_create: cannot create streams");
@@ -1006,9 +1023,12 @@ void dp_destroy(dp_ctx* ctx) {
       if (L.k0) (void)hipEventDestroy(L.k0);
       if (L.k1) (void)hipEventDestroy(L.k1);
       if (L.done) (void)hipEventDestroy(L.done);
+      if (L.copied) (void)hipEventDestroy(L.copied);
     }
-    for (int li = 0; li < kStreams; ++li)  // (lanes li + kStreams... share these)
+    for (int li = 0; li < kStreams; ++li) {  // (lanes li + kStreams... share these)
       if (D.lanes[li].s) (void)hipStreamDestroy(D.lanes[li].s);
+      if (D.lanes[li].cs) (void)hipStreamDestroy(D.lanes[li].cs);
+    }
   }
   delete ctx;
 }
