@@ -264,3 +264,35 @@ def test_packed_forms_of_colliding_problems(seed):
             repeats += int(np.count_nonzero(r[16:].view(np.uint8)[tail + nc + nk:tail + nc + nk + nch]))
     assert fmts.get(5, 0) > 0.3 * a.n, fmts
     assert repeats > 0
+
+
+def test_packed_form_falls_back_when_rows_do_not_imply_lists():
+    """DP_FMT_P16D only where the dependency rows give back the choice lists
+    exactly: a Dependency whose gate folds away (Dependency(v; v) is always
+    true: a choice list without a row) or whose candidates repeat (the Or
+    chain drops the repeat: the row is shorter than the list) leaves the
+    record in DP_FMT_P16 (or U16); every form widens to the same int32
+    record."""
+    from tests.gpu_common import unpack_p16
+    cases = {
+        "self": [V("a", sat.Dependency("a")), V("b")],
+        "repeat": [V("a", sat.Dependency("b", "b")), V("b")],
+        "plain": [V("a", sat.Dependency("b", "c")), V("b"), V("c")],
+        "same-twice": [V("a", sat.Dependency("b"), sat.Dependency("b")), V("b")],
+    }
+    probs = list(cases.values())
+    wire = sat.encode_inputs(probs)
+    a = _lib.Lowered(wire)
+    b = _lib.Lowered(wire, narrow=True, packed=True)
+    L = _lib.lib()
+    fmts = {}
+    for p, name in enumerate(cases):
+        r = np.ascontiguousarray(b.record(p))
+        fmts[name] = int(r[13])
+        out = np.zeros(int(r[10]), np.int32)
+        assert L.dp_rec_widen(r.ctypes.data_as(_lib.c_i32p), len(r), out.ctypes.data_as(_lib.c_i32p)) == 0
+        np.testing.assert_array_equal(out, a.record(p))
+        if fmts[name] in (3, 5):
+            np.testing.assert_array_equal(unpack_p16(r), a.record(p))
+    assert fmts["plain"] == 5 and fmts["same-twice"] == 5
+    assert fmts["self"] != 5 and fmts["repeat"] != 5, fmts
