@@ -131,7 +131,14 @@ __host__ __device__ inline dp_rec_layout rec_layout(const int32_t* h) {
 // body), and the 16-bit form of a record the host checked while narrowing it
 // (the kernel validates only the DP_FMT_U16 copies the host passed through
 // unread, Group::valid_record).
-enum { DP_FMT_REJECT = 2, DP_FMT_U16_CHECKED = 16 };
+enum { DP_FMT_REJECT = 2, DP_FMT_U16_CHECKED = 16, DP_FMT_I32_CHECKED = 17 };
+
+// Multi-wave problems of up to DEV_WATCH_VARS variables cross PCIe as plain
+// int32 records (DP_FMT_I32, no watch lists): the kernel builds their watch
+// lists in its HBM scratch (Layout::wl) with counters in the LDS work area
+// (Group::build_watches_wide).  Larger ones take DP_FMT_I32W.
+constexpr int32_t DEV_WATCH_VARS = 2048;
+__host__ __device__ inline bool device_watches(const int32_t* h) { return h[DP_H_NV] <= DEV_WATCH_VARS; }
 
 struct ImgLayout {
   int32_t w_off, w, words;
@@ -195,6 +202,7 @@ struct Layout {
   int32_t tl;        // u16[2hc] first implications, (slot << 1) | negative       [LDS]
   int32_t fr;        // i32[hc] trail ring: trail[i] at fr[i & (hc - 1)]          [LDS]
   int32_t hc;        // slots (a power of two; 0 when the mode keeps rounds in HBM)
+  int32_t wl;        // multi-wave, DP_FMT_I32 records: device-built w_off[2nv+1], w[ncl+nkl]  [HBM, last]
   int32_t bytes;     // HBM scratch bytes (0 for M_LDS)
   int32_t lds_bytes; // LDS bytes
   int32_t cap, lcap;
@@ -275,6 +283,8 @@ __host__ __device__ inline Layout layout(const int32_t* h) {
   L.l_lits = take(L.lcap * ix, COLD);
   L.dq = take(2 * L.cap * ix, COLD);
   L.stk = take(3 * L.cap * ix, COLD);
+  L.wl = MODE != M_LDS && h[DP_H_FMT] == DP_FMT_I32 && device_watches(h)
+             ? take((2 * nv + 1 + h[DP_H_NCL] + h[DP_H_NKL]) * 4, COLD) : 0;
   L.bytes = og;
   L.lds_bytes = ol;
   return L;

@@ -460,13 +460,17 @@ struct Lowerer {
     int32_t* r = O.rec.data() + base;
     const int64_t words = r[DP_H_WORDS];
     int64_t phys = words;
-    if (!one_wave(r)) {  // a multi-wave problem: its staged form, with watch lists
-      const int64_t ext = 2 * (int64_t)r[DP_H_NV] + 1 + r[DP_H_NCL] + r[DP_H_NKL];
-      O.extend((size_t)ext);  // (may move the storage)
-      r = O.rec.data() + base;
-      build_watches_host(r);
-      r[DP_H_FMT] = DP_FMT_I32W;
-      phys = words + ext;
+    if (!one_wave(r)) {
+      // a multi-wave problem: its staged form -- with watch lists, or as it
+      // is for the kernel to build them (layout.hpp device_watches)
+      if (!device_watches(r)) {
+        const int64_t ext = 2 * (int64_t)r[DP_H_NV] + 1 + r[DP_H_NCL] + r[DP_H_NKL];
+        O.extend((size_t)ext);  // (may move the storage)
+        r = O.rec.data() + base;
+        build_watches_host(r);
+        r[DP_H_FMT] = DP_FMT_I32W;
+        phys = words + ext;
+      }
     } else if (packed && pack16(r)) {
       phys = dp_rec_phys_words(r);
     } else if (dp_rec_fits16(r)) {

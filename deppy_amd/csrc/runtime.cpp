@@ -172,7 +172,7 @@ void read_head(Head& H, const int32_t* h, int64_t avail, int32_t opt_flags, bool
   // 16-bit form (LDS path) or the int32 form with its watch lists
   H.rec_bytes = nar ? (dp_fmt_packed(h[DP_H_FMT]) ? 4 * dp_rec_phys_words(h)
                                                  : 4 * DP_H_SIZE + 2 * ((int64_t)h[DP_H_WORDS] - DP_H_SIZE))
-                    : 4 * (int64_t)img_layout(h).words;
+                    : 4 * (int64_t)img_layout(h).words;  // (lists built on the device are read too)
   if (nar) {
     H.place = M_LDS;
     int k = 0;
@@ -181,7 +181,9 @@ void read_head(Head& H, const int32_t* h, int64_t avail, int32_t opt_flags, bool
     H.direct = aligned && (h[DP_H_FMT] == DP_FMT_U16 || dp_fmt_packed(h[DP_H_FMT]));
     return;
   }
-  H.direct = aligned && h[DP_H_FMT] == DP_FMT_I32W;  // the multi-wave staged form
+  // the multi-wave staged forms: with host-built watch lists, or plain int32
+  // for the kernel to build them (layout.hpp device_watches)
+  H.direct = aligned && (h[DP_H_FMT] == DP_FMT_I32W || (h[DP_H_FMT] == DP_FMT_I32 && dp::device_watches(h)));
   const bool forced = forced_of(opt_flags);
   // (layout arithmetic is int32: variables are capped well below its range)
   const bool sized = h[DP_H_NV] < (1 << 24) && h[DP_H_NID] < (1 << 26) && h[DP_H_WORDS] < (1 << 28);
@@ -476,7 +478,7 @@ bool stage_one(const Plan& P, const int32_t* rec, const int64_t* rec_off, int32_
       for (int64_t j = phys; j < sw; ++j) d[j] = 0;
     }
   } else {
-    d[DP_H_FMT] = DP_FMT_I32;
+    d[DP_H_FMT] = dp::DP_FMT_I32_CHECKED;  // checked here, watch lists built here
     bool ok;
     if (dp_fmt_packed(fmt)) {  // its int32 form, then the checked copy
       static thread_local std::vector<int32_t> wide;

@@ -501,7 +501,8 @@ struct Group {
     if constexpr (MODE == M_LDS)
       if ((h[DP_H_FMT] == DP_FMT_U16 || packed) && !valid_record(body, packed)) return false;
     if constexpr (MODE != M_LDS)
-      if (h[DP_H_FMT] == DP_FMT_I32W && !valid_wide(R, X)) return false;
+      if ((h[DP_H_FMT] == DP_FMT_I32W || h[DP_H_FMT] == DP_FMT_I32) && !valid_wide(R, X, h[DP_H_FMT] == DP_FMT_I32W))
+        return false;
 #ifdef DP_STAMPS
     const int64_t ti2 = stamp();
     sub[1] = ti2 - ti1;
@@ -513,7 +514,13 @@ struct Group {
                     reinterpret_cast<uint32_t*>(lds + L.reason));
       w_off = rv(X.w_off); w = rv(X.w);
     } else {
-      w_off = rv(X.w_off); w = rv(X.w);  // host-built, staged after the record
+      if (h[DP_H_FMT] == DP_FMT_I32) {  // plain int32 record: the lists into scratch (layout.hpp wl)
+        IX* wo = reinterpret_cast<IX*>(hbm + L.wl);
+        build_watches_wide(wo, wo + 2 * nv + 1, reinterpret_cast<uint32_t*>(lds + L.wbuf));
+        w_off = wo; w = wo + 2 * nv + 1;
+      } else {
+        w_off = rv(X.w_off); w = rv(X.w);  // host-built, staged after the record
+      }
     }
 #ifdef DP_STAMPS
     sub[2] = stamp() - ti2;
@@ -618,7 +625,7 @@ struct Group {
   // totals; indices in range; AtMost bounds not negative and each variable's
   // positions one run; w_off from 0, non-decreasing, within w; every listed
   // row a row.  Group-uniform result.
-  __device__ __forceinline__ bool valid_wide(const dp_rec_layout& R, const ImgLayout& X) {
+  __device__ __forceinline__ bool valid_wide(const dp_rec_layout& R, const ImgLayout& X, bool watches) {
     static_assert(MODE != M_LDS, "the int32 form runs on multi-wave groups");
     const int32_t* r = reinterpret_cast<const int32_t*>(clause_off) - R.clause_off;  // the record
     bool bad = false;
@@ -639,7 +646,7 @@ struct Group {
     offsets(R.card_off, nk, nkl, true);
     offsets(R.var_choice_off, nv, nch, true);
     offsets(R.choice_off, nch, nchl, true);
-    offsets(X.w_off, 2 * nv, ncl + nkl, false);
+    if (watches) offsets(X.w_off, 2 * nv, ncl + nkl, false);
     range(R.clause_lits, ncl, 0, 2 * nv);
     range(R.clause_id, nc, 0, nid);
     range(R.card_lits, nkl, 0, nv);
@@ -647,7 +654,7 @@ struct Group {
     range(R.card_id, nk, 0, nid);
     range(R.choice_lits, nchl + na, 0, nv);  // choice_lits then anchors
     if (g_any(bad)) return false;  // the offsets below are now in range
-    range(X.w, r[X.w_off + 2 * nv], 0, nrows);
+    if (watches) range(X.w, r[X.w_off + 2 * nv], 0, nrows);
     for (int k = tid; k < nk; k += NT) {
       const int a = r[R.card_off + k], b = r[R.card_off + k + 1];
       const int32_t* cl = r + R.card_lits;
@@ -825,6 +832,44 @@ struct Group {
     if (lane == 0) vco[0] = enc(0);
     wsync();
     return true;
+  }
+
+  // Watch lists of a multi-wave problem sent as a plain int32 record
+  // (DP_FMT_I32, layout.hpp device_watches): counters in the LDS work area
+  // (cnt: 2nv+1 words, free until the first round), a scan by wavefront 0,
+  // then the fill into the lists in HBM scratch through the counters as
+  // cursors.  Row order within a list is left to the atomics, as in
+  // build_watches.  Ends with a draining barrier: every wavefront reads the
+  // lists after it.
+  __device__ __forceinline__ void build_watches_wide(IX* wo, IX* ww, uint32_t* cnt) {
+    static_assert(MODE != M_LDS, "one-wavefront problems build theirs in LDS");
+    const int n2 = 2 * nv + 1;
+    for (int i = tid; i < n2; i += NT) cnt[i] = 0u;
+    gsync();
+    for (int j = tid; j < ncl; j += NT) atomicAdd(&cnt[((int)clause_lits[j] ^ 1) + 1], 1u);
+    for (int k = tid; k < nk; k += NT)
+      for (int j = card_off[k]; j < (int)card_off[k + 1]; ++j)
+        if (j == (int)card_off[k] || card_lits[j] != card_lits[j - 1]) atomicAdd(&cnt[2 * (int)card_lits[j] + 1], 1u);
+    gsync();
+    if (wid == 0) {
+      int carry = 0;
+      for (int b = 0; b < n2; b += 64) {
+        const int i = b + lane;
+        const int x = i < n2 ? (int)cnt[i] : 0;
+        const int incl = wave_incl_scan(x) + carry;
+        if (i < n2) { wo[i] = incl; cnt[i] = (uint32_t)incl; }
+        carry = __builtin_amdgcn_readlane(incl, 63);
+      }
+    }
+    gsync();
+    for (int r = tid; r < nc; r += NT)
+      for (int j = clause_off[r]; j < (int)clause_off[r + 1]; ++j)
+        ww[atomicAdd(&cnt[(int)clause_lits[j] ^ 1], 1u)] = r;
+    for (int k = tid; k < nk; k += NT)
+      for (int j = card_off[k]; j < (int)card_off[k + 1]; ++j)
+        if (j == (int)card_off[k] || card_lits[j] != card_lits[j - 1])
+          ww[atomicAdd(&cnt[2 * (int)card_lits[j]], 1u)] = nc + k;
+    bar();  // (drains the lists' stores)
   }
 
   // Watch lists of a one-wavefront problem, built in LDS from its record
