@@ -193,7 +193,9 @@ static inline dp_rec_layout dp_rec_layout_of(const int32_t* h) {
  * DP_FMT_I32W: the int32 form followed by its watch lists, the form a
  * problem solved by a multi-wave workgroup is staged in (dp_lower_into
  * DP_LOWER_NARROW emits it for the records that do not run one wavefront
- * per problem, so that they too go to the device as they lie):
+ * per problem and have over 2048 variables, so that they too go to the
+ * device as they lie; smaller multi-wave records stay DP_FMT_I32 and the
+ * kernel builds their watch lists):
  *   int32 w_off[2nv+1]  rows literal l wakes: w[w_off[l] .. w_off[l+1]) (the
  *                       clauses holding ~l; when l = 2v is positive, the
  *                       AtMost rows holding v, once each)
