@@ -1736,6 +1736,36 @@ struct Group {
       violated(best, fu);
       return fu;
     }
+#ifdef DP_FV_FLAT
+    // Flattened: a wavefront takes 64 trail entries, scans their watch-list
+    // lengths, and walks the concatenated (literal, entry) pairs 64 at a
+    // time, so a long list does not hold the other lanes.  Loop bounds
+    // are wave-uniform (i0 per wave, total by shuffle).
+    for (int i0 = 64 * wid; i0 < tlen; i0 += NT) {
+      const int i = i0 + lane;
+      const int l = i < tlen ? (int)trail[i] : 1;
+      int s = 0, n = 0;
+      if (!(l & 1)) { s = (int)w_off[l]; n = (int)w_off[l + 1] - s; }
+      int inc = n;
+      for (int d = 1; d < 64; d <<= 1) {
+        const int t = __shfl_up(inc, d);
+        if (lane >= d) inc += t;
+      }
+      const int total = __shfl(inc, 63);
+      for (int base = 0; base < total; base += 64) {
+        const int f = base + lane;
+        int j = 0;  // lowest lane whose inclusive count exceeds f
+        for (int step = 32; step; step >>= 1)
+          if (__shfl(inc, j + step - 1) <= f) j += step;
+        const int sj = __shfl(s, j), ej = __shfl(inc, j) - __shfl(n, j);
+        if (f < total) {
+          const int c = w[sj + f - ej];
+          int fu;
+          if (c < nc && c < best && row_on(c) && violated(c, fu)) best = c;
+        }
+      }
+    }
+#else
     for (int i = tid; i < tlen; i += NT) {
       const int l = trail[i];
       if (l & 1) continue;  // only variables assigned true own violations
@@ -1745,6 +1775,7 @@ struct Group {
         if (c < nc && c < best && row_on(c) && violated(c, fu)) best = c;
       }
     }
+#endif
     best = g_min(best);
     if (best == INF) return -1;
     int fu;
