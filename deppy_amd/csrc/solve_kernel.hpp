@@ -1736,7 +1736,7 @@ struct Group {
       violated(best, fu);
       return fu;
     }
-#ifdef DP_FV_FLAT
+#ifndef DP_FV_THREAD
     // Flattened: a wavefront takes 64 trail entries, scans their watch-list
     // lengths, and walks the concatenated (literal, entry) pairs 64 at a
     // time, so a long list does not hold the other lanes.  Loop bounds
