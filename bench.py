@@ -257,6 +257,7 @@ def main():
                  "d2h_GBs": round(st["d2h_bytes"] / (elapsed if world == 1 else step_s * args.steps) / 1e9, 2),
                  "h2d_bytes_per_step": st["h2d_bytes"] // args.steps, "peak_GBs": PCIE_PEAK_GBS},
         "host_ms_per_step": {k: round(st[k] / args.steps, 4) for k in ("stage_ms", "plan_ms", "wait_ms", "scatter_ms")},
+        "allocs_in_timed_region": int(st["allocs"]),
         "direct_chunks_per_step": round(st["direct_chunks"] / args.steps, 2),
         "bcp": {"visited_bytes_per_resolution": round(st["bcp_bytes"] / max(st["problems"], 1), 1),
                 "GBs": round(st["bcp_bytes"] / elapsed / 1e9, 2) if elapsed != float("inf") else None,

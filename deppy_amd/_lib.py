@@ -70,7 +70,7 @@ class Stats(ctypes.Structure):
                 ("kernel_ms", ctypes.c_double), ("h2d_bytes", ctypes.c_int64), ("d2h_bytes", ctypes.c_int64),
                 ("rec_bytes", ctypes.c_int64), ("stage_ms", ctypes.c_double), ("plan_ms", ctypes.c_double), ("wait_ms", ctypes.c_double),
                 ("scatter_ms", ctypes.c_double), ("direct_chunks", ctypes.c_int64),
-                ("bcp_bytes", ctypes.c_int64)]
+                ("bcp_bytes", ctypes.c_int64), ("allocs", ctypes.c_int64)]
 
 
 class Batch(ctypes.Structure):

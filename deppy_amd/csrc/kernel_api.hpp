@@ -65,6 +65,9 @@ struct KernelArgs {
   int32_t n_items;
   // test (DP_OPT_TINY_TABLE): round tables of this many slots (0: the layout's)
   int32_t table_cap;
+  // test (DEPPY_GRID_CAP): a queued launch starts at most this many
+  // workgroups (0: as many as the device holds), so each takes several items
+  int32_t grid_cap;
 };
 // Words at the front of the multi-wave scratch holding the launches' queues.
 constexpr int kQueueWords = 64;

@@ -139,6 +139,13 @@ enum { DP_FMT_REJECT = 2, DP_FMT_U16_CHECKED = 16, DP_FMT_I32_CHECKED = 17 };
 // (Group::build_watches_wide).  Larger ones take DP_FMT_I32W.
 constexpr int32_t DEV_WATCH_VARS = 2048;
 __host__ __device__ inline bool device_watches(const int32_t* h) { return h[DP_H_NV] <= DEV_WATCH_VARS; }
+// Its 2nv+1 counters span the work list and the AtMost queue after it
+// (layout() takes them back to back, 16-byte aligned; both are free until the
+// first round).
+static_assert(2 * DEV_WATCH_VARS + 1 <= mode_wbuf(M_SPLIT) + mode_cq(M_SPLIT) &&
+                  2 * DEV_WATCH_VARS + 1 <= mode_wbuf(M_SPLIT4) + mode_cq(M_SPLIT4) &&
+                  2 * DEV_WATCH_VARS + 1 <= mode_wbuf(M_HBM) + mode_cq(M_HBM) && mode_wbuf(M_SPLIT) % 4 == 0,
+              "build_watches_wide: the counters fit wbuf + cardq");
 
 struct ImgLayout {
   int32_t w_off, w, words;

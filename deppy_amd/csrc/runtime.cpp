@@ -634,6 +634,10 @@ dp::KernelArgs kernel_args(const InLayout& I, const OutLayout& O, char* din, cha
   return a;
 }
 
+// Allocations made by growing buffers (hipMalloc / hipHostMalloc), process
+// wide: dp_stats.allocs reports the ones made on behalf of a context.
+std::atomic<int64_t> g_buf_allocs{0};
+
 // A growable buffer, device or pinned host.
 struct Buf {
   char* p = nullptr;
@@ -647,6 +651,7 @@ struct Buf {
                                         hipHostMallocPortable | hipHostMallocMapped | hipHostMallocCoherent)
                         : hipMalloc(reinterpret_cast<void**>(&p), n);
     if (e != hipSuccess) { p = nullptr; cap = 0; return e; }
+    g_buf_allocs.fetch_add(1, std::memory_order_relaxed);
     dev = p;
     if (host && hipHostGetDevicePointer(reinterpret_cast<void**>(&dev), p, 0) != hipSuccess) dev = p;
     cap = n;
@@ -680,6 +685,8 @@ struct Lane {
   int32_t p0 = 0;
   Plan plan;
   OutLayout ol{};
+  std::vector<uint8_t> bad;  // per-problem malformed marks of the chunk being started
+  int dev_index = 0;         // its Device in dp_ctx::dev
 };
 
 struct Device {
@@ -713,6 +720,7 @@ struct dp_ctx {
   bool direct = true;  // copy page-locked batches of staged-form records as they are
   int32_t chunk_problems = kChunkProblems;
   int64_t chunk_bytes = kChunkBytes;
+  int32_t grid_cap = 0;  // test: workgroups of a queued launch (DEPPY_GRID_CAP; 0 = resident maximum)
   dp_stats st{};
   ~dp_ctx() { delete pool; }
 };
@@ -769,6 +777,7 @@ int enqueue_launches(dp_ctx* ctx, const Plan& P, const dp::KernelArgs& base, hip
       a.queue = no_queue ? nullptr : base.scratch + q;
       a.n_items = L.count;
       if (ctx->flags & DP_OPT_TINY_TABLE) a.table_cap = 4;
+      a.grid_cap = ctx->grid_cap;
       ++q;
     }
     HIP_OK(dp::launch_solve(a, L.mode, L.count, L.lds, s));
@@ -807,11 +816,88 @@ int finish_lane(dp_ctx* ctx, Lane& L) {
   return 0;
 }
 
+// Planning storage of `dst` grown to (at least) the sizes `src` uses, with
+// its pages touched, so plan_chunk on dst allocates and faults nothing for a
+// chunk like src's.
+template <class T>
+void grow_vec(std::vector<T>& d, size_t n) {
+  if (d.capacity() >= n) return;
+  const size_t keep = d.size();
+  d.resize(n);
+  d.resize(keep);
+}
+void grow_plan(Plan& dst, const Plan& src) {
+  grow_vec(dst.img_off, src.img_off.size());
+  grow_vec(dst.narrow, src.narrow.size());
+  grow_vec(dst.order, src.order.size());
+  grow_vec(dst.launches, src.launches.size());
+  grow_vec(dst.scratch_off, src.scratch_off.size());
+  grow_vec(dst.skip, src.skip.size());
+  grow_vec(dst.skip_flags, src.skip_flags.size());
+  grow_vec(dst.inst_off, src.inst_off.size());
+  grow_vec(dst.dev_off, src.dev_off.size());
+  grow_vec(dst.direct, src.direct.size());
+  grow_vec(dst.head, src.head.size());
+  for (int k = 0; k < 4; ++k) grow_vec(dst.big[k], src.big[k].size());
+  grow_vec(dst.cnt, src.cnt.capacity());
+  grow_vec(dst.tmp, src.tmp.capacity());
+}
+
+// Buffer sizes a planned chunk needs on its lane.
+struct LaneNeed {
+  size_t h_in, d_in, h_out, d_out, scratch;
+  bool fits(const Lane& L) const {
+    return h_in <= L.h_in.cap && d_in <= L.d_in.cap && h_out <= L.h_out.cap && d_out <= L.d_out.cap &&
+           scratch <= L.scratch.cap;
+  }
+};
+
+int reserve_lane(dp_ctx* ctx, Lane& L, const LaneNeed& n) {
+  HIP_OK(L.h_in.reserve(n.h_in));
+  HIP_OK(L.d_in.reserve(n.d_in));
+  HIP_OK(L.h_out.reserve(n.h_out));
+  HIP_OK(L.d_out.reserve(n.d_out));
+  HIP_OK(L.scratch.reserve(n.scratch));
+  return 0;
+}
+
+// Bytes of planning storage a plan holds (a change means plan_chunk allocated).
+size_t plan_cap(const Plan& P) {
+  size_t c = P.img_off.capacity() + P.inst_off.capacity() + P.dev_off.capacity() + P.scratch_off.capacity() +
+             P.narrow.capacity() + P.direct.capacity() + P.order.capacity() + P.launches.capacity() +
+             P.skip.capacity() + P.skip_flags.capacity() + P.head.capacity() + P.cnt.capacity() + P.tmp.capacity();
+  for (const auto& b : P.big) c += b.capacity();
+  return c;
+}
+
+// A chunk that does not fit its lane's buffers grows every lane of the
+// device to its sizes (and their planning storage to its plan's), not just
+// its own: lanes are taken round-robin, so otherwise each of them would make
+// its first allocation on its first chunk, the last ones well into a serving
+// loop (or a timed region).  After the first batch of a shape no chunk on the
+// device allocates (dp_stats.allocs).  A lane with a chunk in flight is
+// finished first, since the GPU may still use its buffers.
+int grow_device_lanes(dp_ctx* ctx, Lane& L, const LaneNeed& need) {
+  if (reserve_lane(ctx, L, need)) return -1;
+  for (Lane& O : ctx->dev[(size_t)L.dev_index].lanes) {
+    if (&O == &L) continue;
+    grow_plan(O.plan, L.plan);
+    grow_vec(O.bad, L.bad.size());
+    if (need.fits(O)) continue;
+    if (finish_lane(ctx, O)) return -1;
+    if (reserve_lane(ctx, O, need)) return -1;
+  }
+  return 0;
+}
+
 // Stage and enqueue problems [p0, p0+n) of a job on lane L.
 int start_chunk(dp_ctx* ctx, Lane& L, dp_job* job, int32_t p0, int32_t n) {
   HIP_OK(hipSetDevice(L.device));
+  const int64_t allocs0 = g_buf_allocs.load(std::memory_order_relaxed);
+  const size_t bad_cap = L.bad.capacity(), plan_cap0 = plan_cap(L.plan);
   const double t0 = now_ms();
-  std::vector<uint8_t> bad((size_t)n, 0);
+  L.bad.assign((size_t)n, 0);
+  std::vector<uint8_t>& bad = L.bad;
   dp::plan_chunk(L.plan, job->rec, job->rec_off, p0, n, ctx->flags, &bad, ctx->pool);
   const double t_plan = now_ms();
   ctx->st.plan_ms += t_plan - t0;
@@ -843,12 +929,10 @@ int start_chunk(dp_ctx* ctx, Lane& L, dp_job* job, int32_t p0, int32_t n) {
   // follows the copied source range -- the staged records and the tables --
   // with `hin` the address the region's offset 0 would have.
   const size_t rest = direct ? il.img + 4 * (size_t)W : 0;
-  HIP_OK(L.h_in.reserve(il.end - rest));
+  const LaneNeed need{il.end - rest, il.end, L.ol.end, L.ol.end,
+                      (size_t)std::max<int64_t>(L.plan.scratch_words, 1) * 4};
+  if (!need.fits(L) && grow_device_lanes(ctx, L, need)) return -1;
   char* const hin = L.h_in.p - rest;  // (only offsets >= rest are used)
-  HIP_OK(L.d_in.reserve(il.end));
-  HIP_OK(L.h_out.reserve(L.ol.end));
-  HIP_OK(L.d_out.reserve(L.ol.end));
-  HIP_OK(L.scratch.reserve((size_t)std::max<int64_t>(L.plan.scratch_words, 1) * 4));
   const Plan& P = L.plan;
   if (!direct || P.n_direct < n) {  // stage the records (host pool)
     int32_t* img = at<int32_t>(hin, il.img);
@@ -909,6 +993,8 @@ int start_chunk(dp_ctx* ctx, Lane& L, dp_job* job, int32_t p0, int32_t n) {
   ctx->st.h2d_bytes += (int64_t)h2d;
   ctx->st.d2h_bytes += L.zc_out ? 0 : (int64_t)L.ol.d2h;
   ctx->st.rec_bytes += P.rec_bytes;
+  ctx->st.allocs += g_buf_allocs.load(std::memory_order_relaxed) - allocs0 + (L.bad.capacity() != bad_cap) +
+                    (plan_cap(L.plan) != plan_cap0);
   return 0;
 }
 
@@ -987,6 +1073,7 @@ dp_ctx* dp_create(const dp_opts* opts) {
     for (int li = 0; li < kLanes; ++li) {
       Lane& L = D.lanes[li];
       L.device = d;
+      L.dev_index = i;
       if (li >= kStreams) {  // lane li shares the streams of lane li % kStreams
         L.s = D.lanes[li % kStreams].s;
         L.cs = D.lanes[li % kStreams].cs;
@@ -1009,6 +1096,7 @@ dp_ctx* dp_create(const dp_opts* opts) {
   ctx->zc_in = env_i64("DEPPY_ZC_IN", 0) != 0;   // diagnostic: 1 = kernels read staged records over PCIe
   ctx->zc_out = env_i64("DEPPY_ZC_OUT", 1) != 0; // diagnostic: 0 = D2H copy of every chunk
   ctx->direct = env_i64("DEPPY_DIRECT", 1) != 0; // diagnostic: 0 = stage every chunk
+  ctx->grid_cap = (int32_t)std::max<int64_t>(0, env_i64("DEPPY_GRID_CAP", 0));
   ctx->pool = new dp::Pool(dp::host_threads());
   return ctx;
 }

@@ -31,7 +31,10 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 #include <type_traits>
+#include <utility>
 
 #include "kernel_api.hpp"
 #include "layout.hpp"
@@ -2435,23 +2438,50 @@ solve_kernel(KernelArgs a) {
   solve_item<MODE>(a, (int)blockIdx.x, lds4);
 }
 
+// Workgroups of a queued launch's kernel one CU holds at once, by (device,
+// LDS bytes): computed once per pair (the serving loop launches the same few
+// shapes chunk after chunk), with the device's CU count.
+struct GridCache {
+  std::mutex mu;
+  std::map<std::pair<int, int>, int> per_cu;
+  int cus[64] = {};
+};
+template <int MODE, int MINW>
+int resident_grid(int lds_bytes) {
+  static GridCache c;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  std::lock_guard<std::mutex> lk(c.mu);
+  if (c.cus[dev] == 0 && hipDeviceGetAttribute(&c.cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    c.cus[dev] = 0;
+  auto it = c.per_cu.find({dev, lds_bytes});
+  if (it == c.per_cu.end()) {
+    int per = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, solve_kernel<MODE, MINW>, 64 * mode_waves(MODE),
+                                                     lds_bytes) != hipSuccess)
+      per = 0;
+    it = c.per_cu.emplace(std::make_pair(dev, lds_bytes), per).first;
+  }
+  return it->second * c.cus[dev];
+}
+inline bool debug_grid() {
+  static const bool on = std::getenv("DEPPY_DEBUG_GRID") != nullptr;  // diagnostic
+  return on;
+}
+
 // Instantiate and launch one mode (included once per translation unit).
 // A queued (persistent) launch gets as many workgroups as the device holds
-// at once, at most one per item.
+// at once, at most one per item (and at most a.grid_cap when set).
 #define DP_DEFINE_MODE(MODE, MINW, NAME)                                                    \
   hipError_t NAME(const KernelArgs& a, int n_blocks, int lds_bytes, hipStream_t stream) {   \
     if (n_blocks <= 0) return hipSuccess;                                                   \
     int grid = n_blocks;                                                                    \
     if (a.queue) {                                                                          \
-      int dev = 0, cus = 0, per = 0;                                                        \
-      if (hipGetDevice(&dev) == hipSuccess &&                                               \
-          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && \
-          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (solve_kernel<MODE, MINW>),    \
-                                                       64 * mode_waves(MODE), lds_bytes) == hipSuccess && \
-          per > 0 && cus > 0)                                                               \
-        grid = per * cus < n_blocks ? per * cus : n_blocks;                                 \
-      if (std::getenv("DEPPY_DEBUG_GRID"))  /* diagnostic */                                \
-        fprintf(stderr, "solve launch mode %d: %d items, %d cus x %d per cu -> grid %d\n", MODE, n_blocks, cus, per, grid); \
+      const int res = resident_grid<MODE, MINW>(lds_bytes);                                 \
+      if (res > 0 && res < grid) grid = res;                                                \
+      if (a.grid_cap > 0 && a.grid_cap < grid) grid = a.grid_cap;                           \
+      if (debug_grid())                                                                     \
+        fprintf(stderr, "solve launch mode %d: %d items, resident %d -> grid %d\n", MODE, n_blocks, res, grid); \
     }                                                                                       \
     hipLaunchKernelGGL((solve_kernel<MODE, MINW>), dim3((unsigned)grid), dim3(64 * mode_waves(MODE)), \
                        (size_t)lds_bytes, stream, a);                                       \

@@ -405,6 +405,10 @@ typedef struct dp_stats {
   int64_t bcp_bytes; /* bytes unit propagation read (watch entries, row
                         offsets, row literals and their values), summed over
                         the problems (SURVEY.md 8(d) "BCP-visited bytes")    */
+  int64_t allocs;    /* host-side allocations dp_submit made (device / pinned
+                        buffers, planning storage).  The first chunk of a
+                        batch shape grows every lane of its device, so a
+                        serving loop's steady state makes none               */
 } dp_stats;
 int dp_get_stats(dp_ctx* ctx, dp_stats* out, int32_t reset);
 

@@ -148,10 +148,12 @@ def widen(rec_off, rec):
     return np.array(offs, np.int64), (np.concatenate(parts) if parts else np.zeros(0, np.int32))
 
 
-def compare_results(g, o, n, rec_off=None, rec=None):
-    """Bit-exact comparison of GPU and oracle dp_result dicts; returns mismatches."""
+def compare_results(g, o, n, rec_off=None, rec=None, only=None):
+    """Bit-exact comparison of GPU and oracle dp_result dicts (status, flags,
+    steps, installed bitmap, core); returns the mismatches.  only: the
+    problems to compare (default: 0..n-1)."""
     bad = []
-    for p in range(n):
+    for p in (range(n) if only is None else only):
         if g["status"][p] != o["status"][p] or g["flags"][p] != o["flags"][p] \
                 or g["steps"][p] != o["steps"][p]:
             bad.append((p, "status/flags/steps", int(g["status"][p]), int(o["status"][p]),

@@ -297,14 +297,10 @@ def test_malformed_records_are_per_problem_errors(flags):
     finally:
         c.close()
     o = oracle.solve_batch(lw.rec_off, lw.rec, 0, 16)
-    for p in range(lw.n):
-        if p in bad:
-            assert g["status"][p] == -2 and g["flags"][p] == 512 and g["core_len"][p] == 0, p
-        else:
-            assert compare_results({k: v for k, v in g.items()}, o, lw.n) is not None
+    for p in bad:
+        assert g["status"][p] == -2 and g["flags"][p] == 512 and g["core_len"][p] == 0, p
     ok = [p for p in range(lw.n) if p not in bad]
-    for k in ("status", "flags", "steps"):
-        np.testing.assert_array_equal(g[k][ok], o[k][ok])
+    assert compare_results(g, o, lw.n, only=ok) == []  # every field, installed sets and cores too
 
 
 @pytest.mark.parametrize("config,n,seed", [(2, 3000, 81), (3, 9000, 82), (5, 400, 83)])
@@ -355,8 +351,7 @@ def test_malformed_16bit_records_found_by_the_kernel(pinned):
     ok = [p for p in range(lw.n) if p not in bad]
     for p in bad:
         assert g["status"][p] == -2 and g["flags"][p] == 512 and g["core_len"][p] == 0, p
-    for k in ("status", "flags", "steps"):
-        np.testing.assert_array_equal(g[k][ok], ref[k][ok])
+    assert compare_results(g, ref, lw.n, only=ok) == []
 
 
 @pytest.mark.parametrize("config,n,seed,flags", [(2, 3000, 101, 0), (3, 9000, 102, 0), (5, 300, 103, 0),
@@ -416,8 +411,7 @@ def test_malformed_packed_records_found_by_the_kernel():
     ok = [p for p in range(lw.n) if p not in bad]
     for p in bad:
         assert g["status"][p] == -2 and g["flags"][p] == 512 and g["core_len"][p] == 0, p
-    for k in ("status", "flags", "steps"):
-        np.testing.assert_array_equal(g[k][ok], ref[k][ok])
+    assert compare_results(g, ref, lw.n, only=ok) == []
 
 
 def test_explicit_choice_packed_records_bit_exact():
@@ -464,8 +458,7 @@ def test_wide_records_direct_and_validated():
     ok = [p for p in range(b.n) if p not in bad]
     for p in bad:
         assert g["status"][p] == -2 and g["flags"][p] == 512, p
-    for k in ("status", "flags", "steps"):
-        np.testing.assert_array_equal(g[k][ok], ref[k][ok])
+    assert compare_results(g, ref, b.n, only=ok) == []
 
 
 def test_olm_scale_direct_bit_exact(ctx):
@@ -479,3 +472,135 @@ def test_olm_scale_direct_bit_exact(ctx):
     assert compare_results(gb, ga, 2) == []
     o = oracle.solve_batch(a.rec_off, a.rec, 0, 2)
     assert compare_results(gb, o, 2) == []
+
+
+# ---------------------------------------------------------------------------
+# round 3: queued grids at OLM scale, full-size config 5, plain int32
+# multi-wave records, the device-watch-list boundary
+# ---------------------------------------------------------------------------
+def test_olm_scale_queued_grid_bit_exact(monkeypatch):
+    """Config 4 through the persistent (queued) multi-wave grid with fewer
+    workgroups than catalogs (DEPPY_GRID_CAP=4): every workgroup solves
+    several catalogs in turn, re-initialising its LDS and scratch between
+    them (solve_kernel.hpp solve_kernel's queue loop).  Bit-exact with the
+    oracle, catalog by catalog."""
+    monkeypatch.setenv("DEPPY_GRID_CAP", "4")
+    n = 24
+    a = lowered_config(4, n, 171)
+    b = lowered_config(4, n, 171, narrow=True, pinned=True)
+    c = _lib.Context(0, 1)
+    try:
+        gb = c.submit(b.rec_off, b.rec).wait()
+        ga = c.solve(a.rec_off, a.rec)
+    finally:
+        c.close()
+    o = oracle.solve_batch(a.rec_off, a.rec, 0, 16)
+    assert compare_results(ga, o, n) == []
+    assert compare_results(gb, o, n) == []
+
+
+def test_olm_scale_many_catalogs_bit_exact(ctx):
+    """More config-4 catalogs than one launch holds resident (the default
+    queued grid): later catalogs are taken by workgroups that already
+    finished one."""
+    n = 600
+    a = lowered_config(4, n, 181, narrow=True, pinned=True)
+    g = ctx.submit(a.rec_off, a.rec).wait()
+    w = lowered_config(4, n, 181)
+    o = oracle.solve_batch(w.rec_off, w.rec, 0, 16)
+    assert compare_results(g, o, n) == []
+
+
+def test_config5_full_size_bit_exact(ctx):
+    """BASELINE config 5 at its bench size (10k mixed-size catalogs, half of
+    them with an injected infeasibility): every field of every catalog, cores
+    included, equals the oracle's."""
+    n = 10000
+    lw = lowered_config(5, n, 2025, packed=True, pinned=True)
+    g = ctx.submit(lw.rec_off, lw.rec).wait()
+    w = lowered_config(5, n, 2025)
+    o = oracle.solve_batch(w.rec_off, w.rec, 0, 16)
+    bad = compare_results(g, o, n)
+    assert bad == [], bad[:10]
+    assert (g["status"] == -1).sum() > n // 4
+
+
+def test_plain_int32_multiwave_records_validated_by_the_kernel():
+    """Multi-wave records of at most 2048 variables go to the device as plain
+    int32 records (DP_FMT_I32) copied as they lie; the kernel checks them
+    (valid_wide) before building their watch lists.  A clause literal past
+    2nv, decreasing clause offsets and an AtMost variable past nv each give
+    DP_ERROR + DP_F_MALFORMED for that problem only; the rest stay exact."""
+    a = lowered_config(5, 160, 191)
+    b = lowered_config(5, 160, 191, packed=True, pinned=True)
+    plain = [p for p in range(b.n) if b.rec[b.rec_off[p] + 13] == 0]
+    assert len(plain) >= 3
+    ref = oracle.solve_batch(a.rec_off, a.rec, 0, 16)
+    bad = plain[:3]
+    for p, kind in zip(bad, ("lit", "off", "card")):
+        r = b.rec[b.rec_off[p]:b.rec_off[p + 1]]
+        nv, nc, nk, ncl = int(r[1]), int(r[2]), int(r[3]), int(r[7])
+        if kind == "lit":
+            r[16 + nc + 1] = 2 * nv + 1
+        elif kind == "off":
+            r[16 + 1] = r[16 + 2] + 1
+        else:
+            assert nk > 0
+            r[16 + nc + 1 + ncl + nc + nk + 1] = nv + 3
+    c = _lib.Context(0, 1)
+    try:
+        g = c.submit(b.rec_off, b.rec).wait()
+        assert c.stats()["direct_chunks"] > 0
+    finally:
+        c.close()
+    for p in bad:
+        assert g["status"][p] == -2 and g["flags"][p] == 512 and g["core_len"][p] == 0, p
+    ok = [p for p in range(b.n) if p not in bad]
+    assert compare_results(g, ref, b.n, only=ok) == []
+
+
+def chain_catalog(n_vars, seed):
+    """A catalog of exactly n_vars variables (layout.hpp DEV_WATCH_VARS
+    boundary tests): packages of 9 versions newest first, each version
+    depending on a version range of a later package, one uniqueness AtMost
+    per package, and required variables for the rest of the count."""
+    rng = np.random.default_rng(seed)
+    n_pkg = (n_vars - 8) // 10
+    req = n_vars - 10 * n_pkg
+    names = [["p%d-v%d" % (p, 8 - i) for i in range(9)] for p in range(n_pkg)]
+    out = []
+    for p in range(n_pkg):
+        for i in range(9):
+            cons = []
+            if p + 1 < n_pkg and rng.random() < 0.5:
+                q = int(rng.integers(p + 1, min(n_pkg, p + 4)))
+                lo = int(rng.integers(0, 9))
+                cons.append(sat.Dependency(*names[q][lo:min(9, lo + int(rng.integers(1, 4)))]))
+            if rng.random() < 0.05 and p > 0:
+                cons.append(sat.Conflict(names[int(rng.integers(0, p))][int(rng.integers(0, 9))]))
+            out.append(V(names[p][i], *cons))
+        out.append(V("u%d" % p, sat.AtMost(1, *names[p])))
+    for r in range(req):
+        p = int(rng.integers(0, n_pkg))
+        out.append(V("req%d" % r, sat.Mandatory(), sat.Dependency(*names[p])))
+    assert len(out) == n_vars
+    return out
+
+
+@pytest.mark.parametrize("flags", [_lib.OPT_FORCE_GROUP, _lib.OPT_FORCE_MID], ids=["split", "split4"])
+def test_device_watch_boundary_bit_exact(flags):
+    """Catalogs of 2047, 2048 and 2049 variables on the multi-wave paths:
+    up to 2048 the kernel builds the watch lists (2nv+1 counters in the LDS
+    work area), above it the host does (DP_FMT_I32W).  Bit-exact with the
+    oracle on both sides of the boundary."""
+    probs = [chain_catalog(nv, 7 + nv) for nv in (2047, 2048, 2049)]
+    lw = _lib.Lowered(sat.encode_inputs(probs))
+    assert [int(lw.record(p)[1]) for p in range(3)] == [2047, 2048, 2049]
+    c = _lib.Context(0, 1, flags=flags)
+    try:
+        g = c.solve(lw.rec_off, lw.rec)
+    finally:
+        c.close()
+    o = oracle.solve_batch(lw.rec_off, lw.rec, 0, 3)
+    assert compare_results(g, o, 3) == []
+    assert (g["status"] != -2).all()
