@@ -65,6 +65,9 @@ WORKLOADS = {
                    "chains), one 8-wave workgroup per catalog"),
     5: (10000, 80000, "config5: %d mixed-size catalogs per step (P~U{4..400}, 50%% with injected "
                       "infeasibility), UNSAT-heavy"),
+    6: (10000, 80000, "config6: %d problems per step shaped like the reference's BenchmarkInput "
+                      "(pkg/sat/bench_test.go:10-64: 256 variables, 10%% Mandatory, 15%% one Dependency "
+                      "of 1-5, 5%% 1-2 Conflicts; SplitMix64 draws, not Go's math/rand)"),
 }
 
 
@@ -95,6 +98,56 @@ def maybe_relaunch(args) -> None:
     sys.exit(subprocess.call(cmd, env=env))
 
 
+FORMS = {0: "I32", 1: "U16", 3: "P16", 4: "I32W", 5: "P16D"}
+
+
+def record_forms(lw) -> dict:
+    """Records per form (include/deppy_hip.h DP_H_FMT) of a lowered batch."""
+    if lw.n == 0:
+        return {}
+    f, c = np.unique(lw.rec[lw.rec_off[:-1] + 13], return_counts=True)
+    return {FORMS.get(int(a), str(int(a))): int(b) for a, b in zip(f, c)}
+
+
+def end_to_end(ctx, wa, n, steps, depth=2):
+    """Wire format -> results, what the reference's BenchmarkSolve times per
+    problem (NewSolver(WithInput(...)) + Solve, pkg/sat/bench_test.go:66-77):
+    each step lowers the batch (dp_lower_into into page-locked packed
+    records, the host pool) and submits it; `depth` batches in flight, so the
+    GPU solves batch i while the host lowers batch i+1."""
+    from deppy_amd import _lib
+    lws = [_lib.Lowered(wa, narrow=True, pinned=True, packed=True) for _ in range(depth)]
+    outs = [_lib.result_arrays(x.rec_off, x.rec) for x in lws]
+
+    def run(k):
+        jobs = []
+        for i in range(k):
+            j = i % depth
+            if len(jobs) == depth:
+                jobs.pop(0).wait()
+            lws[j].relower(wa)
+            jobs.append(ctx.submit(lws[j].rec_off, lws[j].rec, outs[j]))
+        for job in jobs:
+            job.wait()
+
+    run(depth)
+    t0 = time.perf_counter()
+    run(steps)
+    return n * steps / (time.perf_counter() - t0)
+
+
+def cpu_end_to_end(wa, lw32, n, threads, seconds):
+    """The same on the CPU: lowering to int32 records + the oracle's solve, one
+    solver thread per core, for a bounded time."""
+    from oracle import oracle
+    reps, t0 = 0, time.perf_counter()
+    while reps < 1 or time.perf_counter() - t0 < seconds:
+        lw32.relower(wa)
+        oracle.solve_batch(lw32.rec_off, lw32.rec, 0, threads)
+        reps += 1
+    return reps * n / (time.perf_counter() - t0)
+
+
 def lowered_config(config, n, seed):
     """The batch lowered twice: in the packed 16-bit form into page-locked
     memory (dp_lower_into DP_LOWER_NARROW | DP_LOWER_PACKED | DP_LOWER_PINNED,
@@ -113,7 +166,7 @@ def lowered_config(config, n, seed):
         lw.relower(wa)
         reps += 1
     t_lower = (time.perf_counter() - t0) / reps
-    return lw, lw32, t_lower
+    return lw, lw32, t_lower, wa
 
 
 def output_bytes(res) -> int:
@@ -165,6 +218,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--kernel-steps", type=int, default=20,
                     help="steps of the device-resident (kernel-only) secondary figure; 0: skip")
+    ap.add_argument("--e2e-steps", type=int, default=10,
+                    help="steps of the lowering-inclusive (wire -> results) secondary figure; 0: skip")
     ap.add_argument("--kernel-only", action="store_true",
                     help="skip the host-to-host leg (profiling runs of the solve kernel)")
     ap.add_argument("--flags", type=int, default=0,
@@ -189,7 +244,7 @@ def main():
         total = args.problems or wl[1]
         lo, hi = shard.strong_range(total, rank, world)
         n, first = hi - lo, args.seed + lo
-    lw, lw32, t_lower = lowered_config(args.config, n, first)
+    lw, lw32, t_lower, wa = lowered_config(args.config, n, first)
     ctx = _lib.Context(local, 1, flags=args.flags)
 
     # host-to-host: depth jobs in flight, each the whole batch.  The pipeline
@@ -247,7 +302,7 @@ def main():
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic",
-        "config": {"workload": wl[2] % n, "catalogs_per_step_per_gpu": n,
+        "config": {"workload": wl[2] % n, "catalogs_per_step_per_gpu": n, "record_forms": record_forms(lw),
                    "parallelism": "dp%d (host partition)" % world, "seed": args.seed,
                    "path": "host memory -> host memory (dp_submit/dp_job_wait), %d jobs in flight" % depth},
         "pipeline": {"chunks_per_step": round(chunks / args.steps, 2),
@@ -269,6 +324,13 @@ def main():
         "host_lowering_res_per_s": round(n / t_lower, 1),
         "host_lowering_note": "dp_lower_into (packed 16-bit records, storage reused) on the host pool; not in value",
     }
+    if not args.kernel_only and args.e2e_steps > 0:
+        line["end_to_end"] = {
+            "res_per_s": round(end_to_end(ctx, wa, n, args.e2e_steps), 1),
+            "steps": args.e2e_steps,
+            "note": "wire format -> dp_lower_into -> dp_submit/dp_job_wait -> results, 2 batches in flight "
+                    "(lowering of batch i+1 overlaps the solve of batch i); what BenchmarkSolve times "
+                    "(NewSolver(WithInput)+Solve, bench_test.go:66-77); not value"}
 
     if args.kernel_steps > 0:
         # the solve kernel alone, records resident in HBM (dp_upload): serial
@@ -362,6 +424,11 @@ def main():
                                           "nproc %s, affinity %d, cgroup quota %s"
                                           % (n, reps, cpu_t, share["nproc"], share["affinity"],
                                              share["cgroup_quota"])}
+        if "end_to_end" in line:
+            line["end_to_end"]["cpu_res_per_s"] = round(cpu_end_to_end(wa, lw32, n, threads, 3.0), 1)
+            line["end_to_end"]["cpu_note"] = ("dp_lower_into to int32 records + oracle/sat_oracle.c, %d threads "
+                                              "(the lowering is the product's C++; the reference lowers in Go)"
+                                              % threads)
         line["verified_bit_exact_vs_oracle"] = bool(ok)
         line["verified_note"] = "GPU on the packed 16-bit records vs oracle on the int32 records, every field incl. cores"
     if rank == 0:

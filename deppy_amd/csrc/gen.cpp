@@ -17,6 +17,12 @@
 // the problems get an injected infeasibility (half BCP-level, half search-level);
 // config 4 (OLM-scale): P = 5000, n_q ~ U{5..15} (V ~ 55k), Dependency targets
 // only in packages (q, q+8] (deep chains), R = 50.
+// config 6: the shape of the reference's own benchmark input, BenchmarkInput
+// (pkg/sat/bench_test.go:10-64): 256 variables "0".."255", each with p = 0.1
+// Mandatory, with p = 0.15 one Dependency on 1-5 random other variables, with
+// p = 0.05 1-2 Conflicts with random other variables, in that constraint
+// order (the draws come from SplitMix64, not Go's math/rand, so the problems
+// are of the same distribution, not the same problems).
 #include <algorithm>
 #include <cstring>
 #include <string>
@@ -73,7 +79,37 @@ struct Builder {
 
 std::string bname(int q, int v) { return "p" + std::to_string(q) + "-v" + std::to_string(v); }
 
+// bench_test.go:10-64 (BenchmarkInput), distribution for distribution.
+void gen_bench_input(Builder& B, uint64_t seed) {
+  SplitMix64 r(seed);
+  constexpr int length = 256, nDependency = 6, nConflict = 3;
+  auto other = [&](int i) {
+    int y = i;
+    while (y == i) y = (int)r.uniform(0, length - 1);
+    return std::to_string(y);
+  };
+  for (int i = 0; i < length; ++i) {
+    B.var(std::to_string(i));
+    if (r.bernoulli(0.1)) B.con(DP_MANDATORY, 0, {});
+    if (r.bernoulli(0.15)) {
+      const int n = (int)r.uniform(0, nDependency - 2) + 1;  // rand.Intn(nDependency-1) + 1
+      std::vector<std::string> d;
+      for (int x = 0; x < n; ++x) d.push_back(other(i));
+      B.con(DP_DEPENDENCY, 0, d);
+    }
+    if (r.bernoulli(0.05)) {
+      const int n = (int)r.uniform(0, nConflict - 2) + 1;  // rand.Intn(nConflict-1) + 1
+      for (int x = 0; x < n; ++x) B.con(DP_CONFLICT, 0, {other(i)});
+    }
+  }
+  B.end_problem();
+}
+
 void gen_problem(Builder& B, int config, uint64_t seed) {
+  if (config == 6) {
+    gen_bench_input(B, seed);
+    return;
+  }
   SplitMix64 r(seed);
   int P = config == 2 ? 40 : config == 3 ? (int)r.uniform(4, 12) : config == 4 ? 5000 : (int)r.uniform(4, 400);
   const int vlo = config == 4 ? 5 : 1, vhi = config == 4 ? 15 : 9;
@@ -175,8 +211,8 @@ struct dp_gen {
 extern "C" {
 
 dp_gen* dp_gen_catalogs(int32_t config, int32_t n_problems, uint64_t base_seed) {
-  if (config < 2 || config > 5) {
-    dp::set_global_error("dp_gen_catalogs: config must be 2, 3, 4 or 5");
+  if (config < 2 || config > 6) {
+    dp::set_global_error("dp_gen_catalogs: config must be 2, 3, 4, 5 or 6");
     return nullptr;
   }
   if (n_problems < 0) return nullptr;

@@ -482,7 +482,9 @@ int dp_last_kernel_ms(const dp_ctx* ctx, double* ms);
 
 /* Configurations of BASELINE.json: 2 = ~200-entity catalogs, 3 = small
  * (P~U{4..12}), 4 = OLM-scale (P=5000, V~55k, deep chains), 5 = mixed-size
- * UNSAT-heavy.  seed_i = base_seed + i. */
+ * UNSAT-heavy; 6 = the distribution of the reference's BenchmarkInput
+ * (pkg/sat/bench_test.go:10-64: 256 variables, 10% Mandatory, 15% one
+ * Dependency of 1-5 candidates, 5% 1-2 Conflicts).  seed_i = base_seed + i. */
 typedef struct dp_gen dp_gen; /* owns a dp_wire and its arrays */
 dp_gen* dp_gen_catalogs(int32_t config, int32_t n_problems, uint64_t base_seed);
 const dp_wire* dp_gen_wire(const dp_gen* g);
