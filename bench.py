@@ -419,11 +419,14 @@ def main():
         cpu_t = time.perf_counter() - t0
         line["cpu_baseline"] = {"value": round(reps * n / cpu_t, 1), "unit": "resolutions/s",
                                 "cores": threads, "kind": "port",
+                                "node_cores": threads * world,
+                                "node_value_linear": round(reps * n / cpu_t * world, 1),
                                 "sample": "the timed batch (%d catalogs) solved %d times by "
                                           "oracle/sat_oracle.c, one solver thread per core (%.1f s); "
-                                          "nproc %s, affinity %d, cgroup quota %s"
+                                          "nproc %s, affinity %d, cgroup quota %s; node_cores = this share "
+                                          "x %d ranks (each rank's share), node_value_linear = value x ranks"
                                           % (n, reps, cpu_t, share["nproc"], share["affinity"],
-                                             share["cgroup_quota"])}
+                                             share["cgroup_quota"], world)}
         if "end_to_end" in line:
             line["end_to_end"]["cpu_res_per_s"] = round(cpu_end_to_end(wa, lw32, n, threads, 3.0), 1)
             line["end_to_end"]["cpu_note"] = ("dp_lower_into to int32 records + oracle/sat_oracle.c, %d threads "

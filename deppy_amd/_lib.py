@@ -397,6 +397,9 @@ class Job:
         self.n = len(rec_off) - 1
         self.out = out if out is not None else result_arrays(rec_off, rec)
         self._res = _result_struct(self.out)
+        # the device's worker thread reads the batch after dp_submit returns:
+        # the arrays (possibly converted copies) live as long as the job
+        self._batch_arrays = (rec_off, rec)
         h = ctypes.c_void_p()
         if lib().dp_submit(ctx.h, ctypes.byref(_batch(rec_off, rec)), ctypes.byref(self._res),
                            ctypes.byref(h)) != 0:
@@ -407,7 +410,9 @@ class Job:
         h, self.h = self.h, None
         if h is None:
             raise RuntimeError("dp_job_wait: job already waited")
-        if lib().dp_job_wait(self.ctx.h, h) != 0:
+        rc = lib().dp_job_wait(self.ctx.h, h)
+        self._batch_arrays = None
+        if rc != 0:
             raise RuntimeError("dp_job_wait: " + self.ctx.error())
         out = dict(self.out)
         for k in ("status", "flags", "core_len", "steps"):

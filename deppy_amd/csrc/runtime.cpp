@@ -30,6 +30,7 @@
 #include <chrono>
 #include <climits>
 #include <condition_variable>
+#include <deque>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
@@ -686,13 +687,34 @@ struct Lane {
   Plan plan;
   OutLayout ol{};
   std::vector<uint8_t> bad;  // per-problem malformed marks of the chunk being started
-  int dev_index = 0;         // its Device in dp_ctx::dev
 };
 
+// One piece of a submitted job for a device's worker: problems [p0, p0+n).
+struct Task {
+  dp_job* job;
+  int32_t p0, n;
+};
+
+// A device of the context.  Its pipeline lanes belong to one host worker
+// thread (worker_main): dp_submit only cuts a batch into chunks and queues
+// them here, so a caller thread never plans, stages, waits or scatters, and
+// every device of a multi-device context has its own submitting thread.
 struct Device {
   int ordinal = 0;
   Lane lanes[kLanes];
   int next = 0;  // resident launches: next lane
+  // -- the worker's --
+  std::thread worker;
+  std::mutex qmu;                 // q and stop (and the wake-ups)
+  std::condition_variable qcv;
+  std::deque<Task> q;             // chunks waiting for a lane
+  bool stop = false;
+  int cursor = 0;                 // next lane (round robin)
+  std::deque<Lane*> inflight;     // lanes holding a chunk, oldest first (worker only)
+  dp::Pool* pool = nullptr;       // staging and planning threads of this device
+  bool own_pool = false;
+  std::mutex smu;                 // st
+  dp_stats st{};                  // this device's pipeline counters
 };
 
 struct dp_job {
@@ -701,27 +723,31 @@ struct dp_job {
   const int64_t* rec_off = nullptr;
   bool pinned = false;  // the records are page-locked (pinned_range)
   dp_result res{};
-  int pending = 0;  // chunks in flight
+  // completion: chunks not yet delivered; the waiter sleeps on cv
+  std::mutex m;
+  std::condition_variable cv;
+  int chunks_left = 0;
+  std::atomic<bool> waiting{false};  // dp_job_wait is blocked on it: its chunks are finished eagerly
   int rc = 0;
   std::string err;
 };
 
 struct dp_ctx {
-  std::vector<Device> dev;
+  std::deque<Device> dev;  // (a deque: a Device holds a thread and mutexes, it never moves)
   int64_t budget = kDefaultBudget;
   int32_t flags = 0;  // dp_opt_flag
   std::string err;
-  double last_ms = 0.0;
+  std::atomic<double> last_ms{0.0};
   std::mutex mu;
   dp::Pool* pool = nullptr;
-  int next_lane = 0;  // pipeline cursor over (device, lane)
+  int next_dev = 0;  // pipeline cursor over devices (under mu)
   bool zc_in = false, zc_out = true;  // zero-copy records / results (start_chunk)
   bool copy_streams = false;          // records' H2D on a stream of its own (DEPPY_COPY_STREAM=1)
   bool direct = true;  // copy page-locked batches of staged-form records as they are
   int32_t chunk_problems = kChunkProblems;
   int64_t chunk_bytes = kChunkBytes;
   int32_t grid_cap = 0;  // test: workgroups of a queued launch (DEPPY_GRID_CAP; 0 = resident maximum)
-  dp_stats st{};
+  dp_stats st{};         // the caller-thread paths (resident batches)
   ~dp_ctx() { delete pool; }
 };
 
@@ -750,19 +776,46 @@ struct dp_resident {
 
 namespace {
 
+// The failing call's text, per thread (a device worker reports it to the
+// job, an API function to ctx->err through api_fail).
+thread_local std::string t_err;
 #define HIP_OK(expr)                                                         \
   do {                                                                       \
     hipError_t e_ = (expr);                                                  \
     if (e_ != hipSuccess) {                                                  \
+      (void)ctx;                                                             \
+      t_err = std::string(#expr) + ": " + hipGetErrorString(e_);             \
+      return -1;                                                             \
+    }                                                                        \
+  } while (0)
+int api_fail(dp_ctx* ctx) {
+  ctx->err = t_err;
+  return -1;
+}
+// HIP_OK in an API function on the caller's thread: the text to ctx->err.
+#define API_OK(expr)                                                         \
+  do {                                                                       \
+    if (hipError_t e_ = (expr); e_ != hipSuccess) {                          \
       ctx->err = std::string(#expr) + ": " + hipGetErrorString(e_);          \
       return -1;                                                             \
     }                                                                        \
   } while (0)
 
+void add_stats(dp_stats& a, const dp_stats& b) {
+  a.problems += b.problems; a.chunks += b.chunks; a.launches += b.launches; a.kernel_ms += b.kernel_ms;
+  a.h2d_bytes += b.h2d_bytes; a.d2h_bytes += b.d2h_bytes; a.rec_bytes += b.rec_bytes; a.stage_ms += b.stage_ms;
+  a.plan_ms += b.plan_ms; a.wait_ms += b.wait_ms; a.scatter_ms += b.scatter_ms; a.direct_chunks += b.direct_chunks;
+  a.bcp_bytes += b.bcp_bytes; a.allocs += b.allocs;
+}
+void add_device_stats(Device& D, const dp_stats& b) {
+  std::lock_guard<std::mutex> lk(D.smu);
+  add_stats(D.st, b);
+}
+
 // Enqueue a planned chunk's launches on stream s.
 // Multi-wave launches take their items from a queue (kernel_api.hpp
 // KernelArgs::queue) in the scratch's first words, zeroed here.
-int enqueue_launches(dp_ctx* ctx, const Plan& P, const dp::KernelArgs& base, hipStream_t s) {
+int enqueue_launches(dp_ctx* ctx, const Plan& P, const dp::KernelArgs& base, hipStream_t s, dp_stats& st) {
   static const bool no_queue = [] {  // diagnostic DEPPY_NO_QUEUE=1: one workgroup per item
     const char* e = std::getenv("DEPPY_NO_QUEUE");
     return e && *e && *e != '0';
@@ -781,39 +834,61 @@ int enqueue_launches(dp_ctx* ctx, const Plan& P, const dp::KernelArgs& base, hip
       ++q;
     }
     HIP_OK(dp::launch_solve(a, L.mode, L.count, L.lds, s));
-    ctx->st.launches++;
+    st.launches++;
   }
   return 0;
 }
 
-// Wait for a lane's chunk and deliver its results to its job.
-int finish_lane(dp_ctx* ctx, Lane& L) {
+// Wait for a lane's chunk and scatter its results into its job's dp_result
+// (the job's bookkeeping is deliver()'s).
+int finish_lane(dp_ctx* ctx, Device& D, Lane& L) {
   if (!L.job) return 0;
   dp_job* job = L.job;
   L.job = nullptr;
-  job->pending--;
+  dp_stats st{};
   HIP_OK(hipSetDevice(L.device));
   const double t0 = now_ms();
   HIP_OK(hipEventSynchronize(L.done));
   const double t1 = now_ms();
-  ctx->st.wait_ms += t1 - t0;
+  st.wait_ms += t1 - t0;
   float ms = 0.f;
   if (!L.plan.launches.empty() && hipEventElapsedTime(&ms, L.k0, L.k1) == hipSuccess) {
-    ctx->st.kernel_ms += ms;
-    ctx->last_ms = ms;
+    st.kernel_ms += ms;
+    ctx->last_ms.store(ms);
   }
   const int32_t used = L.zc_out ? 0 : *at<int32_t>(L.h_out.p, L.ol.pool_len);
   const size_t need = L.ol.pool + (size_t)used * 4;
   if (!L.zc_out && need > L.ol.d2h) {  // cores beyond the pipelined window
     HIP_OK(hipMemcpyAsync(L.h_out.p + L.ol.d2h, L.d_out.p + L.ol.d2h, need - L.ol.d2h, hipMemcpyDeviceToHost, L.s));
     HIP_OK(hipStreamSynchronize(L.s));
-    ctx->st.d2h_bytes += (int64_t)(need - L.ol.d2h);
+    st.d2h_bytes += (int64_t)(need - L.ol.d2h);
   }
   scatter(L.plan, L.ol, L.h_out.p, L.p0, &job->res);
   const dp::ProblemOut* po = at<dp::ProblemOut>(L.h_out.p, L.ol.prob);
-  for (int32_t i = 0; i < L.plan.n; ++i) ctx->st.bcp_bytes += (int64_t)po[i].bcp;
-  ctx->st.scatter_ms += now_ms() - t1;
+  for (int32_t i = 0; i < L.plan.n; ++i) st.bcp_bytes += (int64_t)po[i].bcp;
+  st.scatter_ms += now_ms() - t1;
+  add_device_stats(D, st);
   return 0;
+}
+
+// One chunk of `job` is over (delivered, failed or skipped).
+void chunk_done(dp_job* job, int rc) {
+  std::lock_guard<std::mutex> lk(job->m);
+  if (rc && !job->rc) {
+    job->rc = rc;
+    job->err = t_err;
+  }
+  if (--job->chunks_left == 0) job->cv.notify_all();
+}
+
+// Finish lane L (on its device's worker) and account its chunk to its job.
+void deliver(dp_ctx* ctx, Device& D, Lane& L) {
+  dp_job* job = L.job;
+  if (!job) return;
+  auto it = std::find(D.inflight.begin(), D.inflight.end(), &L);
+  if (it != D.inflight.end()) D.inflight.erase(it);
+  const int rc = finish_lane(ctx, D, L);
+  chunk_done(job, rc);
 }
 
 // Planning storage of `dst` grown to (at least) the sizes `src` uses, with
@@ -877,30 +952,31 @@ size_t plan_cap(const Plan& P) {
 // loop (or a timed region).  After the first batch of a shape no chunk on the
 // device allocates (dp_stats.allocs).  A lane with a chunk in flight is
 // finished first, since the GPU may still use its buffers.
-int grow_device_lanes(dp_ctx* ctx, Lane& L, const LaneNeed& need) {
+int grow_device_lanes(dp_ctx* ctx, Device& D, Lane& L, const LaneNeed& need) {
   if (reserve_lane(ctx, L, need)) return -1;
-  for (Lane& O : ctx->dev[(size_t)L.dev_index].lanes) {
+  for (Lane& O : D.lanes) {
     if (&O == &L) continue;
     grow_plan(O.plan, L.plan);
     grow_vec(O.bad, L.bad.size());
     if (need.fits(O)) continue;
-    if (finish_lane(ctx, O)) return -1;
+    deliver(ctx, D, O);  // (an error of its chunk goes to that chunk's job)
     if (reserve_lane(ctx, O, need)) return -1;
   }
   return 0;
 }
 
 // Stage and enqueue problems [p0, p0+n) of a job on lane L.
-int start_chunk(dp_ctx* ctx, Lane& L, dp_job* job, int32_t p0, int32_t n) {
+int start_chunk(dp_ctx* ctx, Device& D, Lane& L, dp_job* job, int32_t p0, int32_t n) {
   HIP_OK(hipSetDevice(L.device));
+  dp_stats st{};
   const int64_t allocs0 = g_buf_allocs.load(std::memory_order_relaxed);
   const size_t bad_cap = L.bad.capacity(), plan_cap0 = plan_cap(L.plan);
   const double t0 = now_ms();
   L.bad.assign((size_t)n, 0);
   std::vector<uint8_t>& bad = L.bad;
-  dp::plan_chunk(L.plan, job->rec, job->rec_off, p0, n, ctx->flags, &bad, ctx->pool);
+  dp::plan_chunk(L.plan, job->rec, job->rec_off, p0, n, ctx->flags, &bad, D.pool);
   const double t_plan = now_ms();
-  ctx->st.plan_ms += t_plan - t0;
+  st.plan_ms += t_plan - t0;
   // Direct: records already in their staged form (16-bit, on a 16-byte
   // boundary; dp_lower_into DP_LOWER_NARROW) in page-locked memory are
   // copied to the device from where they lie: the chunk's source range goes
@@ -931,19 +1007,19 @@ int start_chunk(dp_ctx* ctx, Lane& L, dp_job* job, int32_t p0, int32_t n) {
   const size_t rest = direct ? il.img + 4 * (size_t)W : 0;
   const LaneNeed need{il.end - rest, il.end, L.ol.end, L.ol.end,
                       (size_t)std::max<int64_t>(L.plan.scratch_words, 1) * 4};
-  if (!need.fits(L) && grow_device_lanes(ctx, L, need)) return -1;
+  if (!need.fits(L) && grow_device_lanes(ctx, D, L, need)) return -1;
   char* const hin = L.h_in.p - rest;  // (only offsets >= rest are used)
   const Plan& P = L.plan;
   if (!direct || P.n_direct < n) {  // stage the records (host pool)
     int32_t* img = at<int32_t>(hin, il.img);
-    ctx->pool->run(n, [&](int64_t i) {
+    D.pool->run(n, [&](int64_t i) {
       if (direct && P.direct[(size_t)i]) return;
       if (!dp::stage_one(P, job->rec, job->rec_off, p0, (int32_t)i, img)) bad[(size_t)i] = 1;
-    }, dp::stage_block(n, *ctx->pool));
+    }, dp::stage_block(n, *D.pool));
     // (records found malformed while staging are reported by the kernel)
   }
   fill_in_tables(P, il, hin);
-  ctx->st.stage_ms += now_ms() - t_plan;
+  st.stage_ms += now_ms() - t_plan;
   // Zero-copy results: the kernels write their results straight into the
   // lane's mapped pinned buffer.  With a D2H copy per chunk instead, copies
   // from every stream queue on the same copy engine: a chunk's H2D waited
@@ -967,7 +1043,7 @@ int start_chunk(dp_ctx* ctx, Lane& L, dp_job* job, int32_t p0, int32_t n) {
       HIP_OK(hipMemcpyAsync(L.d_in.p + il.img, job->rec + job->rec_off[p0], src_bytes, hipMemcpyHostToDevice, cs));
     HIP_OK(hipMemcpyAsync(L.d_in.p + rest, L.h_in.p, il.end - rest, hipMemcpyHostToDevice, cs));
     h2d = src_bytes + il.end - rest;
-    ctx->st.direct_chunks++;
+    st.direct_chunks++;
   } else if (!zc_in) {
     HIP_OK(hipMemcpyAsync(L.d_in.p, L.h_in.p, il.end, hipMemcpyHostToDevice, cs));
     h2d = il.end;
@@ -981,20 +1057,20 @@ int start_chunk(dp_ctx* ctx, Lane& L, dp_job* job, int32_t p0, int32_t n) {
   a.core_pool_len = at<int32_t>(L.d_out.p, L.ol.pool_len);
   a.items = at<dp::WorkItem>(din, il.items);
   HIP_OK(hipEventRecord(L.k0, L.s));
-  if (enqueue_launches(ctx, P, a, L.s)) return -1;
+  if (enqueue_launches(ctx, P, a, L.s, st)) return -1;
   HIP_OK(hipEventRecord(L.k1, L.s));
   if (!L.zc_out) HIP_OK(hipMemcpyAsync(L.h_out.p, L.d_out.p, L.ol.d2h, hipMemcpyDeviceToHost, L.s));
   HIP_OK(hipEventRecord(L.done, L.s));
   L.job = job;
   L.p0 = p0;
-  job->pending++;
-  ctx->st.chunks++;
-  ctx->st.problems += n;
-  ctx->st.h2d_bytes += (int64_t)h2d;
-  ctx->st.d2h_bytes += L.zc_out ? 0 : (int64_t)L.ol.d2h;
-  ctx->st.rec_bytes += P.rec_bytes;
-  ctx->st.allocs += g_buf_allocs.load(std::memory_order_relaxed) - allocs0 + (L.bad.capacity() != bad_cap) +
-                    (plan_cap(L.plan) != plan_cap0);
+  st.chunks++;
+  st.problems += n;
+  st.h2d_bytes += (int64_t)h2d;
+  st.d2h_bytes += L.zc_out ? 0 : (int64_t)L.ol.d2h;
+  st.rec_bytes += P.rec_bytes;
+  st.allocs += g_buf_allocs.load(std::memory_order_relaxed) - allocs0 + (L.bad.capacity() != bad_cap) +
+               (plan_cap(L.plan) != plan_cap0);
+  add_device_stats(D, st);
   return 0;
 }
 
@@ -1007,31 +1083,78 @@ int32_t next_chunk(const int64_t* rec_off, int32_t p, int32_t P, int32_t chunk_p
   return q;
 }
 
-Lane& lane_at(dp_ctx* ctx, int k) {
-  const int nd = (int)ctx->dev.size();
-  return ctx->dev[(size_t)(k % nd)].lanes[(k / nd) % kLanes];
+// Start task t on the device's next lane (delivering the chunk that lane
+// holds first).  A job that already failed skips its later chunks.
+void run_task(dp_ctx* ctx, Device& D, const Task& t) {
+  dp_job* job = t.job;
+  bool failed;
+  {
+    std::lock_guard<std::mutex> lk(job->m);
+    failed = job->rc != 0;
+  }
+  if (failed) {
+    chunk_done(job, 0);
+    return;
+  }
+  Lane& L = D.lanes[D.cursor];
+  D.cursor = (D.cursor + 1) % kLanes;
+  deliver(ctx, D, L);
+  if (start_chunk(ctx, D, L, job, t.p0, t.n)) {
+    L.job = nullptr;
+    chunk_done(job, -1);
+    return;
+  }
+  D.inflight.push_back(&L);
 }
 
-int submit_locked(dp_ctx* ctx, dp_job* job) {
+// A device's submitting thread: starts queued chunks on its lanes in order,
+// and in between delivers finished chunks, oldest first -- at once when a
+// waiter is blocked on their job, else when their `done` event has fired
+// (polled every 50 us while chunks are in flight).  Exits once stopped and
+// drained.
+void worker_main(dp_ctx* ctx, Device* Dp) {
+  Device& D = *Dp;
+  (void)hipSetDevice(D.ordinal);
+  std::unique_lock<std::mutex> lk(D.qmu);
+  for (;;) {
+    if (!D.q.empty()) {
+      const Task t = D.q.front();
+      D.q.pop_front();
+      lk.unlock();
+      run_task(ctx, D, t);
+      lk.lock();
+      continue;
+    }
+    if (!D.inflight.empty()) {
+      Lane* o = D.inflight.front();
+      const bool now = D.stop || o->job->waiting.load(std::memory_order_acquire) ||
+                       hipEventQuery(o->done) != hipErrorNotReady;
+      if (now) {
+        lk.unlock();
+        deliver(ctx, D, *o);
+        lk.lock();
+      } else {
+        D.qcv.wait_for(lk, std::chrono::microseconds(50));
+      }
+      continue;
+    }
+    if (D.stop) return;
+    D.qcv.wait(lk);
+  }
+}
+
+// The chunks of a batch: at most chunk_problems problems and chunk_bytes
+// record bytes each, and (several devices) at least one per device.
+void cut_chunks(const dp_ctx* ctx, const dp_job* job, std::vector<std::pair<int32_t, int32_t>>& out) {
   const int32_t P = job->n;
-  int32_t p = 0;
-  while (p < P) {
-    const int32_t q = next_chunk(job->rec_off, p, P, ctx->chunk_problems, ctx->chunk_bytes);
-    Lane& L = lane_at(ctx, ctx->next_lane++);
-    if (ctx->next_lane >= (int)ctx->dev.size() * kLanes) ctx->next_lane = 0;
-    if (finish_lane(ctx, L)) return -1;
-    if (start_chunk(ctx, L, job, p, q - p)) return -1;
-    if (job->rc) return 0;
+  const int nd = (int)ctx->dev.size();
+  int32_t cp = ctx->chunk_problems;
+  if (nd > 1 && P >= nd) cp = std::min<int32_t>(cp, (P + nd - 1) / nd);
+  for (int32_t p = 0; p < P;) {
+    const int32_t q = next_chunk(job->rec_off, p, P, cp, ctx->chunk_bytes);
+    out.emplace_back(p, q - p);
     p = q;
   }
-  return 0;
-}
-
-int wait_job_locked(dp_ctx* ctx, dp_job* job) {
-  for (auto& D : ctx->dev)
-    for (auto& L : D.lanes)
-      if (job->pending > 0 && L.job == job && finish_lane(ctx, L)) return -1;
-  return 0;
 }
 
 }  // namespace
@@ -1052,7 +1175,7 @@ dp_ctx* dp_create(const dp_opts* opts) {
     return nullptr;
   }
   auto* ctx = new dp_ctx;
-  ctx->dev.resize((size_t)cnt);
+  for (int i = 0; i < cnt; ++i) ctx->dev.emplace_back();
   for (int i = 0; i < cnt; ++i) {
     const int d = first + i;
     hipDeviceProp_t prop;
@@ -1073,7 +1196,6 @@ dp_ctx* dp_create(const dp_opts* opts) {
     for (int li = 0; li < kLanes; ++li) {
       Lane& L = D.lanes[li];
       L.device = d;
-      L.dev_index = i;
       if (li >= kStreams) {  // lane li shares the streams of lane li % kStreams
         L.s = D.lanes[li % kStreams].s;
         L.cs = D.lanes[li % kStreams].cs;
@@ -1097,12 +1219,30 @@ dp_ctx* dp_create(const dp_opts* opts) {
   ctx->zc_out = env_i64("DEPPY_ZC_OUT", 1) != 0; // diagnostic: 0 = D2H copy of every chunk
   ctx->direct = env_i64("DEPPY_DIRECT", 1) != 0; // diagnostic: 0 = stage every chunk
   ctx->grid_cap = (int32_t)std::max<int64_t>(0, env_i64("DEPPY_GRID_CAP", 0));
-  ctx->pool = new dp::Pool(dp::host_threads());
+  const int ht = dp::host_threads();
+  ctx->pool = new dp::Pool(ht);
+  const int per = std::max(2, ht / cnt);
+  for (auto& D : ctx->dev) {
+    D.own_pool = cnt > 1;
+    D.pool = D.own_pool ? new dp::Pool(per) : ctx->pool;
+    D.worker = std::thread(worker_main, ctx, &D);
+  }
   return ctx;
 }
 
 void dp_destroy(dp_ctx* ctx) {
   if (!ctx) return;
+  for (auto& D : ctx->dev) {  // the workers drain their queues and lanes, then exit
+    if (!D.worker.joinable()) continue;
+    {
+      std::lock_guard<std::mutex> lk(D.qmu);
+      D.stop = true;
+    }
+    D.qcv.notify_all();
+    D.worker.join();
+    if (D.own_pool) delete D.pool;
+    D.pool = nullptr;
+  }
   for (auto& D : ctx->dev) {
     (void)hipSetDevice(D.ordinal);
     for (int li = 0; li < kStreams; ++li)
@@ -1151,17 +1291,29 @@ int dp_device_bytes(const dp_batch* b, int32_t opt_flags, int64_t* rec_bytes, in
 int dp_submit(dp_ctx* ctx, const dp_batch* b, dp_result* res, dp_job** out) {
   if (!ctx || !b || !res || !out || b->n_problems < 0 || (b->n_problems > 0 && (!b->rec || !b->rec_off)))
     return -1;
-  std::lock_guard<std::mutex> lk(ctx->mu);
   auto* job = new dp_job;
   job->n = b->n_problems;
   job->rec = b->rec;
   job->rec_off = b->rec_off;
   job->pinned = ctx->direct && job->n > 0 && pinned_range(b->rec, 4 * (size_t)b->rec_off[job->n]);
   job->res = *res;
-  if (submit_locked(ctx, job)) {
-    (void)wait_job_locked(ctx, job);
-    delete job;
-    return -1;
+  std::vector<std::pair<int32_t, int32_t>> chunks;
+  cut_chunks(ctx, job, chunks);
+  job->chunks_left = (int)chunks.size();
+  const int nd = (int)ctx->dev.size();
+  int d0;
+  {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    d0 = ctx->next_dev;
+    ctx->next_dev = (int)((ctx->next_dev + chunks.size()) % (size_t)nd);
+  }
+  for (size_t c = 0; c < chunks.size(); ++c) {
+    Device& D = ctx->dev[(d0 + c) % (size_t)nd];
+    {
+      std::lock_guard<std::mutex> lk(D.qmu);
+      D.q.push_back(Task{job, chunks[c].first, chunks[c].second});
+    }
+    D.qcv.notify_one();
   }
   *out = job;
   return 0;
@@ -1169,11 +1321,20 @@ int dp_submit(dp_ctx* ctx, const dp_batch* b, dp_result* res, dp_job** out) {
 
 int dp_job_wait(dp_ctx* ctx, dp_job* job) {
   if (!ctx || !job) return -1;
-  std::lock_guard<std::mutex> lk(ctx->mu);
-  int rc = wait_job_locked(ctx, job);
-  if (!rc && job->rc) {
-    ctx->err = job->err;
+  job->waiting.store(true, std::memory_order_release);
+  for (auto& D : ctx->dev) {  // workers deliver the job's chunks as soon as they are done
+    std::lock_guard<std::mutex> lk(D.qmu);
+    D.qcv.notify_all();
+  }
+  int rc;
+  {
+    std::unique_lock<std::mutex> lk(job->m);
+    job->cv.wait(lk, [&] { return job->chunks_left == 0; });
     rc = job->rc;
+  }
+  if (rc) {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->err = job->err;
   }
   delete job;
   return rc;
@@ -1190,6 +1351,11 @@ int dp_get_stats(dp_ctx* ctx, dp_stats* out, int32_t reset) {
   std::lock_guard<std::mutex> lk(ctx->mu);
   *out = ctx->st;
   if (reset) ctx->st = dp_stats{};
+  for (auto& D : ctx->dev) {
+    std::lock_guard<std::mutex> dl(D.smu);
+    add_stats(*out, D.st);
+    if (reset) D.st = dp_stats{};
+  }
   return 0;
 }
 
@@ -1257,7 +1423,7 @@ int launch_slice(dp_ctx* ctx, Slice& s, int32_t trace_cap) {
   a.trace_len = s.trace_len;
   a.trace_cap = trace_cap;
   HIP_OK(hipEventRecord(s.k0, s.stream));
-  if (enqueue_launches(ctx, s.plan, a, s.stream)) return -1;
+  if (enqueue_launches(ctx, s.plan, a, s.stream, ctx->st)) return -1;
   HIP_OK(hipEventRecord(s.k1, s.stream));
   return 0;
 }
@@ -1272,7 +1438,7 @@ int wait_locked(dp_ctx* ctx, dp_resident* r) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, s.k0, s.k1) == hipSuccess) mx = std::max(mx, (double)ms);
   }
-  ctx->last_ms = mx;
+  ctx->last_ms.store(mx);
   return 0;
 }
 
@@ -1327,7 +1493,7 @@ int dp_upload_traced(dp_ctx* ctx, const dp_batch* b, int32_t trace_cap, dp_resid
     if (build_slice(ctx, s, b, trace_cap)) {
       for (auto& x : r->slices) free_slice(x);
       delete r;
-      return -1;
+      return api_fail(ctx);
     }
   *out = r;
   return 0;
@@ -1336,31 +1502,31 @@ int dp_upload_traced(dp_ctx* ctx, const dp_batch* b, int32_t trace_cap, dp_resid
 int dp_launch(dp_ctx* ctx, dp_resident* r) {
   if (!ctx || !r) return -1;
   std::lock_guard<std::mutex> lk(ctx->mu);
-  return launch_locked(ctx, r);
+  return launch_locked(ctx, r) ? api_fail(ctx) : 0;
 }
 
 int dp_wait(dp_ctx* ctx, dp_resident* r) {
   if (!ctx || !r) return -1;
   std::lock_guard<std::mutex> lk(ctx->mu);
-  return wait_locked(ctx, r);
+  return wait_locked(ctx, r) ? api_fail(ctx) : 0;
 }
 
 int dp_run(dp_ctx* ctx, dp_resident* r) {
   if (!ctx || !r) return -1;
   std::lock_guard<std::mutex> lk(ctx->mu);
-  if (launch_locked(ctx, r)) return -1;
-  return wait_locked(ctx, r);
+  if (launch_locked(ctx, r)) return api_fail(ctx);
+  return wait_locked(ctx, r) ? api_fail(ctx) : 0;
 }
 
 int dp_download(dp_ctx* ctx, dp_resident* r, dp_result* res) {
   if (!ctx || !r || !res) return -1;
   std::lock_guard<std::mutex> lk(ctx->mu);
-  if (wait_locked(ctx, r)) return -1;
+  if (wait_locked(ctx, r)) return api_fail(ctx);
   for (auto& s : r->slices) {
     if (s.p1 == s.p0) continue;
-    HIP_OK(hipSetDevice(ctx->dev[(size_t)s.d].ordinal));
+    API_OK(hipSetDevice(ctx->dev[(size_t)s.d].ordinal));
     std::vector<char> host(s.ol.end);
-    HIP_OK(hipMemcpy(host.data(), s.d_out.p, s.ol.end, hipMemcpyDeviceToHost));
+    API_OK(hipMemcpy(host.data(), s.d_out.p, s.ol.end, hipMemcpyDeviceToHost));
     scatter(s.plan, s.ol, host.data(), s.p0, res);
   }
   return 0;
@@ -1369,7 +1535,7 @@ int dp_download(dp_ctx* ctx, dp_resident* r, dp_result* res) {
 int dp_download_trace(dp_ctx* ctx, dp_resident* r, int32_t* trace, int32_t* trace_len) {
   if (!ctx || !r || !trace || !trace_len) return -1;
   std::lock_guard<std::mutex> lk(ctx->mu);
-  if (wait_locked(ctx, r)) return -1;
+  if (wait_locked(ctx, r)) return api_fail(ctx);
   if (r->trace_cap <= 0) {
     ctx->err = "dp_download_trace: the batch was not uploaded with dp_upload_traced";
     return -1;
@@ -1377,9 +1543,9 @@ int dp_download_trace(dp_ctx* ctx, dp_resident* r, int32_t* trace, int32_t* trac
   for (auto& s : r->slices) {
     const int32_t n = s.p1 - s.p0;
     if (n == 0) continue;
-    HIP_OK(hipSetDevice(ctx->dev[(size_t)s.d].ordinal));
-    HIP_OK(hipMemcpy(trace_len + s.p0, s.trace_len, (size_t)n * 4, hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(trace + (int64_t)r->trace_cap * s.p0, s.trace, (size_t)n * r->trace_cap * 4,
+    API_OK(hipSetDevice(ctx->dev[(size_t)s.d].ordinal));
+    API_OK(hipMemcpy(trace_len + s.p0, s.trace_len, (size_t)n * 4, hipMemcpyDeviceToHost));
+    API_OK(hipMemcpy(trace + (int64_t)r->trace_cap * s.p0, s.trace, (size_t)n * r->trace_cap * 4,
                      hipMemcpyDeviceToHost));
   }
   return 0;
@@ -1411,8 +1577,8 @@ int dp_solve_traced(dp_ctx* ctx, const dp_batch* b, int32_t trace_cap, dp_result
 // epilogue, core] of the last run (not part of include/deppy_hip.h).
 int dp_debug_stamps(dp_ctx* ctx, dp_resident* r, int64_t* out) {
   for (auto& s : r->slices) {
-    HIP_OK(hipSetDevice(ctx->dev[(size_t)s.d].ordinal));
-    HIP_OK(hipMemcpy(out + dp::DP_NSTAMP * (size_t)s.p0, s.stamps, (size_t)(s.p1 - s.p0) * dp::DP_NSTAMP * 8,
+    API_OK(hipSetDevice(ctx->dev[(size_t)s.d].ordinal));
+    API_OK(hipMemcpy(out + dp::DP_NSTAMP * (size_t)s.p0, s.stamps, (size_t)(s.p1 - s.p0) * dp::DP_NSTAMP * 8,
                      hipMemcpyDeviceToHost));
   }
   return 0;
@@ -1421,7 +1587,7 @@ int dp_debug_stamps(dp_ctx* ctx, dp_resident* r, int64_t* out) {
 
 int dp_last_kernel_ms(const dp_ctx* ctx, double* ms) {
   if (!ctx || !ms) return -1;
-  *ms = ctx->last_ms;
+  *ms = ctx->last_ms.load();
   return 0;
 }
 

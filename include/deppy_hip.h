@@ -374,13 +374,15 @@ int32_t dp_num_devices(const dp_ctx* ctx);
 int dp_solve(dp_ctx* ctx, const dp_batch* b, dp_result* res);
 
 /* Asynchronous host-to-host solve (serving loops; no reference counterpart:
- * the reference solves one problem per call).  dp_submit stages the batch
- * chunk by chunk into the context's pinned buffers and enqueues each chunk's
- * H2D copy, solve and D2H copy on the next lane (stream); it returns once the
- * last chunk is enqueued.  b's arrays may be reused after dp_submit returns;
- * res must stay valid until dp_job_wait(job) returns, which delivers the
- * results and frees the job.  Several jobs may be in flight; a later submit
- * that needs a busy lane first delivers that lane's chunk to its job. */
+ * the reference solves one problem per call).  dp_submit cuts the batch into
+ * chunks (at least one per device) and queues them to the devices' submitting
+ * threads, one host thread per device, then returns at once.  Each thread
+ * plans and stages its chunks into its lanes' pinned buffers (or DMAs
+ * page-locked records as they lie) and enqueues copy and solve on the lane's
+ * stream, and delivers finished chunks into res.  b's arrays (the records and
+ * rec_off) and res must stay valid and unchanged until dp_job_wait(job)
+ * returns, which blocks until every chunk is delivered and frees the job.
+ * Several jobs may be in flight, from any number of caller threads. */
 typedef struct dp_job dp_job;
 int dp_submit(dp_ctx* ctx, const dp_batch* b, dp_result* res, dp_job** job);
 int dp_job_wait(dp_ctx* ctx, dp_job* job);

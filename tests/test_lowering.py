@@ -296,3 +296,32 @@ def test_packed_form_falls_back_when_rows_do_not_imply_lists():
             np.testing.assert_array_equal(unpack_p16(r), a.record(p))
     assert fmts["plain"] == 5 and fmts["same-twice"] == 5
     assert fmts["self"] != 5 and fmts["repeat"] != 5, fmts
+
+
+def test_bench_input_config_shape():
+    """Config 6: problems of the reference's BenchmarkInput distribution
+    (pkg/sat/bench_test.go:10-64) -- 256 variables "0".."255"; Mandatory with
+    p=0.1, one Dependency of 1-5 other variables with p=0.15, 1-2 Conflicts
+    with p=0.05, in that order -- lower and solve (oracle) without errors."""
+    from oracle import oracle
+    w = _lib.generate(6, 200, 9)
+    pvo, vco, kind, cao = w["prob_var_off"], w["var_con_off"], w["con_kind"], w["con_arg_off"]
+    assert np.all(np.diff(pvo) == 256)
+    nv = int(pvo[-1])
+    per = np.diff(vco)
+    first = kind[vco[:-1][per > 0]]
+    mand = (kind == 1).sum() / nv
+    dep = kind == 3
+    deps_per_var = np.diff(np.concatenate([[0], np.cumsum(dep)])[vco])
+    assert 0.08 < mand < 0.12 and 0.13 < (deps_per_var > 0).mean() < 0.17 and deps_per_var.max() == 1
+    nargs = np.diff(cao)[dep]
+    assert nargs.min() == 1 and nargs.max() == 5
+    conf_vars = np.diff(np.concatenate([[0], np.cumsum(kind == 4)])[vco])
+    assert 0.035 < (conf_vars > 0).mean() < 0.065 and conf_vars.max() == 2
+    assert set(np.unique(first)) <= {1, 3, 4}
+    lw = _lib.Lowered(_lib.WireArrays(**{k: w[k] for k in (
+        "prob_var_off", "var_id", "var_con_off", "con_kind", "con_n", "con_arg_off", "con_arg",
+        "str_off")}, str_bytes=w["str_bytes"].tobytes()))
+    assert (lw.err == 0).all()
+    res = oracle.solve_batch(lw.rec_off, lw.rec, 0, 4)
+    assert set(np.unique(res["status"])) <= {1, -1}

@@ -1,6 +1,10 @@
 """The N>1 path on CPU: world_size-2 gloo ranks, as bench.py runs them under
-torchrun (one process per GPU, RCCL) but with the oracle standing in for the
-device solve so the sharding + timing reduction are checked here.
+torchrun (one process per GPU, RCCL).  Each rank runs the library's host
+side of the pipeline on its own shard -- packed lowering (dp_lower_into),
+chunk planning and staging (dp_stage_roundtrip), result stitching
+(dp_stitch_selftest), the device partition (dp_partition) -- and the oracle
+stands in for the device solve, so sharding, the host path per rank and the
+timing reduction are checked here.
 """
 import os
 import socket
@@ -22,12 +26,25 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _lowered(config, n, seed):
+def _lowered(config, n, seed, packed=False):
     w = _lib.generate(config, n, seed)
     wa = _lib.WireArrays(**{k: w[k] for k in (
         "prob_var_off", "var_id", "var_con_off", "con_kind", "con_n", "con_arg_off", "con_arg",
         "str_off")}, str_bytes=w["str_bytes"].tobytes())
-    return _lib.Lowered(wa)
+    return _lib.Lowered(wa, narrow=packed, packed=packed)
+
+
+def _host_path(seed, n):
+    """The library's host side of dp_submit on one shard: packed records,
+    their chunked staging round trip, stitched synthetic results, the
+    partition over 2 devices."""
+    lwp = _lowered(2, n, seed, packed=True)
+    staged, firsts = _lib.stage_roundtrip(lwp.rec_off, lwp.rec, 0, chunk_problems=16)
+    st = _lib.stitch_selftest(lwp.rec_off, lwp.rec, 16)
+    cut = _lib.partition(lwp.rec_off, 2)
+    return dict(prec=lwp.rec.copy(), prec_off=lwp.rec_off.copy(), staged=staged, firsts=firsts,
+                st_status=st["status"][:n], st_installed=st["installed"], st_core=st["core"],
+                st_core_len=st["core_len"][:n], cut=cut)
 
 
 def _rank(rank, world, port, outdir):
@@ -35,15 +52,20 @@ def _rank(rank, world, port, outdir):
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     from oracle import oracle
     g = shard.init_from_env("gloo")
-    lw = _lowered(2, N_PER_RANK, shard.shard_seed(7, g.rank, N_PER_RANK))
+    seed = shard.shard_seed(7, g.rank, N_PER_RANK)
+    lw = _lowered(2, N_PER_RANK, seed)
     res = oracle.solve_batch(lw.rec_off, lw.rec, 0, 1)
+    host = _host_path(seed, N_PER_RANK)
+    # the packed records solve like the int32 ones (oracle reads every form)
+    pres = oracle.solve_batch(host["prec_off"], host["prec"], 0, 1)
+    assert np.array_equal(pres["status"], res["status"]) and np.array_equal(pres["steps"], res["steps"])
     g.barrier()
     fake_elapsed = 1.0 + g.rank  # rank 1 is the slowest
     mx = g.max(fake_elapsed)
     all_t = g.gather(fake_elapsed)
     np.savez(os.path.join(outdir, "r%d.npz" % g.rank), rec_off=lw.rec_off, rec=lw.rec,
              status=res["status"], steps=res["steps"], installed=res["installed"],
-             mx=mx, all_t=np.array(all_t))
+             mx=mx, all_t=np.array(all_t), **{"host_" + k: v for k, v in host.items()})
     g.close()
 
 
@@ -81,6 +103,14 @@ def test_two_rank_gloo(tmp_path):
     assert np.array_equal(np.concatenate([r[0]["steps"], r[1]["steps"]]), gres["steps"])
     # no two ranks solved the same catalog
     assert not np.array_equal(r[0]["rec"], r[1]["rec"])
+    # each rank's host path equals the same path run here on that rank's shard
+    for i in range(2):
+        want = _host_path(7 + i * N_PER_RANK, N_PER_RANK)
+        for k, v in want.items():
+            assert np.array_equal(r[i]["host_" + k], v), (i, k)
+        # staging round trip: packed one-wavefront records are staged as they are
+        assert np.array_equal(r[i]["host_staged"], r[i]["host_prec"])
+        assert list(r[i]["host_firsts"]) == list(range(0, N_PER_RANK, 16))
 
 
 def test_strong_scaling_ranges_partition_the_total():
