@@ -66,6 +66,26 @@ __host__ __device__ constexpr int32_t mode_cq(int mode) { return mode == M_LDS ?
 #define DP_IMP16 1
 #endif
 constexpr bool IMP16_LDS = DP_IMP16;
+// Two-watched-literal filter on the multi-wave placements: every clause row
+// keeps the two literals it watches (Layout::wp); a round reaches a row
+// through the occurrence lists as before, but evaluates it only when one of
+// its watches is false, and then moves the watches (solve_kernel.hpp
+// clause_unit).  0: plain occurrence-list propagation (the A/B baseline).
+#ifndef DP_2WL
+#define DP_2WL 1
+#endif
+__host__ __device__ constexpr bool mode_2wl(int mode) { return DP_2WL && mode != M_LDS; }
+// Row slots on the multi-wave placements (the compact hot image of a clause
+// row): 32 bytes per row in the HBM scratch, built during init -- the row's
+// watched pair, its length, and its literals inline when it has at most
+// five (else the row's offset into clause_lits).  A round reaches a row from
+// its watch entry with one 32-byte read instead of the offsets-then-literals
+// chain of the record.
+#ifndef DP_ROWSLOT
+#define DP_ROWSLOT 1
+#endif
+__host__ __device__ constexpr bool mode_rowslot(int mode) { return DP_ROWSLOT && mode != M_LDS; }
+constexpr int32_t ROWSLOT_INLINE = 5;
 
 // wave-shared scalars (S_*), then (multi-wave modes) per-wave reduction slots
 constexpr int32_t NSCAL = 64;
@@ -209,6 +229,8 @@ struct Layout {
   int32_t tl;        // u16[2hc] first implications, (slot << 1) | negative       [LDS]
   int32_t fr;        // i32[hc] trail ring: trail[i] at fr[i & (hc - 1)]          [LDS]
   int32_t hc;        // slots (a power of two; 0 when the mode keeps rounds in HBM)
+  int32_t wp;        // (mode_rowslot) i32[8][nc] row slots {watch x, watch y, len, l0 | offset, l1..l4};
+                     // else (mode_2wl) u64[nc] the two literals clause row r watches, low word first
   int32_t wl;        // multi-wave, DP_FMT_I32 records: device-built w_off[2nv+1], w[ncl+nkl]  [HBM, last]
   int32_t bytes;     // HBM scratch bytes (0 for M_LDS)
   int32_t lds_bytes; // LDS bytes
@@ -290,6 +312,7 @@ __host__ __device__ inline Layout layout(const int32_t* h) {
   L.l_lits = take(L.lcap * ix, COLD);
   L.dq = take(2 * L.cap * ix, COLD);
   L.stk = take(3 * L.cap * ix, COLD);
+  L.wp = mode_rowslot(MODE) ? take(h[DP_H_NC] * 32, COLD) : mode_2wl(MODE) ? take(h[DP_H_NC] * 8, COLD) : 0;
   L.wl = MODE != M_LDS && h[DP_H_FMT] == DP_FMT_I32 && device_watches(h)
              ? take((2 * nv + 1 + h[DP_H_NCL] + h[DP_H_NKL]) * 4, COLD) : 0;
   L.bytes = og;

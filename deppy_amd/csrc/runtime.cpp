@@ -578,33 +578,51 @@ void fill_in_tables(const Plan& P, const InLayout& L, char* base) {
 
 // Results of a chunk (output region `out`, local problems) -> the caller's
 // dp_result at global problems p0...  Cores come from the pool.
-void scatter(const Plan& P, const OutLayout& L, const char* out, int32_t p0, dp_result* res) {
+// Returns the chunk's BCP-visited bytes.  One pass over the per-problem
+// results (in blocks on `pool` when given and the chunk is large).
+uint64_t scatter(const Plan& P, const OutLayout& L, const char* out, int32_t p0, dp_result* res,
+                 dp::Pool* pool = nullptr) {
   const int32_t n = P.n;
   const dp::ProblemOut* po = reinterpret_cast<const dp::ProblemOut*>(out + L.prob);
-  for (int32_t i = 0; i < n; ++i) {
-    res->status[p0 + i] = po[i].status;
-    res->flags[p0 + i] = po[i].flags;
-    res->core_len[p0 + i] = po[i].core_len;
-  }
-  if (res->steps)
-    for (int32_t i = 0; i < n; ++i) res->steps[p0 + i] = po[i].steps;
   const uint32_t* inst = reinterpret_cast<const uint32_t*>(out + L.installed);
-  if (res->inst_off[p0 + n] - res->inst_off[p0] == P.inst_off[(size_t)n]) {
-    std::memcpy(res->installed + res->inst_off[p0], inst, (size_t)P.inst_off[(size_t)n] * 4);
-  } else {  // a caller layout of its own: problem by problem
-    for (int32_t i = 0; i < n; ++i) {
-      const int64_t w = std::min(P.inst_off[(size_t)i + 1] - P.inst_off[(size_t)i],
-                                 res->inst_off[p0 + i + 1] - res->inst_off[p0 + i]);
-      std::memcpy(res->installed + res->inst_off[p0 + i], inst + P.inst_off[(size_t)i], (size_t)w * 4);
+  const int32_t* cpool = reinterpret_cast<const int32_t*>(out + L.pool);
+  const bool same_inst = res->inst_off[p0 + n] - res->inst_off[p0] == P.inst_off[(size_t)n];
+  constexpr int32_t kBlock = 1024;
+  const int32_t nb = (n + kBlock - 1) / kBlock;
+  static thread_local std::vector<uint64_t> part_tl;  // (per calling thread: no allocation once grown)
+  std::vector<uint64_t>& part = part_tl;  // (a local name: the pool's threads write the caller's vector)
+  part.assign((size_t)std::max(nb, 1), 0);
+  auto block = [&](int64_t b) {
+    const int32_t i0 = (int32_t)b * kBlock, i1 = std::min(n, i0 + kBlock);
+    uint64_t bcp = 0;
+    for (int32_t i = i0; i < i1; ++i) {
+      const dp::ProblemOut& o = po[i];
+      res->status[p0 + i] = o.status;
+      res->flags[p0 + i] = o.flags;
+      res->core_len[p0 + i] = o.core_len;
+      if (res->steps) res->steps[p0 + i] = o.steps;
+      bcp += o.bcp;
+      if (o.core_len > 0) {
+        const int64_t cap = res->core_off[p0 + i + 1] - res->core_off[p0 + i];
+        std::memcpy(res->core + res->core_off[p0 + i], cpool + o.core_at,
+                    (size_t)std::min<int64_t>(o.core_len, cap) * 4);
+      }
+      if (!same_inst) {  // a caller layout of its own: problem by problem
+        const int64_t w = std::min(P.inst_off[(size_t)i + 1] - P.inst_off[(size_t)i],
+                                   res->inst_off[p0 + i + 1] - res->inst_off[p0 + i]);
+        std::memcpy(res->installed + res->inst_off[p0 + i], inst + P.inst_off[(size_t)i], (size_t)w * 4);
+      }
     }
-  }
-  const int32_t* pool = reinterpret_cast<const int32_t*>(out + L.pool);
-  for (int32_t i = 0; i < n; ++i)
-    if (po[i].core_len > 0) {
-      const int64_t cap = res->core_off[p0 + i + 1] - res->core_off[p0 + i];
-      std::memcpy(res->core + res->core_off[p0 + i], pool + po[i].core_at,
-                  (size_t)std::min<int64_t>(po[i].core_len, cap) * 4);
+    if (same_inst) {
+      const int64_t w0 = P.inst_off[(size_t)i0], w1 = P.inst_off[(size_t)i1];
+      std::memcpy(res->installed + res->inst_off[p0] + w0, inst + w0, (size_t)(w1 - w0) * 4);
     }
+    part[(size_t)b] = bcp;
+  };
+  if (pool && nb >= 4) pool->run(nb, std::function<void(int64_t)>(block), 1);
+  else for (int32_t b = 0; b < nb; ++b) block(b);
+  uint64_t bcp = 0;
+  for (uint64_t x : part) bcp += x;
   for (size_t q = 0; q < P.skip.size(); ++q) {
     const int32_t i = P.skip[q];
     res->status[p0 + i] = DP_ERROR;
@@ -613,6 +631,7 @@ void scatter(const Plan& P, const OutLayout& L, const char* out, int32_t p0, dp_
     if (res->steps) res->steps[p0 + i] = 0;
     for (int64_t w = res->inst_off[p0 + i]; w < res->inst_off[p0 + i + 1]; ++w) res->installed[w] = 0;
   }
+  return bcp;
 }
 
 template <class T>
@@ -863,9 +882,7 @@ int finish_lane(dp_ctx* ctx, Device& D, Lane& L) {
     HIP_OK(hipStreamSynchronize(L.s));
     st.d2h_bytes += (int64_t)(need - L.ol.d2h);
   }
-  scatter(L.plan, L.ol, L.h_out.p, L.p0, &job->res);
-  const dp::ProblemOut* po = at<dp::ProblemOut>(L.h_out.p, L.ol.prob);
-  for (int32_t i = 0; i < L.plan.n; ++i) st.bcp_bytes += (int64_t)po[i].bcp;
+  st.bcp_bytes += (int64_t)scatter(L.plan, L.ol, L.h_out.p, L.p0, &job->res, D.pool);
   st.scatter_ms += now_ms() - t1;
   add_device_stats(D, st);
   return 0;

@@ -184,6 +184,13 @@ struct Group {
   int8_t* val;
   IX *reason, *rs, *trail, *touched, *d_mark, *l_off, *l_lits, *dq, *stk;
   IMP* imp;  // imp[l] = lowest row implying literal l this round
+  // two-watched-literal filter (mode_2wl): the watched pair of each clause
+  // row; `sweep` (base scope) evaluates the rows it names unfiltered
+  static constexpr bool TWL = mode_2wl(MODE);
+  static constexpr bool RSLOT = mode_rowslot(MODE);  // row slots (layout.hpp): the pair at wpair[4r]
+  static constexpr int WS = RSLOT ? 4 : 1;            // u64 words per row of wpair
+  uint64_t* wpair;
+  bool sweep;
   uint32_t *d_flip, *inS, *extra, *seen, *model, *used, *en, *en2, *dset, *fg;
   IX *wbuf, *cardq;
   int32_t* scal;
@@ -449,6 +456,8 @@ struct Group {
     touched = reinterpret_cast<IX*>(cold + L.touched);
     d_mark = reinterpret_cast<IX*>(cold + L.d_mark);
     imp = reinterpret_cast<IMP*>(cold + L.imp);
+    wpair = reinterpret_cast<uint64_t*>(cold + L.wp);
+    sweep = false;
     d_flip = reinterpret_cast<uint32_t*>(hot + L.d_flip);
     inS = reinterpret_cast<uint32_t*>(hot + L.inS);
     extra = reinterpret_cast<uint32_t*>(hot + L.extra);
@@ -542,6 +551,21 @@ struct Group {
     }
     for (int i = tid; i < mode_nscal(MODE); i += NT) scal[i] = 0;
     if (tid == 0) l_off[0] = 0;
+    if constexpr (TWL || RSLOT)  // every row watches its first two literals (nothing is assigned yet)
+      for (int r = tid; r < nc; r += NT) {
+        const int a = clause_off[r], b = clause_off[r + 1], len = b - a;
+        const int x = len > 0 ? (int)clause_lits[a] : 0, y = len >= 2 ? (int)clause_lits[a + 1] : x;
+        if constexpr (RSLOT) {
+          int lt[ROWSLOT_INLINE];
+#pragma unroll
+          for (int k = 0; k < ROWSLOT_INLINE; ++k) lt[k] = k < len && len <= ROWSLOT_INLINE ? (int)clause_lits[a + k] : 0;
+          int4* sp = reinterpret_cast<int4*>(wpair + 4 * r);
+          sp[0] = make_int4(x, y, len, len <= ROWSLOT_INLINE ? lt[0] : a);
+          sp[1] = make_int4(lt[1], lt[2], lt[3], lt[4]);
+        } else {
+          wpair[r] = (uint64_t)(uint32_t)x | ((uint64_t)(uint32_t)y << 32);
+        }
+      }
     gsync();
     return true;
   }
@@ -1060,8 +1084,143 @@ struct Group {
     if (nun == 0) crow = min(crow, r);
     return nun == 1 ? ul : -1;
   }
+  // Two-watched-literal evaluation of clause row r, whose watched pair has a
+  // false literal: the row's outcome as eval_clause, and its new pair --
+  // its first two non-false literals, else its one non-false literal and its
+  // most recently falsified one, else its two most recently falsified ones
+  // (by rs, ties to row order).  Invariant: a row with two or more non-false
+  // literals watches two of them.  It holds at the start (nothing assigned),
+  // a round's falsifications are repaired in the next round before any
+  // other, and backtracking only ever returns to a propagation fixpoint,
+  // where a row with a false watch has at most one non-false literal unless
+  // that watch (its latest falsification) was undone too.  So a row whose
+  // pair is non-false has two non-false literals: not unit, not false, and
+  // skipped without reading it -- exactly the rows occurrence lists would
+  // have found unit or false are evaluated, and the round is unchanged.  Every
+  // lane that evaluates a row in one round writes the same pair.
+  __device__ __forceinline__ int eval_clause_twl(int r, int a, int b, int& crow) {
+    int nun = 0, ul = -1, n0 = -1, n1 = -1;
+    bool sat = false;
+    vis += 2 * sizeof(IX);
+    for (int j = a; j < b && n1 < 0; j += 4) {
+      int l[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) l[k] = j + k < b ? (int)clause_lits[j + k] : -1;
+      int x[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) x[k] = l[k] >= 0 ? lit_val(l[k]) : -1;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (l[k] < 0 || n1 >= 0) continue;
+        vis += sizeof(IX) + 1;
+        if (x[k] > 0) sat = true;
+        if (x[k] == 0) { ++nun; ul = l[k]; }
+        if (x[k] >= 0) {
+          if (n0 < 0) n0 = l[k];
+          else n1 = l[k];
+        }
+      }
+    }
+    uint32_t px, py;
+    if (n1 >= 0) {
+      px = (uint32_t)n0; py = (uint32_t)n1;
+    } else {
+      // one or no non-false literal: the latest falsified ones
+      int f0 = -1, f1 = -1, r0 = -1, r1 = -1;
+      for (int j = a; j < b; ++j) {
+        const int l = clause_lits[j];
+        if (lit_val(l) >= 0) continue;
+        const int t = (int)rs[l >> 1];
+        vis += sizeof(IX);
+        if (t > r0) { f1 = f0; r1 = r0; f0 = l; r0 = t; }
+        else if (t > r1) { f1 = l; r1 = t; }
+      }
+      if (n0 >= 0) { px = (uint32_t)n0; py = (uint32_t)(f0 >= 0 ? f0 : n0); }
+      else { px = (uint32_t)f0; py = (uint32_t)(f1 >= 0 ? f1 : f0); }
+    }
+    __hip_atomic_store(&wpair[WS * r], (uint64_t)px | ((uint64_t)py << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (sat || n1 >= 0) return -1;
+    if (nun == 0) crow = min(crow, r);
+    return nun == 1 ? ul : -1;
+  }
+
+  // A row of at most ROWSLOT_INLINE literals from its slot (registers): the
+  // row's outcome (eval_clause), and with TWL its new pair (eval_clause_twl).
+  __device__ __forceinline__ int eval_inline(int r, const int (&lt)[ROWSLOT_INLINE], int len, int& crow) {
+    int nun = 0, ul = -1, n0 = -1, n1 = -1;
+    bool sat = false;
+    int x[ROWSLOT_INLINE];
+#pragma unroll
+    for (int k = 0; k < ROWSLOT_INLINE; ++k) x[k] = k < len ? lit_val(lt[k]) : -1;
+    vis += (uint32_t)len * 1u;
+#pragma unroll
+    for (int k = 0; k < ROWSLOT_INLINE; ++k) {
+      if (k >= len) continue;
+      if (x[k] > 0) sat = true;
+      if (x[k] == 0) { ++nun; ul = lt[k]; }
+      if (x[k] >= 0) {
+        if (n0 < 0) n0 = lt[k];
+        else if (n1 < 0) n1 = lt[k];
+      }
+    }
+    if constexpr (TWL) {
+      uint32_t px, py;
+      if (n1 >= 0) {
+        px = (uint32_t)n0; py = (uint32_t)n1;
+      } else {
+        int f0 = -1, f1 = -1, r0 = -1, r1 = -1;
+        int t[ROWSLOT_INLINE];
+#pragma unroll
+        for (int k = 0; k < ROWSLOT_INLINE; ++k) t[k] = k < len && x[k] < 0 ? (int)rs[lt[k] >> 1] : -1;
+#pragma unroll
+        for (int k = 0; k < ROWSLOT_INLINE; ++k) {
+          if (t[k] < 0) continue;
+          vis += sizeof(IX);
+          if (t[k] > r0) { f1 = f0; r1 = r0; f0 = lt[k]; r0 = t[k]; }
+          else if (t[k] > r1) { f1 = lt[k]; r1 = t[k]; }
+        }
+        if (n0 >= 0) { px = (uint32_t)n0; py = (uint32_t)(f0 >= 0 ? f0 : n0); }
+        else { px = (uint32_t)f0; py = (uint32_t)(f1 >= 0 ? f1 : f0); }
+      }
+      __hip_atomic_store(&wpair[WS * r], (uint64_t)px | ((uint64_t)py << 32), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (sat || n1 >= 0) return -1;
+    if (nun == 0) crow = min(crow, r);
+    return nun == 1 ? ul : -1;
+  }
+
   // a clause row (r < nc) or a learned row (r >= nrows)
   __device__ __forceinline__ int clause_unit(int r, int& crow) {
+    if constexpr (RSLOT) {
+      if (r < nc) {
+        // the slot: the pair (coherent: other wavefronts move it), then the
+        // row's length and literals (written once, at init) -- one hop
+        const int32_t* sp = reinterpret_cast<const int32_t*>(wpair + 4 * r);
+        uint64_t wv = 0;
+        if (TWL && !sweep) wv = __hip_atomic_load(&wpair[4 * r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int2 q = *reinterpret_cast<const int2*>(sp + 2);
+        const int4 t = *reinterpret_cast<const int4*>(sp + 4);
+        vis += 32;
+        if (TWL && !sweep && lit_val((int)(uint32_t)wv) >= 0 && lit_val((int)(uint32_t)(wv >> 32)) >= 0) return -1;
+        if (q.x <= ROWSLOT_INLINE) {
+          const int lt[ROWSLOT_INLINE] = {q.y, t.x, t.y, t.z, t.w};
+          return eval_inline(r, lt, q.x, crow);
+        }
+        if constexpr (TWL) return eval_clause_twl(r, q.y, q.y + q.x, crow);
+        else return eval_clause(r, clause_lits, q.y, q.y + q.x, crow);
+      }
+    }
+    if constexpr (TWL) {
+      if (r < nc) {
+        if (!sweep) {
+          const uint64_t wv = __hip_atomic_load(&wpair[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          vis += 8;
+          if (lit_val((int)(uint32_t)wv) >= 0 && lit_val((int)(uint32_t)(wv >> 32)) >= 0) return -1;
+        }
+        return eval_clause_twl(r, clause_off[r], clause_off[r + 1], crow);
+      }
+    }
     if (r < nc) return eval_clause(r, clause_lits, clause_off[r], clause_off[r + 1], crow);
     const int j = r - nrows;
     return eval_clause(r, l_lits, DP_CHK((int)l_off[j], 0, lcap + 1, 33), DP_CHK((int)l_off[j + 1], 0, lcap + 1, 34), crow);
@@ -1541,6 +1700,7 @@ struct Group {
   __device__ __forceinline__ int base_propagate() {
     const int r = run_round([&](int& crow) {
       int ncq = 0;
+      sweep = true;  // (rows of one literal are unit on the empty assignment: no filter)
       for (int i0 = 0; i0 < nrows; i0 += NT) {
         const int row = i0 + tid;
         const bool f = row < nc ? (int)clause_off[row + 1] - (int)clause_off[row] <= 1
@@ -1548,6 +1708,7 @@ struct Group {
         make_room(crow, ncq);
         visit(f ? row : -1, crow, ncq);
       }
+      sweep = false;
       flush_cards(crow, ncq);
       eval_learned(crow);
     });
