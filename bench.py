@@ -148,7 +148,7 @@ def cpu_end_to_end(wa, lw32, n, threads, seconds):
     return reps * n / (time.perf_counter() - t0)
 
 
-def lowered_config(config, n, seed):
+def lowered_config(config, n, seed, form="packed"):
     """The batch lowered twice: in the packed 16-bit form into page-locked
     memory (dp_lower_into DP_LOWER_NARROW | DP_LOWER_PACKED | DP_LOWER_PINNED,
     as a serving loop keeps its lowering storage; what the GPU path is given)
@@ -160,7 +160,7 @@ def lowered_config(config, n, seed):
         "prob_var_off", "var_id", "var_con_off", "con_kind", "con_n", "con_arg_off", "con_arg",
         "str_off")}, str_bytes=w["str_bytes"].tobytes())
     lw32 = _lib.Lowered(wa)
-    lw = _lib.Lowered(wa, narrow=True, pinned=True, packed=True)
+    lw = _lib.Lowered(wa, narrow=form != "i32", pinned=True, packed=form == "packed")
     reps, t0 = 0, time.perf_counter()
     while reps < 3 or time.perf_counter() - t0 < 1.0:
         lw.relower(wa)
@@ -218,6 +218,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--kernel-steps", type=int, default=20,
                     help="steps of the device-resident (kernel-only) secondary figure; 0: skip")
+    ap.add_argument("--record-form", choices=("packed", "u16", "i32"), default="packed",
+                    help="the records the GPU legs are given: dp_lower_into NARROW|PACKED (P16D/P16, default), "
+                         "NARROW (U16) or int32 (staged by the host)")
     ap.add_argument("--e2e-steps", type=int, default=10,
                     help="steps of the lowering-inclusive (wire -> results) secondary figure; 0: skip")
     ap.add_argument("--kernel-only", action="store_true",
@@ -244,7 +247,7 @@ def main():
         total = args.problems or wl[1]
         lo, hi = shard.strong_range(total, rank, world)
         n, first = hi - lo, args.seed + lo
-    lw, lw32, t_lower, wa = lowered_config(args.config, n, first)
+    lw, lw32, t_lower, wa = lowered_config(args.config, n, first, args.record_form)
     ctx = _lib.Context(local, 1, flags=args.flags)
 
     # host-to-host: depth jobs in flight, each the whole batch.  The pipeline

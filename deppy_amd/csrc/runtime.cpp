@@ -55,12 +55,44 @@ constexpr int64_t kDefaultBudget = 1 << 16;        // BCP invocations per proble
 // (160 KiB / 10, / 5, / 3, / 2, / 1.  Config 5, 30 steps: 588k res/s with
 // 8/16/24/32/48/64/96/160 ceilings, 608k with these; configs 2 and 3 make
 // one launch either way.)
-constexpr int kCeilings[] = {16 << 10, 32 << 10, 53 << 10, 80 << 10, 160 << 10};
-constexpr int kNBuckets = (int)(sizeof(kCeilings) / sizeof(kCeilings[0]));
+// Coarse ceilings (the default): 160 KiB / 10, / 5, / 3, / 2, / 1.
+// DEPPY_CEILINGS=fine: one bucket per residency, the largest footprint of
+// which k problems share a CU (160 KiB / k, in 512-byte LDS allocation
+// units), k = 16 .. 1.  The one-wavefront kernel is latency-bound per wave:
+// its throughput follows residency almost linearly (config 2, kernel only:
+// 2 per CU 6.2M res/s, 4: 11.5M, 6: 16.7M, 8: 20.4M, 9: 22.3M;
+// profiles/r03_config2_residency_sweep.jsonl).  But a chunk's launches run
+// one after another on its stream, each as long as its slowest problem:
+// fine buckets split config 2 into 2-3 launches and it fell from 22.1M to
+// 14.3M res/s (profiles/r03_buckets_ab.jsonl).  Residency has to come from
+// smaller footprints, not from more launches.
+constexpr int kNBuckets = 16;
+struct Ceilings {
+  int c[kNBuckets];
+  int n;
+};
+const Ceilings& ceilings() {
+  static const Ceilings t = [] {
+    Ceilings x{};
+    const char* e = std::getenv("DEPPY_CEILINGS");
+    if (!e || std::strcmp(e, "fine") != 0) {
+      const int coarse[] = {16 << 10, 32 << 10, 53 << 10, 80 << 10, 160 << 10};
+      x.n = 5;
+      for (int i = 0; i < 5; ++i) x.c[i] = coarse[i];
+    } else {
+      x.n = kNBuckets;
+      for (int k = kNBuckets; k >= 1; --k) x.c[kNBuckets - k] = (160 * 1024 / k) / 512 * 512;
+      x.c[kNBuckets - 1] = 160 * 1024;
+    }
+    return x;
+  }();
+  return t;
+}
 constexpr int kStreams = 4;          // streams per device, one per hardware queue
 constexpr int kLanes = 8;            // chunk slots per device, two per stream: a stream always has
                                      // the next chunk queued behind the running one (no host gap)
 constexpr double kMergeRatio = 0.5;  // bucket merging (plan_chunk)
+constexpr int32_t kMinLaunch = 512;   // a smaller bucket rides along in a larger one's launch
 // Routed-off catalogs under kMidMaxVars variables run in 4-wave groups
 // (M_SPLIT4), larger ones in 8-wave groups (profiles/r01_group_waves_ab.jsonl).
 constexpr int32_t kMidMaxVars = 8192;
@@ -123,7 +155,7 @@ struct Launch {
 // chunk sit a record apart and every one is a cache miss).
 struct Head {
   int8_t place;   // -1 malformed, -2 too large, else the Mode
-  int8_t bucket;  // M_LDS: the LDS bucket (kCeilings)
+  int8_t bucket;  // M_LDS: the LDS bucket (ceilings())
   bool direct;    // the record is its own staged form (16-bit, 16-byte aligned)
   int32_t lds, inst_words, nid;
   int64_t sw, rec_bytes;
@@ -177,7 +209,8 @@ void read_head(Head& H, const int32_t* h, int64_t avail, int32_t opt_flags, bool
   if (nar) {
     H.place = M_LDS;
     int k = 0;
-    while (H.lds > kCeilings[k]) ++k;
+    const Ceilings& C = ceilings();
+    while (k < C.n - 1 && H.lds > C.c[k]) ++k;
     H.bucket = (int8_t)k;
     H.direct = aligned && (h[DP_H_FMT] == DP_FMT_U16 || dp_fmt_packed(h[DP_H_FMT]));
     return;
@@ -302,8 +335,10 @@ void plan_chunk(Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0,
     P.order.insert(P.order.end(), bg.begin(), bg.end());
   }
   P.big_base = 0;  // scratch_off is indexed from the first multi-wave workgroup (order index 0)
-  // Adjacent LDS buckets are merged into one launch while the merged request
-  // keeps at least kMergeRatio of the first bucket's workgroups per CU.
+  // LDS buckets, largest footprint first, are merged into the launch of the
+  // bucket before them (whose largest footprint the launch requests) while
+  // their members keep at least kMergeRatio of their own residency, or when
+  // they are too few for a launch of their own (its tail would be most of it).
   static const double merge = [] {  // diagnostic DEPPY_BUCKET_MERGE
     const char* m = std::getenv("DEPPY_BUCKET_MERGE");
     return m ? std::atof(m) : kMergeRatio;
@@ -311,18 +346,13 @@ void plan_chunk(Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0,
   int group_of[kNBuckets];
   Launch bl[kNBuckets];
   int64_t gsize[kNBuckets] = {};
-  int ng = 0, first_lds = 0;
-  for (int k = 0; k < kNBuckets; ++k) {
+  int ng = 0;
+  for (int k = kNBuckets - 1; k >= 0; --k) {
     if (!bcount[k]) continue;
-    const bool join = ng > 0 && merge > 0 &&
-                      (double)(kMaxLdsBytes / std::max(bmax[k], bl[ng - 1].lds)) >=
-                          merge * (double)(kMaxLdsBytes / first_lds);
-    if (join) {
-      bl[ng - 1].lds = std::max(bl[ng - 1].lds, bmax[k]);
-    } else {
-      first_lds = bmax[k];
-      bl[ng++] = Launch{0, 0, M_LDS, bmax[k]};
-    }
+    const bool join = ng > 0 && (bcount[k] < kMinLaunch ||
+                                 (merge > 0 && (double)(kMaxLdsBytes / bl[ng - 1].lds) >=
+                                                   merge * (double)(kMaxLdsBytes / bmax[k])));
+    if (!join) bl[ng++] = Launch{0, 0, M_LDS, bmax[k]};
     group_of[k] = ng - 1;
     gsize[ng - 1] += bcount[k];
   }
