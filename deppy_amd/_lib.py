@@ -334,7 +334,16 @@ class Context:
         the device-resident form and also returns the search trace
         (dp_upload_traced): trace[P, trace_cap], trace_len[P]."""
         if trace_cap <= 0:
-            return self.submit(rec_off, rec).wait()
+            rec_off = np.ascontiguousarray(rec_off, np.int64)
+            rec = np.ascontiguousarray(rec if len(rec) else np.zeros(1, np.int32), np.int32)
+            out = result_arrays(rec_off, rec)
+            r = _result_struct(out)
+            if lib().dp_solve(self.h, ctypes.byref(_batch(rec_off, rec)), ctypes.byref(r)) != 0:
+                raise RuntimeError("dp_solve: " + self.error())
+            n = len(rec_off) - 1
+            for k in ("status", "flags", "core_len", "steps"):
+                out[k] = out[k][:n]
+            return out
         r = self.upload(rec_off, rec, trace_cap)
         try:
             r.run()

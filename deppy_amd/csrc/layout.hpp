@@ -66,23 +66,28 @@ __host__ __device__ constexpr int32_t mode_cq(int mode) { return mode == M_LDS ?
 #define DP_IMP16 1
 #endif
 constexpr bool IMP16_LDS = DP_IMP16;
-// Two-watched-literal filter on the multi-wave placements: every clause row
-// keeps the two literals it watches (Layout::wp); a round reaches a row
-// through the occurrence lists as before, but evaluates it only when one of
-// its watches is false, and then moves the watches (solve_kernel.hpp
-// clause_unit).  0: plain occurrence-list propagation (the A/B baseline).
+// Two-watched-literal filter on the multi-wave placements (-DDP_2WL=1):
+// every clause row keeps the two literals it watches (Layout::wp); a round
+// reaches a row through the occurrence lists as before, but evaluates it only
+// when one of its watches is false, and then moves the watches
+// (solve_kernel.hpp clause_unit).  Bit-exact, and measured slower: config 4
+// kernel only 7.64k -> 6.50k res/s, config 5 720k -> 654k (the pair is one
+// more dependent read before a row, the rows it skips were short;
+// profiles/r03_c4_*.json, r03_c5_*.json).  Off: occurrence lists.
 #ifndef DP_2WL
-#define DP_2WL 1
+#define DP_2WL 0
 #endif
 __host__ __device__ constexpr bool mode_2wl(int mode) { return DP_2WL && mode != M_LDS; }
-// Row slots on the multi-wave placements (the compact hot image of a clause
-// row): 32 bytes per row in the HBM scratch, built during init -- the row's
-// watched pair, its length, and its literals inline when it has at most
-// five (else the row's offset into clause_lits).  A round reaches a row from
-// its watch entry with one 32-byte read instead of the offsets-then-literals
-// chain of the record.
+// Row slots on the multi-wave placements (-DDP_ROWSLOT=1; the compact hot
+// image of a clause row): 32 bytes per row in the HBM scratch, built during
+// init -- the row's watched pair, its length, and its literals inline when
+// it has at most five (else the row's offset into clause_lits).  A round
+// reaches a row from its watch entry with one 32-byte read instead of the
+// offsets-then-literals chain of the record.  Bit-exact, and measured
+// slower: config 4 kernel only 7.64k -> 7.30k res/s, with 2WL 6.41k (the
+// slots add 32 B a row to a working set that already misses L2).  Off.
 #ifndef DP_ROWSLOT
-#define DP_ROWSLOT 1
+#define DP_ROWSLOT 0
 #endif
 __host__ __device__ constexpr bool mode_rowslot(int mode) { return DP_ROWSLOT && mode != M_LDS; }
 constexpr int32_t ROWSLOT_INLINE = 5;

@@ -748,10 +748,27 @@ struct Task {
 // thread (worker_main): dp_submit only cuts a batch into chunks and queues
 // them here, so a caller thread never plans, stages, waits or scatters, and
 // every device of a multi-device context has its own submitting thread.
+// The latency path of a small synchronous dp_solve (the reference's one
+// problem per Solve, solve.go:53-119): on the caller's thread, through a
+// stream of its own, with the records read by the kernel from mapped pinned
+// memory (no H2D copy) and the results written back into it, completion
+// polled without sleeping.  Buffers grow once and stay.
+struct FastLane {
+  std::mutex mu;
+  hipStream_t s = nullptr;
+  hipEvent_t done = nullptr;
+  Buf h_in{nullptr, 0, true}, h_out{nullptr, 0, true};
+  Plan plan;
+  std::vector<uint8_t> bad;
+};
+constexpr int32_t kFastProblems = 16;    // dp_solve batches up to this many problems
+constexpr int64_t kFastWords = 1 << 16;  // and this many record words take the latency path
+
 struct Device {
   int ordinal = 0;
   Lane lanes[kLanes];
   int next = 0;  // resident launches: next lane
+  FastLane fast;
   // -- the worker's --
   std::thread worker;
   std::mutex qmu;                 // q and stop (and the wake-ups)
@@ -796,6 +813,7 @@ struct dp_ctx {
   int32_t chunk_problems = kChunkProblems;
   int64_t chunk_bytes = kChunkBytes;
   int32_t grid_cap = 0;  // test: workgroups of a queued launch (DEPPY_GRID_CAP; 0 = resident maximum)
+  bool fast_path = true;  // small dp_solve batches on the latency path (DEPPY_FAST_PATH=0: off)
   dp_stats st{};         // the caller-thread paths (resident batches)
   ~dp_ctx() { delete pool; }
 };
@@ -1190,6 +1208,39 @@ void worker_main(dp_ctx* ctx, Device* Dp) {
   }
 }
 
+// The latency path (FastLane): 0 solved, -1 error (ctx->err), 1 the batch
+// needs the pipeline (a multi-wave or malformed problem).
+int fast_solve(dp_ctx* ctx, Device& D, const dp_batch* b, dp_result* res) {
+  FastLane& F = D.fast;
+  std::lock_guard<std::mutex> lk(F.mu);
+  const int32_t n = b->n_problems;
+  F.bad.assign((size_t)n, 0);
+  dp::plan_chunk(F.plan, b->rec, b->rec_off, 0, n, ctx->flags, &F.bad, nullptr);
+  const Plan& P = F.plan;
+  if (!P.skip.empty() || !P.scratch_off.empty()) return 1;
+  if (hipSetDevice(D.ordinal) != hipSuccess) return 1;
+  const InLayout il = in_layout(P);
+  const OutLayout ol = out_layout(P);
+  if (F.h_in.reserve(il.end) != hipSuccess || F.h_out.reserve(ol.end) != hipSuccess) return 1;
+  int32_t* img = at<int32_t>(F.h_in.p, il.img);
+  for (int32_t i = 0; i < n; ++i)
+    if (!dp::stage_one(P, b->rec, b->rec_off, 0, i, img)) F.bad[(size_t)i] = 1;
+  fill_in_tables(P, il, F.h_in.p);
+  *at<int32_t>(F.h_out.p, ol.pool_len) = 0;
+  dp::KernelArgs a = kernel_args(il, ol, F.h_in.dev, F.h_out.dev, nullptr, ctx->budget);
+  dp_stats st{};
+  if (enqueue_launches(ctx, P, a, F.s, st) || hipEventRecord(F.done, F.s) != hipSuccess) return api_fail(ctx);
+  // poll: a sleeping wait costs more than the solve of one small catalog
+  hipError_t e;
+  while ((e = hipEventQuery(F.done)) == hipErrorNotReady) __builtin_ia32_pause();
+  if (e != hipSuccess) {
+    ctx->err = std::string("dp_solve (latency path): ") + hipGetErrorString(e);
+    return -1;
+  }
+  scatter(P, ol, F.h_out.p, 0, res);
+  return 0;
+}
+
 // The chunks of a batch: at most chunk_problems problems and chunk_bytes
 // record bytes each, and (several devices) at least one per device.
 void cut_chunks(const dp_ctx* ctx, const dp_job* job, std::vector<std::pair<int32_t, int32_t>>& out) {
@@ -1266,10 +1317,17 @@ dp_ctx* dp_create(const dp_opts* opts) {
   ctx->zc_out = env_i64("DEPPY_ZC_OUT", 1) != 0; // diagnostic: 0 = D2H copy of every chunk
   ctx->direct = env_i64("DEPPY_DIRECT", 1) != 0; // diagnostic: 0 = stage every chunk
   ctx->grid_cap = (int32_t)std::max<int64_t>(0, env_i64("DEPPY_GRID_CAP", 0));
+  ctx->fast_path = env_i64("DEPPY_FAST_PATH", 1) != 0;
   const int ht = dp::host_threads();
   ctx->pool = new dp::Pool(ht);
   const int per = std::max(2, ht / cnt);
   for (auto& D : ctx->dev) {
+    if (hipSetDevice(D.ordinal) != hipSuccess || hipStreamCreateWithFlags(&D.fast.s, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&D.fast.done, hipEventDisableTiming) != hipSuccess) {
+      dp::set_global_error("dp_create: cannot create the latency stream");
+      dp_destroy(ctx);
+      return nullptr;
+    }
     D.own_pool = cnt > 1;
     D.pool = D.own_pool ? new dp::Pool(per) : ctx->pool;
     D.worker = std::thread(worker_main, ctx, &D);
@@ -1289,6 +1347,14 @@ void dp_destroy(dp_ctx* ctx) {
     D.worker.join();
     if (D.own_pool) delete D.pool;
     D.pool = nullptr;
+  }
+  for (auto& D : ctx->dev) {
+    (void)hipSetDevice(D.ordinal);
+    if (D.fast.s) (void)hipStreamSynchronize(D.fast.s);
+    D.fast.h_in.release();
+    D.fast.h_out.release();
+    if (D.fast.done) (void)hipEventDestroy(D.fast.done);
+    if (D.fast.s) (void)hipStreamDestroy(D.fast.s);
   }
   for (auto& D : ctx->dev) {
     (void)hipSetDevice(D.ordinal);
@@ -1388,6 +1454,12 @@ int dp_job_wait(dp_ctx* ctx, dp_job* job) {
 }
 
 int dp_solve(dp_ctx* ctx, const dp_batch* b, dp_result* res) {
+  if (!ctx || !b || !res || b->n_problems < 0 || (b->n_problems > 0 && (!b->rec || !b->rec_off))) return -1;
+  if (b->n_problems > 0 && b->n_problems <= kFastProblems && b->rec_off[b->n_problems] <= kFastWords &&
+      ctx->fast_path) {
+    const int r = fast_solve(ctx, ctx->dev[0], b, res);
+    if (r <= 0) return r;  // (1: not for the latency path)
+  }
   dp_job* job = nullptr;
   if (dp_submit(ctx, b, res, &job)) return -1;
   return dp_job_wait(ctx, job);

@@ -369,8 +369,11 @@ int32_t dp_num_devices(const dp_ctx* ctx);
 /* Synchronous batch solve, host memory to host memory: the batched form of
  * (Solver).Solve (solve.go:53-119), which the reference also calls on host
  * memory.  Returns 0, or a negative whole-batch error (text in
- * dp_last_error); per-problem outcomes in res.  Equivalent to dp_submit +
- * dp_job_wait. */
+ * dp_last_error); per-problem outcomes in res.  The results equal dp_submit +
+ * dp_job_wait's.  A small batch of one-wavefront problems (up to 16, the
+ * reference's one problem per Solve) takes a latency path on the calling
+ * thread: the kernel reads the staged records from mapped pinned memory and
+ * writes the results back into it, and completion is polled. */
 int dp_solve(dp_ctx* ctx, const dp_batch* b, dp_result* res);
 
 /* Asynchronous host-to-host solve (serving loops; no reference counterpart:
