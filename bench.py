@@ -227,7 +227,7 @@ def main():
                     help="skip the host-to-host leg (profiling runs of the solve kernel)")
     ap.add_argument("--flags", type=int, default=0,
                     help="dp_opts.flags (diagnostic placements: 1 group, 2 HBM, 4 mid groups)")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02_pmc_traffic.jsonl"),
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r03_pmc_traffic.jsonl"),
                     help="HBM bytes per solve kernel dispatch from separate rocprofv3 --pmc passes; "
                          "used for roofline.traffic when its config/problems match")
     args = ap.parse_args()
@@ -317,10 +317,14 @@ def main():
         "host_ms_per_step": {k: round(st[k] / args.steps, 4) for k in ("stage_ms", "plan_ms", "wait_ms", "scatter_ms")},
         "allocs_in_timed_region": int(st["allocs"]),
         "direct_chunks_per_step": round(st["direct_chunks"] / args.steps, 2),
-        "bcp": {"visited_bytes_per_resolution": round(st["bcp_bytes"] / max(st["problems"], 1), 1),
-                "GBs": round(st["bcp_bytes"] / elapsed / 1e9, 2) if elapsed != float("inf") else None,
+        "bcp": {"visited_bytes_per_resolution": round(st["bcp_bytes"] / max(st["problems"], 1), 1)
+                if st["bcp_bytes"] else None,
+                "GBs": round(st["bcp_bytes"] / elapsed / 1e9, 2) if elapsed != float("inf") and st["bcp_bytes"]
+                else None,
                 "note": "bytes unit propagation reads (watch entries, row offsets, literals, values; in LDS "
-                        "for one-wavefront problems, HBM for multi-wave), counted in the kernel (dp_stats)"},
+                        "for one-wavefront problems, HBM for multi-wave), counted in the kernel (dp_stats); "
+                        "null: not counted (the register-capped one-wavefront build, used for small "
+                        "footprints, leaves the counter out to stay spill-free)"},
         "records_pinned": bool(lw.pinned),
         "classes": class_mix(res) if res is not None else None,
         "deterministic": bool(deterministic),

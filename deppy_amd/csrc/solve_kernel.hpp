@@ -58,6 +58,17 @@ enum { RS_SAT = 1, RS_UNSAT = -1, RS_BUDGET = 2 };
 #define DP_MAKE_ROOM 0
 #endif
 
+// BCP-visited bytes, counted per thread; -DDP_VIS=0 compiles
+// the counter out (register-pressure A/B).
+#ifndef DP_VIS
+#define DP_VIS 1
+#endif
+#if DP_VIS
+#define DP_VIS_ADD(x) vis_add(x)
+#else
+#define DP_VIS_ADD(x) ((void)0)
+#endif
+
 // Lanes of the wave hand values to each other through the working set (LDS,
 // or HBM): complete every access before the next phase.
 #ifndef DP_WSYNC_FENCE
@@ -131,9 +142,14 @@ __device__ __forceinline__ int64_t wallclock() {
 #endif
 namespace {
 
-template <int MODE>
+// MINW: the waves per SIMD the kernel is built for (solve_kernel).  The
+// register-capped one-wavefront build (config 3's small catalogs) does not
+// count BCP-visited bytes: the counter's VGPR took its spills from 3 to 12
+// VGPRs (an LDS counter per lane: 9).  The unbounded build counts them.
+template <int MODE, int MINW = 1>
 struct Group {
   using IX = typename std::conditional<MODE == M_LDS, uint16_t, int32_t>::type;
+  static constexpr bool NO_VIS = MODE == M_LDS && MINW > 1;
   static constexpr int NW = mode_waves(MODE);  // wavefronts per problem
   static constexpr int NT = 64 * NW;           // threads per problem
   static constexpr int WBUF = mode_wbuf(MODE);
@@ -180,6 +196,14 @@ struct Group {
   // BCP-visited bytes (this thread): the watch entries, row offsets, row
   // literals and their values that propagation reads
   uint32_t vis;
+  __device__ __forceinline__ void vis_add(uint32_t x) {
+    if constexpr (!NO_VIS) vis += x;
+  }
+  // the problem's BCP-visited bytes (group-uniform; 0: not counted)
+  __device__ __forceinline__ uint32_t vis_total() {
+    if constexpr (NO_VIS) return 0u;
+    else return (uint32_t)g_sum((int)vis);
+  }
   // ---- working set ----
   int8_t* val;
   IX *reason, *rs, *trail, *touched, *d_mark, *l_off, *l_lits, *dq, *stk;
@@ -1065,18 +1089,22 @@ struct Group {
 
   // clause row evaluation; the literal loads are issued four at a time.
   // Returns the row's one unassigned literal when it is unit, else -1.
+#ifndef DP_EVAL_UNROLL
+#define DP_EVAL_UNROLL 4
+#endif
   __device__ __forceinline__ int eval_clause(int r, const IX* lits, int a, int b, int& crow) {
     int nun = 0, ul = -1;
-    vis += 2 * sizeof(IX) + (uint32_t)(b - a) * (sizeof(IX) + 1);  // offsets, literals, their values
-    for (int j = a; j < b; j += 4) {
-      int l[4];
+    DP_VIS_ADD(2 * sizeof(IX) + (uint32_t)(b - a) * (sizeof(IX) + 1));  // offsets, literals, their values
+    constexpr int U = DP_EVAL_UNROLL;
+    for (int j = a; j < b; j += U) {
+      int l[U];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) l[k] = j + k < b ? (int)lits[j + k] : -1;
-      int x[4];
+      for (int k = 0; k < U; ++k) l[k] = j + k < b ? (int)lits[j + k] : -1;
+      int x[U];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) x[k] = l[k] >= 0 ? lit_val(l[k]) : -1;
+      for (int k = 0; k < U; ++k) x[k] = l[k] >= 0 ? lit_val(l[k]) : -1;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < U; ++k) {
         if (x[k] > 0) return -1;  // satisfied
         if (x[k] == 0) { ++nun; ul = l[k]; }
       }
@@ -1101,7 +1129,7 @@ struct Group {
   __device__ __forceinline__ int eval_clause_twl(int r, int a, int b, int& crow) {
     int nun = 0, ul = -1, n0 = -1, n1 = -1;
     bool sat = false;
-    vis += 2 * sizeof(IX);
+    DP_VIS_ADD(2 * sizeof(IX));
     for (int j = a; j < b && n1 < 0; j += 4) {
       int l[4];
 #pragma unroll
@@ -1112,7 +1140,7 @@ struct Group {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         if (l[k] < 0 || n1 >= 0) continue;
-        vis += sizeof(IX) + 1;
+        DP_VIS_ADD(sizeof(IX) + 1);
         if (x[k] > 0) sat = true;
         if (x[k] == 0) { ++nun; ul = l[k]; }
         if (x[k] >= 0) {
@@ -1131,7 +1159,7 @@ struct Group {
         const int l = clause_lits[j];
         if (lit_val(l) >= 0) continue;
         const int t = (int)rs[l >> 1];
-        vis += sizeof(IX);
+        DP_VIS_ADD(sizeof(IX));
         if (t > r0) { f1 = f0; r1 = r0; f0 = l; r0 = t; }
         else if (t > r1) { f1 = l; r1 = t; }
       }
@@ -1152,7 +1180,7 @@ struct Group {
     int x[ROWSLOT_INLINE];
 #pragma unroll
     for (int k = 0; k < ROWSLOT_INLINE; ++k) x[k] = k < len ? lit_val(lt[k]) : -1;
-    vis += (uint32_t)len * 1u;
+    DP_VIS_ADD((uint32_t)len * 1u);
 #pragma unroll
     for (int k = 0; k < ROWSLOT_INLINE; ++k) {
       if (k >= len) continue;
@@ -1175,7 +1203,7 @@ struct Group {
 #pragma unroll
         for (int k = 0; k < ROWSLOT_INLINE; ++k) {
           if (t[k] < 0) continue;
-          vis += sizeof(IX);
+          DP_VIS_ADD(sizeof(IX));
           if (t[k] > r0) { f1 = f0; r1 = r0; f0 = lt[k]; r0 = t[k]; }
           else if (t[k] > r1) { f1 = lt[k]; r1 = t[k]; }
         }
@@ -1201,7 +1229,7 @@ struct Group {
         if (TWL && !sweep) wv = __hip_atomic_load(&wpair[4 * r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int2 q = *reinterpret_cast<const int2*>(sp + 2);
         const int4 t = *reinterpret_cast<const int4*>(sp + 4);
-        vis += 32;
+        DP_VIS_ADD(32);
         if (TWL && !sweep && lit_val((int)(uint32_t)wv) >= 0 && lit_val((int)(uint32_t)(wv >> 32)) >= 0) return -1;
         if (q.x <= ROWSLOT_INLINE) {
           const int lt[ROWSLOT_INLINE] = {q.y, t.x, t.y, t.z, t.w};
@@ -1215,7 +1243,7 @@ struct Group {
       if (r < nc) {
         if (!sweep) {
           const uint64_t wv = __hip_atomic_load(&wpair[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          vis += 8;
+          DP_VIS_ADD(8);
           if (lit_val((int)(uint32_t)wv) >= 0 && lit_val((int)(uint32_t)(wv >> 32)) >= 0) return -1;
         }
         return eval_clause_twl(r, clause_off[r], clause_off[r + 1], crow);
@@ -1230,7 +1258,7 @@ struct Group {
   __device__ __forceinline__ void card_serial(int r, int& crow) {
     const int k = r - nc, a = card_off[k], b = card_off[k + 1];
     int cnt = 0, nun = 0;
-    vis += 3 * sizeof(IX) + (uint32_t)(b - a) * (sizeof(IX) + 1);
+    DP_VIS_ADD(3 * sizeof(IX) + (uint32_t)(b - a) * (sizeof(IX) + 1));
     for (int j = a; j < b; ++j) {
       const int x = val[card_lits[j]];
       cnt += (x > 0);
@@ -1268,7 +1296,7 @@ struct Group {
   // ncq counts the queue in the one-wavefront mode (a register); with several
   // wavefronts the queue length is the LDS counter S_NK.
   __device__ __forceinline__ void visit(int r, int& crow, int& ncq) {
-    vis += r >= 0 ? sizeof(IX) : 0;  // the watch entry
+    DP_VIS_ADD(r >= 0 ? sizeof(IX) : 0);  // the watch entry
     const bool ok = r >= 0 && row_on(r);
     const bool card = ok && r >= nc && r < nrows;
     const uint64_t m = __ballot(card);
@@ -1324,7 +1352,7 @@ struct Group {
       }
       const int v = lane < len ? (int)card_lits[a + lane] : -1;
       const int x = v >= 0 ? val[v] : 0;
-      vis += (v >= 0 ? sizeof(IX) + 1 : 0) + (lane == 0 ? 3 * sizeof(IX) : 0);  // positions, values; offsets, bound
+      DP_VIS_ADD((v >= 0 ? sizeof(IX) + 1 : 0) + (lane == 0 ? 3 * sizeof(IX) : 0));  // positions, values; offsets, bound
       const int cnt = __popcll(__ballot(v >= 0 && x > 0));
       if (cnt > bound) { crow = min(crow, r); continue; }
       if (!__ballot(v >= 0 && x == 0)) continue;
@@ -1342,7 +1370,7 @@ struct Group {
       const int j = j0 + lane;
       const int v = j < len ? (int)card_lits[a + j] : -1;
       const int x = v >= 0 ? val[v] : 0;
-      vis += v >= 0 ? sizeof(IX) + 1 : 0;
+      DP_VIS_ADD(v >= 0 ? sizeof(IX) + 1 : 0);
       cnt += __popcll(__ballot(v >= 0 && x > 0));
       any |= __ballot(v >= 0 && x == 0) != 0ull;
     }
@@ -2486,7 +2514,7 @@ __device__ __forceinline__ void put_out(ProblemOut* o, int status, int32_t flags
 }
 
 // Item k of the launch: one problem, start to finish.
-template <int MODE>
+template <int MODE, int MINW>
 __device__ __forceinline__ void solve_item(const KernelArgs& a, int k, int4* lds4) {
 #ifdef DP_STAMPS
   int64_t t[6];
@@ -2496,7 +2524,7 @@ __device__ __forceinline__ void solve_item(const KernelArgs& a, int k, int4* lds
   const WorkItem it = a.items[k];
   const int pid = it.pid;
   const int32_t* grec = a.rec + it.rec_off;
-  Group<MODE> W;
+  Group<MODE, MINW> W;
   char* hbm = MODE == M_LDS ? nullptr : reinterpret_cast<char*>(a.scratch + a.scratch_off[k]);
   if (!W.init(reinterpret_cast<char*>(lds4), hbm, grec)) {
     if (threadIdx.x == 0) {  // a malformed record: no solve (dp_rec_validate's verdict)
@@ -2511,7 +2539,7 @@ __device__ __forceinline__ void solve_item(const KernelArgs& a, int k, int4* lds
   if (a.stamps) W.dbg = reinterpret_cast<unsigned long long*>(a.stamps + (int64_t)DP_NSTAMP * pid + 12);
 #endif
   W.budget = a.budget;
-  if constexpr (Group<MODE>::LR)
+  if constexpr (Group<MODE, MINW>::LR)
     if (a.table_cap > 0 && a.table_cap - 1 < W.hmask) W.hmask = a.table_cap - 1;  // (a power of two)
   if (a.trace) {
     W.tr = a.trace + (int64_t)a.trace_cap * pid;
@@ -2520,7 +2548,7 @@ __device__ __forceinline__ void solve_item(const KernelArgs& a, int k, int4* lds
   uint32_t* inst = a.installed + it.inst_off;
   int32_t flags = 0;
   int status;
-  for (int i = W.tid; i < W.nbv; i += Group<MODE>::NT) inst[i] = 0;
+  for (int i = W.tid; i < W.nbv; i += Group<MODE, MINW>::NT) inst[i] = 0;
   DP_STAMP(1);
   const int base = W.base_propagate();
   DP_STAMP(2);
@@ -2567,7 +2595,7 @@ __device__ __forceinline__ void solve_item(const KernelArgs& a, int k, int4* lds
   }
 #endif
   if (W.tr_stop) flags |= DP_F_TRACE_TRUNCATED;
-  const uint64_t bcp = (uint32_t)W.g_sum((int)W.vis);  // (a problem reads well under 2 GB)
+  const uint64_t bcp = W.vis_total();  // (a problem reads well under 2 GB)
   if (W.tid == 0) {
     if (a.trace) a.trace_len[pid] = W.tr_len;
     put_out(a.out + pid, status, flags, clen, cat, W.steps, bcp);
@@ -2592,11 +2620,11 @@ solve_kernel(KernelArgs a) {
         const int k = *slot;
         __syncthreads();
         if (k >= a.n_items) return;
-        solve_item<MODE>(a, k, lds4);
+        solve_item<MODE, MINW>(a, k, lds4);
       }
     }
   }
-  solve_item<MODE>(a, (int)blockIdx.x, lds4);
+  solve_item<MODE, MINW>(a, (int)blockIdx.x, lds4);
 }
 
 // Workgroups of a queued launch's kernel one CU holds at once, by (device,
