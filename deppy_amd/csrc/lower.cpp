@@ -238,10 +238,16 @@ struct Fast {
   std::vector<int64_t> store64;
   int32_t *clause_off, *clause_lits, *clause_id, *card_off, *card_lits, *card_bound, *card_id;
   int32_t *var_choice_off, *choice_off, *choice_lits, *anchors, *owner_v, *owner_c, *first_s, *seq, *seq2;
+  int32_t* list_id;  // [nch] the identity of choice list k's Dependency (-1: folded to T)
   int64_t* first_c;
+  // DP_FMT_P16D sources of the choice lists (choice_sources' answer, known
+  // while the lists are made): valid while src_ok
+  uint8_t* src;
+  bool src_ok;
   int32_t nc, ncl, nk, nkl, nch, nchl, na, nid;
   void reset(size_t nv, size_t C, size_t A) {
-    const size_t need = (C + 1) + (A + C) + C + (C + 1) + A + C + C + (nv + 1) + (C + 1) + A + nv + 4 * C + 2 * (A + 1);
+    const size_t need = (C + 1) + (A + C) + C + (C + 1) + A + C + C + (nv + 1) + (C + 1) + A + nv + 5 * C + 2 * (A + 1) +
+                        (C + 4) / 4;
     if (store.size() < need) store.resize(need + need / 4);
     if (store64.size() < C + 1) store64.resize(C + 1 + C / 4);
     int32_t* q = store.data();
@@ -250,9 +256,12 @@ struct Fast {
     card_off = take(C + 1); card_lits = take(A); card_bound = take(C); card_id = take(C);
     var_choice_off = take(nv + 1); choice_off = take(C + 1); choice_lits = take(A); anchors = take(nv);
     owner_v = take(C); owner_c = take(C); first_s = take(C); seq2 = take(A + 1); seq = take(A + 1);
+    list_id = take(C);
+    src = reinterpret_cast<uint8_t*>(take((C + 4) / 4));
     (void)take(C);
     first_c = store64.data();
     nc = ncl = nk = nkl = nch = nchl = na = nid = 0;
+    src_ok = true;
     clause_off[0] = card_off[0] = var_choice_off[0] = choice_off[0] = 0;
   }
   void close_clause(int32_t id) {
@@ -455,7 +464,9 @@ struct Lowerer {
   // record of a DP_LOWER_NARROW batch then ends on a 16-byte boundary, so
   // each one's 16-bit form is the staged form as it is (runtime.cpp
   // start_chunk copies such batches to the device without staging them).
-  void narrow_last(Out& O, size_t base) const {
+  // src: the DP_FMT_P16D sources of its choice lists when the caller knows
+  // them (lower_fast), else nullptr (pack16 derives them: choice_sources).
+  void narrow_last(Out& O, size_t base, const uint8_t* src = nullptr) const {
     if (!narrow || O.nrec == base) return;
     int32_t* r = O.rec.data() + base;
     const int64_t words = r[DP_H_WORDS];
@@ -471,7 +482,7 @@ struct Lowerer {
         r[DP_H_FMT] = DP_FMT_I32W;
         phys = words + ext;
       }
-    } else if (packed && pack16(r)) {
+    } else if (packed && pack16(r, src)) {
       phys = dp_rec_phys_words(r);
     } else if (dp_rec_fits16(r)) {
       uint16_t* u = reinterpret_cast<uint16_t*>(r + DP_H_SIZE);
@@ -493,18 +504,23 @@ struct Lowerer {
   // (every identity one row, each row kind's identities ascending, lengths
   // below 256, DP_P16_TAIL_MAX): DP_FMT_P16D when its dependency rows imply
   // its choice lists, else DP_FMT_P16.  False leaves r as it is.
-  static bool pack16(int32_t* r) {
+  static bool pack16(int32_t* r, const uint8_t* src_known = nullptr) {
     if (!dp_rec_fits16(r) || r[DP_H_NID] != r[DP_H_NC] + r[DP_H_NK]) return false;
     const dp_rec_layout L = dp_rec_layout_of(r);
     const int32_t nc = r[DP_H_NC], nk = r[DP_H_NK], nv = r[DP_H_NV], nch = r[DP_H_NCH], nid = r[DP_H_NID];
     // DP_FMT_P16D when the dependency rows imply the choice lists exactly
     static thread_local std::vector<uint8_t> srcs;
-    if (srcs.size() < (size_t)nch + 1) srcs.resize((size_t)nch + 1);
     static const bool no_p16d = [] {  // diagnostic DEPPY_NO_P16D=1: explicit choice lists (DP_FMT_P16)
       const char* e = std::getenv("DEPPY_NO_P16D");
       return e && *e && *e != '0';
     }();
-    const bool derived = !no_p16d && choice_sources(r, L, srcs.data());
+    const uint8_t* sp = src_known;
+    bool derived = !no_p16d && sp;
+    if (!no_p16d && !sp) {
+      if (srcs.size() < (size_t)nch + 1) srcs.resize((size_t)nch + 1);
+      derived = choice_sources(r, L, srcs.data());
+      sp = srcs.data();
+    }
     for (int32_t i = 1; i < nc; ++i)
       if (r[L.clause_id + i] <= r[L.clause_id + i - 1]) return false;
     for (int32_t i = 1; i < nk; ++i)
@@ -541,7 +557,7 @@ struct Lowerer {
       put_lens(L.var_choice_off, nv);
       put_lens(L.choice_off, nch);
     } else {
-      std::memcpy(t, srcs.data(), (size_t)nch);
+      std::memcpy(t, sp, (size_t)nch);
       t += nch;
     }
     for (int32_t k = 0; k < nk; ++k) t[r[L.card_id + k] >> 3] |= (uint8_t)(1u << (r[L.card_id + k] & 7));
@@ -703,37 +719,136 @@ struct Lowerer {
     const int nv = (int)(v1 - v0);
     if (nv >= (1 << 28)) return 0;
     const uint64_t nstr = (uint64_t)w.n_strs;
+    const int64_t* const var_id = w.var_id;
+    const int64_t* const var_con_off = w.var_con_off;
+    const int32_t* const con_kind = w.con_kind;
+    const int32_t* const con_n = w.con_n;
+    const int64_t* const con_arg_off = w.con_arg_off;
+    const int64_t* const con_arg = w.con_arg;
+    uint64_t* const st_tag = W.st_tag.data();
+    int32_t* const st_idx = W.st_idx.data();
     // this path's stamps carry a tag of their own (lower_one may follow)
     const uint64_t tag = W.tag_of(p, true);
     for (int i = 0; i < nv; ++i) {
-      const uint64_t sid = (uint64_t)w.var_id[v0 + i];
-      if (sid >= nstr || w.var_con_off[v0 + i + 1] < w.var_con_off[v0 + i]) return -1;
-      if (W.st_tag[sid] == tag) return 0;  // a duplicate: lower_one reports it
-      W.st_tag[sid] = tag;
-      W.st_idx[sid] = i;
+      const uint64_t sid = (uint64_t)var_id[v0 + i];
+      if (sid >= nstr || var_con_off[v0 + i + 1] < var_con_off[v0 + i]) return -1;
+      if (st_tag[sid] == tag) return 0;  // a duplicate: lower_one reports it
+      st_tag[sid] = tag;
+      st_idx[sid] = i;
     }
-    const int64_t cb = nv ? w.var_con_off[v0] : 0, ce = nv ? w.var_con_off[v1] : 0;
-    const int64_t C = ce - cb, A = nv ? w.con_arg_off[ce] - w.con_arg_off[cb] : 0;
+    const int64_t cb = nv ? var_con_off[v0] : 0, ce = nv ? var_con_off[v1] : 0;
+    const int64_t C = ce - cb, A = nv ? con_arg_off[ce] - con_arg_off[cb] : 0;
     if (A < 0) return -1;
     // var of string id sid, -1 if not a variable of this problem, -2 if out of range
     auto var = [&](int64_t sid) -> int32_t {
       if ((uint64_t)sid >= nstr) return -2;
-      return W.st_tag[(size_t)sid] == tag ? W.st_idx[(size_t)sid] : -1;
+      return st_tag[(size_t)sid] == tag ? st_idx[(size_t)sid] : -1;
     };
     Fast& F = W.fast;
     F.reset((size_t)nv, (size_t)C, (size_t)A);
     W.fkey.reset();
+    // the record's counters and arrays in locals: stores through the int32
+    // arrays could alias F's int32 counters, which would then be reloaded
+    // and stored around every element
+    int32_t nc = 0, ncl = 0, nk = 0, nkl = 0, nch = 0, nchl = 0, na = 0, nid = 0;
+    bool src_ok = true;
+    int32_t* const clause_off = F.clause_off;
+    int32_t* const clause_lits = F.clause_lits;
+    int32_t* const clause_id = F.clause_id;
+    int32_t* const card_off = F.card_off;
+    int32_t* const card_lits = F.card_lits;
+    int32_t* const card_bound = F.card_bound;
+    int32_t* const card_id = F.card_id;
+    int32_t* const var_choice_off = F.var_choice_off;
+    int32_t* const choice_off = F.choice_off;
+    int32_t* const choice_lits = F.choice_lits;
+    int32_t* const anchors = F.anchors;
+    int32_t* const owner_v = F.owner_v;
+    int32_t* const owner_c = F.owner_c;
+    int32_t* const first_s = F.first_s;
+    int32_t* const list_id = F.list_id;
+    int64_t* const first_c = F.first_c;
+    uint8_t* const src = F.src;
+    auto close_clause = [&](int32_t id) {
+      clause_id[nc] = id;
+      clause_off[++nc] = ncl;
+    };
     for (int vi = 0; vi < nv; ++vi) {
-      const int64_t c0 = w.var_con_off[v0 + vi], c1 = w.var_con_off[v0 + vi + 1];
+      const int64_t c0 = var_con_off[v0 + vi], c1 = var_con_off[v0 + vi + 1];
       bool anchor = false;
       for (int64_t c = c0; c < c1; ++c) {
-        const int32_t kind = w.con_kind[c];
-        const int64_t a0 = w.con_arg_off[c], a1 = w.con_arg_off[c + 1];
+        const int32_t kind = con_kind[c];
+        const int64_t a0 = con_arg_off[c], a1 = con_arg_off[c + 1];
         if (a1 < a0) return -1;
         uint64_t key = 0;
         bool taut = false, hashed = false;
         int32_t* seq = F.seq;
         int32_t ns = 0;
+        const int ci = (int)(c - c0);
+        if (kind == DP_DEPENDENCY && a1 > a0) {
+          seq = choice_lits + nchl;  // the arguments are the Order() list, search.go:59-69
+          for (int64_t a = a0; a < a1; ++a) {
+            const int32_t d = var(con_arg[a]);
+            if (d < 0) return d == -2 ? -1 : 0;
+            seq[ns++] = d;
+          }
+          const int32_t k = nch;  // this constraint's choice list
+          nchl += ns;
+          choice_off[++nch] = nchl;
+          if (seq[0] == vi) {  // Or(!x_s, x_s) = T: a list without a row
+            list_id[k] = -1;
+            src_ok = false;
+            continue;
+          }
+          // K_DEP: only a Dependency of the same subject over the same
+          // candidate sequence builds the same Or chain, and a variable's
+          // constraints are lowered together, so the term is known iff an
+          // earlier list of this subject equals this one (its first
+          // writer's: the earliest such list)
+          int32_t k0 = var_choice_off[vi];
+          for (; k0 < k; ++k0) {
+            if (list_id[k0] < 0) continue;
+            const int32_t b0 = choice_off[k0];
+            if (choice_off[k0 + 1] - b0 == ns && std::equal(seq, seq + ns, choice_lits + b0)) break;
+          }
+          if (k0 < k) {
+            const int32_t id = list_id[k0];
+            list_id[k] = id;
+            owner_v[id] = vi;  // last writer wins, lit_mapping.go:69-72
+            owner_c[id] = ci;
+            // a repeat of the list that took the row (choice_sources: the
+            // nearest earlier list of the subject with this content and a row)
+            if (k - k0 > 255) src_ok = false;
+            else src[k] = (uint8_t)(k - k0);
+            continue;
+          }
+          const int32_t id = nid++;
+          list_id[k] = id;
+          owner_v[id] = vi;
+          owner_c[id] = ci;
+          first_c[id] = c;
+          first_s[id] = vi;
+          // the row (!s, d1..dn), each candidate once; none when s recurs (T)
+          const int32_t start = ncl;
+          clause_lits[ncl++] = 2 * vi + 1;
+          bool tautology = false;
+          for (int32_t j = 0; j < ns; ++j) {
+            const int32_t d = seq[j];
+            if (d == vi) { tautology = true; break; }
+            bool seen = false;
+            for (int32_t q = start + 1; q < ncl; ++q) seen |= clause_lits[q] == 2 * d;
+            if (!seen) clause_lits[ncl++] = 2 * d;
+          }
+          if (tautology) {
+            ncl = start;
+            src_ok = false;  // a list without a row
+          } else {
+            src_ok &= ncl - start == ns + 1;  // a repeated candidate: the row is shorter than the list
+            close_clause(id);
+          }
+          src[k] = 0;
+          continue;
+        }
         switch (kind) {
           case DP_MANDATORY:
             if (a1 != a0) return -1;
@@ -744,26 +859,12 @@ struct Lowerer {
             if (a1 != a0) return -1;
             key = key1(K_NEG, (uint32_t)vi);
             break;
-          case DP_DEPENDENCY: {
-            if (a1 == a0) { key = key1(K_NEG, (uint32_t)vi); break; }
-            uint64_t h = hmix(0x6465707300000000ULL, (uint64_t)vi);
-            seq = F.choice_lits + F.nchl;  // the arguments are the Order() list, search.go:59-69
-            for (int64_t a = a0; a < a1; ++a) {
-              const int32_t d = var(w.con_arg[a]);
-              if (d < 0) return d == -2 ? -1 : 0;
-              seq[ns++] = d;
-              h = hmix(h, (uint64_t)d);
-            }
-            F.nchl += ns;
-            F.choice_off[++F.nch] = F.nchl;
-            if (seq[0] == vi) { taut = true; break; }  // Or(!x_s, x_s) = T
-            key = keyh(K_DEP, h);
-            hashed = true;
+          case DP_DEPENDENCY:  // without candidates: !x_s
+            key = key1(K_NEG, (uint32_t)vi);
             break;
-          }
           case DP_CONFLICT: {
             if (a1 - a0 != 1) return -1;
-            const int32_t t = var(w.con_arg[a0]);
+            const int32_t t = var(con_arg[a0]);
             if (t < 0) return t == -2 ? -1 : 0;
             seq[ns++] = t;
             key = t == vi ? key1(K_NEG, (uint32_t)vi) : key2(K_CONF, (uint32_t)vi, (uint32_t)t);
@@ -771,17 +872,22 @@ struct Lowerer {
           }
           case DP_ATMOST: {
             const int64_t N = a1 - a0;
-            const int32_t n = w.con_n[c];
+            const int32_t n = con_n[c];
             for (int64_t a = a0; a < a1; ++a) {
-              const int32_t d = var(w.con_arg[a]);
+              const int32_t d = var(con_arg[a]);
               if (d < 0) return d == -2 ? -1 : 0;
               seq[ns++] = d;
             }
             if (n < 0) { key = key1(K_F, 0); break; }
             if (n >= N) { taut = true; break; }
             int32_t* srt = F.seq2;
-            std::copy(seq, seq + ns, srt);
-            std::sort(srt, srt + ns);
+            // insertion sort (AtMost rows are short)
+            for (int32_t j = 0; j < ns; ++j) {
+              const int32_t x = seq[j];
+              int32_t q = j;
+              for (; q > 0 && srt[q - 1] > x; --q) srt[q] = srt[q - 1];
+              srt[q] = x;
+            }
             for (int32_t j = 1; j < ns; ++j)
               if (srt[j] == srt[j - 1]) return 0;  // multiplicity: exact path
             if (N == 1) key = key1(K_NEG, (uint32_t)seq[0]);
@@ -798,58 +904,46 @@ struct Lowerer {
             return -1;
         }
         if (taut) continue;
-        const int ci = (int)(c - c0);
-        int32_t* slot = W.fkey.find_or_insert(key, F.nid);
-        if (*slot != F.nid) {  // a known term
+        int32_t* slot = W.fkey.find_or_insert(key, nid);
+        if (*slot != nid) {  // a known term
           const int32_t id = *slot;
-          if (hashed && !same_term(F, id, c, vi, seq, ns, var)) return 0;
-          F.owner_v[id] = vi;  // last writer wins, lit_mapping.go:69-72
-          F.owner_c[id] = ci;
+          if (hashed && !same_term(first_c, first_s, id, c, vi, seq, ns, var)) return 0;
+          owner_v[id] = vi;  // last writer wins, lit_mapping.go:69-72
+          owner_c[id] = ci;
           continue;
         }
-        const int32_t id = F.nid++;
-        F.owner_v[id] = vi;
-        F.owner_c[id] = ci;
-        F.first_c[id] = c;
-        F.first_s[id] = vi;
+        const int32_t id = nid++;
+        owner_v[id] = vi;
+        owner_c[id] = ci;
+        first_c[id] = c;
+        first_s[id] = vi;
         // the rows of a new identity, from its first writer (emit_rows)
         const uint64_t tg = key >> 60;
         if (tg == K_F) {
-          F.close_clause(id);
+          close_clause(id);
         } else if (tg == K_POS || tg == K_NEG) {
-          F.clause_lits[F.ncl++] = 2 * (int32_t)(key & 0x3fffffff) + (tg == K_NEG);
-          F.close_clause(id);
-        } else if (kind == DP_DEPENDENCY) {
-          const int32_t start = F.ncl;
-          F.clause_lits[F.ncl++] = 2 * vi + 1;
-          bool tautology = false;
-          for (int32_t j = 0; j < ns; ++j) {
-            const int32_t d = seq[j];
-            if (d == vi) { tautology = true; break; }
-            bool seen = false;
-            for (int32_t k = start; k < F.ncl; ++k) seen |= F.clause_lits[k] == 2 * d;
-            if (!seen) F.clause_lits[F.ncl++] = 2 * d;
-          }
-          if (tautology) F.ncl = start;  // no row
-          else F.close_clause(id);
+          clause_lits[ncl++] = 2 * (int32_t)(key & 0x3fffffff) + (tg == K_NEG);
+          close_clause(id);
         } else if (kind == DP_CONFLICT) {
-          F.clause_lits[F.ncl++] = 2 * vi + 1;
-          F.clause_lits[F.ncl++] = 2 * seq[0] + 1;
-          F.close_clause(id);
+          clause_lits[ncl++] = 2 * vi + 1;
+          clause_lits[ncl++] = 2 * seq[0] + 1;
+          close_clause(id);
         } else {  // AtMost over distinct variables
-          std::copy(seq, seq + ns, F.card_lits + F.nkl);
-          F.nkl += ns;
-          F.card_off[++F.nk] = F.nkl;
-          F.card_bound[F.nk - 1] = w.con_n[c];
-          F.card_id[F.nk - 1] = id;
+          std::copy(seq, seq + ns, card_lits + nkl);
+          nkl += ns;
+          card_off[++nk] = nkl;
+          card_bound[nk - 1] = con_n[c];
+          card_id[nk - 1] = id;
         }
       }
-      F.var_choice_off[vi + 1] = F.nch;
-      if (anchor) F.anchors[F.na++] = vi;
+      var_choice_off[vi + 1] = nch;
+      if (anchor) anchors[na++] = vi;
     }
+    F.nc = nc; F.ncl = ncl; F.nk = nk; F.nkl = nkl; F.nch = nch; F.nchl = nchl; F.na = na; F.nid = nid;
+    F.src_ok = src_ok;
     const size_t base = O.nrec;
     emit_fast(F, O, nv);
-    narrow_last(O, base);
+    narrow_last(O, base, src_ok ? src : nullptr);
     return 1;
   }
 
@@ -894,11 +988,11 @@ struct Lowerer {
   // resolved in seq[0..ns)) the one of identity id's first writer?  Same
   // kind, subject and argument sequence (and bound) build the same term.
   template <class Var>
-  bool same_term(const Fast& F, int32_t id, int64_t c, int s, const int32_t* seq, int32_t ns,
-                 const Var& var) const {
-    const int64_t f = F.first_c[id];
+  bool same_term(const int64_t* first_c, const int32_t* first_s, int32_t id, int64_t c, int s, const int32_t* seq,
+                 int32_t ns, const Var& var) const {
+    const int64_t f = first_c[id];
     if (w.con_kind[f] != w.con_kind[c]) return false;
-    if (w.con_kind[c] == DP_DEPENDENCY && F.first_s[id] != s) return false;
+    if (w.con_kind[c] == DP_DEPENDENCY && first_s[id] != s) return false;
     if (w.con_kind[c] == DP_ATMOST && w.con_n[f] != w.con_n[c]) return false;
     const int64_t a0 = w.con_arg_off[f], a1 = w.con_arg_off[f + 1];
     if (a1 - a0 != (int64_t)ns) return false;

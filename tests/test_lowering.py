@@ -219,6 +219,33 @@ def test_fast_lowering_equals_exact_aig(seed, monkeypatch):
         compare(fast, p, ref)
 
 
+@pytest.mark.parametrize("seed", [1, 5, 11])
+def test_fast_packed_records_equal_exact(seed, monkeypatch):
+    """The key path knows each choice list's DP_FMT_P16D source while it makes
+    the lists (a Dependency's first writer takes its row, a repeat names the
+    first writer's list); the exact path derives them from the finished
+    record (choice_sources).  Packed records are byte-for-byte equal, repeated
+    and folded Dependencies included."""
+    probs = _random_problems(seed, 400) + [
+        [V("a", sat.Dependency("b", "c"), sat.Dependency("c"), sat.Dependency("b", "c")), V("b", sat.Dependency("c")),
+         V("c")],
+        [V("a", sat.Dependency("b", "b")), V("b")],
+        [V("a", sat.Dependency("a")), V("b")],
+        [V("a", sat.Dependency("b", "a")), V("b", sat.Dependency("a"), sat.Dependency("a"))]]
+    wire = sat.encode_inputs(probs)
+    fast = _lib.Lowered(wire, narrow=True, packed=True)
+    monkeypatch.setenv("DEPPY_LOWER_EXACT", "1")
+    exact = _lib.Lowered(wire, narrow=True, packed=True)
+    assert exact.n_exact == len(probs) and fast.n_exact < 0.5 * len(probs)
+    np.testing.assert_array_equal(fast.rec_off, exact.rec_off)
+    np.testing.assert_array_equal(fast.rec, exact.rec)
+    np.testing.assert_array_equal(fast.ident_var, exact.ident_var)
+    np.testing.assert_array_equal(fast.ident_con, exact.ident_con)
+    assert fast.msg == exact.msg
+    fmts = np.array([int(fast.record(p)[13]) for p in range(fast.n)])
+    assert (fmts == 5).sum() > 0.3 * fast.n
+
+
 def test_relower_reuses_storage():
     a, b = _random_problems(7, 50), _random_problems(8, 80)
     lw = _lib.Lowered(sat.encode_inputs(a))
