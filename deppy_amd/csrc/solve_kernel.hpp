@@ -940,7 +940,19 @@ struct Group {
     const int n2 = 2 * nv + 1;
     for (int i = tid; i < n2; i += NT) cnt[i] = 0u;
     wsync();
-    for (int j = tid; j < ncl; j += NT) atomicAdd(&cnt[((int)clause_lits[j] ^ 1) + 1], 1u);
+    // four positions per lane per step: the loads first, then the atomics
+    // (one LDS round trip per step instead of one per position)
+    for (int j0 = 0; j0 < ncl; j0 += 4 * NT) {
+      int l[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int j = j0 + i * NT + tid;
+        l[i] = j < ncl ? (int)clause_lits[j] : -1;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (l[i] >= 0) atomicAdd(&cnt[(l[i] ^ 1) + 1], 1u);
+    }
     for (int k = tid; k < nk; k += NT) {
       const int a = card_off[k], b = card_off[k + 1];
       for (int j0 = a; j0 < b; j0 += 8) {
@@ -954,14 +966,26 @@ struct Group {
       }
     }
     wsync();
-    // lanes over 64 consecutive counters, DPP scan, carry across chunks
+    // eight consecutive counters per lane (independent loads), their sum
+    // scanned across the wave by DPP, then each lane's running prefix: one
+    // scan per 512 counters (a config-2 catalog has ~480)
     int carry = 0;
-    for (int b = 0; b < n2; b += 64) {
-      const int i = b + lane;
-      const int x = i < n2 ? (int)cnt[i] : 0;
-      const int incl = wave_incl_scan(x) + carry;
-      if (i < n2) { wo[i] = enc(incl); cnt[i] = (uint32_t)incl; }
-      carry = __builtin_amdgcn_readlane(incl, 63);
+    for (int b = 0; b < n2; b += 8 * NT) {
+      const int i0 = b + 8 * lane;
+      int x[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) x[q] = i0 + q < n2 ? (int)cnt[i0 + q] : 0;
+      int s = 0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s += x[q];
+      const int incl = wave_incl_scan(s);
+      int run = carry + incl - s;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        run += x[q];
+        if (i0 + q < n2) { wo[i0 + q] = enc(run); cnt[i0 + q] = (uint32_t)run; }
+      }
+      carry += __builtin_amdgcn_readlane(incl, 63);
     }
     wsync();
     for (int r = tid; r < nc; r += NT) {
