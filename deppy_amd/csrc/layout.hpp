@@ -111,6 +111,12 @@ __host__ __device__ inline int64_t p16_tail_bytes(const int32_t* h) {
   const int64_t vc = h[DP_H_FMT] == DP_FMT_P16D ? 0 : (int64_t)h[DP_H_NV];
   return (int64_t)h[DP_H_NC] + h[DP_H_NK] + h[DP_H_NCH] + vc + ((int64_t)h[DP_H_NID] + 7) / 8;
 }
+// Byte offset (in the M_LDS body region) of the packed tail's copy while the
+// kernel decodes it: the first 16-byte boundary past the decoded 16-bit
+// arrays, which end where the record's int32 form would (2 (words - 16)).
+__host__ __device__ inline int32_t p16_tail_copy(const int32_t* h) {
+  return (2 * (h[DP_H_WORDS] - DP_H_SIZE) + 15) & ~15;
+}
 
 // dp_rec_layout_of (include/deppy_hip.h) for host and device code.
 __host__ __device__ inline dp_rec_layout rec_layout(const int32_t* h) {
@@ -279,7 +285,15 @@ __host__ __device__ inline Layout layout(const int32_t* h) {
   L.cap = h[DP_H_NA] + h[DP_H_NCH] + 2;
   L.lcap = nv + 64;
   const ImgLayout X = img_layout(h);
-  L.body = MODE == M_LDS ? take((X.words - DP_H_SIZE + 8) * ix, COLD) : 0;  // +8: dwordx4 copy slack
+  // M_LDS: the record (16-bit) and its watch lists, +8 words of dwordx4 copy
+  // slack.  A packed record's tail is copied to p16_tail_copy (where the
+  // watch lists go later) while it is decoded: the region covers that copy.
+  int32_t body_bytes = (X.words - DP_H_SIZE + 8) * ix;
+  if (MODE == M_LDS && (h[DP_H_FMT] == DP_FMT_P16 || h[DP_H_FMT] == DP_FMT_P16D)) {
+    const int32_t need = p16_tail_copy(h) + (int32_t)((p16_tail_bytes(h) + 15) & ~15);
+    body_bytes = body_bytes > need ? body_bytes : need;
+  }
+  L.body = MODE == M_LDS ? take(body_bytes, COLD) : 0;
   L.scal = take(mode_nscal(MODE) * 4, WORK);
   L.wbuf = take(mode_wbuf(MODE) * ix, WORK);
   L.cardq = take(mode_cq(MODE) * ix, WORK);

@@ -88,6 +88,7 @@ const Ceilings& ceilings() {
   }();
   return t;
 }
+constexpr int kXcds = 8;             // MI355X: the dispatcher deals workgroups round-robin to 8 XCDs
 constexpr int kStreams = 4;          // streams per device, one per hardware queue
 constexpr int kLanes = 8;            // chunk slots per device, two per stream: a stream always has
                                      // the next chunk queued behind the running one (no host gap)
@@ -373,9 +374,33 @@ void plan_chunk(Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0,
   P.order.resize((size_t)o);
   for (int32_t i = 0; i < n; ++i)
     if (head[i].place == M_LDS) P.order[(size_t)at[group_of[head[i].bucket]]++] = i;
+  // XCD-contiguous order for one-wavefront launches up to this LDS request
+  // (DEPPY_XCD_ORDER, bytes; 0: longest record first everywhere).  Measured
+  // on one box against LPT: config 2 host to host 18.4-18.5M -> 20.3-20.6M
+  // res/s, kernel only 22.4M -> 23.9-24.2M; config 3 PMC writes per run
+  // 10.9 -> 6.5 MB; config 5 and 6 unchanged (scripts/xcd_ab.sh,
+  // profiles/r03_xcd_order_ab.txt).
+  static const int64_t xcd_order = env_i64("DEPPY_XCD_ORDER", kMaxLdsBytes);
   for (int r = 0; r < ng; ++r) {
     const int g = ix[r];
-    lpt(P.order.data() + bl[g].first, (size_t)bl[g].count);
+    if (xcd_order && bl[g].lds <= xcd_order) {
+      // XCD-contiguous: workgroup b runs on XCD b % kXcds, so the launch's
+      // members (in problem order) are cut into kXcds contiguous ranges and
+      // XCD x takes range x in problem order: neighbouring records (sharing
+      // their boundary lines) are read, and neighbouring results written,
+      // through one XCD's L2 at about the same time
+      int32_t* v = P.order.data() + bl[g].first;
+      const int32_t m = bl[g].count, base = m / kXcds, rem = m % kXcds;
+      P.tmp.assign(v, v + m);
+      int32_t start[kXcds];
+      for (int x = 0, s = 0; x < kXcds; ++x) {
+        start[x] = s;
+        s += base + (x < rem);
+      }
+      for (int32_t b = 0; b < m; ++b) v[b] = P.tmp[(size_t)(start[b % kXcds] + b / kXcds)];
+    } else {
+      lpt(P.order.data() + bl[g].first, (size_t)bl[g].count);
+    }
     P.launches.push_back(bl[g]);
   }
   static const int pad_kb = (int)env_i64("DEPPY_LDS_PAD_KB", 0);  // diagnostic (occupancy study)

@@ -75,7 +75,11 @@ enum { RS_SAT = 1, RS_UNSAT = -1, RS_BUDGET = 2 };
 #define DP_WSYNC_FENCE 1
 #endif
 __device__ __forceinline__ void wsync() {
-#if DP_WSYNC_FENCE
+#if DP_WSYNC_FENCE == 2
+  // (A/B) wavefront scope: a compiler barrier only -- one wave's LDS
+  // operations execute in program order, so no s_waitcnt is emitted
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#elif DP_WSYNC_FENCE
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
 #endif
   __builtin_amdgcn_wave_barrier();
@@ -95,6 +99,19 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
   y += __builtin_amdgcn_update_dpp(0, y, 0x118, 0xf, 0xc, false);  // row_shr:8, banks 2-3
   y += __builtin_amdgcn_update_dpp(0, y, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
   y += __builtin_amdgcn_update_dpp(0, y, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return y;
+}
+
+// Inclusive prefix maximum of non-negative values, the same DPP pattern.
+__device__ __forceinline__ int wave_incl_max(int x) {
+  int y = x;
+  y = max(y, __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true));   // row_shr:1
+  y = max(y, __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true));   // row_shr:2
+  y = max(y, __builtin_amdgcn_update_dpp(0, x, 0x113, 0xf, 0xf, true));   // row_shr:3
+  y = max(y, __builtin_amdgcn_update_dpp(0, y, 0x114, 0xf, 0xe, false));  // row_shr:4, banks 1-3
+  y = max(y, __builtin_amdgcn_update_dpp(0, y, 0x118, 0xf, 0xc, false));  // row_shr:8, banks 2-3
+  y = max(y, __builtin_amdgcn_update_dpp(0, y, 0x142, 0xa, 0xf, false));  // row_bcast:15 -> rows 1, 3
+  y = max(y, __builtin_amdgcn_update_dpp(0, y, 0x143, 0xc, 0xf, false));  // row_bcast:31 -> rows 2, 3
   return y;
 }
 
@@ -249,7 +266,8 @@ struct Group {
   // cycles, learned-row cycles, watch entries visited, frontier literals of
   // flattened rounds, learned rows evaluated, AtMost rows flushed
   unsigned long long* lacc;  // LDS phase accumulators (thread 0 adds; no registers held)
-  int64_t sub[3];           // init: record staging, validation, watch-list build cycles
+  int64_t sub[6];           // init: record staging, validation, watch-list build cycles;
+                            // the build's count, scan and fill
   unsigned long long* dbg;  // [first code, value, bound, failures]
   __device__ __noinline__ int chk_fail(int x, int hi, int code) {
     if (dbg) {
@@ -456,7 +474,7 @@ struct Group {
         card_id = q;     q += nk;
         if (derived) choice_lits = q;
         if (!unpack16(reinterpret_cast<const char*>(b) + p16_tail_at(h), (int)p16_tail_bytes(h), derived,
-                      lds + L.reason))
+                      lds + L.reason, reinterpret_cast<uint8_t*>(b) + p16_tail_copy(h)))
           return false;
       }
     } else {
@@ -535,7 +553,7 @@ struct Group {
     sub[0] = ti1 - ti0;
 #endif
     if constexpr (MODE == M_LDS)
-      if ((h[DP_H_FMT] == DP_FMT_U16 || packed) && !valid_record(body, packed)) return false;
+      if ((h[DP_H_FMT] == DP_FMT_U16 || packed) && !valid_record(body, packed, h[DP_H_FMT] == DP_FMT_P16D)) return false;
     if constexpr (MODE != M_LDS)
       if ((h[DP_H_FMT] == DP_FMT_I32W || h[DP_H_FMT] == DP_FMT_I32) && !valid_wide(R, X, h[DP_H_FMT] == DP_FMT_I32W))
         return false;
@@ -601,16 +619,26 @@ struct Group {
   // in an AtMost row form one run (16-bit bounds cannot be negative).  The
   // host checked every other staged form (DP_FMT_U16_CHECKED, DP_FMT_I32).
   // Array by array, two 16-bit words per LDS load.  Group-uniform result.
-  __device__ __forceinline__ bool valid_record(const IX* base, bool packed) {
+  __device__ __forceinline__ bool valid_record(const IX* base, bool packed, bool derived) {
     static_assert(MODE == M_LDS, "16-bit records run one wavefront per problem");
     // (base: the body's start, 16-byte aligned; arrays anywhere after it)
     const uint32_t* b32 = reinterpret_cast<const uint32_t*>(base);
     bool bad = false;
     auto range = [&](const IX* arr, int n, int hi) {
       const int a = (int)(arr - base), e = a + n;
-      for (int q = (a >> 1) + tid; 2 * q < e; q += NT) {
-        const uint32_t x = b32[q];
-        bad |= (2 * q >= a && (int)(x & 0xffffu) >= hi) || (2 * q + 1 < e && (int)(x >> 16) >= hi);
+      // four words per lane per step: the loads first
+      for (int q0 = (a >> 1); 2 * q0 < e; q0 += 4 * NT) {
+        uint32_t x[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int q = q0 + i * NT + tid;
+          x[i] = 2 * q < e ? b32[q] : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int q = q0 + i * NT + tid;
+          bad |= 2 * q < e && ((2 * q >= a && (int)(x[i] & 0xffffu) >= hi) || (2 * q + 1 < e && (int)(x[i] >> 16) >= hi));
+        }
       }
     };
     auto offsets = [&](const IX* arr, int n, int total) {  // n + 1 words
@@ -641,7 +669,7 @@ struct Group {
     }
     range(clause_lits, ncl, 2 * nv);
     range(card_lits, nkl, nv);
-    range(choice_lits, nchl, nv);
+    if (!derived) range(choice_lits, nchl, nv);  // (derived lists: unpack16 checked every index)
     range(anchors, na, nv);
     if (g_any(bad)) return false;  // the offsets below are now in range
     // a lane per AtMost row: its positions in registers (rows of up to 16:
@@ -718,35 +746,33 @@ struct Group {
 
   // DP_FMT_P16 tail (include/deppy_hip.h) -> the offsets arrays and the row
   // identities, in place after the uint16 arrays.  The tail (at most
-  // DP_P16_TAIL_MAX bytes) is first read into registers, 16 bytes a lane,
-  // since the decoded arrays overwrite it; a byte of it is then fetched from
-  // its lane by ds_bpermute.  Lengths become offsets by a DPP scan, the mask
-  // becomes clause / AtMost identities by ballot ranks.  False when the mask
-  // does not have nc clear and nk set bits (a malformed record).
+  // DP_P16_TAIL_MAX bytes) is first copied to `tcopy` (p16_tail_copy: past
+  // the decoded arrays, where the watch lists go later; layout() sizes the
+  // body for it), since the decoded arrays overwrite it; its bytes are then
+  // plain LDS loads.  Lengths become offsets by a DPP scan, the mask becomes
+  // clause / AtMost identities by ballot ranks.  False when the mask does
+  // not have nc clear and nk set bits (a malformed record).
   // DP_FMT_P16D (derived): the choice lists from the dependency rows and the
   // lists' sources (include/deppy_hip.h; lower.cpp implied_choices), with
   // `scratch` (the per-literal arrays' LDS, not yet in use) for the
   // dependency rows by rank, each list's row and the per-subject counts.
-  __device__ __forceinline__ bool unpack16(const char* tail, int tb, bool derived, char* scratch) {
+  __device__ __forceinline__ bool unpack16(const char* tail, int tb, bool derived, char* scratch, uint8_t* tcopy) {
     static_assert(MODE == M_LDS, "16-bit records run one wavefront per problem");
-    uint4 r = make_uint4(0u, 0u, 0u, 0u);
-    if (16 * lane < tb) r = *reinterpret_cast<const uint4*>(tail + 16 * lane);
-    wsync();
-    auto tbyte = [&](int i) -> int {  // wave-converged; i in [0, DP_P16_TAIL_MAX)
-      const int q = (i >> 4) & 63, sel = (i >> 2) & 3;
-      const uint32_t d0 = (uint32_t)__shfl((int)r.x, q), d1 = (uint32_t)__shfl((int)r.y, q);
-      const uint32_t d2 = (uint32_t)__shfl((int)r.z, q), d3 = (uint32_t)__shfl((int)r.w, q);
-      const uint32_t d = sel == 0 ? d0 : sel == 1 ? d1 : sel == 2 ? d2 : d3;
-      return (int)((d >> ((i & 3) * 8)) & 0xffu);
-    };
+    {
+      uint4 r = make_uint4(0u, 0u, 0u, 0u);
+      if (16 * lane < tb) r = *reinterpret_cast<const uint4*>(tail + 16 * lane);
+      if (16 * lane < tb) *reinterpret_cast<uint4*>(tcopy + 16 * lane) = r;
+      wsync();
+    }
+    auto tbyte = [&](int i) -> int { return (int)tcopy[i]; };  // i in [0, tb)
     int at = 0;
     auto lens = [&](const IX* off_c, int n) {
       IX* off = const_cast<IX*>(off_c);
       int carry = 0;
       for (int c = 0; c < n; c += 64) {
         const int j = c + lane;
-        const int x = tbyte(at + min(j, n - 1));
-        const int incl = wave_incl_scan(j < n ? x : 0) + carry;
+        const int x = j < n ? tbyte(at + j) : 0;
+        const int incl = wave_incl_scan(x) + carry;
         if (j < n) off[j + 1] = enc(incl);
         carry = __builtin_amdgcn_readlane(incl, 63);
       }
@@ -769,7 +795,7 @@ struct Group {
     for (int c = 0; c < nid; c += 64) {
       const int i = c + lane;
       const bool valid = i < nid;
-      const int byte = tbyte(at + (min(i, nid - 1) >> 3));
+      const int byte = valid ? tbyte(at + (i >> 3)) : 0;
       const bool bit = valid && ((byte >> (i & 7)) & 1);
       const uint64_t mb = __ballot(bit), mv = __ballot(valid);
       if (valid) {
@@ -803,8 +829,14 @@ struct Group {
       bool dep = false;
       if (r < nc) {
         const int a = clause_off[r], e = clause_off[r + 1];
-        dep = e - a >= 2 && ((int)clause_lits[a] & 1);
-        for (int j = a + 1; j < e && dep; ++j) dep = !((int)clause_lits[j] & 1);
+        // the row's first eight literals by independent loads, then the rest
+        int l[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) l[q] = a + q < e ? (int)clause_lits[a + q] : 0;
+        dep = e - a >= 2 && (l[0] & 1);
+#pragma unroll
+        for (int q = 1; q < 8; ++q) dep = dep && !(l[q] & 1);
+        for (int j = a + 8; j < e && dep; ++j) dep = !((int)clause_lits[j] & 1);
       }
       const uint64_t m = __ballot(dep);
       const int j = nd + __popcll(m & lt);
@@ -816,19 +848,19 @@ struct Group {
     int taken = 0, n0 = 0, smax = -1;
     for (int c = 0; c < nch; c += 64) {
       const int k = c + lane;
-      const int sv = tbyte(src_at + min(k, nch - 1));
+      const int sv = k < nch ? tbyte(src_at + k) : 0;
       const bool zero = k < nch && sv == 0;
       const uint64_t mz = __ballot(zero);
       const int j = taken + __popcll(mz & lt);
       taken += __popcll(mz);
+      // a repeat names an earlier list that took a row (written below, or
+      // in an earlier chunk)
+      const int ks = k - sv;
+      const int ss = k < nch && ks >= 0 ? tbyte(src_at + ks) : 1;
       if (zero) {
         bad |= j >= nd;
         rowk[k] = j < nd ? depr[j] : (uint16_t)0;
       }
-      // a repeat names an earlier list that took a row (written above or
-      // in an earlier chunk)
-      const int ks = k - sv;
-      const int ss = tbyte(src_at + max(0, min(ks, nch - 1)));
       wsync();
       if (k < nch && !zero) {
         bad |= ks < 0 || ss != 0;
@@ -844,22 +876,29 @@ struct Group {
       }
       const int incl = wave_incl_scan(x);
       const int n = n0 + incl - x;
-      int pm = s;  // the highest subject of the lists up to this one
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const int y = __shfl_up(pm, d);
-        if (lane >= d) pm = max(pm, y);
-      }
-      const int up = __shfl_up(pm, 1);
+      // the highest subject of the lists up to this one (a DPP max-scan of s + 1)
+      const int pm = wave_incl_max(s + 1) - 1;
+      const int up = __builtin_amdgcn_update_dpp(0, pm + 1, 0x138, 0xf, 0xf, false) - 1;  // wave_shr:1
       const int before = max(smax, lane > 0 ? up : -1);
       if (k < nch) {
         if (s >= nv || s < before || n + x > nchl) {
           bad = true;
         } else {
-          for (int q = 0; q < x; ++q) {
-            const int l = clause_lits[a + 1 + q];
-            bad |= (l >> 1) >= nv;
-            cl[n + q] = enc(l >> 1);
+          // the list: the row's literals after the first (eight by
+          // independent loads, then the rest)
+          int l[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) l[q] = q < x ? (int)clause_lits[a + 1 + q] : 0;
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            if (q < x) {
+              bad |= (l[q] >> 1) >= nv;
+              cl[n + q] = enc(l[q] >> 1);
+            }
+          for (int q = 8; q < x; ++q) {
+            const int lq = clause_lits[a + 1 + q];
+            bad |= (lq >> 1) >= nv;
+            cl[n + q] = enc(lq >> 1);
           }
           co[k + 1] = enc(n + x);
           atomicAdd(&cnt[s], 1u);
@@ -938,6 +977,9 @@ struct Group {
   __device__ __forceinline__ void build_watches(IX* wo, IX* ww, uint32_t* cnt) {
     static_assert(MODE == M_LDS, "the multi-wave modes read host-built watch lists");
     const int n2 = 2 * nv + 1;
+#ifdef DP_STAMPS
+    const int64_t tb0 = stamp();
+#endif
     for (int i = tid; i < n2; i += NT) cnt[i] = 0u;
     wsync();
     // four positions per lane per step: the loads first, then the atomics
@@ -966,6 +1008,10 @@ struct Group {
       }
     }
     wsync();
+#ifdef DP_STAMPS
+    const int64_t tb1 = stamp();
+    sub[3] = tb1 - tb0;
+#endif
     // eight consecutive counters per lane (independent loads), their sum
     // scanned across the wave by DPP, then each lane's running prefix: one
     // scan per 512 counters (a config-2 catalog has ~480)
@@ -988,6 +1034,10 @@ struct Group {
       carry += __builtin_amdgcn_readlane(incl, 63);
     }
     wsync();
+#ifdef DP_STAMPS
+    const int64_t tb2 = stamp();
+    sub[4] = tb2 - tb1;
+#endif
     for (int r = tid; r < nc; r += NT) {
       const int a = clause_off[r], b = clause_off[r + 1];
       for (int j0 = a; j0 < b; j0 += 8) {
@@ -1012,6 +1062,9 @@ struct Group {
       }
     }
     wsync();
+#ifdef DP_STAMPS
+    sub[5] = stamp() - tb2;
+#endif
   }
 
   // ------------------------------------------------------------------
@@ -1037,7 +1090,9 @@ struct Group {
     if constexpr (IMP16) {
       uint32_t* w32 = reinterpret_cast<uint32_t*>(imp) + (l >> 1);
       const int sh = (l & 1) * 16;
-      uint32_t old = *w32;
+      // optimistic first attempt: neither literal of the variable implied
+      // yet this round (the common case) -- no load before the first CAS
+      uint32_t old = 0xffffffffu;
       for (;;) {
         const uint32_t cur = (old >> sh) & 0xffffu;
         if ((uint32_t)r >= cur) return false;
@@ -1737,6 +1792,18 @@ struct Group {
   __device__ __forceinline__ bool card_fires(int k) const {
     const int a = card_off[k], b = card_off[k + 1], bound = card_bound[k];
     if (b - a <= bound) return false;
+    if (b - a <= 16) {  // the positions by independent loads, runs in registers
+      int v[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = a + i < b ? (int)card_lits[a + i] : -1 - i;
+      int run = 1, best = 1;
+#pragma unroll
+      for (int i = 1; i < 16; ++i) {
+        run = v[i] == v[i - 1] ? run + 1 : 1;
+        best = max(best, run);
+      }
+      return best > bound;
+    }
     for (int j = a; j < b;) {
       int e = j + 1;
       while (e < b && card_lits[e] == card_lits[j]) ++e;
@@ -2615,6 +2682,7 @@ __device__ __forceinline__ void solve_item(const KernelArgs& a, int k, int4* lds
     o[11] = wallclock();
     for (int i = 5; i < 16; ++i) o[11 + i] = (int64_t)W.lacc[i];
     for (int i = 0; i < 3; ++i) o[27 + i] = W.sub[i];
+    for (int i = 3; i < 6; ++i) o[45 + i] = W.sub[i];
     for (int i = 16; i < 32; ++i) o[16 + i] = (int64_t)W.lacc[i];
   }
 #endif

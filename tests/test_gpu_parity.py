@@ -414,6 +414,36 @@ def test_malformed_packed_records_found_by_the_kernel():
     assert compare_results(g, ref, lw.n, only=ok) == []
 
 
+def test_packed_tail_larger_than_watch_room_bit_exact():
+    """The kernel copies a packed record's tail past the decoded arrays (where
+    the watch lists go later) while it decodes it; layout() grows the body
+    when the tail is larger than that room: few variables with many repeated
+    Dependencies (DP_FMT_P16D with 200 repeats; DP_FMT_P16 with 200 repeats of
+    a Dependency that names its candidate twice, whose row is shorter than its
+    list), beside an ordinary catalog."""
+    probs = [[V("a", *[sat.Dependency("b") for _ in range(200)]), V("b", sat.Mandatory())],
+             [V("x", sat.Mandatory(), *[sat.Dependency("y", "y") for _ in range(200)]), V("y")],
+             [V("p", sat.Mandatory(), sat.Dependency("q")), V("q", sat.Prohibited())]]
+    wire = sat.encode_inputs(probs)
+    a = _lib.Lowered(wire)
+    b = _lib.Lowered(wire, narrow=True, packed=True, pinned=True)
+    fmts = [int(b.record(p)[13]) for p in range(b.n)]
+    assert fmts[0] == 5 and fmts[1] == 3, fmts
+    for p in range(b.n):  # the tail is larger than the record's watch-list room
+        h = b.record(p)
+        nv, nc, nk, nch, nid, ncl, nkl = (int(h[i]) for i in (1, 2, 3, 4, 6, 7, 8))
+        tb = nc + nk + nch + (nid + 7) // 8 + (nv if fmts[p] == 3 else 0)
+        if p < 2:
+            assert tb > 2 * (2 * nv + 1 + ncl + nkl), (p, tb)
+    c = _lib.Context(0, 1)
+    try:
+        g = c.submit(b.rec_off, b.rec).wait()
+    finally:
+        c.close()
+    assert compare_results(g, oracle.solve_batch(a.rec_off, a.rec, 0, 16), a.n) == []
+    assert list(g["status"]) == [1, 1, -1]
+
+
 def test_explicit_choice_packed_records_bit_exact():
     """DP_FMT_P16 records (explicit choice lists, as a producer that does not
     derive them packs them) are decoded by the kernel like DP_FMT_P16D."""
