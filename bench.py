@@ -52,7 +52,8 @@ sys.path.insert(0, ROOT)
 METRIC = "resolutions/sec (node) on synthetic catalogs at 1/2/4/8 GPUs; BCP HBM GB/s"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 PCIE_PEAK_GBS = 64.0   # PCIe Gen5 x16, one direction
-LANES = 8              # chunk slots per device (deppy_amd/csrc/runtime.cpp kLanes)
+# chunk slots per device: two per lane stream (deppy_amd/csrc/runtime.cpp, DEPPY_STREAMS, default 4)
+LANES = 2 * max(1, min(16, int(os.environ.get("DEPPY_STREAMS", "4") or 4)))
 
 # BASELINE.json configs as bench workloads: (catalogs per GPU, strong-scaling
 # total, description)

@@ -89,9 +89,10 @@ const Ceilings& ceilings() {
   return t;
 }
 constexpr int kXcds = 8;             // MI355X: the dispatcher deals workgroups round-robin to 8 XCDs
-constexpr int kStreams = 4;          // streams per device, one per hardware queue
-constexpr int kLanes = 8;            // chunk slots per device, two per stream: a stream always has
-                                     // the next chunk queued behind the running one (no host gap)
+constexpr int kStreams = 4;          // streams per device, one per hardware queue (DEPPY_STREAMS)
+constexpr int kMaxStreams = 16;
+constexpr int kMaxLanes = 2 * kMaxStreams;  // chunk slots per device, two per stream: a stream always
+                                            // has the next chunk queued behind the running one (no host gap)
 constexpr double kMergeRatio = 0.5;  // bucket merging (plan_chunk)
 constexpr int32_t kMinLaunch = 512;   // a smaller bucket rides along in a larger one's launch
 // Routed-off catalogs under kMidMaxVars variables run in 4-wave groups
@@ -511,7 +512,7 @@ int64_t stage_block(int64_t n, const Pool& pool) {
 // its staged copy is marked DP_FMT_REJECT and the kernel reports DP_ERROR /
 // DP_F_MALFORMED for it.
 bool stage_one(const Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0, int32_t i,
-               int32_t* dst) {
+               int32_t* dst, bool host_check) {
   const int64_t at = P.dev_off[(size_t)i], sw = P.img_off[(size_t)i + 1] - P.img_off[(size_t)i];
   if (sw == 0) return true;  // skipped (header already rejected)
   const int32_t* src = rec + rec_off[p0 + i];
@@ -524,6 +525,19 @@ bool stage_one(const Plan& P, const int32_t* rec, const int64_t* rec_off, int32_
       d[DP_H_FMT] = DP_FMT_U16_CHECKED;
       uint16_t* o = reinterpret_cast<uint16_t*>(d + DP_H_SIZE);
       if (!convert(src, src + DP_H_SIZE, o)) {
+        d[DP_H_FMT] = DP_FMT_REJECT;
+        return false;
+      }
+      for (int64_t j = body; j < 2 * (sw - DP_H_SIZE); ++j) o[j] = 0;
+    } else if (host_check) {
+      // a 16-bit form checked and expanded here (the latency path: one
+      // catalog's decode and validation cost the kernel more than the host)
+      static thread_local std::vector<int32_t> wide;
+      wide.resize((size_t)words);
+      d[DP_H_FMT] = DP_FMT_U16_CHECKED;
+      uint16_t* o = reinterpret_cast<uint16_t*>(d + DP_H_SIZE);
+      if (dp_rec_widen(src, rec_off[p0 + i + 1] - rec_off[p0 + i], wide.data()) != 0 ||
+          !convert(wide.data(), wide.data() + DP_H_SIZE, o)) {
         d[DP_H_FMT] = DP_FMT_REJECT;
         return false;
       }
@@ -791,7 +805,8 @@ constexpr int64_t kFastWords = 1 << 16;  // and this many record words take the 
 
 struct Device {
   int ordinal = 0;
-  Lane lanes[kLanes];
+  Lane lanes[kMaxLanes];
+  int nstreams = kStreams, nlanes = 2 * kStreams;
   int next = 0;  // resident launches: next lane
   FastLane fast;
   // -- the worker's --
@@ -1044,7 +1059,8 @@ size_t plan_cap(const Plan& P) {
 // finished first, since the GPU may still use its buffers.
 int grow_device_lanes(dp_ctx* ctx, Device& D, Lane& L, const LaneNeed& need) {
   if (reserve_lane(ctx, L, need)) return -1;
-  for (Lane& O : D.lanes) {
+  for (int li = 0; li < D.nlanes; ++li) {
+    Lane& O = D.lanes[li];
     if (&O == &L) continue;
     grow_plan(O.plan, L.plan);
     grow_vec(O.bad, L.bad.size());
@@ -1104,7 +1120,7 @@ int start_chunk(dp_ctx* ctx, Device& D, Lane& L, dp_job* job, int32_t p0, int32_
     int32_t* img = at<int32_t>(hin, il.img);
     D.pool->run(n, [&](int64_t i) {
       if (direct && P.direct[(size_t)i]) return;
-      if (!dp::stage_one(P, job->rec, job->rec_off, p0, (int32_t)i, img)) bad[(size_t)i] = 1;
+      if (!dp::stage_one(P, job->rec, job->rec_off, p0, (int32_t)i, img, false)) bad[(size_t)i] = 1;
     }, dp::stage_block(n, *D.pool));
     // (records found malformed while staging are reported by the kernel)
   }
@@ -1187,7 +1203,7 @@ void run_task(dp_ctx* ctx, Device& D, const Task& t) {
     return;
   }
   Lane& L = D.lanes[D.cursor];
-  D.cursor = (D.cursor + 1) % kLanes;
+  D.cursor = (D.cursor + 1) % D.nlanes;
   deliver(ctx, D, L);
   if (start_chunk(ctx, D, L, job, t.p0, t.n)) {
     L.job = nullptr;
@@ -1249,7 +1265,7 @@ int fast_solve(dp_ctx* ctx, Device& D, const dp_batch* b, dp_result* res) {
   if (F.h_in.reserve(il.end) != hipSuccess || F.h_out.reserve(ol.end) != hipSuccess) return 1;
   int32_t* img = at<int32_t>(F.h_in.p, il.img);
   for (int32_t i = 0; i < n; ++i)
-    if (!dp::stage_one(P, b->rec, b->rec_off, 0, i, img)) F.bad[(size_t)i] = 1;
+    if (!dp::stage_one(P, b->rec, b->rec_off, 0, i, img, true)) F.bad[(size_t)i] = 1;
   fill_in_tables(P, il, F.h_in.p);
   *at<int32_t>(F.h_out.p, ol.pool_len) = 0;
   dp::KernelArgs a = kernel_args(il, ol, F.h_in.dev, F.h_out.dev, nullptr, ctx->budget);
@@ -1316,14 +1332,18 @@ dp_ctx* dp_create(const dp_opts* opts) {
     Device& D = ctx->dev[(size_t)i];
     D.ordinal = d;
     ctx->copy_streams = env_i64("DEPPY_COPY_STREAM", 0) != 0;
-    for (int li = 0; li < kLanes; ++li) {
+    // diagnostic DEPPY_STREAMS: lane streams per device (two lanes each);
+    // more than GPU_MAX_HW_QUEUES (4) share hardware queues
+    D.nstreams = (int)std::min<int64_t>(kMaxStreams, std::max<int64_t>(1, env_i64("DEPPY_STREAMS", kStreams)));
+    D.nlanes = 2 * D.nstreams;
+    for (int li = 0; li < D.nlanes; ++li) {
       Lane& L = D.lanes[li];
       L.device = d;
-      if (li >= kStreams) {  // lane li shares the streams of lane li % kStreams
-        L.s = D.lanes[li % kStreams].s;
-        L.cs = D.lanes[li % kStreams].cs;
+      if (li >= D.nstreams) {  // lane li shares the streams of lane li % nstreams
+        L.s = D.lanes[li % D.nstreams].s;
+        L.cs = D.lanes[li % D.nstreams].cs;
       }
-      if ((li < kStreams && (hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking) != hipSuccess ||
+      if ((li < D.nstreams && (hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking) != hipSuccess ||
                              (ctx->copy_streams && hipStreamCreateWithFlags(&L.cs, hipStreamNonBlocking) != hipSuccess))) ||
           hipEventCreateWithFlags(&L.copied, hipEventDisableTiming) != hipSuccess ||
           hipEventCreate(&L.k0) != hipSuccess || hipEventCreate(&L.k1) != hipSuccess ||
@@ -1383,9 +1403,9 @@ void dp_destroy(dp_ctx* ctx) {
   }
   for (auto& D : ctx->dev) {
     (void)hipSetDevice(D.ordinal);
-    for (int li = 0; li < kStreams; ++li)
+    for (int li = 0; li < D.nstreams; ++li)
       if (D.lanes[li].s) (void)hipStreamSynchronize(D.lanes[li].s);
-    for (int li = 0; li < kLanes; ++li) {
+    for (int li = 0; li < D.nlanes; ++li) {
       Lane& L = D.lanes[li];
       for (Buf* b : {&L.h_in, &L.d_in, &L.h_out, &L.d_out, &L.scratch}) b->release();
       if (L.k0) (void)hipEventDestroy(L.k0);
@@ -1393,7 +1413,7 @@ void dp_destroy(dp_ctx* ctx) {
       if (L.done) (void)hipEventDestroy(L.done);
       if (L.copied) (void)hipEventDestroy(L.copied);
     }
-    for (int li = 0; li < kStreams; ++li) {  // (lanes li + kStreams... share these)
+    for (int li = 0; li < D.nstreams; ++li) {  // (lanes li + nstreams... share these)
       if (D.lanes[li].s) (void)hipStreamDestroy(D.lanes[li].s);
       if (D.lanes[li].cs) (void)hipStreamDestroy(D.lanes[li].cs);
     }
@@ -1533,7 +1553,7 @@ int build_slice(dp_ctx* ctx, Slice& s, const dp_batch* b, int32_t trace_cap) {
   int32_t* img = reinterpret_cast<int32_t*>(host.data() + s.il.img);
   const Plan& P = s.plan;
   ctx->pool->run(n, [&](int64_t i) {
-    if (!dp::stage_one(P, b->rec, b->rec_off, s.p0, (int32_t)i, img)) bad[(size_t)i] = 1;
+    if (!dp::stage_one(P, b->rec, b->rec_off, s.p0, (int32_t)i, img, false)) bad[(size_t)i] = 1;
   }, dp::stage_block(n, *ctx->pool));
   fill_in_tables(P, s.il, host.data());
   s.d_in.host = s.d_out.host = s.scratch.host = false;
@@ -1557,7 +1577,7 @@ int launch_slice(dp_ctx* ctx, Slice& s, int32_t trace_cap) {
   Device& D = ctx->dev[(size_t)s.d];
   HIP_OK(hipSetDevice(D.ordinal));
   s.stream = D.lanes[D.next].s;
-  D.next = (D.next + 1) % kLanes;
+  D.next = (D.next + 1) % D.nlanes;
   HIP_OK(hipMemsetAsync(s.d_out.p + s.ol.pool_len, 0, 4, s.stream));
   dp::KernelArgs a = kernel_args(s.il, s.ol, s.d_in.p, s.d_out.p, reinterpret_cast<int32_t*>(s.scratch.p),
                                  ctx->budget);
@@ -1756,7 +1776,7 @@ int dp_stage_roundtrip(const dp_batch* b, int32_t opt_flags, int32_t chunk_probl
     dp::plan_chunk(plan, b->rec, b->rec_off, p, q - p, opt_flags, &bad, &hook_pool());
     if (staged.size() < (size_t)plan.img_off[(size_t)plan.n] + 1) staged.resize((size_t)plan.img_off[(size_t)plan.n] + 1);
     hook_pool().run(q - p, [&](int64_t i) {
-      if (!dp::stage_one(plan, b->rec, b->rec_off, p, (int32_t)i, staged.data())) bad[(size_t)i] = 1;
+      if (!dp::stage_one(plan, b->rec, b->rec_off, p, (int32_t)i, staged.data(), false)) bad[(size_t)i] = 1;
     }, dp::stage_block(q - p, hook_pool()));
     for (auto x : bad)
       if (x) return -1;
