@@ -4,11 +4,12 @@
                     [--scaling weak|strong]
 
 The reference's Solve is a host-memory-to-host-memory call
-(pkg/sat/solve.go:53-119) and its benchmark times that whole call
-(pkg/sat/bench_test.go:66-77).  One step here is the same contract for a batch:
-lowered records in host memory -> dp_submit (stage, H2D, solve, D2H) ->
-results in host memory (dp_job_wait), for one batch of BASELINE config 2 by
-default: 10,000 synthetic operator catalogs (~200 bundle entities,
+(pkg/sat/solve.go:53-119).  Its benchmark times NewSolver(WithInput(...)) and
+Solve together (pkg/sat/bench_test.go:66-77), lowering included: that is the
+`end_to_end` figure below.  `value` times the leg BASELINE.md §3 defines for
+both the GPU and the CPU baseline: lowered records in host memory ->
+dp_submit (plan, H2D, solve, results into mapped host memory) -> results in
+host memory (dp_job_wait), for one batch of BASELINE config 2 by default: 10,000 synthetic operator catalogs (~200 bundle entities,
 Dependency + Conflict + AtMost; SURVEY.md §8(d) generator).  `--depth` jobs
 are in flight, as a serving loop keeps them (default: enough to give each of the
 pipeline's 8 chunk slots a chunk, 8 for a one-chunk batch): step i is submitted
@@ -18,8 +19,10 @@ result lands in host memory.
 `value` = resolutions/s over all ranks, host to host.  Secondary figures:
 `kernel_only` (the batch resident in HBM, relaunched: the rate the solve
 kernel alone sustains), `host_lowering_res_per_s` (wire format -> records,
-dp_lower, not in `value`), `latency` (one catalog alone, host to host, beside
-one CPU thread of the oracle).
+dp_lower, not in `value`), `end_to_end` (wire format -> lowering -> solve ->
+results, what BenchmarkSolve times, beside lowering + the oracle on the same
+cores), `latency` (one catalog alone, host to host, beside one CPU thread of
+the oracle).
 
 Multi-GPU: one process per GPU (torchrun); without WORLD_SIZE and --gpus N>1
 this script relaunches itself under torch.distributed.run before touching any
@@ -52,8 +55,7 @@ sys.path.insert(0, ROOT)
 METRIC = "resolutions/sec (node) on synthetic catalogs at 1/2/4/8 GPUs; BCP HBM GB/s"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 PCIE_PEAK_GBS = 64.0   # PCIe Gen5 x16, one direction
-# chunk slots per device: two per lane stream (deppy_amd/csrc/runtime.cpp, DEPPY_STREAMS, default 4)
-LANES = 2 * max(1, min(16, int(os.environ.get("DEPPY_STREAMS", "4") or 4)))
+LANES = 8  # chunk slots per device; replaced by the context's own count (dp_lanes) once it exists
 
 # BASELINE.json configs as bench workloads: (catalogs per GPU, strong-scaling
 # total, description)
@@ -250,10 +252,13 @@ def main():
         n, first = hi - lo, args.seed + lo
     lw, lw32, t_lower, wa = lowered_config(args.config, n, first, args.record_form)
     ctx = _lib.Context(local, 1, flags=args.flags)
+    global LANES
+    LANES = ctx.lanes()
 
     # host-to-host: depth jobs in flight, each the whole batch.  The pipeline
-    # has LANES chunk slots per device (runtime.cpp kLanes, two per stream);
-    # by default as many jobs are in flight as fill them.
+    # has LANES chunk slots per device (dp_lanes: two per lane stream, one
+    # stream per hardware queue); by default as many jobs are in flight as
+    # fill them.
     depth = args.depth
     if depth <= 0 and not args.kernel_only:  # (profiling runs count solve dispatches: none extra)
         ctx.stats(reset=True)

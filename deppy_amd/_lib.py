@@ -13,6 +13,12 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libdeppy_hip.so")
+# The pipeline runs 8 lane streams per device, each on a hardware queue of its
+# own: the HIP runtime opens GPU_MAX_HW_QUEUES (default 4) queues when it
+# initialises, so ask for 8 unless the caller chose (measured on one box,
+# config 2: host to host 20.9M -> 22.0M res/s, kernel only 25.5M -> 27.0M;
+# DESIGN.md §4).  Set before any HIP call of the process.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 # dp_opt_flag (include/deppy_hip.h): placement overrides
 OPT_FORCE_GROUP = 1 << 0
 OPT_FORCE_HBM = 1 << 1
@@ -35,7 +41,7 @@ EXPORTS = [
     "dp_rec_validate", "dp_lower", "dp_lowered_free", "dp_lowered_num_problems",
     "dp_lowered_rec_off", "dp_lowered_rec", "dp_lowered_ident_off", "dp_lowered_ident_var",
     "dp_lowered_ident_con", "dp_lowered_error", "dp_result_layout", "dp_create", "dp_destroy",
-    "dp_last_error", "dp_last_global_error", "dp_num_devices", "dp_solve", "dp_upload", "dp_run",
+    "dp_last_error", "dp_last_global_error", "dp_num_devices", "dp_lanes", "dp_solve", "dp_upload", "dp_run",
     "dp_launch", "dp_wait", "dp_download", "dp_resident_free", "dp_last_kernel_ms", "dp_gen_catalogs", "dp_gen_wire",
     "dp_gen_free", "dp_upload_traced", "dp_download_trace", "dp_solve_traced", "dp_lowered_errors",
     "dp_device_bytes", "dp_lower_into", "dp_lowered_new", "dp_lowered_exact_count", "dp_lowered_pinned", "dp_rec_widen", "dp_submit", "dp_job_wait", "dp_get_stats", "dp_stage_roundtrip",
@@ -122,6 +128,8 @@ def lib():
     L.dp_last_error.restype = ctypes.c_char_p
     L.dp_last_global_error.restype = ctypes.c_char_p
     L.dp_num_devices.argtypes = [vp]
+    L.dp_lanes.argtypes = [vp]
+    L.dp_lanes.restype = ctypes.c_int32
     L.dp_solve.argtypes = [vp, ctypes.POINTER(Batch), ctypes.POINTER(Result)]
     L.dp_upload.argtypes = [vp, ctypes.POINTER(Batch), ctypes.POINTER(vp)]
     L.dp_upload_traced.argtypes = [vp, ctypes.POINTER(Batch), ctypes.c_int32, ctypes.POINTER(vp)]
@@ -325,6 +333,10 @@ class Context:
 
     def error(self) -> str:
         return lib().dp_last_error(self.h).decode()
+
+    def lanes(self) -> int:
+        """Pipeline chunk slots per device (dp_lanes): chunks a serving loop keeps in flight."""
+        return int(lib().dp_lanes(self.h))
 
     def upload(self, rec_off: np.ndarray, rec: np.ndarray, trace_cap: int = 0) -> "Resident":
         return Resident(self, rec_off, rec, trace_cap)

@@ -1332,9 +1332,13 @@ dp_ctx* dp_create(const dp_opts* opts) {
     Device& D = ctx->dev[(size_t)i];
     D.ordinal = d;
     ctx->copy_streams = env_i64("DEPPY_COPY_STREAM", 0) != 0;
-    // diagnostic DEPPY_STREAMS: lane streams per device (two lanes each);
-    // more than GPU_MAX_HW_QUEUES (4) share hardware queues
-    D.nstreams = (int)std::min<int64_t>(kMaxStreams, std::max<int64_t>(1, env_i64("DEPPY_STREAMS", kStreams)));
+    // lane streams per device (two lanes each): one per hardware queue the
+    // HIP runtime opened (GPU_MAX_HW_QUEUES, 4 by default; the Python binding
+    // asks for 8), at most 8 -- 16 streams measured far slower host to host;
+    // DEPPY_STREAMS overrides (A/B)
+    const int64_t hwq = env_i64("GPU_MAX_HW_QUEUES", kStreams);
+    D.nstreams = (int)std::min<int64_t>(kMaxStreams, std::max<int64_t>(
+                                                         1, env_i64("DEPPY_STREAMS", std::min<int64_t>(hwq, 8))));
     D.nlanes = 2 * D.nstreams;
     for (int li = 0; li < D.nlanes; ++li) {
       Lane& L = D.lanes[li];
@@ -1423,6 +1427,7 @@ void dp_destroy(dp_ctx* ctx) {
 
 const char* dp_last_error(const dp_ctx* ctx) { return ctx ? ctx->err.c_str() : dp_last_global_error(); }
 int32_t dp_num_devices(const dp_ctx* ctx) { return ctx ? (int32_t)ctx->dev.size() : 0; }
+int32_t dp_lanes(const dp_ctx* ctx) { return ctx && !ctx->dev.empty() ? (int32_t)ctx->dev[0].nlanes : 0; }
 
 int dp_result_layout(const dp_batch* b, int64_t* inst_off, int64_t* core_off) {
   if (!b || !inst_off || !core_off || b->n_problems < 0) return -1;

@@ -365,6 +365,11 @@ void dp_destroy(dp_ctx* ctx);
 const char* dp_last_error(const dp_ctx* ctx);
 const char* dp_last_global_error(void);
 int32_t dp_num_devices(const dp_ctx* ctx);
+/* Pipeline chunk slots (lanes) per device: two per lane stream.  The
+ * streams per device follow GPU_MAX_HW_QUEUES (one stream per hardware
+ * queue, at most 8; 4 when it is not set) unless DEPPY_STREAMS says.  A
+ * serving loop keeps this many chunks in flight per device. */
+int32_t dp_lanes(const dp_ctx* ctx);
 
 /* Synchronous batch solve, host memory to host memory: the batched form of
  * (Solver).Solve (solve.go:53-119), which the reference also calls on host
