@@ -15,10 +15,15 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libdeppy_hip.so")
 # The pipeline runs 8 lane streams per device, each on a hardware queue of its
 # own: the HIP runtime opens GPU_MAX_HW_QUEUES (default 4) queues when it
-# initialises, so ask for 8 unless the caller chose (measured on one box,
+# initialises, so raise it to 8 (a larger setting stays; measured on one box,
 # config 2: host to host 20.9M -> 22.0M res/s, kernel only 25.5M -> 27.0M;
 # DESIGN.md §4).  Set before any HIP call of the process.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+try:
+    _hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)
+except ValueError:
+    _hwq = 0
+if _hwq < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 # dp_opt_flag (include/deppy_hip.h): placement overrides
 OPT_FORCE_GROUP = 1 << 0
 OPT_FORCE_HBM = 1 << 1
