@@ -75,6 +75,10 @@ constexpr int kQueueWords = 64;
 // Launch one workgroup per problem of order[0..n_blocks) with lds_bytes of
 // LDS: one wavefront (mode M_LDS) or BIG_WAVES wavefronts (M_SPLIT, M_HBM).
 hipError_t launch_solve(const KernelArgs& a, int mode, int n_blocks, int lds_bytes, hipStream_t stream);
+// Before a multi-wave launch (mode M_SPLIT / M_SPLIT4 / M_HBM) of n_items
+// items: the watch lists of its DP_FMT_I32 records above DEV_WATCH_VARS
+// variables into their scratch (watch_build.hip).  Other items are skipped.
+hipError_t launch_watch_build(const KernelArgs& a, int mode, int n_items, hipStream_t stream);
 // Raise the kernel's dynamic-LDS limit to the device maximum.
 hipError_t configure_solve_kernel(int max_lds_bytes);
 

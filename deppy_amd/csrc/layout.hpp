@@ -164,10 +164,12 @@ __host__ __device__ inline dp_rec_layout rec_layout(const int32_t* h) {
 // unread, Group::valid_record).
 enum { DP_FMT_REJECT = 2, DP_FMT_U16_CHECKED = 16, DP_FMT_I32_CHECKED = 17 };
 
-// Multi-wave problems of up to DEV_WATCH_VARS variables cross PCIe as plain
-// int32 records (DP_FMT_I32, no watch lists): the kernel builds their watch
-// lists in its HBM scratch (Layout::wl) with counters in the LDS work area
-// (Group::build_watches_wide).  Larger ones take DP_FMT_I32W.
+// Multi-wave problems cross PCIe as plain int32 records (DP_FMT_I32, no watch
+// lists), and their watch lists are built on the device in the problem's HBM
+// scratch (Layout::wl): up to DEV_WATCH_VARS variables by the solving
+// workgroup with counters in the LDS work area (Group::build_watches_wide),
+// above it by grid-wide passes before the launch (watch_build.hip).  A
+// caller may also send DP_FMT_I32W (record + host-built lists).
 constexpr int32_t DEV_WATCH_VARS = 2048;
 __host__ __device__ inline bool device_watches(const int32_t* h) { return h[DP_H_NV] <= DEV_WATCH_VARS; }
 // Its 2nv+1 counters span the work list and the AtMost queue after it
@@ -242,7 +244,7 @@ struct Layout {
   int32_t hc;        // slots (a power of two; 0 when the mode keeps rounds in HBM)
   int32_t wp;        // (mode_rowslot) i32[8][nc] row slots {watch x, watch y, len, l0 | offset, l1..l4};
                      // else (mode_2wl) u64[nc] the two literals clause row r watches, low word first
-  int32_t wl;        // multi-wave, DP_FMT_I32 records: device-built w_off[2nv+1], w[ncl+nkl]  [HBM, last]
+  int32_t wl;        // multi-wave, DP_FMT_I32 records: device-built w_off[2nv+2], w[ncl+nkl]  [HBM, last]
   int32_t bytes;     // HBM scratch bytes (0 for M_LDS)
   int32_t lds_bytes; // LDS bytes
   int32_t cap, lcap;
@@ -332,8 +334,7 @@ __host__ __device__ inline Layout layout(const int32_t* h) {
   L.dq = take(2 * L.cap * ix, COLD);
   L.stk = take(3 * L.cap * ix, COLD);
   L.wp = mode_rowslot(MODE) ? take(h[DP_H_NC] * 32, COLD) : mode_2wl(MODE) ? take(h[DP_H_NC] * 8, COLD) : 0;
-  L.wl = MODE != M_LDS && h[DP_H_FMT] == DP_FMT_I32 && device_watches(h)
-             ? take((2 * nv + 1 + h[DP_H_NCL] + h[DP_H_NKL]) * 4, COLD) : 0;
+  L.wl = MODE != M_LDS && h[DP_H_FMT] == DP_FMT_I32 ? take((2 * nv + 2 + h[DP_H_NCL] + h[DP_H_NKL]) * 4, COLD) : 0;
   L.bytes = og;
   L.lds_bytes = ol;
   return L;

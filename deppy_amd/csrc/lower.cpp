@@ -457,7 +457,11 @@ struct Lowerer {
   const dp_wire& w;
   const bool narrow;  // DP_LOWER_NARROW: records that fit 16 bits in the DP_FMT_U16 form
   const bool packed;  // DP_LOWER_PACKED: ... in the DP_FMT_P16 form where they allow it
-  Lowerer(const dp_wire& wire, bool narrow16, bool packed16) : w(wire), narrow(narrow16), packed(packed16) {}
+  // diagnostic DEPPY_HOST_WATCHES=1: multi-wave records above DEV_WATCH_VARS
+  // variables carry host-built watch lists (DP_FMT_I32W), as before round 3
+  const bool host_watches;
+  Lowerer(const dp_wire& wire, bool narrow16, bool packed16, bool host_lists)
+      : w(wire), narrow(narrow16), packed(packed16), host_watches(host_lists) {}
 
   // The last record appended to O (int32 words from `base`) in the 16-bit
   // form, in place (word j -> halfword j never overtakes word j).  Every
@@ -472,9 +476,9 @@ struct Lowerer {
     const int64_t words = r[DP_H_WORDS];
     int64_t phys = words;
     if (!one_wave(r)) {
-      // a multi-wave problem: its staged form -- with watch lists, or as it
-      // is for the kernel to build them (layout.hpp device_watches)
-      if (!device_watches(r)) {
+      // a multi-wave problem: its staged form is the int32 record as it is
+      // (the device builds its watch lists, layout.hpp DEV_WATCH_VARS)
+      if (host_watches && !device_watches(r)) {
         const int64_t ext = 2 * (int64_t)r[DP_H_NV] + 1 + r[DP_H_NCL] + r[DP_H_NKL];
         O.extend((size_t)ext);  // (may move the storage)
         r = O.rec.data() + base;
@@ -1250,8 +1254,10 @@ int dp_lower_into(const dp_wire* wire, int32_t flags, dp_lowered* lw) {
   }
   lw->pieces.resize((size_t)nchunks);
   lw->n_exact.store(0);
-  dp::Lowerer L(*wire, (flags & DP_LOWER_NARROW) != 0, (flags & (DP_LOWER_NARROW | DP_LOWER_PACKED)) ==
-                                                          (DP_LOWER_NARROW | DP_LOWER_PACKED));
+  const char* hw = std::getenv("DEPPY_HOST_WATCHES");
+  dp::Lowerer L(*wire, (flags & DP_LOWER_NARROW) != 0,
+                (flags & (DP_LOWER_NARROW | DP_LOWER_PACKED)) == (DP_LOWER_NARROW | DP_LOWER_PACKED),
+                hw && *hw && *hw != '0');
   std::atomic<bool> bad{false};
   auto lower_chunk = [&](int64_t c, int t) {
     dp::Work& W = lw->work[(size_t)t];

@@ -150,6 +150,7 @@ namespace dp {
 // ---------------------------------------------------------------------------
 struct Launch {
   int first, count, mode, lds;
+  bool dev_lists;  // holds int32 records whose watch lists the grid-wide passes build (watch_build.hip)
 };
 
 // What the plan needs of one record, from its header alone (one cache line
@@ -218,8 +219,8 @@ void read_head(Head& H, const int32_t* h, int64_t avail, int32_t opt_flags, bool
     return;
   }
   // the multi-wave staged forms: with host-built watch lists, or plain int32
-  // for the kernel to build them (layout.hpp device_watches)
-  H.direct = aligned && (h[DP_H_FMT] == DP_FMT_I32W || (h[DP_H_FMT] == DP_FMT_I32 && dp::device_watches(h)));
+  // for the device to build them (layout.hpp DEV_WATCH_VARS)
+  H.direct = aligned && (h[DP_H_FMT] == DP_FMT_I32W || h[DP_H_FMT] == DP_FMT_I32);
   const bool forced = forced_of(opt_flags);
   // (layout arithmetic is int32: variables are capped well below its range)
   const bool sized = h[DP_H_NV] < (1 << 24) && h[DP_H_NID] < (1 << 26) && h[DP_H_WORDS] < (1 << 28);
@@ -323,9 +324,10 @@ void plan_chunk(Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0,
     if (bg.empty()) continue;
     lpt(bg.data(), bg.size());
     int mx = 0;
-    Launch L{(int)P.order.size(), (int)bg.size(), mode, 0};
+    Launch L{(int)P.order.size(), (int)bg.size(), mode, 0, false};
     for (int32_t i : bg) {
       const int32_t* h = rec + rec_off[p0 + i];
+      L.dev_lists |= h[DP_H_FMT] == DP_FMT_I32 && !dp::device_watches(h);
       const Layout Y = mode == M_SPLIT ? layout<M_SPLIT>(h) : mode == M_SPLIT4 ? layout<M_SPLIT4>(h) : layout<M_HBM>(h);
       mx = std::max(mx, Y.lds_bytes);
       if (P.scratch_words == 0) P.scratch_words = dp::kQueueWords;  // the launches' queues first
@@ -939,6 +941,7 @@ int enqueue_launches(dp_ctx* ctx, const Plan& P, const dp::KernelArgs& base, hip
       if (ctx->flags & DP_OPT_TINY_TABLE) a.table_cap = 4;
       a.grid_cap = ctx->grid_cap;
       ++q;
+      if (L.dev_lists) HIP_OK(dp::launch_watch_build(a, L.mode, L.count, s));
     }
     HIP_OK(dp::launch_solve(a, L.mode, L.count, L.lds, s));
     st.launches++;

@@ -568,10 +568,11 @@ struct Group {
                     reinterpret_cast<uint32_t*>(lds + L.reason));
       w_off = rv(X.w_off); w = rv(X.w);
     } else {
-      if (h[DP_H_FMT] == DP_FMT_I32) {  // plain int32 record: the lists into scratch (layout.hpp wl)
+      if (h[DP_H_FMT] == DP_FMT_I32) {  // plain int32 record: the lists in scratch (layout.hpp wl)
         IX* wo = reinterpret_cast<IX*>(hbm + L.wl);
-        build_watches_wide(wo, wo + 2 * nv + 1, reinterpret_cast<uint32_t*>(lds + L.wbuf));
-        w_off = wo; w = wo + 2 * nv + 1;
+        if (device_watches(h)) build_watches_wide(wo, wo + 2 * nv + 2, reinterpret_cast<uint32_t*>(lds + L.wbuf));
+        // (else built by the passes before this launch, watch_build.hip)
+        w_off = wo; w = wo + 2 * nv + 2;
       } else {
         w_off = rv(X.w_off); w = rv(X.w);  // host-built, staged after the record
       }

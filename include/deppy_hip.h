@@ -190,12 +190,12 @@ static inline dp_rec_layout dp_rec_layout_of(const int32_t* h) {
  *   zero padding to a 16-byte boundary (from the body's start)
  *   uint8  clause_len[nc], card_len[nk], src[nch], card_mask[(nid+7)/8]
  *
- * DP_FMT_I32W: the int32 form followed by its watch lists, the form a
- * problem solved by a multi-wave workgroup is staged in (dp_lower_into
- * DP_LOWER_NARROW emits it for the records that do not run one wavefront
- * per problem and have over 2048 variables, so that they too go to the
- * device as they lie; smaller multi-wave records stay DP_FMT_I32 and the
- * kernel builds their watch lists):
+ * DP_FMT_I32W: the int32 form followed by its watch lists, a form a problem
+ * solved by a multi-wave workgroup may be staged in as it lies.  dp_lower_into
+ * emits multi-wave records as DP_FMT_I32 (the device builds their watch
+ * lists: in the solving workgroup up to 2048 variables, by grid-wide passes
+ * before the launch above it); a caller that has the lists may send this form
+ * instead, and the kernel checks their bounds:
  *   int32 w_off[2nv+1]  rows literal l wakes: w[w_off[l] .. w_off[l+1]) (the
  *                       clauses holding ~l; when l = 2v is positive, the
  *                       AtMost rows holding v, once each)

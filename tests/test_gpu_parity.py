@@ -461,12 +461,14 @@ def test_explicit_choice_packed_records_bit_exact():
     assert compare_results(g, oracle.solve_batch(a.rec_off, a.rec, 0, 16), a.n) == []
 
 
-def test_wide_records_direct_and_validated():
+def test_wide_records_direct_and_validated(monkeypatch):
     """Multi-wave records in the DP_FMT_I32W form (record + watch lists, as
-    dp_lower_into DP_LOWER_NARROW emits them) go to the device as they lie;
-    the kernel checks their bounds: a watch entry past the rows, a clause
-    literal past 2nv -> DP_F_MALFORMED for that problem, the rest exact."""
+    dp_lower_into emits them under DEPPY_HOST_WATCHES=1) go to the device as
+    they lie; the kernel checks their bounds: a watch entry past the rows, a
+    clause literal past 2nv -> DP_F_MALFORMED for that problem, the rest
+    exact."""
     a = lowered_config(5, 120, 121)
+    monkeypatch.setenv("DEPPY_HOST_WATCHES", "1")
     b = lowered_config(5, 120, 121, packed=True, pinned=True)
     wide = [p for p in range(b.n) if b.rec[b.rec_off[p] + 13] == 4]
     assert len(wide) >= 3
@@ -491,10 +493,12 @@ def test_wide_records_direct_and_validated():
     assert compare_results(g, ref, b.n, only=ok) == []
 
 
-def test_olm_scale_direct_bit_exact(ctx):
-    """One OLM-scale catalog (config 4) lowered to DP_FMT_I32W and copied
-    directly: the same result as its int32 form and the oracle."""
+def test_olm_scale_direct_bit_exact(ctx, monkeypatch):
+    """OLM-scale catalogs (config 4) lowered to DP_FMT_I32W (host-built watch
+    lists, DEPPY_HOST_WATCHES=1) and copied directly: the same result as
+    their int32 form, whose lists the device builds, and the oracle."""
     a = lowered_config(4, 2, 131)
+    monkeypatch.setenv("DEPPY_HOST_WATCHES", "1")
     b = lowered_config(4, 2, 131, narrow=True, pinned=True)
     assert np.all(b.rec[b.rec_off[:-1] + 13] == 4)
     gb = ctx.submit(b.rec_off, b.rec).wait()
@@ -617,12 +621,14 @@ def chain_catalog(n_vars, seed):
     return out
 
 
-@pytest.mark.parametrize("flags", [_lib.OPT_FORCE_GROUP, _lib.OPT_FORCE_MID], ids=["split", "split4"])
+@pytest.mark.parametrize("flags", [_lib.OPT_FORCE_GROUP, _lib.OPT_FORCE_MID, _lib.OPT_FORCE_HBM],
+                         ids=["split", "split4", "hbm"])
 def test_device_watch_boundary_bit_exact(flags):
     """Catalogs of 2047, 2048 and 2049 variables on the multi-wave paths:
-    up to 2048 the kernel builds the watch lists (2nv+1 counters in the LDS
-    work area), above it the host does (DP_FMT_I32W).  Bit-exact with the
-    oracle on both sides of the boundary."""
+    up to 2048 the solving workgroup builds the watch lists (2nv+1 counters
+    in the LDS work area), above it the grid-wide passes before the launch
+    do (watch_build.hip).  Bit-exact with the oracle on both sides of the
+    boundary."""
     probs = [chain_catalog(nv, 7 + nv) for nv in (2047, 2048, 2049)]
     lw = _lib.Lowered(sat.encode_inputs(probs))
     assert [int(lw.record(p)[1]) for p in range(3)] == [2047, 2048, 2049]
@@ -634,3 +640,45 @@ def test_device_watch_boundary_bit_exact(flags):
     o = oracle.solve_batch(lw.rec_off, lw.rec, 0, 3)
     assert compare_results(g, o, 3) == []
     assert (g["status"] != -2).all()
+
+
+def test_olm_scale_device_lists_bit_exact():
+    """Config 4 as dp_lower_into emits it (plain int32, no watch lists): the
+    records go to the device as they lie and the grid-wide passes build every
+    catalog's lists before the launch (watch_build.hip).  Bit-exact with the
+    oracle, catalog by catalog."""
+    n = 12
+    a = lowered_config(4, n, 181)
+    b = lowered_config(4, n, 181, packed=True, pinned=True)
+    assert np.all(b.rec[b.rec_off[:-1] + 13] == 0)
+    c = _lib.Context(0, 1)
+    try:
+        g = c.submit(b.rec_off, b.rec).wait()
+        assert c.stats(reset=True)["direct_chunks"] > 0
+    finally:
+        c.close()
+    assert compare_results(g, oracle.solve_batch(a.rec_off, a.rec, 0, 16), n) == []
+
+
+def test_olm_scale_device_lists_malformed():
+    """The list passes run before the kernel validates a record: a clause
+    literal past 2nv, and clause offsets out of range, in two OLM-scale
+    records -> DP_F_MALFORMED for those two (their lists stay in bounds),
+    every other catalog exact."""
+    n = 6
+    a = lowered_config(4, n, 191)
+    b = lowered_config(4, n, 191, packed=True, pinned=True)
+    ref = oracle.solve_batch(a.rec_off, a.rec, 0, 16)
+    r1 = b.rec[b.rec_off[1]:b.rec_off[2]]
+    nc1, nv1 = int(r1[2]), int(r1[1])
+    r1[16 + nc1 + 1 + 7] = 2 * nv1 + 1            # a clause literal past 2nv
+    r3 = b.rec[b.rec_off[3]:b.rec_off[4]]
+    r3[16 + 5] = int(r3[7]) + 1000                # clause_off[5] past ncl
+    c = _lib.Context(0, 1)
+    try:
+        g = c.submit(b.rec_off, b.rec).wait()
+    finally:
+        c.close()
+    for p in (1, 3):
+        assert g["status"][p] == -2 and g["flags"][p] == 512, p
+    assert compare_results(g, ref, n, only=[0, 2, 4, 5]) == []

@@ -125,15 +125,12 @@ def test_narrow_lowering_is_the_16bit_form(config, n):
     np.testing.assert_array_equal(rec, a.rec)
     for p in range(n):
         r = b.record(p)
-        # 16-bit for one-wavefront problems; multi-wave ones as int32 with
-        # their watch lists (DP_FMT_I32W), or plain int32 up to 2048
-        # variables (the kernel builds the lists, layout.hpp device_watches)
-        multi = (0, 4) if int(r[1]) <= 2048 else (4,)
-        assert int(r[13]) in ((1,) + multi if config == 5 else (1,) if config != 4 else (4,))
-        assert int(r[13]) != 0 or int(r[1]) <= 2048
+        # 16-bit for one-wavefront problems; multi-wave ones as plain int32
+        # (the device builds their watch lists, layout.hpp DEV_WATCH_VARS)
+        assert int(r[13]) in ((1, 0) if config == 5 else (1,) if config != 4 else (0,))
         assert _lib.lib().dp_rec_validate(np.ascontiguousarray(r).ctypes.data_as(_lib.c_i32p), len(r)) == 0
     np.testing.assert_array_equal(b.ident_var, a.ident_var)
-    assert b.rec_off[-1] < a.rec_off[-1] or config in (4, 5)  # (multi-wave records carry watch lists)
+    assert b.rec_off[-1] <= a.rec_off[-1]
 
 
 @pytest.mark.parametrize("flags", [0, _lib.OPT_FORCE_GROUP])
