@@ -144,14 +144,16 @@ __host__ __device__ inline dp_rec_layout rec_layout(const int32_t* h) {
 // every word after it becomes a uint16), so PCIe and the LDS-DMA of init move
 // half the bytes and the kernel has nothing to convert.
 //
-// The record is extended by
-//   w_off[2nv+1], w[ncl+nkl]  watch lists: rows to evaluate when literal l
-//                             becomes true (clauses holding ~l; AtMost rows
-//                             holding var(l) when l is positive, one entry
-//                             per distinct variable)
-// right after it: built by the kernel in LDS during init for one-wavefront
-// problems (Group::build_watches), and by the host while staging for the
-// multi-wave ones, whose staged image is read in place from HBM
+// Each record has watch lists
+//   w_off[2nv+1], w[ncl+nkl]  rows to evaluate when literal l becomes true
+//                             (clauses holding ~l; AtMost rows holding
+//                             var(l) when l is positive, one entry per
+//                             distinct variable)
+// built on the device: in LDS during init for one-wavefront problems, right
+// after the record (Group::build_watches); in the problem's HBM scratch for
+// the multi-wave ones (Layout::wl: build_watches_wide, or watch_build.hip's
+// passes above DEV_WATCH_VARS).  A DP_FMT_I32W record brings its own, and
+// the host builds them after a record it converts while staging
 // (runtime.cpp stage_one).  Rows that can fire on the empty assignment
 // (clauses of length <= 1, AtMost rows in which some variable's multiplicity
 // exceeds the bound) are found by a sweep of the row offsets
