@@ -296,6 +296,17 @@ struct alignas(128) Work {  // per-thread scratch
   // while st_tag matches the problem's tag (no clearing between problems)
   std::vector<uint64_t> st_tag;
   std::vector<int32_t> st_idx;
+  // the fast path's: (problem stamp << 32 | variable) per string id, one load
+  // per lookup; a stamp per problem lowered (0 never used, wrap clears)
+  std::vector<uint64_t> fst;
+  uint32_t fstamp = 0;
+  uint32_t next_fstamp() {
+    if (++fstamp == 0) {
+      std::fill(fst.begin(), fst.end(), 0);
+      fstamp = 1;
+    }
+    return fstamp;
+  }
   uint64_t gen = 0;  // dp_lower call number of this scratch
   uint64_t tag_of(int32_t p, bool fast) const { return gen << 33 | (uint64_t)(p + 1) << 1 | (fast ? 1u : 0u); }
   std::unordered_map<std::string_view, int32_t> names;
@@ -729,16 +740,14 @@ struct Lowerer {
     const int32_t* const con_n = w.con_n;
     const int64_t* const con_arg_off = w.con_arg_off;
     const int64_t* const con_arg = w.con_arg;
-    uint64_t* const st_tag = W.st_tag.data();
-    int32_t* const st_idx = W.st_idx.data();
-    // this path's stamps carry a tag of their own (lower_one may follow)
-    const uint64_t tag = W.tag_of(p, true);
+    // this path's stamps are its own (lower_one may follow)
+    uint64_t* const fst = W.fst.data();
+    const uint64_t stamp = (uint64_t)W.next_fstamp() << 32;
     for (int i = 0; i < nv; ++i) {
       const uint64_t sid = (uint64_t)var_id[v0 + i];
       if (sid >= nstr || var_con_off[v0 + i + 1] < var_con_off[v0 + i]) return -1;
-      if (st_tag[sid] == tag) return 0;  // a duplicate: lower_one reports it
-      st_tag[sid] = tag;
-      st_idx[sid] = i;
+      if ((fst[sid] & ~0xffffffffULL) == stamp) return 0;  // a duplicate: lower_one reports it
+      fst[sid] = stamp | (uint32_t)i;
     }
     const int64_t cb = nv ? var_con_off[v0] : 0, ce = nv ? var_con_off[v1] : 0;
     const int64_t C = ce - cb, A = nv ? con_arg_off[ce] - con_arg_off[cb] : 0;
@@ -746,7 +755,8 @@ struct Lowerer {
     // var of string id sid, -1 if not a variable of this problem, -2 if out of range
     auto var = [&](int64_t sid) -> int32_t {
       if ((uint64_t)sid >= nstr) return -2;
-      return st_tag[(size_t)sid] == tag ? st_idx[(size_t)sid] : -1;
+      const uint64_t e = fst[(size_t)sid];
+      return (e & ~0xffffffffULL) == stamp ? (int32_t)(uint32_t)e : -1;
     };
     Fast& F = W.fast;
     F.reset((size_t)nv, (size_t)C, (size_t)A);
@@ -1246,6 +1256,7 @@ int dp_lower_into(const dp_wire* wire, int32_t flags, dp_lowered* lw) {
     if (wire->interned && W.st_tag.size() < (size_t)wire->n_strs) {
       W.st_tag.resize((size_t)wire->n_strs, 0);
       W.st_idx.resize((size_t)wire->n_strs, 0);
+      W.fst.resize((size_t)wire->n_strs, 0);
     }
   }
   for (auto& O : lw->outs) {
