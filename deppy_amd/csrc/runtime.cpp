@@ -809,6 +809,10 @@ struct Device {
   int ordinal = 0;
   Lane lanes[kMaxLanes];
   int nstreams = kStreams, nlanes = 2 * kStreams;
+  // the event after the last chunk's record copies, and the chunks left of
+  // the current pipeline fill (worker only; start_chunk)
+  hipEvent_t last_copied = nullptr;
+  int fill_left = 0;
   int next = 0;  // resident launches: next lane
   FastLane fast;
   // -- the worker's --
@@ -1146,6 +1150,23 @@ int start_chunk(dp_ctx* ctx, Device& D, Lane& L, dp_job* job, int32_t p0, int32_
   size_t h2d = 0;
   // (lane buffers are free: finish_lane waited for the lane's last chunk)
   hipStream_t cs = L.cs ? L.cs : L.s;
+  // Filling an idle pipeline with large chunks, copies go in submission
+  // order: the first chunks (one per stream) each wait for the previous
+  // one's copy instead of sharing PCIe with all of them, so the first
+  // kernels start after one chunk's copy rather than after every stream's.
+  // Only while filling (the streams are idle, so a copy never waits behind
+  // another stream's kernel), and only for chunks of at least
+  // DEPPY_COPY_CHAIN_MB (default 64; 0: off): measured on one box, configs 4
+  // and 5 (564 / 322 MB chunks) gain 10-11% host to host at 20 steps, while
+  // configs 2 and 6 (19 / 10 MB) lose half (scripts/chain_ab.sh).
+  static const int64_t chain_mb = env_i64("DEPPY_COPY_CHAIN_MB", 64);
+  const size_t copy_bytes = direct ? 4 * (size_t)W + (il.end - rest) : zc_in ? 0 : il.end;
+  if (D.inflight.empty()) D.fill_left = D.nstreams;
+  const bool chain = chain_mb > 0 && D.fill_left > 0 && copy_bytes >= (size_t)chain_mb << 20;
+  if (D.fill_left > 0) --D.fill_left;
+  if (chain && D.last_copied && hipEventQuery(D.last_copied) == hipErrorNotReady)
+    HIP_OK(hipStreamWaitEvent(cs, D.last_copied, 0));
+  (void)hipGetLastError();  // (hipEventQuery's not-ready status)
   if (direct) {
     const size_t src_bytes = 4 * (size_t)W;
     if (src_bytes)
@@ -1157,10 +1178,9 @@ int start_chunk(dp_ctx* ctx, Device& D, Lane& L, dp_job* job, int32_t p0, int32_
     HIP_OK(hipMemcpyAsync(L.d_in.p, L.h_in.p, il.end, hipMemcpyHostToDevice, cs));
     h2d = il.end;
   }
-  if (cs != L.s) {
-    HIP_OK(hipEventRecord(L.copied, cs));
-    HIP_OK(hipStreamWaitEvent(L.s, L.copied, 0));
-  }
+  if (cs != L.s || chain) HIP_OK(hipEventRecord(L.copied, cs));
+  if (cs != L.s) HIP_OK(hipStreamWaitEvent(L.s, L.copied, 0));
+  D.last_copied = chain ? L.copied : nullptr;  // (a chain restarts after an unchained chunk)
   HIP_OK(hipMemsetAsync(L.d_out.p + L.ol.pool_len, 0, 4, L.s));
   dp::KernelArgs a = kernel_args(il, L.ol, din, dout, reinterpret_cast<int32_t*>(L.scratch.p), ctx->budget);
   a.core_pool_len = at<int32_t>(L.d_out.p, L.ol.pool_len);
