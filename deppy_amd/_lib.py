@@ -13,17 +13,58 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libdeppy_hip.so")
-# The pipeline runs 8 lane streams per device, each on a hardware queue of its
-# own: the HIP runtime opens GPU_MAX_HW_QUEUES (default 4) queues when it
-# initialises, so raise it to 8 (a larger setting stays; measured on one box,
-# config 2: host to host 20.9M -> 22.0M res/s, kernel only 25.5M -> 27.0M;
-# DESIGN.md §4).  Set before any HIP call of the process.
-try:
-    _hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)
-except ValueError:
-    _hwq = 0
-if _hwq < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+# The pipeline runs one lane stream per hardware queue the HIP runtime opens,
+# at most 8.  HIP opens GPU_MAX_HW_QUEUES queues (default 4; the GPU boxes
+# export 4) once, when it initialises: measured on one box, config 2 host to
+# host 20.9M res/s on 4 queues, 22.0M on 8 (kernel only 25.5M -> 27.0M), and
+# 8 streams on 4 queues 20.9-21.2M.  So before HIP starts, the
+# binding raises the setting to 8 (DEPPY_KEEP_HW_QUEUES=1 keeps the operator's
+# value); once HIP is up (another library initialised it first) the setting
+# can no longer take effect, and the runtime sizes its streams from the queues
+# HIP actually runs with.  Either way DEPPY_HW_QUEUES tells dp_create that
+# number (runtime.cpp lane_streams).
+def _hsa_up() -> bool:
+    """Has this process opened the ROCm kernel driver (HIP initialised)?"""
+    try:
+        fds = os.listdir("/proc/self/fd")
+    except OSError:
+        return False
+    for fd in fds:
+        try:
+            if os.readlink("/proc/self/fd/" + fd) == "/dev/kfd":
+                return True
+        except OSError:
+            pass
+    return False
+
+
+def hw_queue_plan(env_value, hsa_up: bool, keep: bool = False):
+    """-> (value to set GPU_MAX_HW_QUEUES to, or None; queues HIP runs with).
+    HIP reads the setting once, when it initialises (default 4)."""
+    try:
+        q = int(env_value) if env_value not in (None, "") else 4
+    except ValueError:
+        q = 4
+    if hsa_up or keep or q >= 8:
+        return None, q
+    return "8", 8
+
+
+def _plan_hw_queues() -> None:
+    up = _hsa_up()
+    env = os.environ.get("GPU_MAX_HW_QUEUES")
+    set_to, q = hw_queue_plan(env, up, os.environ.get("DEPPY_KEEP_HW_QUEUES") == "1")
+    if set_to is not None:
+        os.environ["GPU_MAX_HW_QUEUES"] = set_to
+    elif up and q < 8:
+        import warnings
+        warnings.warn("deppy_amd: HIP was initialised before the binding was imported, with %d hardware "
+                      "queues; the pipeline runs %d lane streams per device (import deppy_amd first for 8)"
+                      % (q, q), RuntimeWarning, stacklevel=3)
+    os.environ["DEPPY_HW_QUEUES"] = str(q)
+
+
+_plan_hw_queues()
 # dp_opt_flag (include/deppy_hip.h): placement overrides
 OPT_FORCE_GROUP = 1 << 0
 OPT_FORCE_HBM = 1 << 1

@@ -204,11 +204,15 @@ void read_head(Head& H, const int32_t* h, int64_t avail, int32_t opt_flags, bool
     nar = H.lds <= dp::group_above();
   }
   H.sw = staged_words(h, nar);
-  // the record image the kernel reads: the packed form as it is, else the
-  // 16-bit form (LDS path) or the int32 form with its watch lists
+  // algorithmic input bytes (roofline.achieved): the record as the kernel
+  // reads it -- the packed form as it is, else the 16-bit form (LDS path) or
+  // the int32 form.  Watch lists are derived data and not counted, whether
+  // the device builds them (in LDS, or in HBM scratch by the multi-wave
+  // passes) or they come with the record (DP_FMT_I32W, host staging): the
+  // lists' HBM traffic shows in the PMC figure, not in the compulsory bytes.
   H.rec_bytes = nar ? (dp_fmt_packed(h[DP_H_FMT]) ? 4 * dp_rec_phys_words(h)
                                                  : 4 * DP_H_SIZE + 2 * ((int64_t)h[DP_H_WORDS] - DP_H_SIZE))
-                    : 4 * (int64_t)img_layout(h).words;  // (lists built on the device are read too)
+                    : 4 * (int64_t)h[DP_H_WORDS];
   if (nar) {
     H.place = M_LDS;
     int k = 0;
@@ -572,6 +576,25 @@ bool stage_one(const Plan& P, const int32_t* rec, const int64_t* rec_off, int32_
   return true;
 }
 
+// Which multi-wave launches need the grid-wide watch-list passes
+// (watch_build.hip): those holding a record copied to the device as it lies in
+// DP_FMT_I32 above DEV_WATCH_VARS variables.  plan_chunk assumes every record
+// goes as it lies; a record the chunk stages instead (stage_one) carries
+// host-built lists, and a chunk staged whole (not direct, the latency path,
+// dp_upload) launches no passes.
+void settle_dev_lists(Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0, bool direct) {
+  for (auto& L : P.launches) {
+    if (L.mode == M_LDS || !L.dev_lists) continue;
+    bool any = false;
+    for (int k = L.first; direct && k < L.first + L.count && !any; ++k) {
+      const int32_t i = P.order[(size_t)k];
+      const int32_t* h = rec + rec_off[p0 + i];
+      any = P.direct[(size_t)i] && h[DP_H_FMT] == DP_FMT_I32 && !device_watches(h);
+    }
+    L.dev_lists = any;
+  }
+}
+
 void* pinned_alloc(size_t bytes) {
   int n = 0;
   void* p = nullptr;
@@ -852,6 +875,7 @@ struct dp_ctx {
   std::atomic<double> last_ms{0.0};
   std::mutex mu;
   dp::Pool* pool = nullptr;
+  mutable std::mutex err_mu;  // err: written by any caller thread (set_err), read by dp_last_error
   int next_dev = 0;  // pipeline cursor over devices (under mu)
   bool zc_in = false, zc_out = true;  // zero-copy records / results (start_chunk)
   bool copy_streams = false;          // records' H2D on a stream of its own (DEPPY_COPY_STREAM=1)
@@ -901,15 +925,22 @@ thread_local std::string t_err;
       return -1;                                                             \
     }                                                                        \
   } while (0)
+// The context's last error.  Jobs may be submitted and waited on from any
+// number of caller threads, so every write takes err_mu, and dp_last_error
+// hands each thread its own copy.
+void set_err(dp_ctx* ctx, std::string e) {
+  std::lock_guard<std::mutex> lk(ctx->err_mu);
+  ctx->err = std::move(e);
+}
 int api_fail(dp_ctx* ctx) {
-  ctx->err = t_err;
+  set_err(ctx, t_err);
   return -1;
 }
 // HIP_OK in an API function on the caller's thread: the text to ctx->err.
 #define API_OK(expr)                                                         \
   do {                                                                       \
     if (hipError_t e_ = (expr); e_ != hipSuccess) {                          \
-      ctx->err = std::string(#expr) + ": " + hipGetErrorString(e_);          \
+      set_err(ctx, std::string(#expr) + ": " + hipGetErrorString(e_));       \
       return -1;                                                             \
     }                                                                        \
   } while (0)
@@ -1112,6 +1143,7 @@ int start_chunk(dp_ctx* ctx, Device& D, Lane& L, dp_job* job, int32_t p0, int32_
     }
     Q.img_words = o;
   }
+  dp::settle_dev_lists(L.plan, job->rec, job->rec_off, p0, direct);
   const InLayout il = in_layout(L.plan);
   L.ol = out_layout(L.plan);
   // The host side of the input region: all of it, or (direct) only what
@@ -1158,7 +1190,7 @@ int start_chunk(dp_ctx* ctx, Device& D, Lane& L, dp_job* job, int32_t p0, int32_
   // another stream's kernel), and only for chunks of at least
   // DEPPY_COPY_CHAIN_MB (default 64; 0: off): measured on one box, configs 4
   // and 5 (564 / 322 MB chunks) gain 10-11% host to host at 20 steps, while
-  // configs 2 and 6 (19 / 10 MB) lose half (scripts/chain_ab.sh).
+  // configs 2 and 6 (19 / 10 MB) lose half (profiles/r03_copy_chain_ab_unsized.txt).
   static const int64_t chain_mb = env_i64("DEPPY_COPY_CHAIN_MB", 64);
   const size_t copy_bytes = direct ? 4 * (size_t)W + (il.end - rest) : zc_in ? 0 : il.end;
   if (D.inflight.empty()) D.fill_left = D.nstreams;
@@ -1280,6 +1312,7 @@ int fast_solve(dp_ctx* ctx, Device& D, const dp_batch* b, dp_result* res) {
   const int32_t n = b->n_problems;
   F.bad.assign((size_t)n, 0);
   dp::plan_chunk(F.plan, b->rec, b->rec_off, 0, n, ctx->flags, &F.bad, nullptr);
+  dp::settle_dev_lists(F.plan, b->rec, b->rec_off, 0, false);
   const Plan& P = F.plan;
   if (!P.skip.empty() || !P.scratch_off.empty()) return 1;
   if (hipSetDevice(D.ordinal) != hipSuccess) return 1;
@@ -1298,7 +1331,7 @@ int fast_solve(dp_ctx* ctx, Device& D, const dp_batch* b, dp_result* res) {
   hipError_t e;
   while ((e = hipEventQuery(F.done)) == hipErrorNotReady) __builtin_ia32_pause();
   if (e != hipSuccess) {
-    ctx->err = std::string("dp_solve (latency path): ") + hipGetErrorString(e);
+    set_err(ctx, std::string("dp_solve (latency path): ") + hipGetErrorString(e));
     return -1;
   }
   scatter(P, ol, F.h_out.p, 0, res);
@@ -1317,6 +1350,20 @@ void cut_chunks(const dp_ctx* ctx, const dp_job* job, std::vector<std::pair<int3
     out.emplace_back(p, q - p);
     p = q;
   }
+}
+
+// Lane streams per device (two lanes each): one per hardware queue the HIP
+// runtime opened, at most 8 (16 streams measured far slower host to host,
+// and 8 streams on 4 queues 5% slower than 4; profiles/r03_streams_ab.txt).
+// HIP opens GPU_MAX_HW_QUEUES queues (4 by default) when it initialises; the
+// binding (deppy_amd/_lib.py, the cgo shim) raises the setting before that
+// and reports in DEPPY_HW_QUEUES how many HIP actually runs with -- which
+// differs from the setting when something initialised HIP first.  Without
+// the binding the setting is the best guess.  DEPPY_STREAMS overrides (A/B).
+int lane_streams() {
+  const int64_t hwq = env_i64("DEPPY_HW_QUEUES", env_i64("GPU_MAX_HW_QUEUES", kStreams));
+  return (int)std::min<int64_t>(kMaxStreams,
+                                std::max<int64_t>(1, env_i64("DEPPY_STREAMS", std::min<int64_t>(hwq, 8))));
 }
 
 }  // namespace
@@ -1355,13 +1402,7 @@ dp_ctx* dp_create(const dp_opts* opts) {
     Device& D = ctx->dev[(size_t)i];
     D.ordinal = d;
     ctx->copy_streams = env_i64("DEPPY_COPY_STREAM", 0) != 0;
-    // lane streams per device (two lanes each): one per hardware queue the
-    // HIP runtime opened (GPU_MAX_HW_QUEUES, 4 by default; the Python binding
-    // asks for 8), at most 8 -- 16 streams measured far slower host to host;
-    // DEPPY_STREAMS overrides (A/B)
-    const int64_t hwq = env_i64("GPU_MAX_HW_QUEUES", kStreams);
-    D.nstreams = (int)std::min<int64_t>(kMaxStreams, std::max<int64_t>(
-                                                         1, env_i64("DEPPY_STREAMS", std::min<int64_t>(hwq, 8))));
+    D.nstreams = lane_streams();
     D.nlanes = 2 * D.nstreams;
     for (int li = 0; li < D.nlanes; ++li) {
       Lane& L = D.lanes[li];
@@ -1448,7 +1489,13 @@ void dp_destroy(dp_ctx* ctx) {
   delete ctx;
 }
 
-const char* dp_last_error(const dp_ctx* ctx) { return ctx ? ctx->err.c_str() : dp_last_global_error(); }
+const char* dp_last_error(const dp_ctx* ctx) {
+  if (!ctx) return dp_last_global_error();
+  static thread_local std::string copy;  // valid until this thread's next call
+  std::lock_guard<std::mutex> lk(ctx->err_mu);
+  copy = ctx->err;
+  return copy.c_str();
+}
 int32_t dp_num_devices(const dp_ctx* ctx) { return ctx ? (int32_t)ctx->dev.size() : 0; }
 int32_t dp_lanes(const dp_ctx* ctx) { return ctx && !ctx->dev.empty() ? (int32_t)ctx->dev[0].nlanes : 0; }
 
@@ -1520,7 +1567,7 @@ int dp_job_wait(dp_ctx* ctx, dp_job* job) {
   }
   if (rc) {
     std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->err = job->err;
+    set_err(ctx, job->err);
   }
   delete job;
   return rc;
@@ -1575,6 +1622,7 @@ int build_slice(dp_ctx* ctx, Slice& s, const dp_batch* b, int32_t trace_cap) {
   const int32_t n = s.p1 - s.p0;
   std::vector<uint8_t> bad((size_t)std::max(n, 1), 0);
   dp::plan_chunk(s.plan, b->rec, b->rec_off, s.p0, n, ctx->flags, &bad, ctx->pool);
+  dp::settle_dev_lists(s.plan, b->rec, b->rec_off, s.p0, false);  // (every record staged)
   s.il = in_layout(s.plan);
   s.ol = out_layout(s.plan);
   std::vector<char> host(s.il.end);
@@ -1729,7 +1777,7 @@ int dp_download_trace(dp_ctx* ctx, dp_resident* r, int32_t* trace, int32_t* trac
   std::lock_guard<std::mutex> lk(ctx->mu);
   if (wait_locked(ctx, r)) return api_fail(ctx);
   if (r->trace_cap <= 0) {
-    ctx->err = "dp_download_trace: the batch was not uploaded with dp_upload_traced";
+    set_err(ctx, "dp_download_trace: the batch was not uploaded with dp_upload_traced");
     return -1;
   }
   for (auto& s : r->slices) {

@@ -365,10 +365,14 @@ void dp_destroy(dp_ctx* ctx);
 const char* dp_last_error(const dp_ctx* ctx);
 const char* dp_last_global_error(void);
 int32_t dp_num_devices(const dp_ctx* ctx);
-/* Pipeline chunk slots (lanes) per device: two per lane stream.  The
- * streams per device follow GPU_MAX_HW_QUEUES (one stream per hardware
- * queue, at most 8; 4 when it is not set) unless DEPPY_STREAMS says.  A
- * serving loop keeps this many chunks in flight per device. */
+/* Pipeline chunk slots (lanes) per device: two per lane stream.  One lane
+ * stream per hardware queue the HIP runtime opened, at most 8: HIP opens
+ * GPU_MAX_HW_QUEUES queues (4 when it is not set) once, when it initialises.
+ * The bindings raise that setting to 8 before HIP starts and pass the count
+ * HIP actually runs with in DEPPY_HW_QUEUES (the setting no longer takes
+ * effect once something else initialised HIP); without them the setting is
+ * used.  DEPPY_STREAMS overrides.  A serving loop keeps this many chunks in
+ * flight per device. */
 int32_t dp_lanes(const dp_ctx* ctx);
 
 /* Synchronous batch solve, host memory to host memory: the batched form of
@@ -455,7 +459,8 @@ int dp_solve_traced(dp_ctx* ctx, const dp_batch* b, int32_t trace_cap, dp_result
  * compulsory input of SURVEY §8(d)): on the LDS path the 16-bit form (a
  * DP_FMT_P16 record as it is, else 64 header bytes + 2 per word; the kernel
  * builds the watch lists itself), on the multi-wave paths the int32 form
- * with its watch lists (DP_FMT_I32W).  img_bytes = the staged copies as
+ * (watch lists are derived data and not counted, wherever they are built).
+ * img_bytes = the staged copies as
  * they cross PCIe when staged (16-byte aligned).  opt_flags as
  * dp_opts.flags.  Returns 0 or -1. */
 int dp_device_bytes(const dp_batch* b, int32_t opt_flags, int64_t* rec_bytes, int64_t* img_bytes);

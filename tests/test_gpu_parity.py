@@ -630,11 +630,16 @@ def test_device_watch_boundary_bit_exact(flags):
     do (watch_build.hip).  Bit-exact with the oracle on both sides of the
     boundary."""
     probs = [chain_catalog(nv, 7 + nv) for nv in (2047, 2048, 2049)]
-    lw = _lib.Lowered(sat.encode_inputs(probs))
+    # page-locked plain int32 records on 16-byte boundaries, as dp_lower_into
+    # emits multi-wave records: dp_submit copies them as they lie, so the
+    # device builds every list (a staged record would bring host-built ones)
+    lw = _lib.Lowered(sat.encode_inputs(probs), narrow=True, packed=True, pinned=True)
     assert [int(lw.record(p)[1]) for p in range(3)] == [2047, 2048, 2049]
+    assert [int(lw.record(p)[13]) for p in range(3)] == [0, 0, 0]  # DP_FMT_I32
     c = _lib.Context(0, 1, flags=flags)
     try:
-        g = c.solve(lw.rec_off, lw.rec)
+        g = c.submit(lw.rec_off, lw.rec).wait()
+        assert c.stats(reset=True)["direct_chunks"] > 0
     finally:
         c.close()
     o = oracle.solve_batch(lw.rec_off, lw.rec, 0, 3)

@@ -281,3 +281,23 @@ def test_stage_roundtrip_packed_source():
     lw = lowered_config(2, 120, 23, packed=True)
     out, _ = _lib.stage_roundtrip(lw.rec_off, lw.rec, chunk_problems=50)
     np.testing.assert_array_equal(out, lw.rec)
+
+
+def test_hw_queue_plan():
+    """GPU_MAX_HW_QUEUES is read by HIP once, when it initialises: the binding
+    raises it to 8 only while HIP is not up, and otherwise reports the queues
+    HIP really runs with, so the runtime opens one lane stream per real queue
+    (runtime.cpp lane_streams reads DEPPY_HW_QUEUES)."""
+    plan = _lib.hw_queue_plan
+    assert plan(None, False) == ("8", 8)
+    assert plan("4", False) == ("8", 8)          # the boxes' exported default
+    assert plan("16", False) == (None, 16)       # a larger setting stays
+    assert plan("4", False, keep=True) == (None, 4)
+    # HIP initialised before the binding: the setting cannot take effect any
+    # more; the streams follow what HIP opened, not what the binding wants
+    assert plan(None, True) == (None, 4)
+    assert plan("4", True) == (None, 4)
+    assert plan("8", True) == (None, 8)
+    assert plan("junk", True) == (None, 4)
+    import os
+    assert os.environ["DEPPY_HW_QUEUES"] == str(int(os.environ.get("GPU_MAX_HW_QUEUES", "4")))
