@@ -139,6 +139,53 @@ def end_to_end(ctx, wa, n, steps, depth=2):
     return n * steps / (time.perf_counter() - t0)
 
 
+def solve_batch_api(ctx, wa, n, steps):
+    """The shipped API path, one batch at a time: deppy_amd.sat.solve_wire (the
+    wire -> results half of SolveBatch, what the cgo shim does): dp_lower_into
+    NARROW|PACKED|PINNED into reused storage, then dp_solve on the batch as it
+    lies.  No batches overlap (a caller waiting on each SolveBatch)."""
+    from deppy_amd import sat
+    sat.solve_wire(wa, ctx)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        sat.solve_wire(wa, ctx)
+    return n * steps / (time.perf_counter() - t0)
+
+
+# Issue model of one CU (MI355X_MICROARCH.md): 4 SIMD-32 vector units, each
+# issuing a wave64 VALU instruction over 2 cycles, and one scalar unit (one
+# SALU instruction per cycle per CU); 256 CUs at 2.4 GHz.
+CUS, CLOCK_HZ = 256, 2.4e9
+VALU_PEAK = CUS * 4 * CLOCK_HZ / 2   # wave64 VALU instructions / s
+SALU_PEAK = CUS * CLOCK_HZ           # SALU instructions / s
+
+
+def issue_roofline(sq_json, config, res_per_s):
+    """Instructions per resolution of the one-wavefront kernel (a wave per
+    catalog; SQ counters of the same build, scripts/pmc_sq_r02.sh) times the
+    kernel-only rate, against the VALU and SALU issue peaks."""
+    if not sq_json or not os.path.exists(sq_json) or not res_per_s:
+        return None
+    with open(sq_json) as f:
+        d = json.load(f).get(str(config))
+    if not d:
+        return None
+    pw = d["per_wave"]
+    valu, salu = pw["SQ_INSTS_VALU"], pw["SQ_INSTS_SALU"]
+    return {"valu_per_resolution": round(valu, 1), "salu_per_resolution": round(salu, 1),
+            "lds_per_resolution": round(pw["SQ_INSTS_LDS"], 1),
+            "all_per_resolution": round(sum(pw.values()), 1),
+            "valu_frac": round(valu * res_per_s / VALU_PEAK, 4),
+            "salu_frac": round(salu * res_per_s / SALU_PEAK, 4),
+            "wave_issuing_frac": d.get("active_frac"), "wave_waiting_frac": d.get("wait_any_frac"),
+            "source": os.path.relpath(sq_json, ROOT),
+            "note": "kernel_only res/s x instructions per catalog (one wavefront each) / the chip's issue peak: "
+                    "VALU %.3g/s (4 SIMD-32 per CU, a wave64 instruction per 2 cycles), SALU %.3g/s (one "
+                    "scalar unit per CU). Both well below 1 with the waves waiting most of their cycles: the "
+                    "kernel is bound by each wave's dependent LDS chain (latency), not by issue or HBM"
+                    % (VALU_PEAK, SALU_PEAK)}
+
+
 def cpu_end_to_end(wa, lw32, n, threads, seconds):
     """The same on the CPU: lowering to int32 records + the oracle's solve, one
     solver thread per core, for a bounded time."""
@@ -233,6 +280,9 @@ def main():
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r03_pmc_traffic.jsonl"),
                     help="HBM bytes per solve kernel dispatch from separate rocprofv3 --pmc passes; "
                          "used for roofline.traffic when its config/problems match")
+    ap.add_argument("--sq-json", default=os.path.join(ROOT, "profiles", "r04_sq_split.json"),
+                    help="SQ instruction counts per wave of this build (scripts/pmc_sq_r02.sh + sq_summary.py), "
+                         "for roofline.issue")
     args = ap.parse_args()
     maybe_relaunch(args)
 
@@ -344,6 +394,12 @@ def main():
             "note": "wire format -> dp_lower_into -> dp_submit/dp_job_wait -> results, 2 batches in flight "
                     "(lowering of batch i+1 overlaps the solve of batch i); what BenchmarkSolve times "
                     "(NewSolver(WithInput)+Solve, bench_test.go:66-77); not value"}
+        line["solve_batch_api"] = {
+            "res_per_s": round(solve_batch_api(ctx, wa, n, max(2, args.e2e_steps // 2)), 1),
+            "steps": max(2, args.e2e_steps // 2),
+            "note": "deppy_amd.sat.solve_wire (SolveBatch from the wire format to host results, as the cgo "
+                    "shim calls the library): dp_lower_into NARROW|PACKED|PINNED into reused storage + dp_solve, "
+                    "one batch at a time; not value"}
 
     if args.kernel_steps > 0:
         # the solve kernel alone, records resident in HBM (dp_upload): serial
@@ -396,7 +452,9 @@ def main():
                             "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                             "kernel": "solve_kernel (one launch of the batch, serial, records in HBM)",
                             "kernel_ms": round(k_ms, 4), "algorithmic_bytes_per_launch": int(alg),
-                            "traffic_over_algorithmic": round(traffic / alg, 3) if traffic else None}
+                            "traffic_over_algorithmic": round(traffic / alg, 3) if traffic else None,
+                            "issue": issue_roofline(args.sq_json, args.config,
+                                                    n * args.kernel_steps / tk if tk == tk else None)}
 
     if rank == 0 and not args.no_cpu:
         from oracle import oracle  # CPU baseline + checker only

@@ -78,6 +78,22 @@ constexpr bool IMP16_LDS = DP_IMP16;
 #define DP_2WL 0
 #endif
 __host__ __device__ constexpr bool mode_2wl(int mode) { return DP_2WL && mode != M_LDS; }
+// Two-watched-literal propagation on the one-wavefront path (-DDP_TWL_LDS=1):
+// a clause row of 3..254 literals sits in the watch lists of two of its
+// positions only (Layout::wpos, a byte each); a round that falsifies one of
+// them moves that watch to another non-false position, so the row leaves
+// that literal's list and joins the new one's (per-literal live ends in
+// Layout::wend, within the occurrence-count capacity the lists already
+// have).  Row literals are never reordered (Solve()'s decision is the first
+// unassigned positive literal in row order).  Shorter and longer rows, and
+// AtMost rows, stay in every list they occur in.  Bit-exact with the
+// occurrence lists (solve_kernel.hpp visit_twl argues it).
+#ifndef DP_TWL_LDS
+#define DP_TWL_LDS 0
+#endif
+__host__ __device__ constexpr bool mode_twl_lds(int mode) { return DP_TWL_LDS && mode == M_LDS; }
+constexpr int32_t TWL_MIN_LEN = 3, TWL_MAX_LEN = 254;
+
 // Row slots on the multi-wave placements (-DDP_ROWSLOT=1; the compact hot
 // image of a clause row): 32 bytes per row in the HBM scratch, built during
 // init -- the row's watched pair, its length, and its literals inline when
@@ -247,6 +263,10 @@ struct Layout {
   int32_t wp;        // (mode_rowslot) i32[8][nc] row slots {watch x, watch y, len, l0 | offset, l1..l4};
                      // else (mode_2wl) u64[nc] the two literals clause row r watches, low word first
   int32_t wl;        // multi-wave, DP_FMT_I32 records: device-built w_off[2nv+2], w[ncl+nkl]  [HBM, last]
+  int32_t wpos;      // (mode_twl_lds) u8[2nc] watched positions of each clause row
+  int32_t wend;      // (mode_twl_lds) u16[2nv] live end of each literal's watch list
+  int32_t wfi;       // (mode_twl_lds) u8[wbuf] frontier literal of each flattened work-list entry
+  int32_t fcur;      // (mode_twl_lds) i32[64] compaction cursor per frontier literal of a chunk
   int32_t bytes;     // HBM scratch bytes (0 for M_LDS)
   int32_t lds_bytes; // LDS bytes
   int32_t cap, lcap;
@@ -337,6 +357,10 @@ __host__ __device__ inline Layout layout(const int32_t* h) {
   L.stk = take(3 * L.cap * ix, COLD);
   L.wp = mode_rowslot(MODE) ? take(h[DP_H_NC] * 32, COLD) : mode_2wl(MODE) ? take(h[DP_H_NC] * 8, COLD) : 0;
   L.wl = MODE != M_LDS && h[DP_H_FMT] == DP_FMT_I32 ? take((2 * nv + 2 + h[DP_H_NCL] + h[DP_H_NKL]) * 4, COLD) : 0;
+  L.wpos = mode_twl_lds(MODE) ? take(2 * h[DP_H_NC], COLD) : 0;
+  L.wend = mode_twl_lds(MODE) ? take(4 * nv, COLD) : 0;
+  L.wfi = mode_twl_lds(MODE) ? take(mode_wbuf(MODE), COLD) : 0;
+  L.fcur = mode_twl_lds(MODE) ? take(64 * 4, COLD) : 0;
   L.bytes = og;
   L.lds_bytes = ol;
   return L;

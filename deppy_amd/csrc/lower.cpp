@@ -525,13 +525,9 @@ struct Lowerer {
     const int32_t nc = r[DP_H_NC], nk = r[DP_H_NK], nv = r[DP_H_NV], nch = r[DP_H_NCH], nid = r[DP_H_NID];
     // DP_FMT_P16D when the dependency rows imply the choice lists exactly
     static thread_local std::vector<uint8_t> srcs;
-    static const bool no_p16d = [] {  // diagnostic DEPPY_NO_P16D=1: explicit choice lists (DP_FMT_P16)
-      const char* e = std::getenv("DEPPY_NO_P16D");
-      return e && *e && *e != '0';
-    }();
     const uint8_t* sp = src_known;
-    bool derived = !no_p16d && sp;
-    if (!no_p16d && !sp) {
+    bool derived = !no_p16d() && sp;
+    if (!no_p16d() && !sp) {
       if (srcs.size() < (size_t)nch + 1) srcs.resize((size_t)nch + 1);
       derived = choice_sources(r, L, srcs.data());
       sp = srcs.data();
@@ -588,6 +584,77 @@ struct Lowerer {
     uint8_t* b = reinterpret_cast<uint8_t*>(r + DP_H_SIZE);
     std::memset(reinterpret_cast<uint8_t*>(u), 0, (size_t)(b + at - reinterpret_cast<uint8_t*>(u)));
     std::memcpy(b + at, tail.data(), (size_t)tb);
+    std::memset(b + at + tb, 0, (size_t)((4 - (at + tb) % 4) % 4));  // to the last word's end
+    return true;
+  }
+
+  static bool no_p16d() {  // diagnostic DEPPY_NO_P16D=1: explicit choice lists (DP_FMT_P16)
+    static const bool v = [] {
+      const char* e = std::getenv("DEPPY_NO_P16D");
+      return e && *e && *e != '0';
+    }();
+    return v;
+  }
+
+  // The fast path's record written straight in DP_FMT_P16D, the form
+  // emit_fast + narrow_last + pack16 give it, without the int32 record in
+  // between (a third of the lowering's memory traffic): when the batch asks
+  // for packed records, the record runs one wavefront per problem (decided
+  // on its int32 header, as narrow_last does) and the form applies (every
+  // identity one row -- the fast path numbers identities in row order, so
+  // each row kind's are ascending -- row lengths below 256, choice lists
+  // implied, tail within DP_P16_TAIL_MAX).  False: nothing written.
+  bool emit_p16d(const Fast& F, Out& O, int nv) const {
+    if (!narrow || !packed || !F.src_ok || no_p16d() || F.nid != F.nc + F.nk) return false;
+    int32_t hdr[DP_H_SIZE] = {0};
+    hdr[DP_H_MAGIC] = DP_REC_MAGIC;
+    hdr[DP_H_NV] = nv;
+    hdr[DP_H_NC] = F.nc;
+    hdr[DP_H_NK] = F.nk;
+    hdr[DP_H_NCH] = F.nch;
+    hdr[DP_H_NA] = F.na;
+    hdr[DP_H_NID] = F.nid;
+    hdr[DP_H_NCL] = F.ncl;
+    hdr[DP_H_NKL] = F.nkl;
+    hdr[DP_H_NCHL] = F.nchl;
+    hdr[DP_H_WORDS] = dp_rec_layout_of(hdr).words;
+    if (!one_wave(hdr)) return false;  // (fits16 included)
+    for (int32_t i = 0; i < F.nc; ++i)
+      if (F.clause_off[i + 1] - F.clause_off[i] > 255) return false;
+    for (int32_t k = 0; k < F.nk; ++k)
+      if (F.card_off[k + 1] - F.card_off[k] > 255) return false;
+    hdr[DP_H_FMT] = DP_FMT_P16D;
+    const int64_t tb = dp_p16_tail_bytes(hdr);
+    if (tb > DP_P16_TAIL_MAX) return false;
+    const int64_t at = dp_p16_tail_at(hdr);
+    const int64_t phys = DP_H_SIZE + (at + tb + 3) / 4, padded = (phys + 3) & ~3LL;
+    int32_t* r = O.extend((size_t)padded);
+    std::memcpy(r, hdr, sizeof hdr);
+    uint16_t* u = reinterpret_cast<uint16_t*>(r + DP_H_SIZE);
+    auto put16 = [&](const int32_t* a, int32_t n) {
+      for (int32_t j = 0; j < n; ++j) u[j] = (uint16_t)a[j];
+      u += n;
+    };
+    put16(F.clause_lits, F.ncl);
+    put16(F.card_lits, F.nkl);
+    put16(F.card_bound, F.nk);
+    put16(F.anchors, F.na);
+    uint8_t* const b = reinterpret_cast<uint8_t*>(r + DP_H_SIZE);
+    uint8_t* t = reinterpret_cast<uint8_t*>(u);
+    std::memset(t, 0, (size_t)(b + at - t));
+    t = b + at;
+    for (int32_t i = 0; i < F.nc; ++i) *t++ = (uint8_t)(F.clause_off[i + 1] - F.clause_off[i]);
+    for (int32_t k = 0; k < F.nk; ++k) *t++ = (uint8_t)(F.card_off[k + 1] - F.card_off[k]);
+    std::memcpy(t, F.src, (size_t)F.nch);
+    t += F.nch;
+    std::memset(t, 0, (size_t)(reinterpret_cast<uint8_t*>(r + padded) - t));  // mask, then the padding
+    for (int32_t k = 0; k < F.nk; ++k) t[F.card_id[k] >> 3] |= (uint8_t)(1u << (F.card_id[k] & 7));
+    O.rec_len.push_back(padded);
+    O.ivar.insert(O.ivar.end(), F.owner_v, F.owner_v + F.nid);
+    O.icon.insert(O.icon.end(), F.owner_c, F.owner_c + F.nid);
+    O.ident_len.push_back(F.nid);
+    O.err.push_back(DP_LOWER_OK);
+    O.msg.emplace_back();
     return true;
   }
 
@@ -955,6 +1022,7 @@ struct Lowerer {
     }
     F.nc = nc; F.ncl = ncl; F.nk = nk; F.nkl = nkl; F.nch = nch; F.nchl = nchl; F.na = na; F.nid = nid;
     F.src_ok = src_ok;
+    if (emit_p16d(F, O, nv)) return 1;
     const size_t base = O.nrec;
     emit_fast(F, O, nv);
     narrow_last(O, base, src_ok ? src : nullptr);

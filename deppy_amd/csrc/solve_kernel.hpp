@@ -232,6 +232,19 @@ struct Group {
   static constexpr int WS = RSLOT ? 4 : 1;            // u64 words per row of wpair
   uint64_t* wpair;
   bool sweep;
+  // two-watched-literal lists of the one-wavefront path (mode_twl_lds):
+  // watched positions (a byte each) per clause row, live end per list, and
+  // for the flattened work list each entry's frontier literal and each
+  // frontier literal's compaction cursor.  twl_on: this problem's watch
+  // entries carry the slot in bit 15 (every row id below 32768).
+  static constexpr bool TWLL = mode_twl_lds(MODE);
+  uint8_t *wpos8, *wfi;
+  uint16_t* wend16;
+  int32_t* fcur;
+  bool twl_on;
+  __device__ __forceinline__ bool twl_dyn(int len) const {
+    return TWLL && twl_on && len >= TWL_MIN_LEN && len <= TWL_MAX_LEN;
+  }
   uint32_t *d_flip, *inS, *extra, *seen, *model, *used, *en, *en2, *dset, *fg;
   IX *wbuf, *cardq;
   int32_t* scal;
@@ -500,6 +513,14 @@ struct Group {
     imp = reinterpret_cast<IMP*>(cold + L.imp);
     wpair = reinterpret_cast<uint64_t*>(cold + L.wp);
     sweep = false;
+    twl_on = false;
+    if constexpr (TWLL) {
+      wpos8 = reinterpret_cast<uint8_t*>(lds + L.wpos);
+      wend16 = reinterpret_cast<uint16_t*>(lds + L.wend);
+      wfi = reinterpret_cast<uint8_t*>(lds + L.wfi);
+      fcur = reinterpret_cast<int32_t*>(lds + L.fcur);
+      twl_on = nrows < 32768;
+    }
     d_flip = reinterpret_cast<uint32_t*>(hot + L.d_flip);
     inS = reinterpret_cast<uint32_t*>(hot + L.inS);
     extra = reinterpret_cast<uint32_t*>(hot + L.extra);
@@ -1041,6 +1062,12 @@ struct Group {
 #endif
     for (int r = tid; r < nc; r += NT) {
       const int a = clause_off[r], b = clause_off[r + 1];
+      if (twl_dyn(b - a)) {  // two-watched: positions 0 and 1 (slot in bit 15)
+        ww[atomicAdd(&cnt[(int)clause_lits[a] ^ 1], 1u)] = enc(r);
+        ww[atomicAdd(&cnt[(int)clause_lits[a + 1] ^ 1], 1u)] = enc(r | 0x8000);
+        reinterpret_cast<uint16_t*>(wpos8)[r] = 0x0100;
+        continue;
+      }
       for (int j0 = a; j0 < b; j0 += 8) {
         int l[8];
 #pragma unroll
@@ -1063,6 +1090,10 @@ struct Group {
       }
     }
     wsync();
+    if constexpr (TWLL) {  // the cursors end where each list's entries end
+      for (int l = tid; l < 2 * nv; l += NT) wend16[l] = (uint16_t)cnt[l];
+      wsync();
+    }
 #ifdef DP_STAMPS
     sub[5] = stamp() - tb2;
 #endif
@@ -1409,6 +1440,181 @@ struct Group {
     }
   }
 
+  // ---- two-watched-literal rounds (mode_twl_lds) ----
+  // A clause row of TWL_MIN_LEN..TWL_MAX_LEN literals is in the lists of
+  // its two watched positions only (wpos8[2r], wpos8[2r + 1]; the entry in
+  // position p's list carries slot bit (p == the second watch) << 15).
+  // Visited through slot k, whose literal a round falsified, against the
+  // assignment at the start of the round (nothing is committed during it):
+  //  - the other watch true: nothing (the row is satisfied), keep the entry;
+  //  - else the row's outcome exactly as eval_clause -- with at most one
+  //    non-false position it is unit on that one (unassigned), satisfied
+  //    (true) or conflicting (none); with two or more, neither -- and slot k
+  //    moves to N[k] when the other watch is false too (both were falsified
+  //    by the last round, and each slot's visit takes its own one of the
+  //    first two non-false positions N[0], N[1]), else to the first of them
+  //    that is not the other watch.  Nothing to move to: keep the entry.
+  // The two visits of a row whose watches fell together may run in either
+  // order or in one instruction: a slot rewritten by the other visit holds
+  // N[j], non-false, and "the first of N not the other" then gives the same
+  // N[k].  A moved watch's literal z is non-false, so its list (~z) is not
+  // one this round iterates: it is appended to (atomicAdd on its live end),
+  // never compacted, within the occurrence-count capacity.
+  // Why every row that becomes unit or false is reached (so every round
+  // equals the occurrence lists' round, lowest rows and all): a row whose
+  // watches are both non-false has at most one of them falsified per round
+  // before it is visited; a row left with a false watch has its other watch
+  // true (assigned no later than the false one) or is unit / conflicting
+  // with the false watch among its latest falsified literals -- and every
+  // backtrack returns to a propagation fixpoint (a round boundary, where no
+  // row is unit), which un-assigns that watch whenever it would matter.
+  // Checked on the CPU against the occurrence lists, bit-exact on configs
+  // 2, 3, 5 and 6, and by the GPU parity tests.
+  __device__ __forceinline__ bool twl_row(int r, int k, int a, int b, int& crow) {
+    const uint32_t wp = reinterpret_cast<const uint16_t*>(wpos8)[r];
+    const int po = k ? (int)(wp & 0xffu) : (int)(wp >> 8);
+    const int vo = lit_val(clause_lits[a + po]);
+    DP_VIS_ADD(2 * sizeof(IX) + 2 + sizeof(IX) + 1);
+    if (vo > 0) return true;
+    // the first two non-false positions (and their literals)
+    int n0 = -1, n1 = -1, z0 = 0, z1 = 0;
+    for (int j = a; j < b && n1 < 0; j += 4) {
+      int l[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) l[q] = j + q < b ? (int)clause_lits[j + q] : -1;
+      int x[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) x[q] = l[q] >= 0 ? lit_val(l[q]) : -1;
+      DP_VIS_ADD(4 * (sizeof(IX) + 1));
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (x[q] >= 0) {
+          if (n0 < 0) { n0 = j + q - a; z0 = l[q]; }
+          else if (n1 < 0) { n1 = j + q - a; z1 = l[q]; }
+        }
+    }
+    if (n1 < 0) {
+      if (n0 < 0) crow = min(crow, r);           // every literal false
+      else if (lit_val(z0) == 0) note(z0, r);    // unit
+    }
+    int q, z;
+    if (vo < 0) { q = k ? n1 : n0; z = k ? z1 : z0; }
+    else if (n0 != po) { q = n0; z = z0; }
+    else { q = n1; z = z1; }
+    if (q < 0) return true;
+    wpos8[2 * r + k] = (uint8_t)q;
+    const int li = z ^ 1;
+    const uint32_t sh = 16u * (uint32_t)(li & 1);
+    const uint32_t old = atomicAdd(reinterpret_cast<uint32_t*>(wend16) + (li >> 1), 1u << sh);
+    const_cast<IX*>(w)[(old >> sh) & 0xffffu] = enc(r | (k << 15));
+    return false;
+  }
+
+  // visit() for a two-watched problem: entry e (or -1) -> keep it in its list?
+  __device__ __forceinline__ bool visit_twl(int e, int& crow, int& ncq) {
+    DP_VIS_ADD(e >= 0 ? sizeof(IX) : 0);  // the watch entry
+    const int r = e >= 0 ? (e & 0x7fff) : -1, k = (e >> 15) & 1;
+    const bool ok = r >= 0 && row_on(r);
+    const bool card = ok && r >= nc;
+    const uint64_t m = __ballot(card);
+    const bool fits = ncq + __popcll(m) <= CQ;  // queue full: evaluate in-lane
+    bool keep = true;
+    if (card && fits) cardq[ncq + __popcll(m & lanemask_lt())] = enc(r);
+    else if (card) card_serial(r, crow);
+    else if (ok) {
+      const int a = clause_off[r], b = clause_off[r + 1];
+      if (twl_dyn(b - a)) {
+        keep = twl_row(r, k, a, b, crow);
+      } else {
+        const int ul = eval_clause(r, clause_lits, a, b, crow);
+        if (ul >= 0) note(ul, r);
+      }
+    }
+    if (fits) ncq += __popcll(m);
+    return keep;
+  }
+
+  // One frontier literal's list [w_off[l], wend[l]): visited 64 entries at a
+  // time, the kept ones compacted to its front by ballot rank (a moved
+  // entry is written only once an earlier one left).
+  __device__ __forceinline__ int twl_list(int l, int& crow, int& ncq) {
+    IX* wm = const_cast<IX*>(w);
+    const int a = w_off[l], e = wend16[l];
+    int kept = 0;
+    for (int k0 = a; k0 < e; k0 += NT) {
+      const int j = k0 + tid;
+      const int ent = j < e ? (int)w[j] : -1;
+      const bool kk = visit_twl(ent, crow, ncq) && ent >= 0;
+      const uint64_t km = __ballot(kk);
+      const int at = a + kept + __popcll(km & lanemask_lt());
+      if (kk && at != j) wm[at] = enc(ent);
+      kept += __popcll(km);
+    }
+    if (tid == 0) wend16[l] = (uint16_t)(a + kept);
+    return e - a;
+  }
+
+  // The frontier trail[lo..hi) of a two-watched problem.  Larger frontiers
+  // are flattened as on the occurrence lists, each work-list entry tagged
+  // with its frontier literal (wfi); the entries of one list are contiguous,
+  // so each is compacted by its rank among the kept entries of its segment
+  // plus its list's cursor (fcur), which the segment's last lane advances.
+  template <class FR>
+  __device__ __forceinline__ void frontier_twl(int lo, int hi, int& crow, int& ncq, FR&& front) {
+    if (hi - lo == 1) {
+      const int n = twl_list(DP_CHK(front(lo), 0, 2 * nv, 10), crow, ncq);
+      (void)n;
+      DP_ACC(12, n);
+      return;
+    }
+    IX* wm = const_cast<IX*>(w);
+    for (int b = lo; b < hi; b += NT) {
+      const int i = b + tid;
+      int cnt = 0, a = 0, l = 0;
+      if (i < hi) {
+        l = DP_CHK(front(i), 0, 2 * nv, 11);
+        a = w_off[l];
+        cnt = (int)wend16[l] - a;
+      }
+      const int incl = wave_incl_scan(cnt);
+      const int total = __builtin_amdgcn_readlane(incl, 63);
+      DP_ACC(26, total);
+      if (total <= WBUF) {
+        for (int k = 0, at = incl - cnt; k < cnt; ++k) {
+          wbuf[at + k] = enc(a + k);
+          wfi[at + k] = (uint8_t)tid;
+        }
+        if (i < hi) fcur[tid] = a;
+        wsync();
+        for (int t0 = 0; t0 < total; t0 += NT) {
+          const int t = t0 + tid;
+          const bool valid = t < total;
+          const int pos = valid ? (int)wbuf[t] : 0;
+          const int f = valid ? (int)wfi[t] : -1;
+          const int ent = valid ? (int)w[pos] : -1;
+          const bool kk = visit_twl(ent, crow, ncq) && valid;
+          const int fp = __shfl_up(f, 1), fn = __shfl_down(f, 1);
+          const uint64_t sm = __ballot(valid && (lane == 0 || fp != f));
+          const uint64_t le = lanemask_lt() | (1ull << lane);
+          const uint64_t seg = ~((1ull << (63 - __clzll(sm & le))) - 1ull);  // (valid lanes: a start at or below)
+          const uint64_t km = __ballot(kk);
+          const int base = valid ? fcur[f] : 0;
+          const int at = base + __popcll(km & lanemask_lt() & seg);
+          if (kk && at != pos) wm[at] = enc(ent);
+          if (valid && (lane == 63 || t + 1 >= total || fn != f)) fcur[f] = at + (kk ? 1 : 0);
+          wsync();
+        }
+        if (i < hi) wend16[l] = (uint16_t)fcur[tid];
+        wsync();
+      } else {
+        // a very large chunk: one frontier literal at a time
+        const int n = min(NT, hi - b);
+        for (int e = 0; e < n; ++e) twl_list(front(b + e), crow, ncq);
+      }
+    }
+    DP_ACC(13, hi - lo);
+  }
+
   // AtMost rows, one at a time per wavefront, lanes over positions (oracle:
   // eval_row): counts by ballot; a variable listed m times is a run of m
   // positions, forced false when the count plus m exceeds the bound.
@@ -1709,6 +1915,18 @@ struct Group {
       const int64_t t0 = stamp();
 #endif
       int ncq = 0;
+      if constexpr (TWLL) {
+        if (twl_on) {
+          frontier_twl(lo, hi, crow, ncq, front);
+          flush_cards(crow, ncq);
+          eval_learned(crow);
+#ifdef DP_STAMPS
+          DP_ACC(hi - lo == 1 ? 8 : 9, stamp() - t0);
+          DP_ACC(1, stamp() - t0);
+#endif
+          return;
+        }
+      }
       if (hi - lo == 1) {  // one new literal: threads over its watch list
         const int l = DP_CHK(front(lo), 0, 2 * nv, 10);
         const int a = w_off[l], e = w_off[l + 1];
@@ -2007,7 +2225,9 @@ struct Group {
   __device__ __forceinline__ int first_violated_() {
 #endif
     int best = INF;
-    if (nc <= 4 * NT) {
+    // (two-watched lists no longer hold every row a true literal occurs in:
+    // scan the rows)
+    if (nc <= 4 * NT || (TWLL && twl_on)) {
       // few rows: every thread scans its rows in ascending order (the
       // oracle's scan, a short dependent chain per thread)
       for (int c = tid; c < nc; c += NT) {

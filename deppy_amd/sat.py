@@ -443,6 +443,38 @@ def _replay_trace(tracer: Tracer, variables: list, lw, p: int, res: dict, j: int
         tracer.Trace(_Position([variables[v] for v in vs], conflicts))
 
 
+# Lowering storage reused by solve_wire, per calling thread: the records of
+# the last batch (page-locked, packed) stay valid until that thread's next call.
+_lowering = threading.local()
+LOWER_FLAGS = dict(narrow=True, packed=True, pinned=True)  # DP_LOWER_NARROW | PACKED | PINNED
+
+
+def _reused_lowered(wire: _lib.WireArrays) -> _lib.Lowered:
+    lw = getattr(_lowering, "lw", None)
+    if lw is None:
+        lw = _lowering.lw = _lib.Lowered(wire, **LOWER_FLAGS)
+    else:
+        lw.relower(wire)
+    return lw
+
+
+def solve_wire(wire: _lib.WireArrays, context: Optional[_lib.Context] = None, trace_cap: int = 0):
+    """The shipped path of SolveBatch from the wire format to host results:
+    dp_lower_into(NARROW | PACKED | PINNED) into this thread's reused,
+    page-locked storage, then dp_solve on the batch as it lies (dp_submit +
+    dp_job_wait; up to 16 catalogs on the latency path).  The records are the
+    form the GPU reads and are DMA'd without staging (the bench's `value` and
+    `end_to_end` legs time the same records).  Problems the lowering rejected
+    keep an empty record, solved as nothing and reported from lw.err.
+    Returns (lowered, results); both stay valid until this thread's next
+    call.  trace_cap > 0 solves through the traced device-resident form."""
+    lw = _reused_lowered(wire)
+    with (contextlib.nullcontext() if context else _ctx_lock):
+        ctx = context or device_context()
+        res = ctx.solve(lw.rec_off, lw.rec, trace_cap)
+    return lw, res
+
+
 def SolveBatch(inputs: Sequence[Sequence[Variable]], tracer: Optional[Tracer] = None,
                context: Optional[_lib.Context] = None) -> list:
     """Solve many independent problems in one GPU launch.
@@ -454,64 +486,58 @@ def SolveBatch(inputs: Sequence[Sequence[Variable]], tracer: Optional[Tracer] = 
     Returns [(installed | None, error | None)] in input order."""
     inputs = [list(v) for v in inputs]
     traced = tracer is not None and not isinstance(tracer, DefaultTracer)
-    lw = _lib.Lowered(encode_inputs(inputs), narrow=True)  # 16-bit records: the staged form
     out: list = [None] * len(inputs)
-    ok = [p for p in range(len(inputs)) if lw.err[p] == 0]
-    for p in range(len(inputs)):
-        if lw.err[p] == 1:
-            vid = _dup_id(inputs[p])
-            out[p] = (None, DuplicateIdentifier(vid, lw.msg[p]))
-        elif lw.err[p] == 2:
-            out[p] = (None, LookupErrors(lw.msg[p]))
-    if ok:
-        offs = [0]
-        parts = []
-        for p in ok:
-            r = lw.record(p)
-            parts.append(r)
-            offs.append(offs[-1] + len(r))
-        rec = np.concatenate(parts).astype(np.int32)
+    if not inputs:
+        return out
+    lw, res = solve_wire(encode_inputs(inputs), context, TRACE_CAP if traced else 0)
+    retraced = {}
+    if traced:
         with (contextlib.nullcontext() if context else _ctx_lock):
             ctx = context or device_context()
-            res = ctx.solve(np.array(offs, np.int64), rec, TRACE_CAP if traced else 0)
-            retraced = {}
-            if traced:
-                for j, p in enumerate(ok):
-                    rj, jj, cap = res, j, TRACE_CAP
-                    while rj["flags"][jj] & _lib.F_TRACE_TRUNCATED and cap < TRACE_CAP_MAX:
-                        cap *= 16
-                        r1 = lw.record(p).astype(np.int32)
-                        rj, jj = ctx.solve(np.array([0, len(r1)], np.int64), r1, cap), 0
-                    if rj["flags"][jj] & _lib.F_TRACE_TRUNCATED:
-                        # the reference's tracer sees every unsatisfiable step
-                        # (search.go:173); this one would miss the steps past
-                        # the largest reservation
-                        warnings.warn("deppy_amd: search trace of problem %d truncated at %d words; "
-                                      "the tracer sees only its first steps" % (p, TRACE_CAP_MAX),
-                                      RuntimeWarning, stacklevel=2)
-                    retraced[j] = (rj, jj)
-        for j, p in enumerate(ok):
-            variables = inputs[p]
-            if traced:
-                rj, jj = retraced[j]
-                _replay_trace(tracer, variables, lw, p, rj, jj)
-            st = int(res["status"][j])
-            if st == SAT:
-                inst = _lib.installed_list(res, j, len(variables))
-                out[p] = ([variables[v] for v in inst] or None, None)
-            elif st == UNSAT:
-                i0 = int(lw.ident_off[p])
-                applied = []
-                for ident in _lib.core_list(res, j):
-                    vi = int(lw.ident_var[i0 + ident])
-                    ci = int(lw.ident_con[i0 + ident])
-                    var = variables[vi]
-                    applied.append(AppliedConstraint(var, var.Constraints()[ci]))
-                out[p] = (None, NotSatisfiable(applied))
-            elif st == INCOMPLETE:
-                out[p] = (None, ErrIncomplete)
-            else:
-                out[p] = (None, InternalError("unexpected internal error"))
+            for p in range(len(inputs)):
+                if lw.err[p]:
+                    continue
+                rj, jj, cap = res, p, TRACE_CAP
+                while rj["flags"][jj] & _lib.F_TRACE_TRUNCATED and cap < TRACE_CAP_MAX:
+                    cap *= 16
+                    r1 = np.ascontiguousarray(lw.record(p))
+                    rj, jj = ctx.solve(np.array([0, len(r1)], np.int64), r1, cap), 0
+                if rj["flags"][jj] & _lib.F_TRACE_TRUNCATED:
+                    # the reference's tracer sees every unsatisfiable step
+                    # (search.go:173); this one would miss the steps past the
+                    # largest reservation
+                    warnings.warn("deppy_amd: search trace of problem %d truncated at %d words; "
+                                  "the tracer sees only its first steps" % (p, TRACE_CAP_MAX),
+                                  RuntimeWarning, stacklevel=2)
+                retraced[p] = (rj, jj)
+    for p in range(len(inputs)):
+        variables = inputs[p]
+        if lw.err[p] == 1:
+            out[p] = (None, DuplicateIdentifier(_dup_id(variables), lw.msg[p]))
+            continue
+        if lw.err[p] == 2:
+            out[p] = (None, LookupErrors(lw.msg[p]))
+            continue
+        if traced:
+            rj, jj = retraced[p]
+            _replay_trace(tracer, variables, lw, p, rj, jj)
+        st = int(res["status"][p])
+        if st == SAT:
+            inst = _lib.installed_list(res, p, len(variables))
+            out[p] = ([variables[v] for v in inst] or None, None)
+        elif st == UNSAT:
+            i0 = int(lw.ident_off[p])
+            applied = []
+            for ident in _lib.core_list(res, p):
+                vi = int(lw.ident_var[i0 + ident])
+                ci = int(lw.ident_con[i0 + ident])
+                var = variables[vi]
+                applied.append(AppliedConstraint(var, var.Constraints()[ci]))
+            out[p] = (None, NotSatisfiable(applied))
+        elif st == INCOMPLETE:
+            out[p] = (None, ErrIncomplete)
+        else:
+            out[p] = (None, InternalError("unexpected internal error"))
     return out
 
 
