@@ -150,7 +150,8 @@ namespace dp {
 // ---------------------------------------------------------------------------
 struct Launch {
   int first, count, mode, lds;
-  bool dev_lists;  // holds int32 records whose watch lists the grid-wide passes build (watch_build.hip)
+  bool dev_lists;  // holds DP_FMT_I32 records above DEV_WATCH_VARS variables, whose watch lists the
+                   // grid-wide passes build (watch_build.hip); copied as they lie or by stage_one alike
 };
 
 // What the plan needs of one record, from its header alone (one cache line
@@ -509,10 +510,11 @@ int64_t stage_block(int64_t n, const Pool& pool) {
 
 // Stage local problem i of the plan into dst (the staged image area): the
 // int32 header with its format word, then the body in the form the plan
-// chose.  A 16-bit record to a 16-bit copy, or an int32 record to an int32
-// copy, is copied as it is; a 16-bit record for a multi-wave problem is
-// widened.  Every body is checked once: a 16-bit record copied as it is by
-// the kernel (valid_record, DP_FMT_U16), any other here, while narrowing it
+// chose.  A 16-bit record to a 16-bit copy, or a plain int32 record to a
+// multi-wave group, is copied as it is; a 16-bit record for a multi-wave
+// problem is widened.  Every body is checked once: a record copied as it is
+// by the kernel (valid_record for DP_FMT_U16, valid_wide for DP_FMT_I32, whose
+// watch lists the device builds), any other here, while narrowing it
 // (DP_FMT_U16_CHECKED) or before building its watch lists.  Returns false for
 // a malformed record:
 // its staged copy is marked DP_FMT_REJECT and the kernel reports DP_ERROR /
@@ -553,6 +555,14 @@ bool stage_one(const Plan& P, const int32_t* rec, const int64_t* rec_off, int32_
       std::memcpy(d + DP_H_SIZE, src + DP_H_SIZE, 4 * (size_t)(phys - DP_H_SIZE));
       for (int64_t j = phys; j < sw; ++j) d[j] = 0;
     }
+  } else if (fmt == DP_FMT_I32) {
+    // a plain int32 record for a multi-wave group: copied as it is, like a
+    // record DMA'd as it lies -- the kernel checks it (valid_wide) and the
+    // device builds its watch lists (the solving workgroup, or the grid-wide
+    // passes above DEV_WATCH_VARS).  Building them here cost one host thread
+    // ~2 ms per OLM-scale catalog inside a latency call.
+    std::memcpy(d + DP_H_SIZE, src + DP_H_SIZE, 4 * (size_t)body);
+    for (int64_t j = words; j < sw; ++j) d[j] = 0;
   } else {
     d[DP_H_FMT] = dp::DP_FMT_I32_CHECKED;  // checked here, watch lists built here
     bool ok;
@@ -574,25 +584,6 @@ bool stage_one(const Plan& P, const int32_t* rec, const int64_t* rec_off, int32_
     for (int64_t j = end; j < sw; ++j) d[j] = 0;
   }
   return true;
-}
-
-// Which multi-wave launches need the grid-wide watch-list passes
-// (watch_build.hip): those holding a record copied to the device as it lies in
-// DP_FMT_I32 above DEV_WATCH_VARS variables.  plan_chunk assumes every record
-// goes as it lies; a record the chunk stages instead (stage_one) carries
-// host-built lists, and a chunk staged whole (not direct, the latency path,
-// dp_upload) launches no passes.
-void settle_dev_lists(Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0, bool direct) {
-  for (auto& L : P.launches) {
-    if (L.mode == M_LDS || !L.dev_lists) continue;
-    bool any = false;
-    for (int k = L.first; direct && k < L.first + L.count && !any; ++k) {
-      const int32_t i = P.order[(size_t)k];
-      const int32_t* h = rec + rec_off[p0 + i];
-      any = P.direct[(size_t)i] && h[DP_H_FMT] == DP_FMT_I32 && !device_watches(h);
-    }
-    L.dev_lists = any;
-  }
 }
 
 void* pinned_alloc(size_t bytes) {
@@ -1143,7 +1134,6 @@ int start_chunk(dp_ctx* ctx, Device& D, Lane& L, dp_job* job, int32_t p0, int32_
     }
     Q.img_words = o;
   }
-  dp::settle_dev_lists(L.plan, job->rec, job->rec_off, p0, direct);
   const InLayout il = in_layout(L.plan);
   L.ol = out_layout(L.plan);
   // The host side of the input region: all of it, or (direct) only what
@@ -1312,7 +1302,6 @@ int fast_solve(dp_ctx* ctx, Device& D, const dp_batch* b, dp_result* res) {
   const int32_t n = b->n_problems;
   F.bad.assign((size_t)n, 0);
   dp::plan_chunk(F.plan, b->rec, b->rec_off, 0, n, ctx->flags, &F.bad, nullptr);
-  dp::settle_dev_lists(F.plan, b->rec, b->rec_off, 0, false);
   const Plan& P = F.plan;
   if (!P.skip.empty() || !P.scratch_off.empty()) return 1;
   if (hipSetDevice(D.ordinal) != hipSuccess) return 1;
@@ -1622,7 +1611,6 @@ int build_slice(dp_ctx* ctx, Slice& s, const dp_batch* b, int32_t trace_cap) {
   const int32_t n = s.p1 - s.p0;
   std::vector<uint8_t> bad((size_t)std::max(n, 1), 0);
   dp::plan_chunk(s.plan, b->rec, b->rec_off, s.p0, n, ctx->flags, &bad, ctx->pool);
-  dp::settle_dev_lists(s.plan, b->rec, b->rec_off, s.p0, false);  // (every record staged)
   s.il = in_layout(s.plan);
   s.ol = out_layout(s.plan);
   std::vector<char> host(s.il.end);
