@@ -775,6 +775,32 @@ struct Buf {
 struct dp_job;
 
 // One stream with its own buffers; holds at most one chunk in flight.
+// A chunk's one-wavefront launches after its first, spread over other
+// lane streams of the device (DEPPY_SPREAD=1, A/B): each waits for the
+// chunk's copies (`start`, recorded on the chunk's stream before its first
+// launch) and the chunk's stream waits for each (`fin`), so launches of
+// different LDS buckets run side by side -- the dispatcher packs workgroups
+// of both onto a CU -- instead of one after another, each with its own tail.
+constexpr int kMaxSpread = 4;
+struct Spread {
+  hipStream_t s[kMaxSpread] = {};
+  int n = 0;
+  hipEvent_t start = nullptr, fin[kMaxSpread] = {};
+  int create() {
+    if (hipEventCreateWithFlags(&start, hipEventDisableTiming) != hipSuccess) return -1;
+    for (auto& e : fin)
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return -1;
+    return 0;
+  }
+  void destroy() {
+    if (start) (void)hipEventDestroy(start);
+    for (auto& e : fin)
+      if (e) (void)hipEventDestroy(e);
+    start = nullptr;
+    for (auto& e : fin) e = nullptr;
+  }
+};
+
 struct Lane {
   int device = 0;
   hipStream_t s = nullptr;
@@ -783,6 +809,7 @@ struct Lane {
   // runs while the stream's current kernel does; `copied` orders the launch
   hipStream_t cs = nullptr;
   hipEvent_t copied = nullptr;
+  Spread spread;  // (DEPPY_SPREAD) its events; the sibling streams are set per chunk
   Buf h_in{nullptr, 0, true}, d_in, h_out{nullptr, 0, true}, d_out, scratch;
   bool zc_out = false;  // the chunk's kernels wrote their results straight into h_out
   // the chunk in flight
@@ -875,6 +902,7 @@ struct dp_ctx {
   int64_t chunk_bytes = kChunkBytes;
   int32_t grid_cap = 0;  // test: workgroups of a queued launch (DEPPY_GRID_CAP; 0 = resident maximum)
   bool fast_path = true;  // small dp_solve batches on the latency path (DEPPY_FAST_PATH=0: off)
+  bool spread = false;    // DEPPY_SPREAD=1: a chunk's later one-wavefront launches on sibling streams
   dp_stats st{};         // the caller-thread paths (resident batches)
   ~dp_ctx() { delete pool; }
 };
@@ -893,6 +921,7 @@ struct Slice {
   int64_t* stamps = nullptr;
   hipStream_t stream = nullptr;  // lane of the last launch
   hipEvent_t k0 = nullptr, k1 = nullptr;
+  Spread spread;
 };
 
 struct dp_resident {
@@ -950,14 +979,24 @@ void add_device_stats(Device& D, const dp_stats& b) {
 // Enqueue a planned chunk's launches on stream s.
 // Multi-wave launches take their items from a queue (kernel_api.hpp
 // KernelArgs::queue) in the scratch's first words, zeroed here.
-int enqueue_launches(dp_ctx* ctx, const Plan& P, const dp::KernelArgs& base, hipStream_t s, dp_stats& st) {
+int enqueue_launches(dp_ctx* ctx, const Plan& P, const dp::KernelArgs& base, hipStream_t s, dp_stats& st,
+                     Spread* sp = nullptr) {
   static const bool no_queue = [] {  // diagnostic DEPPY_NO_QUEUE=1: one workgroup per item
     const char* e = std::getenv("DEPPY_NO_QUEUE");
     return e && *e && *e != '0';
   }();
   if (!P.scratch_off.empty()) HIP_OK(hipMemsetAsync(base.scratch, 0, 4 * dp::kQueueWords, s));
-  int q = 0;
+  int nlds = 0;
+  for (const auto& L : P.launches) nlds += L.mode == dp::M_LDS;
+  const bool spread = sp && sp->n > 0 && nlds > 1;
+  if (spread) HIP_OK(hipEventRecord(sp->start, s));
+  int q = 0, jl = 0, nf = 0;
   for (const auto& L : P.launches) {
+    hipStream_t t = s;
+    if (spread && L.mode == dp::M_LDS && jl++ > 0 && nf < kMaxSpread) {
+      t = sp->s[(jl - 2) % sp->n];
+      HIP_OK(hipStreamWaitEvent(t, sp->start, 0));
+    }
     dp::KernelArgs a = base;
     a.items = base.items + L.first;
     if (L.mode != dp::M_LDS) {
@@ -969,10 +1008,22 @@ int enqueue_launches(dp_ctx* ctx, const Plan& P, const dp::KernelArgs& base, hip
       ++q;
       if (L.dev_lists) HIP_OK(dp::launch_watch_build(a, L.mode, L.count, s));
     }
-    HIP_OK(dp::launch_solve(a, L.mode, L.count, L.lds, s));
+    HIP_OK(dp::launch_solve(a, L.mode, L.count, L.lds, t));
+    if (t != s) {
+      HIP_OK(hipEventRecord(sp->fin[nf], t));
+      HIP_OK(hipStreamWaitEvent(s, sp->fin[nf], 0));
+      ++nf;
+    }
     st.launches++;
   }
   return 0;
+}
+
+// The sibling streams of lane stream i (the device's other lane streams).
+void set_siblings(const Device& D, int i, Spread& sp, bool on) {
+  sp.n = 0;
+  if (!on) return;
+  for (int j = 1; j < D.nstreams && sp.n < kMaxSpread; ++j) sp.s[sp.n++] = D.lanes[(i + j) % D.nstreams].s;
 }
 
 // Wait for a lane's chunk and scatter its results into its job's dp_result
@@ -1208,7 +1259,8 @@ int start_chunk(dp_ctx* ctx, Device& D, Lane& L, dp_job* job, int32_t p0, int32_
   a.core_pool_len = at<int32_t>(L.d_out.p, L.ol.pool_len);
   a.items = at<dp::WorkItem>(din, il.items);
   HIP_OK(hipEventRecord(L.k0, L.s));
-  if (enqueue_launches(ctx, P, a, L.s, st)) return -1;
+  set_siblings(D, (int)(&L - D.lanes) % D.nstreams, L.spread, ctx->spread);
+  if (enqueue_launches(ctx, P, a, L.s, st, &L.spread)) return -1;
   HIP_OK(hipEventRecord(L.k1, L.s));
   if (!L.zc_out) HIP_OK(hipMemcpyAsync(L.h_out.p, L.d_out.p, L.ol.d2h, hipMemcpyDeviceToHost, L.s));
   HIP_OK(hipEventRecord(L.done, L.s));
@@ -1404,7 +1456,7 @@ dp_ctx* dp_create(const dp_opts* opts) {
                              (ctx->copy_streams && hipStreamCreateWithFlags(&L.cs, hipStreamNonBlocking) != hipSuccess))) ||
           hipEventCreateWithFlags(&L.copied, hipEventDisableTiming) != hipSuccess ||
           hipEventCreate(&L.k0) != hipSuccess || hipEventCreate(&L.k1) != hipSuccess ||
-          hipEventCreateWithFlags(&L.done, hipEventDisableTiming) != hipSuccess) {
+          hipEventCreateWithFlags(&L.done, hipEventDisableTiming) != hipSuccess || L.spread.create() != 0) {
         dp::set_global_error("dp_create: cannot create streams");
         dp_destroy(ctx);
         return nullptr;
@@ -1420,6 +1472,7 @@ dp_ctx* dp_create(const dp_opts* opts) {
   ctx->direct = env_i64("DEPPY_DIRECT", 1) != 0; // diagnostic: 0 = stage every chunk
   ctx->grid_cap = (int32_t)std::max<int64_t>(0, env_i64("DEPPY_GRID_CAP", 0));
   ctx->fast_path = env_i64("DEPPY_FAST_PATH", 1) != 0;
+  ctx->spread = env_i64("DEPPY_SPREAD", 0) != 0;
   const int ht = dp::host_threads();
   ctx->pool = new dp::Pool(ht);
   const int per = std::max(2, ht / cnt);
@@ -1469,6 +1522,7 @@ void dp_destroy(dp_ctx* ctx) {
       if (L.k1) (void)hipEventDestroy(L.k1);
       if (L.done) (void)hipEventDestroy(L.done);
       if (L.copied) (void)hipEventDestroy(L.copied);
+      L.spread.destroy();
     }
     for (int li = 0; li < D.nstreams; ++li) {  // (lanes li + nstreams... share these)
       if (D.lanes[li].s) (void)hipStreamDestroy(D.lanes[li].s);
@@ -1601,6 +1655,7 @@ void free_slice(Slice& s) {
     if (p) (void)hipFree(p);
   if (s.k0) (void)hipEventDestroy(s.k0);
   if (s.k1) (void)hipEventDestroy(s.k1);
+  s.spread.destroy();
   s = Slice{};
 }
 
@@ -1608,6 +1663,7 @@ int build_slice(dp_ctx* ctx, Slice& s, const dp_batch* b, int32_t trace_cap) {
   HIP_OK(hipSetDevice(s.ordinal));
   HIP_OK(hipEventCreate(&s.k0));
   HIP_OK(hipEventCreate(&s.k1));
+  if (s.spread.create()) HIP_OK(hipErrorOutOfMemory);
   const int32_t n = s.p1 - s.p0;
   std::vector<uint8_t> bad((size_t)std::max(n, 1), 0);
   dp::plan_chunk(s.plan, b->rec, b->rec_off, s.p0, n, ctx->flags, &bad, ctx->pool);
@@ -1641,6 +1697,7 @@ int launch_slice(dp_ctx* ctx, Slice& s, int32_t trace_cap) {
   Device& D = ctx->dev[(size_t)s.d];
   HIP_OK(hipSetDevice(D.ordinal));
   s.stream = D.lanes[D.next].s;
+  set_siblings(D, D.next % D.nstreams, s.spread, ctx->spread);
   D.next = (D.next + 1) % D.nlanes;
   HIP_OK(hipMemsetAsync(s.d_out.p + s.ol.pool_len, 0, 4, s.stream));
   dp::KernelArgs a = kernel_args(s.il, s.ol, s.d_in.p, s.d_out.p, reinterpret_cast<int32_t*>(s.scratch.p),
@@ -1651,7 +1708,7 @@ int launch_slice(dp_ctx* ctx, Slice& s, int32_t trace_cap) {
   a.trace_len = s.trace_len;
   a.trace_cap = trace_cap;
   HIP_OK(hipEventRecord(s.k0, s.stream));
-  if (enqueue_launches(ctx, s.plan, a, s.stream, ctx->st)) return -1;
+  if (enqueue_launches(ctx, s.plan, a, s.stream, ctx->st, &s.spread)) return -1;
   HIP_OK(hipEventRecord(s.k1, s.stream));
   return 0;
 }
