@@ -32,27 +32,47 @@ def lib():
     if _lib is None:
         if not os.path.exists(_LIB):
             build()
-        L = ctypes.CDLL(_LIB)
-        L.oracle_solve.argtypes = [_i32p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int32), _u32p,
-                                   _i32p, ctypes.POINTER(ctypes.c_int32),
-                                   ctypes.POINTER(ctypes.c_int64)]
-        L.oracle_solve.restype = ctypes.c_int
-        L.oracle_solve_batch.argtypes = [ctypes.c_int32, _i64p, _i32p, ctypes.c_int64,
-                                         ctypes.c_int32, _i8p, _i32p, _u32p, _i64p, _i32p,
-                                         _i64p, _i32p, _i64p]
-        L.oracle_solve_batch_traced.argtypes = [ctypes.c_int32, _i64p, _i32p, ctypes.c_int64,
-                                                ctypes.c_int32, _i8p, _i32p, _u32p, _i64p, _i32p,
-                                                _i64p, _i32p, _i64p, _i32p, ctypes.c_int32, _i32p]
-        L.oracle_search_scripted.argtypes = [_i32p, _i32p, ctypes.c_int32, _i32p, ctypes.c_int32,
-                                             ctypes.POINTER(ctypes.c_int32), _i32p,
-                                             ctypes.POINTER(ctypes.c_int32),
-                                             ctypes.POINTER(ctypes.c_int32)]
-        L.oracle_refute.argtypes = [_i32p, ctypes.c_void_p, ctypes.c_int64]
-        L.oracle_refute.restype = ctypes.c_int
-        L.oracle_check_model.argtypes = [_i32p, _u32p]
-        L.oracle_check_model.restype = ctypes.c_int
-        _lib = L
+        _lib = _bind(ctypes.CDLL(_LIB))
     return _lib
+
+
+_twl = None
+
+
+def twl_lib():
+    """The restatement with the kernel's two-watched-literal lists (make's
+    libsat_oracle_twl.so, -DORACLE_TWL), plus its round counters."""
+    global _twl
+    if _twl is None:
+        path = os.path.join(_HERE, "libsat_oracle_twl.so")
+        if not os.path.exists(path):
+            build()
+        L = _bind(ctypes.CDLL(path))
+        L.oracle_twl_stats.argtypes = [np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS"), ctypes.c_int]
+        _twl = L
+    return _twl
+
+
+def _bind(L):
+    L.oracle_solve.argtypes = [_i32p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int32), _u32p,
+                               _i32p, ctypes.POINTER(ctypes.c_int32),
+                               ctypes.POINTER(ctypes.c_int64)]
+    L.oracle_solve.restype = ctypes.c_int
+    L.oracle_solve_batch.argtypes = [ctypes.c_int32, _i64p, _i32p, ctypes.c_int64,
+                                     ctypes.c_int32, _i8p, _i32p, _u32p, _i64p, _i32p,
+                                     _i64p, _i32p, _i64p]
+    L.oracle_solve_batch_traced.argtypes = [ctypes.c_int32, _i64p, _i32p, ctypes.c_int64,
+                                            ctypes.c_int32, _i8p, _i32p, _u32p, _i64p, _i32p,
+                                            _i64p, _i32p, _i64p, _i32p, ctypes.c_int32, _i32p]
+    L.oracle_search_scripted.argtypes = [_i32p, _i32p, ctypes.c_int32, _i32p, ctypes.c_int32,
+                                         ctypes.POINTER(ctypes.c_int32), _i32p,
+                                         ctypes.POINTER(ctypes.c_int32),
+                                         ctypes.POINTER(ctypes.c_int32)]
+    L.oracle_refute.argtypes = [_i32p, ctypes.c_void_p, ctypes.c_int64]
+    L.oracle_refute.restype = ctypes.c_int
+    L.oracle_check_model.argtypes = [_i32p, _u32p]
+    L.oracle_check_model.restype = ctypes.c_int
+    return L
 
 
 def nv_of(rec) -> int:
@@ -77,7 +97,7 @@ def solve(rec: np.ndarray, budget: int = 0):
 
 
 def solve_batch(rec_off: np.ndarray, rec: np.ndarray, budget: int = 0, nthreads: int = 1,
-                trace_cap: int = 0):
+                trace_cap: int = 0, L=None):
     """Batch solve; returns dict of arrays (same layout as dp_result).  With
     trace_cap > 0 also the search trace: trace[P, trace_cap], trace_len[P]."""
     rec_off = np.ascontiguousarray(rec_off, dtype=np.int64)
@@ -97,12 +117,12 @@ def solve_batch(rec_off: np.ndarray, rec: np.ndarray, budget: int = 0, nthreads:
     if trace_cap > 0:
         out["trace"] = np.zeros((n, trace_cap), np.int32)
         out["trace_len"] = np.zeros(n, np.int32)
-        lib().oracle_solve_batch_traced(n, rec_off, rec, budget, nthreads, out["status"],
+        (L or lib()).oracle_solve_batch_traced(n, rec_off, rec, budget, nthreads, out["status"],
                                         out["flags"], out["installed"], inst_off, out["core"],
                                         core_off, out["core_len"], out["steps"], out["trace"],
                                         trace_cap, out["trace_len"])
         return out
-    lib().oracle_solve_batch(n, rec_off, rec, budget, nthreads, out["status"], out["flags"],
+    (L or lib()).oracle_solve_batch(n, rec_off, rec, budget, nthreads, out["status"], out["flags"],
                              out["installed"], inst_off, out["core"], core_off, out["core_len"],
                              out["steps"])
     return out

@@ -57,6 +57,12 @@ typedef struct {
   int32_t* wide; /* the int32 copy of a 16-bit-form record (widen), or NULL */
   /* watch lists: rows to evaluate when literal l becomes TRUE */
   int32_t *w_off, *w;
+#ifdef ORACLE_TWL
+  /* two-watched-literal lists (the kernel's DP_TWL_LDS variant): live end
+   * of each list, watched positions per clause row, dynamic rows */
+  int32_t *wend, *wpos;
+  uint8_t* dyn;
+#endif
   /* assignment */
   int8_t* val; /* 0 unassigned, 1 true, -1 false */
   int32_t *reason, *rnd, *trail;
@@ -97,6 +103,22 @@ typedef struct {
   int32_t* trace;
   int32_t trace_cap, trace_len, trace_stop;
 } st_t;
+
+#ifdef ORACLE_TWL
+/* Round counters of the two-watched-literal variant (single-threaded use:
+ * oracle_twl_stats): rounds, watch entries visited, 64-entry batches a
+ * wavefront would take (one frontier literal: its list; several: their lists
+ * flattened 64 literals at a time), two-watched row visits, watch moves, and
+ * what the occurrence lists would have visited in the same rounds: entries
+ * and batches (a list's capacity is its occurrence count). */
+static long long g_twl_stats[7];
+void oracle_twl_stats(long long* out, int reset) {
+  for (int i = 0; i < 7; ++i) {
+    out[i] = g_twl_stats[i];
+    if (reset) g_twl_stats[i] = 0;
+  }
+}
+#endif
 
 /* learned-row store: at most L_MAX rows and nv+64 literals */
 #define L_MAX 64
@@ -235,11 +257,34 @@ static int st_init(st_t* s, const int32_t* rec) {
   s->w = xcalloc((size_t)s->w_off[nl], sizeof(int32_t));
   int32_t* cur = xcalloc((size_t)nl, sizeof(int32_t));
   for (int l = 0; l < nl; ++l) cur[l] = s->w_off[l];
+#ifdef ORACLE_TWL
+  /* a clause row of 3..254 literals sits in the lists of its positions 0 and
+   * 1 only (entry r | slot << 30); shorter and longer rows in every one */
+  s->dyn = xcalloc((size_t)p->nc, 1);
+  s->wpos = xcalloc((size_t)p->nc * 2, sizeof(int32_t));
+  for (int r = 0; r < p->nc; ++r) {
+    const int a = p->clause_off[r], len = p->clause_off[r + 1] - a;
+    s->dyn[r] = len >= 3 && len <= 254;
+    if (s->dyn[r]) {
+      s->wpos[2 * r] = 0;
+      s->wpos[2 * r + 1] = 1;
+      s->w[cur[p->clause_lits[a] ^ 1]++] = r;
+      s->w[cur[p->clause_lits[a + 1] ^ 1]++] = r | (1 << 30);
+    } else {
+      for (int j = a; j < a + len; ++j) s->w[cur[p->clause_lits[j] ^ 1]++] = r;
+    }
+  }
+#else
   for (int r = 0; r < p->nc; ++r)
     for (int j = p->clause_off[r]; j < p->clause_off[r + 1]; ++j) s->w[cur[p->clause_lits[j] ^ 1]++] = r;
+#endif
   for (int k = 0; k < p->nk; ++k)
     for (int j = p->card_off[k]; j < p->card_off[k + 1]; ++j) s->w[cur[2 * p->card_lits[j]]++] = p->nc + k;
+#ifdef ORACLE_TWL
+  s->wend = cur;
+#else
   free(cur);
+#endif
   int nv = p->nv;
   s->val = xcalloc((size_t)nv, 1);
   s->reason = xcalloc((size_t)nv, sizeof(int32_t));
@@ -271,6 +316,9 @@ static int st_init(st_t* s, const int32_t* rec) {
 
 static void st_free(st_t* s) {
   free(s->wide);
+#ifdef ORACLE_TWL
+  free(s->wend); free(s->wpos); free(s->dyn);
+#endif
   free(s->w_off); free(s->w); free(s->val); free(s->reason); free(s->rnd); free(s->trail);
   free(s->imp_pos); free(s->imp_neg); free(s->touched); free(s->is_extra); free(s->seen);
   free(s->used); free(s->uacc); free(s->work); free(s->inS); free(s->model); free(s->d_lit); free(s->d_mark);
@@ -405,6 +453,41 @@ static void eval_learned(st_t* s, int* crow) {
   for (int j = s->learn_lo; j < s->nl; ++j) eval_row(s, s->p.nrows + j, crow);
 }
 
+#ifdef ORACLE_TWL
+/* The kernel's two-watched-literal visit (solve_kernel.hpp twl_row) of
+ * dynamic clause row r through slot k, whose literal a round falsified:
+ * nothing when the other watch is true; else the row's outcome exactly as
+ * eval_clause gives it, and slot k moves to N[k] (both watches false) or to
+ * the first of N that is not the other watch, N being the row's first two
+ * non-false positions.  Returns 1 to keep the entry in its list. */
+static int twl_visit(st_t* s, int r, int k, int* crow) {
+  const prob_t* p = &s->p;
+  const int32_t* L = p->clause_lits;
+  const int a = p->clause_off[r], b = p->clause_off[r + 1];
+  const int po = s->wpos[2 * r + 1 - k];
+  const int vo = lit_val(s, L[a + po]);
+  g_twl_stats[3]++;
+  if (vo > 0) return 1;
+  int n0 = -1, n1 = -1;
+  for (int j = a; j < b && n1 < 0; ++j)
+    if (lit_val(s, L[j]) >= 0) {
+      if (n0 < 0) n0 = j - a;
+      else n1 = j - a;
+    }
+  if (n1 < 0) {
+    if (n0 < 0) { if (r < *crow) *crow = r; }
+    else if (lit_val(s, L[a + n0]) == 0) note(s, L[a + n0], r);
+  }
+  const int q = vo < 0 ? (k ? n1 : n0) : (n0 != po ? n0 : n1);
+  if (q < 0) return 1;
+  s->wpos[2 * r + k] = q;
+  const int li = L[a + q] ^ 1;
+  s->w[s->wend[li]++] = r | (k << 30);
+  g_twl_stats[4]++;
+  return 0;
+}
+#endif
+
 static int propagate(st_t* s) {
   for (;;) {
     if (s->qhead == s->tlen) {
@@ -417,11 +500,40 @@ static int propagate(st_t* s) {
     }
     int lo = s->qhead, hi = s->tlen, rd = ++s->round, crow = INF;
     s->qhead = hi;
+#ifdef ORACLE_TWL
+    g_twl_stats[0]++;
+    for (int c = lo; c < hi; c += 64) {
+      int t = 0, o = 0;
+      for (int i = c; i < hi && i < c + 64; ++i) {
+        t += s->wend[s->trail[i]] - s->w_off[s->trail[i]];
+        o += s->w_off[s->trail[i] + 1] - s->w_off[s->trail[i]];
+      }
+      g_twl_stats[2] += (t + 63) / 64;
+      g_twl_stats[5] += o;
+      g_twl_stats[6] += (o + 63) / 64;
+    }
+    for (int i = lo; i < hi; ++i) {
+      const int l = s->trail[i], e = s->wend[l];
+      int at = s->w_off[l];
+      for (int k = s->w_off[l]; k < e; ++k) {
+        const int ent = s->w[k], r = ent & ~(1 << 30);
+        int keep = 1;
+        g_twl_stats[1]++;
+        if (row_on(s, r)) {
+          if (r < s->p.nc && s->dyn[r]) keep = twl_visit(s, r, ent >> 30, &crow);
+          else eval_row(s, r, &crow);
+        }
+        if (keep) s->w[at++] = ent;
+      }
+      s->wend[l] = at;
+    }
+#else
     for (int i = lo; i < hi; ++i) {
       int l = s->trail[i];
       for (int k = s->w_off[l]; k < s->w_off[l + 1]; ++k)
         if (row_on(s, s->w[k])) eval_row(s, s->w[k], &crow);
     }
+#endif
     eval_learned(s, &crow);
     if (finish_round(s, rd, crow) < 0) return -1;
   }
