@@ -174,8 +174,9 @@ def lib():
     L.dp_last_error.restype = ctypes.c_char_p
     L.dp_last_global_error.restype = ctypes.c_char_p
     L.dp_num_devices.argtypes = [vp]
-    L.dp_lanes.argtypes = [vp]
-    L.dp_lanes.restype = ctypes.c_int32
+    if hasattr(L, "dp_lanes"):  # (an older build loaded as a measurement variant may lack it)
+        L.dp_lanes.argtypes = [vp]
+        L.dp_lanes.restype = ctypes.c_int32
     L.dp_solve.argtypes = [vp, ctypes.POINTER(Batch), ctypes.POINTER(Result)]
     L.dp_upload.argtypes = [vp, ctypes.POINTER(Batch), ctypes.POINTER(vp)]
     L.dp_upload_traced.argtypes = [vp, ctypes.POINTER(Batch), ctypes.c_int32, ctypes.POINTER(vp)]
@@ -382,7 +383,7 @@ class Context:
 
     def lanes(self) -> int:
         """Pipeline chunk slots per device (dp_lanes): chunks a serving loop keeps in flight."""
-        return int(lib().dp_lanes(self.h))
+        return int(lib().dp_lanes(self.h)) if hasattr(lib(), "dp_lanes") else 8
 
     def upload(self, rec_off: np.ndarray, rec: np.ndarray, trace_cap: int = 0) -> "Resident":
         return Resident(self, rec_off, rec, trace_cap)
