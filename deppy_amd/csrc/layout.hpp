@@ -52,7 +52,7 @@ __host__ __device__ constexpr int32_t mode_waves(int mode) {
 }
 // work list of one propagation chunk (rows watched by <= 64*waves frontier literals)
 #ifndef DP_WBUF_LDS
-#define DP_WBUF_LDS 256
+#define DP_WBUF_LDS 128
 #endif
 #ifndef DP_CQ_LDS
 #define DP_CQ_LDS 64
@@ -127,11 +127,30 @@ __host__ __device__ inline int64_t p16_tail_bytes(const int32_t* h) {
   const int64_t vc = h[DP_H_FMT] == DP_FMT_P16D ? 0 : (int64_t)h[DP_H_NV];
   return (int64_t)h[DP_H_NC] + h[DP_H_NK] + h[DP_H_NCH] + vc + ((int64_t)h[DP_H_NID] + 7) / 8;
 }
+// 16-bit words of a record's body (the arrays after the header) as the
+// one-wavefront kernel decodes it into LDS: the int32 form's, except that
+// DP_FMT_P16D's choice lists stay in the dependency rows they are implied
+// by -- one row reference per list (nch words) in place of choice_off
+// (nch + 1) and choice_lits (nchl).  The watch lists follow.
+// The packed forms (DP_FMT_P16 / P16D) also keep their identities as the
+// record's AtMost-identity mask (u32 words) with a prefix count per word, in
+// place of clause_id (nc) and card_id (nk): every identity owns exactly one
+// row, so the kernel works on rows and maps to identities only for the
+// outputs (solve_kernel.hpp row_of).
+__host__ __device__ inline int32_t id_mask_words16(const int32_t* h) {
+  return 3 * bits_words(h[DP_H_NID]) + 2;  // mask (2 halves a word) + counts (nbi + 1) + alignment
+}
+__host__ __device__ inline int32_t lds_body_words(const int32_t* h) {
+  int32_t b = h[DP_H_WORDS] - DP_H_SIZE;
+  if (h[DP_H_FMT] == DP_FMT_P16 || h[DP_H_FMT] == DP_FMT_P16D)
+    b += id_mask_words16(h) - h[DP_H_NC] - h[DP_H_NK];
+  return h[DP_H_FMT] == DP_FMT_P16D ? b - 1 - h[DP_H_NCHL] : b;
+}
 // Byte offset (in the M_LDS body region) of the packed tail's copy while the
 // kernel decodes it: the first 16-byte boundary past the decoded 16-bit
-// arrays, which end where the record's int32 form would (2 (words - 16)).
+// arrays (lds_body_words).
 __host__ __device__ inline int32_t p16_tail_copy(const int32_t* h) {
-  return (2 * (h[DP_H_WORDS] - DP_H_SIZE) + 15) & ~15;
+  return (2 * lds_body_words(h) + 15) & ~15;
 }
 
 // dp_rec_layout_of (include/deppy_hip.h) for host and device code.
@@ -244,6 +263,7 @@ struct Layout {
   int32_t used;      // bits[nid] identities met by a refutation                   [LDS unless M_HBM]
   int32_t en;        // bits[nid] identities enabled (core search)                 [LDS unless M_HBM]
   int32_t en2;       // bits[nid]                                                  [LDS unless M_HBM]
+  int32_t idt;       // (M_LDS) bits[nid] rows -> identities for the outputs (row_of)  [LDS]
   int32_t l_off;     // IX[L_MAX+1] learned rows (rows nrows..)
   int32_t l_lits;    // IX[lcap]
   int32_t dq;        // IX[2*cap] deque of choices (list, idx)
@@ -313,6 +333,7 @@ __host__ __device__ inline Layout layout(const int32_t* h) {
   // slack.  A packed record's tail is copied to p16_tail_copy (where the
   // watch lists go later) while it is decoded: the region covers that copy.
   int32_t body_bytes = (X.words - DP_H_SIZE + 8) * ix;
+  if (MODE == M_LDS) body_bytes = (lds_body_words(h) + (X.words - h[DP_H_WORDS]) + 8) * ix;
   if (MODE == M_LDS && (h[DP_H_FMT] == DP_FMT_P16 || h[DP_H_FMT] == DP_FMT_P16D)) {
     const int32_t need = p16_tail_copy(h) + (int32_t)((p16_tail_bytes(h) + 15) & ~15);
     body_bytes = body_bytes > need ? body_bytes : need;
@@ -345,6 +366,7 @@ __host__ __device__ inline Layout layout(const int32_t* h) {
   L.used = take(nbi * 4, HOT);
   L.en = take(nbi * 4, HOT);
   L.en2 = take(nbi * 4, HOT);
+  L.idt = MODE == M_LDS ? take(nbi * 4, HOT) : 0;
   L.reason = take(nv * ix, COLD);
   L.rs = take(nv * ix, COLD);
   L.trail = take(nv * ix, COLD);

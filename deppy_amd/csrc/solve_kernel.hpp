@@ -208,6 +208,28 @@ struct Group {
   const IX *clause_off, *clause_lits, *clause_id;
   const IX *card_off, *card_lits, *card_bound, *card_id;
   const IX *var_choice_off, *choice_off, *choice_lits, *anchors;
+  // DP_FMT_P16D in LDS: choice list k is dependency row rowref[k] after its
+  // first literal (layout.hpp lds_body_words); else nullptr and the lists
+  // are choice_off / choice_lits
+  const IX* rowref;
+  // Packed records on M_LDS (rowspace): identities as the AtMost-identity
+  // mask (idmask, u32 words) and its per-word prefix counts (idpc), no
+  // clause_id / card_id.  Identity i is AtMost row nc + rank1(i) when its
+  // mask bit is set, else clause row i - rank1(i) (layout.hpp
+  // lds_body_words).  `used`, `en`, `en2` and `enabled` are then indexed by
+  // row; the outputs (cores, trace) go back to identities through idt.
+  bool rowspace;
+  const uint32_t* idmask;
+  const uint16_t* idpc;
+  uint32_t* idt;
+  __device__ __forceinline__ int row_of(int id) const {
+    const uint32_t m = idmask[id >> 5];
+    const int sh = id & 31;
+    const int r1 = (int)idpc[id >> 5] + __popc(m & ((1u << sh) - 1u));
+    return (m >> sh) & 1u ? nc + r1 : id - r1;
+  }
+  // the bit a row sets in used / en / enabled
+  __device__ __forceinline__ int row_key(int r) const { return rowspace ? r : row_ident(r); }
   const IX *w_off, *w;  // watch lists, built by build_watches
   int nwatch, dthr;
   // BCP-visited bytes (this thread): the watch entries, row offsets, row
@@ -441,6 +463,8 @@ struct Group {
     nbv = bits_words(nv); nbi = bits_words(nid);
     const IX* body;
     bool packed = false;
+    rowref = nullptr;
+    rowspace = false;
     if constexpr (MODE == M_LDS) {
       // The record -> LDS, as it is: the host stages one-wavefront records in
       // a 16-bit form (DP_FMT_U16, or DP_FMT_P16 whose tail is decoded below),
@@ -482,10 +506,12 @@ struct Group {
         clause_off = q;  q += nc + 1;
         card_off = q;    q += nk + 1;
         var_choice_off = q; q += nv + 1;
-        choice_off = q;  q += nch + 1;
-        clause_id = q;   q += nc;
-        card_id = q;     q += nk;
-        if (derived) choice_lits = q;
+        if (derived) { rowref = q; q += nch; }
+        else { choice_off = q; q += nch + 1; }
+        q += (q - b) & 1;  // (4-byte alignment)
+        idmask = reinterpret_cast<const uint32_t*>(q); q += 2 * nbi;
+        idpc = reinterpret_cast<const uint16_t*>(q);   q += nbi + 1;
+        rowspace = true;
         if (!unpack16(reinterpret_cast<const char*>(b) + p16_tail_at(h), (int)p16_tail_bytes(h), derived,
                       lds + L.reason, reinterpret_cast<uint8_t*>(b) + p16_tail_copy(h)))
           return false;
@@ -531,6 +557,7 @@ struct Group {
     used = reinterpret_cast<uint32_t*>(hot + L.used);
     en = reinterpret_cast<uint32_t*>(hot + L.en);
     en2 = reinterpret_cast<uint32_t*>(hot + L.en2);
+    idt = reinterpret_cast<uint32_t*>(lds + L.idt);
     l_off = reinterpret_cast<IX*>(cold + L.l_off);
     l_lits = reinterpret_cast<IX*>(cold + L.l_lits);
     dq = reinterpret_cast<IX*>(cold + L.dq);
@@ -585,9 +612,9 @@ struct Group {
     // the watch lists follow the record (M_LDS) or live in the problem's
     // scratch; M_LDS counts on the per-literal arrays, initialised below
     if constexpr (MODE == M_LDS) {
-      build_watches(const_cast<IX*>(rv(X.w_off)), const_cast<IX*>(rv(X.w)),
-                    reinterpret_cast<uint32_t*>(lds + L.reason));
-      w_off = rv(X.w_off); w = rv(X.w);
+      IX* wo = const_cast<IX*>(body) + lds_body_words(h);  // right after the decoded arrays
+      build_watches(wo, wo + 2 * nv + 1, reinterpret_cast<uint32_t*>(lds + L.reason));
+      w_off = wo; w = wo + 2 * nv + 1;
     } else {
       if (h[DP_H_FMT] == DP_FMT_I32) {  // plain int32 record: the lists in scratch (layout.hpp wl)
         IX* wo = reinterpret_cast<IX*>(hbm + L.wl);
@@ -678,9 +705,9 @@ struct Group {
       // decoded (unpack16): offsets are prefix sums of byte lengths (from 0,
       // non-decreasing), identities come from the mask (in range); only the
       // totals remain to check
-      if (tid == 0)
+      if (tid == 0)  // (DP_FMT_P16D: unpack16 counted the lists' nchl variables)
         bad = (int)clause_off[nc] != ncl || (int)card_off[nk] != nkl || (int)var_choice_off[nv] != nch ||
-              (int)choice_off[nch] != nchl;
+              (!derived && (int)choice_off[nch] != nchl);
     } else {
       offsets(clause_off, nc, ncl);
       range(clause_id, nc, nid);
@@ -691,7 +718,7 @@ struct Group {
     }
     range(clause_lits, ncl, 2 * nv);
     range(card_lits, nkl, nv);
-    if (!derived) range(choice_lits, nchl, nv);  // (derived lists: unpack16 checked every index)
+    if (!derived) range(choice_lits, nchl, nv);  // (derived lists are rows: clause_lits, above)
     range(anchors, na, nv);
     if (g_any(bad)) return false;  // the offsets below are now in range
     // a lane per AtMost row: its positions in registers (rows of up to 16:
@@ -810,38 +837,36 @@ struct Group {
     } else {
       at += nch;
     }
-    IX* cid = const_cast<IX*>(clause_id);
-    IX* kid = const_cast<IX*>(card_id);
-    int c0 = 0, c1 = 0;
     const uint64_t lt = lanemask_lt();
-    for (int c = 0; c < nid; c += 64) {
-      const int i = c + lane;
-      const bool valid = i < nid;
-      const int byte = valid ? tbyte(at + (i >> 3)) : 0;
-      const bool bit = valid && ((byte >> (i & 7)) & 1);
-      const uint64_t mb = __ballot(bit), mv = __ballot(valid);
-      if (valid) {
-        if (bit) {
-          const int k = c1 + __popcll(mb & lt);
-          if (k < nk) kid[k] = enc(i);
-        } else {
-          const int k = c0 + __popcll(~mb & mv & lt);
-          if (k < nc) cid[k] = enc(i);
-        }
+    // the identity mask as u32 words (bits past nid clear) and the
+    // popcount of the words before each (a DPP scan), for row_of
+    uint32_t* mk = const_cast<uint32_t*>(idmask);
+    uint16_t* pc = const_cast<uint16_t*>(idpc);
+    int carry1 = 0;
+    for (int c = 0; c < nbi; c += 64) {
+      const int wd = c + lane;
+      uint32_t x = 0;
+      if (wd < nbi) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (4 * wd + q < (nid + 7) / 8) x |= (uint32_t)tbyte(at + 4 * wd + q) << (8 * q);
+        if (32 * wd + 32 > nid) x &= (1u << (nid & 31)) - 1u;
+        mk[wd] = x;
       }
-      c1 += __popcll(mb);
-      c0 += __popcll(~mb & mv);
+      const int n1 = __popc(x);
+      const int incl = wave_incl_scan(n1) + carry1;
+      if (wd < nbi) pc[wd + 1] = (uint16_t)incl;
+      carry1 = __builtin_amdgcn_readlane(incl, 63);
     }
+    if (lane == 0) pc[0] = 0;
     wsync();
-    if (c0 != nc || c1 != nk) return false;
+    if (carry1 != nk || nid != nc + nk) return false;
     if (!derived) return true;
     // -- DP_FMT_P16D: the choice lists --
     if ((int)clause_off[nc] != ncl) return false;  // (rows read below stay in clause_lits)
     uint16_t* depr = reinterpret_cast<uint16_t*>(scratch);  // [nch] dependency rows by rank
-    uint16_t* rowk = depr + nch;                             // [nch] each list's row
-    uint32_t* cnt = reinterpret_cast<uint32_t*>(scratch + ((4 * nch + 15) & ~15));  // [nv + 1]
-    IX* co = const_cast<IX*>(choice_off);
-    IX* cl = const_cast<IX*>(choice_lits);
+    IX* rowk = const_cast<IX*>(rowref);                      // [nch] each list's row (kept)
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(scratch + ((2 * nch + 15) & ~15));  // [nv + 1]
     IX* vco = const_cast<IX*>(var_choice_off);
     for (int i = tid; i <= nv; i += NT) cnt[i] = 0u;
     bool bad = false;
@@ -881,12 +906,12 @@ struct Group {
       const int ss = k < nch && ks >= 0 ? tbyte(src_at + ks) : 1;
       if (zero) {
         bad |= j >= nd;
-        rowk[k] = j < nd ? depr[j] : (uint16_t)0;
+        rowk[k] = j < nd ? enc(depr[j]) : enc(0);
       }
       wsync();
       if (k < nch && !zero) {
         bad |= ks < 0 || ss != 0;
-        rowk[k] = ks >= 0 ? rowk[ks] : (uint16_t)0;
+        rowk[k] = ks >= 0 ? rowk[ks] : enc(0);
       }
       wsync();
       int x = 0, s = -1, a = 0;
@@ -903,33 +928,14 @@ struct Group {
       const int up = __builtin_amdgcn_update_dpp(0, pm + 1, 0x138, 0xf, 0xf, false) - 1;  // wave_shr:1
       const int before = max(smax, lane > 0 ? up : -1);
       if (k < nch) {
-        if (s >= nv || s < before || n + x > nchl) {
-          bad = true;
-        } else {
-          // the list: the row's literals after the first (eight by
-          // independent loads, then the rest)
-          int l[8];
-#pragma unroll
-          for (int q = 0; q < 8; ++q) l[q] = q < x ? (int)clause_lits[a + 1 + q] : 0;
-#pragma unroll
-          for (int q = 0; q < 8; ++q)
-            if (q < x) {
-              bad |= (l[q] >> 1) >= nv;
-              cl[n + q] = enc(l[q] >> 1);
-            }
-          for (int q = 8; q < x; ++q) {
-            const int lq = clause_lits[a + 1 + q];
-            bad |= (lq >> 1) >= nv;
-            cl[n + q] = enc(lq >> 1);
-          }
-          co[k + 1] = enc(n + x);
-          atomicAdd(&cnt[s], 1u);
-        }
+        // the list is the row's literals after the first, read in place
+        // (list_at); valid_record checks every clause literal below 2nv
+        if (s >= nv || s < before || n + x > nchl) bad = true;
+        else atomicAdd(&cnt[s], 1u);
       }
       n0 += __builtin_amdgcn_readlane(incl, 63);
       smax = max(smax, __builtin_amdgcn_readlane(pm, 63));
     }
-    if (lane == 0) co[0] = enc(0);
     bad |= taken != nd || n0 != nchl;
     wsync();
     if (__ballot(bad)) return false;
@@ -1105,7 +1111,7 @@ struct Group {
   __device__ __forceinline__ int row_ident(int r) const {
     return r < nc ? (int)clause_id[r] : r < nrows ? (int)card_id[r - nc] : -1;
   }
-  __device__ __forceinline__ bool row_on(int r) const { return !enabled || getb(enabled, row_ident(r)); }
+  __device__ __forceinline__ bool row_on(int r) const { return !enabled || getb(enabled, row_key(r)); }
   __device__ __forceinline__ int lit_val(int l) const {
     const int x = val[l >> 1];
     return (l & 1) ? -x : x;
@@ -2120,7 +2126,7 @@ struct Group {
     if (r < nc || r >= nrows) {
       const IX* lits = clause_lits;
       int a, b;
-      if (r < nc) { a = clause_off[r]; b = clause_off[r + 1]; set_bit_atomic(used, clause_id[r]); }
+      if (r < nc) { a = clause_off[r]; b = clause_off[r + 1]; set_bit_atomic(used, row_key(r)); }
       else {
         lits = l_lits;
         a = DP_CHK((int)l_off[r - nrows], 0, lcap + 1, 35);
@@ -2132,7 +2138,7 @@ struct Group {
       }
     } else {
       const int k = r - nc;
-      set_bit_atomic(used, card_id[k]);
+      set_bit_atomic(used, row_key(r));
       for (int j = card_off[k]; j < card_off[k + 1]; ++j) {
         const int v = card_lits[j];
         if (v != u && val[v] > 0 && (int)rs[v] < bound) mark_push(v);
@@ -2393,10 +2399,17 @@ struct Group {
 
   // choice lists: rows 0..nch-1; the singleton list of anchor v is nch + v
   __device__ __forceinline__ int list_len(int list) const {
-    return list >= nch ? 1 : (int)choice_off[list + 1] - (int)choice_off[list];
+    if (list >= nch) return 1;
+    if (rowref) {
+      const int r = rowref[list];
+      return (int)clause_off[r + 1] - (int)clause_off[r] - 1;
+    }
+    return (int)choice_off[list + 1] - (int)choice_off[list];
   }
   __device__ __forceinline__ int list_at(int list, int i) const {
-    return list >= nch ? list - nch : (int)choice_lits[(int)choice_off[list] + i];
+    if (list >= nch) return list - nch;
+    if (rowref) return (int)clause_lits[(int)clause_off[rowref[list]] + 1 + i] >> 1;
+    return (int)choice_lits[(int)choice_off[list] + i];
   }
   __device__ __forceinline__ void dq_push_back(int list, int idx) {
     int at = dq_head + dq_n;
@@ -2609,6 +2622,24 @@ struct Group {
     return len;
   }
 
+  // Bits over rows (rowspace) -> the same set over identities, in idt (a
+  // lane per identity: its row's bit, ballot per 64); outside rowspace the
+  // set itself.  For the outputs, which list identities ascending.
+  __device__ __forceinline__ const uint32_t* to_idents(const uint32_t* src) {
+    if (!rowspace) return src;
+    for (int b = 0; b < nid; b += NT) {
+      const int id = b + tid;
+      const uint64_t m = __ballot(id < nid && getb(src, row_of(id)));
+      const int wd = b >> 5;
+      if (lane == 0) {
+        idt[wd] = (uint32_t)m;
+        if (wd + 1 < nbi) idt[wd + 1] = (uint32_t)(m >> 32);
+      }
+    }
+    gsync();
+    return idt;
+  }
+
   // Tracer.Trace(SearchPosition) at an unsatisfiable search step
   // (search.go:173; oracle: trace_event).  Record [n, guessed variables in
   // stack order, m, identities ascending]: the identities of the failure's
@@ -2641,7 +2672,7 @@ struct Group {
       }
       o[k] = ni;
     }
-    emit_bits(used, nbi, o + 2 + ngv);
+    emit_bits(to_idents(used), nbi, o + 2 + ngv);
     tr_len += 2 + ngv + ni;
     gsync();
     if (!from_solve) fill_bits(used, nid, false);
@@ -2705,15 +2736,24 @@ struct Group {
     for (int i = tid; i < nbi; i += NT) any |= en[i] != 0u;
     int r = g_any(any) ? RS_UNSAT : RS_BUDGET;
     if (r == RS_UNSAT) {
+      // identities in ascending order (rowspace: through their rows, with
+      // the set mirrored over identities in idt for the empty-word skip)
+      const uint32_t* ids = to_idents(en);
       for (int id = 0; id < nid; ++id) {
-        if ((id & 31) == 0 && en[id >> 5] == 0) { id += 31; continue; }  // empty word
-        if (!getb(en, id)) continue;
+        if ((id & 31) == 0 && ids[id >> 5] == 0) { id += 31; continue; }  // empty word
+        if (!getb(ids, id)) continue;
+        const int key = rowspace ? row_of(id) : id;
         copy_bits(en2, en, nid);
-        if (tid == 0) en2[id >> 5] &= ~(1u << (id & 31));
+        if (tid == 0) en2[key >> 5] &= ~(1u << (key & 31));
         gsync();
         r = refute(en2);
-        if (r == RS_UNSAT) copy_bits(en, used, nid);
-        else if (r == RS_BUDGET) { flags |= DP_F_CORE_BUDGET; break; }
+        if (r == RS_UNSAT) {
+          copy_bits(en, used, nid);
+          ids = to_idents(en);
+        } else if (r == RS_BUDGET) {
+          flags |= DP_F_CORE_BUDGET;
+          break;
+        }
       }
       int c = 0;
       for (int i = tid; i < nbi; i += NT) c += __popc(ld_bits(&en[i]));
@@ -2721,7 +2761,7 @@ struct Group {
       int a0 = 0;
       if (tid == 0 && c > 0) a0 = atomicAdd(pool_len, c);
       at = g_bcast0(a0);
-      len = emit_bits(en, nbi, pool + at);  // ascending identity ids
+      len = emit_bits(to_idents(en), nbi, pool + at);  // ascending identity ids
     } else {
       flags |= DP_F_CORE_BUDGET;
     }
