@@ -273,6 +273,9 @@ def main():
                          "NARROW (U16) or int32 (staged by the host)")
     ap.add_argument("--e2e-steps", type=int, default=10,
                     help="steps of the lowering-inclusive (wire -> results) secondary figure; 0: skip")
+    ap.add_argument("--kernel-depth", type=int, default=0,
+                    help="kernel-only batches in flight; 0: one per pipeline lane, 2 for config 4 (each of its "
+                         "launches is a persistent grid that fills the device)")
     ap.add_argument("--kernel-only", action="store_true",
                     help="skip the host-to-host leg (profiling runs of the solve kernel)")
     ap.add_argument("--flags", type=int, default=0,
@@ -407,7 +410,8 @@ def main():
         # events on the launch's stream; rocprofv3 --kernel-trace of
         # `bench.py --kernel-only` reports the same kernels), then one batch
         # per pipeline lane in flight gives the rate the kernel sustains
-        slots = [ctx.upload(lw.rec_off, lw.rec) for _ in range(1 if args.kernel_only else LANES)]
+        kdepth = args.kernel_depth or (2 if args.config == 4 else LANES)
+        slots = [ctx.upload(lw.rec_off, lw.rec) for _ in range(1 if args.kernel_only else kdepth)]
         slots[0].run()
         kms = []
         for _ in range(args.kernel_steps):
@@ -419,8 +423,8 @@ def main():
                 s_.run()
             t0 = time.perf_counter()
             for i in range(args.kernel_steps):
-                s_ = slots[i % LANES]
-                if i >= LANES:
+                s_ = slots[i % kdepth]
+                if i >= kdepth:
                     s_.wait()
                 s_.launch()
             for s_ in slots:
@@ -440,7 +444,8 @@ def main():
                                "ms_per_step": round(tk / args.kernel_steps * 1e3, 4),
                                "serial_launch_ms": round(k_ms, 4),
                                "identical_to_host_path": bool(same_results(kres, res)) if res is not None else None,
-                               "note": "records resident in HBM, %d batches in flight; not value" % LANES}
+                               "batches_in_flight": kdepth,
+                               "note": "records resident in HBM, %d batches in flight; not value" % kdepth}
         traffic = None
         if args.pmc_json and os.path.exists(args.pmc_json):
             with open(args.pmc_json) as f:

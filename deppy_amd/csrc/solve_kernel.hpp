@@ -1956,6 +1956,9 @@ struct Group {
           // flatten: a group-wide prefix sum of the watch-range lengths
           const int incl = wave_incl_scan(cnt);
           int total = __builtin_amdgcn_readlane(incl, 63), before = 0;
+#ifdef DP_STAMPS
+          if constexpr (NW == 1) DP_ACC(26, total);  // watch entries a flattened chunk visits
+#endif
           if constexpr (NW > 1) {
             const int32_t* sl = exchange(incl, lane == 63);
             total = 0;

@@ -4,7 +4,8 @@
 # product library): GPU parity tests of each, then interleaved kernel-only
 # and host-to-host rates of configs 2, 3 and 6; then config 2 with one launch
 # per residency class (DEPPY_CEILINGS=fine, merge only at equal residency),
-# serial on the chunk's stream or spread over sibling streams (DEPPY_SPREAD=1).
+# serial on the chunk's stream or spread over sibling streams (DEPPY_SPREAD=1),
+# only with FINE=1 in the environment.
 set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-r04_twl}
@@ -13,6 +14,7 @@ timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 rc=$?; tail -1 $OUT/tests_occ.log; [ $rc -eq 0 ] || exit 1
 DEPPY_VARIANT_LIB=libdeppy_hip_twl.so timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/tests_twl.log 2>&1
 rc=$?; tail -1 $OUT/tests_twl.log; [ $rc -eq 0 ] || exit 1
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit 1
 timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_c2.json 2>$OUT/bench_c2.err || exit 1
 tail -c 300 $OUT/bench_c2.json; echo
 for rep in 1 2; do
@@ -24,6 +26,7 @@ for cfg in 2 3 6; do
   done
 done
 done
+[ -n "$FINE" ] || exit 0
 for rep in 1 2; do
   for v in "-" "DEPPY_CEILINGS=fine DEPPY_BUCKET_MERGE=0.99" "DEPPY_CEILINGS=fine DEPPY_BUCKET_MERGE=0.99 DEPPY_SPREAD=1"; do
     envs=""; [ "$v" != "-" ] && envs="$v"
