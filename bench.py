@@ -274,13 +274,12 @@ def main():
     ap.add_argument("--e2e-steps", type=int, default=10,
                     help="steps of the lowering-inclusive (wire -> results) secondary figure; 0: skip")
     ap.add_argument("--kernel-depth", type=int, default=0,
-                    help="kernel-only batches in flight; 0: one per pipeline lane, 2 for config 4 (each of its "
-                         "launches is a persistent grid that fills the device)")
+                    help="kernel-only batches in flight; 0: one per pipeline lane (dp_lanes)")
     ap.add_argument("--kernel-only", action="store_true",
                     help="skip the host-to-host leg (profiling runs of the solve kernel)")
     ap.add_argument("--flags", type=int, default=0,
                     help="dp_opts.flags (diagnostic placements: 1 group, 2 HBM, 4 mid groups)")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r03_pmc_traffic.jsonl"),
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r04_pmc_traffic.jsonl"),
                     help="HBM bytes per solve kernel dispatch from separate rocprofv3 --pmc passes; "
                          "used for roofline.traffic when its config/problems match")
     ap.add_argument("--sq-json", default=os.path.join(ROOT, "profiles", "r04_sq_split.json"),
@@ -410,7 +409,7 @@ def main():
         # events on the launch's stream; rocprofv3 --kernel-trace of
         # `bench.py --kernel-only` reports the same kernels), then one batch
         # per pipeline lane in flight gives the rate the kernel sustains
-        kdepth = args.kernel_depth or (2 if args.config == 4 else LANES)
+        kdepth = args.kernel_depth or LANES
         slots = [ctx.upload(lw.rec_off, lw.rec) for _ in range(1 if args.kernel_only else kdepth)]
         slots[0].run()
         kms = []

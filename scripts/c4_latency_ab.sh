@@ -22,8 +22,8 @@ done
 # phase stamps of the current build (diagnostic library): one catalog alone
 # and 16 together
 timeout -k 10 300 python -u scripts/phases.py 4 1,16 > $OUT/phases_c4.jsonl 2> $OUT/phases_c4.err || exit 1
-# config 4's kernel-only leg with 1, 2, 4 and 8 resident batches in flight
-for kd in 1 2 4 8; do
+# config 4's kernel-only leg with 8, 16 and 24 resident batches in flight
+for kd in 8 16 24; do
   timeout -k 10 300 python bench.py --config 4 --steps 20 --warmup 3 --kernel-steps 12 --kernel-depth $kd --no-cpu --e2e-steps 0 > $OUT/kdepth_$kd.json 2>&1 || exit 1
   python3 -c "import json; d=json.loads(open('$OUT/kdepth_$kd.json').read().strip().splitlines()[-1]); print('kernel depth $kd', 'h2h', d['value'], 'kernel_only', d['kernel_only']['res_per_s'], 'serial_ms', d['kernel_only']['serial_launch_ms'])"
 done
