@@ -217,6 +217,15 @@ static_assert(2 * DEV_WATCH_VARS + 1 <= mode_wbuf(M_SPLIT) + mode_cq(M_SPLIT) &&
                   2 * DEV_WATCH_VARS + 1 <= mode_wbuf(M_HBM) + mode_cq(M_HBM) && mode_wbuf(M_SPLIT) % 4 == 0,
               "build_watches_wide: the counters fit wbuf + cardq");
 
+// A row's literal range in one word, for the 8-byte entries of device-built
+// multi-wave watch lists (solve_kernel.hpp Group::w8): first position << 8 |
+// length, or ROW_INFO_NONE (read the row's offsets) for a row of 255 or more
+// positions or one starting at or past 2^24.
+constexpr uint32_t ROW_INFO_NONE = 0xffffffffu;
+__host__ __device__ inline uint32_t row_info(int32_t a, int32_t len) {
+  return a >= 0 && a < (1 << 24) && len >= 0 && len < 255 ? ((uint32_t)a << 8) | (uint32_t)len : ROW_INFO_NONE;
+}
+
 struct ImgLayout {
   int32_t w_off, w, words;
 };
@@ -269,7 +278,7 @@ struct Layout {
   int32_t dq;        // IX[2*cap] deque of choices (list, idx)
   int32_t stk;       // IX[3*cap] guess stack (list, idx | G_SKIP, mark)
   int32_t wbuf;      // IX[wbuf] flattened work list (watch-list positions)       [LDS]
-  int32_t cardq;     // IX[cq] AtMost rows queued this round                      [LDS]
+  int32_t cardq;     // IX[cq] AtMost rows queued this round (multi-wave: then their row_info)  [LDS]
   int32_t scal;      // i32[nscal] wave-shared scalars and reduction slots        [LDS]
   // M_SPLIT / M_SPLIT4 round state in LDS (mode_lds_rounds): a round's
   // implications in an open-addressing table keyed by variable, the list of
@@ -282,7 +291,8 @@ struct Layout {
   int32_t hc;        // slots (a power of two; 0 when the mode keeps rounds in HBM)
   int32_t wp;        // (mode_rowslot) i32[8][nc] row slots {watch x, watch y, len, l0 | offset, l1..l4};
                      // else (mode_2wl) u64[nc] the two literals clause row r watches, low word first
-  int32_t wl;        // multi-wave, DP_FMT_I32 records: device-built w_off[2nv+2], w[ncl+nkl]  [HBM, last]
+  int32_t wl;        // multi-wave, DP_FMT_I32 records: device-built w_off[2nv+2], then
+                     // int2[ncl+nkl] entries {row, row_info} (8-byte aligned)  [HBM, last]
   int32_t wpos;      // (mode_twl_lds) u8[2nc] watched positions of each clause row
   int32_t wend;      // (mode_twl_lds) u16[2nv] live end of each literal's watch list
   int32_t wfi;       // (mode_twl_lds) u8[wbuf] frontier literal of each flattened work-list entry
@@ -341,7 +351,8 @@ __host__ __device__ inline Layout layout(const int32_t* h) {
   L.body = MODE == M_LDS ? take(body_bytes, COLD) : 0;
   L.scal = take(mode_nscal(MODE) * 4, WORK);
   L.wbuf = take(mode_wbuf(MODE) * ix, WORK);
-  L.cardq = take(mode_cq(MODE) * ix, WORK);
+  // (multi-wave: each queued row's row_info after the queue, cardq[cq + i])
+  L.cardq = take(mode_cq(MODE) * ix * (MODE == M_LDS ? 1 : 2), WORK);
   // the table shrinks (to 64 slots at least) when the catalog's per-variable
   // state leaves less LDS, so it never moves a catalog off this placement
   L.hc = mode_lds_rounds(MODE) ? round_slots(nv) : 0;
@@ -378,7 +389,7 @@ __host__ __device__ inline Layout layout(const int32_t* h) {
   L.dq = take(2 * L.cap * ix, COLD);
   L.stk = take(3 * L.cap * ix, COLD);
   L.wp = mode_rowslot(MODE) ? take(h[DP_H_NC] * 32, COLD) : mode_2wl(MODE) ? take(h[DP_H_NC] * 8, COLD) : 0;
-  L.wl = MODE != M_LDS && h[DP_H_FMT] == DP_FMT_I32 ? take((2 * nv + 2 + h[DP_H_NCL] + h[DP_H_NKL]) * 4, COLD) : 0;
+  L.wl = MODE != M_LDS && h[DP_H_FMT] == DP_FMT_I32 ? take((2 * nv + 2) * 4 + (h[DP_H_NCL] + h[DP_H_NKL]) * 8, COLD) : 0;
   L.wpos = mode_twl_lds(MODE) ? take(2 * h[DP_H_NC], COLD) : 0;
   L.wend = mode_twl_lds(MODE) ? take(4 * nv, COLD) : 0;
   L.wfi = mode_twl_lds(MODE) ? take(mode_wbuf(MODE), COLD) : 0;

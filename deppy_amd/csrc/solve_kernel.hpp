@@ -231,6 +231,12 @@ struct Group {
   // the bit a row sets in used / en / enabled
   __device__ __forceinline__ int row_key(int r) const { return rowspace ? r : row_ident(r); }
   const IX *w_off, *w;  // watch lists, built by build_watches
+  // Multi-wave problems whose lists are built on the device (DP_FMT_I32,
+  // layout.hpp Layout::wl): 8-byte entries {row, row_info(row)} carrying the
+  // row's literal range, so a visit reads the row's literals without first
+  // reading its offsets (one dependent HBM read less per row; w is unused).
+  // nullptr: 4-byte row entries in w.
+  const int2* w8;
   int nwatch, dthr;
   // BCP-visited bytes (this thread): the watch entries, row offsets, row
   // literals and their values that propagation reads
@@ -538,6 +544,7 @@ struct Group {
     d_mark = reinterpret_cast<IX*>(cold + L.d_mark);
     imp = reinterpret_cast<IMP*>(cold + L.imp);
     wpair = reinterpret_cast<uint64_t*>(cold + L.wp);
+    w8 = nullptr;
     sweep = false;
     twl_on = false;
     if constexpr (TWLL) {
@@ -618,9 +625,10 @@ struct Group {
     } else {
       if (h[DP_H_FMT] == DP_FMT_I32) {  // plain int32 record: the lists in scratch (layout.hpp wl)
         IX* wo = reinterpret_cast<IX*>(hbm + L.wl);
-        if (device_watches(h)) build_watches_wide(wo, wo + 2 * nv + 2, reinterpret_cast<uint32_t*>(lds + L.wbuf));
+        int2* we = reinterpret_cast<int2*>(wo + 2 * nv + 2);
+        if (device_watches(h)) build_watches_wide(wo, we, reinterpret_cast<uint32_t*>(lds + L.wbuf));
         // (else built by the passes before this launch, watch_build.hip)
-        w_off = wo; w = wo + 2 * nv + 2;
+        w_off = wo; w = nullptr; w8 = we;
       } else {
         w_off = rv(X.w_off); w = rv(X.w);  // host-built, staged after the record
       }
@@ -757,17 +765,35 @@ struct Group {
     static_assert(MODE != M_LDS, "the int32 form runs on multi-wave groups");
     const int32_t* r = reinterpret_cast<const int32_t*>(clause_off) - R.clause_off;  // the record
     bool bad = false;
+    // VU independent loads per thread and step, so a thread has that many in
+    // flight instead of one (an OLM-scale record is ~400k words: one load at
+    // a time per thread took ~720k cycles, 0.3 ms a catalog)
+    constexpr int VU = 8;
     auto offsets = [&](int at, int n, int total, bool exact) {
-      for (int i = tid; i <= n; i += NT) {
-        const int x = r[at + i];
-        bad |= i == 0 ? x != 0 : x < r[at + i - 1];
-        bad |= i == n && (exact ? x != total : x > total);
+      for (int i0 = tid; i0 <= n; i0 += VU * NT) {
+        int x[VU], y[VU];
+#pragma unroll
+        for (int u = 0; u < VU; ++u) {
+          const int i = i0 + u * NT;
+          x[u] = i <= n ? r[at + i] : 0;
+          y[u] = i <= n && i > 0 ? r[at + i - 1] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < VU; ++u) {
+          const int i = i0 + u * NT;
+          if (i > n) continue;
+          bad |= i == 0 ? x[u] != 0 : x[u] < y[u];
+          bad |= i == n && (exact ? x[u] != total : x[u] > total);
+        }
       }
     };
     auto range = [&](int at, int n, int lo, int hi) {
-      for (int i = tid; i < n; i += NT) {
-        const int x = r[at + i];
-        bad |= x < lo || x >= hi;
+      for (int i0 = tid; i0 < n; i0 += VU * NT) {
+        int x[VU];
+#pragma unroll
+        for (int u = 0; u < VU; ++u) x[u] = i0 + u * NT < n ? r[at + i0 + u * NT] : lo;
+#pragma unroll
+        for (int u = 0; u < VU; ++u) bad |= x[u] < lo || x[u] >= hi;
       }
     };
     offsets(R.clause_off, nc, ncl, true);
@@ -783,9 +809,21 @@ struct Group {
     range(R.choice_lits, nchl + na, 0, nv);  // choice_lits then anchors
     if (g_any(bad)) return false;  // the offsets below are now in range
     if (watches) range(X.w, r[X.w_off + 2 * nv], 0, nrows);
+    // each variable's positions in an AtMost row form one run: rows of up to
+    // 16 positions by independent loads into registers, longer ones in place
     for (int k = tid; k < nk; k += NT) {
       const int a = r[R.card_off + k], b = r[R.card_off + k + 1];
       const int32_t* cl = r + R.card_lits;
+      if (b - a <= 16) {
+        int v[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = a + i < b ? cl[a + i] : -1 - i;
+#pragma unroll
+        for (int j = 1; j < 16; ++j)
+#pragma unroll
+          for (int i = 0; i < j - 1; ++i) bad |= v[j] != v[j - 1] && v[i] == v[j];
+        continue;
+      }
       for (int j = a + 1; j < b; ++j)
         if (cl[j] != cl[j - 1])
           for (int i = a; i < j - 1; ++i) bad |= cl[i] == cl[j];
@@ -959,7 +997,7 @@ struct Group {
   // cursors.  Row order within a list is left to the atomics, as in
   // build_watches.  Ends with a draining barrier: every wavefront reads the
   // lists after it.
-  __device__ __forceinline__ void build_watches_wide(IX* wo, IX* ww, uint32_t* cnt) {
+  __device__ __forceinline__ void build_watches_wide(IX* wo, int2* ww, uint32_t* cnt) {
     static_assert(MODE != M_LDS, "one-wavefront problems build theirs in LDS");
     const int n2 = 2 * nv + 1;
     for (int i = tid; i < n2; i += NT) cnt[i] = 0u;
@@ -980,13 +1018,17 @@ struct Group {
       }
     }
     gsync();
-    for (int r = tid; r < nc; r += NT)
-      for (int j = clause_off[r]; j < (int)clause_off[r + 1]; ++j)
-        ww[atomicAdd(&cnt[(int)clause_lits[j] ^ 1], 1u)] = r;
-    for (int k = tid; k < nk; k += NT)
-      for (int j = card_off[k]; j < (int)card_off[k + 1]; ++j)
-        if (j == (int)card_off[k] || card_lits[j] != card_lits[j - 1])
-          ww[atomicAdd(&cnt[2 * (int)card_lits[j]], 1u)] = nc + k;
+    for (int r = tid; r < nc; r += NT) {
+      const int a = clause_off[r], b = clause_off[r + 1];
+      const int2 e = make_int2(r, (int)row_info(a, b - a));
+      for (int j = a; j < b; ++j) ww[atomicAdd(&cnt[(int)clause_lits[j] ^ 1], 1u)] = e;
+    }
+    for (int k = tid; k < nk; k += NT) {
+      const int a = card_off[k], b = card_off[k + 1];
+      const int2 e = make_int2(nc + k, (int)row_info(a, b - a));
+      for (int j = a; j < b; ++j)
+        if (j == a || card_lits[j] != card_lits[j - 1]) ww[atomicAdd(&cnt[2 * (int)card_lits[j]], 1u)] = e;
+    }
     bar();  // (drains the lists' stores)
   }
 
@@ -1112,6 +1154,18 @@ struct Group {
     return r < nc ? (int)clause_id[r] : r < nrows ? (int)card_id[r - nc] : -1;
   }
   __device__ __forceinline__ bool row_on(int r) const { return !enabled || getb(enabled, row_key(r)); }
+  // watch entry j: {row, row_info} (w8), or {row, ROW_INFO_NONE}
+  __device__ __forceinline__ int2 went(int j) const {
+    if constexpr (MODE != M_LDS) {
+      if (w8) return w8[j];
+    }
+    return make_int2((int)w[j], (int)ROW_INFO_NONE);
+  }
+  // visit() of watch entry j, or of nothing (j < 0)
+  __device__ __forceinline__ void visit_at(int j, int& crow, int& ncq) {
+    const int2 e = j >= 0 ? went(j) : make_int2(-1, (int)ROW_INFO_NONE);
+    visit(e.x, crow, ncq, (uint32_t)e.y);
+  }
   __device__ __forceinline__ int lit_val(int l) const {
     const int x = val[l >> 1];
     return (l & 1) ? -x : x;
@@ -1335,8 +1389,9 @@ struct Group {
     return nun == 1 ? ul : -1;
   }
 
-  // a clause row (r < nc) or a learned row (r >= nrows)
-  __device__ __forceinline__ int clause_unit(int r, int& crow) {
+  // a clause row (r < nc) or a learned row (r >= nrows); info: the row's
+  // literal range from its watch entry (row_info), or ROW_INFO_NONE
+  __device__ __forceinline__ int clause_unit(int r, int& crow, uint32_t info = ROW_INFO_NONE) {
     if constexpr (RSLOT) {
       if (r < nc) {
         // the slot: the pair (coherent: other wavefronts move it), then the
@@ -1364,6 +1419,12 @@ struct Group {
           if (lit_val((int)(uint32_t)wv) >= 0 && lit_val((int)(uint32_t)(wv >> 32)) >= 0) return -1;
         }
         return eval_clause_twl(r, clause_off[r], clause_off[r + 1], crow);
+      }
+    }
+    if constexpr (MODE != M_LDS) {
+      if (r < nc && info != ROW_INFO_NONE) {
+        const int a = (int)(info >> 8);
+        return eval_clause(r, clause_lits, a, a + (int)(info & 255u), crow);
       }
     }
     if (r < nc) return eval_clause(r, clause_lits, clause_off[r], clause_off[r + 1], crow);
@@ -1412,21 +1473,21 @@ struct Group {
   // from wave-converged code: every active lane passes its row (or -1).
   // ncq counts the queue in the one-wavefront mode (a register); with several
   // wavefronts the queue length is the LDS counter S_NK.
-  __device__ __forceinline__ void visit(int r, int& crow, int& ncq) {
+  __device__ __forceinline__ void visit(int r, int& crow, int& ncq, uint32_t info = ROW_INFO_NONE) {
     DP_VIS_ADD(r >= 0 ? sizeof(IX) : 0);  // the watch entry
     const bool ok = r >= 0 && row_on(r);
     const bool card = ok && r >= nc && r < nrows;
     const uint64_t m = __ballot(card);
     if constexpr (NW == 1 && DP_MAKE_ROOM) {
       if (card) cardq[ncq + __popcll(m & lanemask_lt())] = enc(r);
-      note_all(ok && !card ? clause_unit(r, crow) : -1, r);
+      note_all(ok && !card ? clause_unit(r, crow, info) : -1, r);
       ncq += __popcll(m);
     } else if constexpr (NW == 1) {
       const bool q = ncq + __popcll(m) <= CQ;  // queue full: evaluate in-lane
       if (card && q) cardq[ncq + __popcll(m & lanemask_lt())] = enc(r);
       else if (card) card_serial(r, crow);
       else if (ok) {
-        const int ul = clause_unit(r, crow);
+        const int ul = clause_unit(r, crow, info);
         if (ul >= 0) note(ul, r);
       }
       if (q) ncq += __popcll(m);
@@ -1437,10 +1498,12 @@ struct Group {
         if (lane == 0) b = atomicAdd(&scal[S_NK], __popcll(m));
         pos = __shfl(b, 0) + __popcll(m & lanemask_lt());
       }
-      if (card && pos < CQ) cardq[pos] = enc(r);
-      else if (card) card_serial(r, crow);  // queue full: evaluate in-lane
+      if (card && pos < CQ) {
+        cardq[pos] = enc(r);
+        cardq[CQ + pos] = (IX)info;  // (IX = int32 here)
+      } else if (card) card_serial(r, crow);  // queue full: evaluate in-lane
       else if (ok) {
-        const int ul = clause_unit(r, crow);
+        const int ul = clause_unit(r, crow, info);
         if (ul >= 0) note(ul, r);
       }
     }
@@ -1637,7 +1700,16 @@ struct Group {
     }
     for (int q = q0; q < ncq; q += qs) {
       const int r = DP_CHK((int)cardq[q], nc, nrows, 3), k = r - nc;
-      const int a = card_off[k], len = (int)card_off[k + 1] - a, bound = card_bound[k];
+      int a, len;
+      const uint32_t info = NW > 1 ? (uint32_t)cardq[CQ + q] : ROW_INFO_NONE;
+      if (info != ROW_INFO_NONE) {  // the range from the row's watch entry
+        a = (int)(info >> 8);
+        len = (int)(info & 255u);
+      } else {
+        a = card_off[k];
+        len = (int)card_off[k + 1] - a;
+      }
+      const int bound = card_bound[k];
       if (len > 64) {  // long rows: the wavefront in chunks of 64 positions
         card_long(r, a, len, bound, crow);
         continue;
@@ -1938,7 +2010,7 @@ struct Group {
         const int a = w_off[l], e = w_off[l + 1];
         for (int k0 = a; k0 < e; k0 += NT) {
           make_room(crow, ncq);
-          visit(k0 + tid < e ? (int)w[k0 + tid] : -1, crow, ncq);
+          visit_at(k0 + tid < e ? k0 + tid : -1, crow, ncq);
         }
 #ifdef DP_STAMPS
         DP_ACC(8, stamp() - t0);
@@ -1975,8 +2047,7 @@ struct Group {
             gsync();
             for (int t0 = 0; t0 < total; t0 += NT) {
               make_room(crow, ncq);
-              visit(t0 + tid < total ? DP_CHK((int)w[DP_CHK((int)wbuf[t0 + tid], 0, nwatch, 12)], 0, nrows, 13) : -1,
-                    crow, ncq);
+              visit_at(t0 + tid < total ? DP_CHK((int)wbuf[t0 + tid], 0, nwatch, 12) : -1, crow, ncq);
             }
             // wbuf is reused by the next chunk; after the last one the
             // AtMost flush's barrier (several wavefronts) comes first
@@ -1989,7 +2060,7 @@ struct Group {
               const int a2 = w_off[l], e2 = w_off[l + 1];
               for (int k0 = a2; k0 < e2; k0 += NT) {
                 make_room(crow, ncq);
-                visit(k0 + tid < e2 ? (int)w[k0 + tid] : -1, crow, ncq);
+                visit_at(k0 + tid < e2 ? k0 + tid : -1, crow, ncq);
               }
             }
           }
@@ -2202,9 +2273,17 @@ struct Group {
   // Is clause row c violated by the all-false completion of the current
   // assignment?  (oracle: first_violated)  fu = its first unassigned
   // positive literal.
-  __device__ __forceinline__ bool violated(int c, int& fu) const {
+  __device__ __forceinline__ bool violated(int c, int& fu, uint32_t info = ROW_INFO_NONE) const {
     fu = -1;
-    for (int j = clause_off[c]; j < clause_off[c + 1]; ++j) {
+    int ja, jb;
+    if (MODE != M_LDS && info != ROW_INFO_NONE) {
+      ja = (int)(info >> 8);
+      jb = ja + (int)(info & 255u);
+    } else {
+      ja = clause_off[c];
+      jb = clause_off[c + 1];
+    }
+    for (int j = ja; j < jb; ++j) {
       const int l = clause_lits[j];
       const int x = val[l >> 1];
       if (l & 1) {
@@ -2272,9 +2351,10 @@ struct Group {
           if (__shfl(inc, j + step - 1) <= f) j += step;
         const int sj = __shfl(s, j), ej = __shfl(inc, j) - __shfl(n, j);
         if (f < total) {
-          const int c = w[sj + f - ej];
+          const int2 e = went(sj + f - ej);
+          const int c = e.x;
           int fu;
-          if (c < nc && c < best && row_on(c) && violated(c, fu)) best = c;
+          if (c < nc && c < best && row_on(c) && violated(c, fu, (uint32_t)e.y)) best = c;
         }
       }
     }
@@ -2283,9 +2363,10 @@ struct Group {
       const int l = trail[i];
       if (l & 1) continue;  // only variables assigned true own violations
       for (int k = w_off[l]; k < (int)w_off[l + 1]; ++k) {
-        const int c = w[k];
+        const int2 e = went(k);
+        const int c = e.x;
         int fu;
-        if (c < nc && c < best && row_on(c) && violated(c, fu)) best = c;
+        if (c < nc && c < best && row_on(c) && violated(c, fu, (uint32_t)e.y)) best = c;
       }
     }
 #endif

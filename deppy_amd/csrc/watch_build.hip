@@ -11,7 +11,9 @@
 //          positive l the AtMost rows holding var(l), once per distinct
 //          variable; the same rows as build_watches_host),
 //   scan   the counts into list offsets (one workgroup per record),
-//   fill   the lists through the offsets as cursors.
+//   fill   the lists through the offsets as cursors: 8-byte entries {row,
+//          row_info(row)} (layout.hpp), so a round reads a row's literals
+//          straight from its entry.
 // Counts go to wo[l + 2] and cursors run on wo[l + 1], so when the fill ends
 // wo[l] is the start of list l (wo[2nv] their total) with no pass to shift
 // the offsets back.  Row order within a list is left to the atomics, as in
@@ -35,7 +37,7 @@ constexpr int kScanThreads = 1024;  // one scan workgroup per record
 
 struct WbRec {
   const int32_t* h;
-  int32_t* wo;  // [2nv + 2] counters / offsets, then the lists [ncl + nkl]
+  int32_t* wo;  // [2nv + 2] counters / offsets, then the lists: int2[ncl + nkl] {row, row_info}
   dp_rec_layout R;
 };
 
@@ -74,18 +76,19 @@ __global__ __launch_bounds__(kWbThreads) void wb_rows(KernelArgs a) {
   const int32_t* ko = h + x.R.card_off;
   const int32_t* kl = h + x.R.card_lits;
   int32_t* wo = x.wo;
-  int32_t* ww = wo + 2 * nv + 2;
+  int2* ww = reinterpret_cast<int2*>(wo + 2 * nv + 2);
   const unsigned cap = (unsigned)(ncl + nkl), nl = (unsigned)(2 * nv);
   const int t = s * kWbThreads + (int)threadIdx.x, T = kWbSlices * kWbThreads;
   for (int r = t; r < nc; r += T) {
     const int b0 = co[r], b1 = co[r + 1];
     if (b0 < 0 || b0 > b1 || b1 > ncl) continue;
+    const int2 e = make_int2(r, (int)row_info(b0, b1 - b0));
     for (int j = b0; j < b1; ++j) {
       const int l = cl[j] ^ 1;  // the literal whose assignment falsifies position j
       if ((unsigned)l >= nl) continue;
       if constexpr (FILL) {
         const unsigned at = (unsigned)atomicAdd(&wo[l + 1], 1);
-        if (at < cap) ww[at] = r;
+        if (at < cap) ww[at] = e;
       } else {
         atomicAdd(&wo[l + 2], 1);
       }
@@ -94,12 +97,13 @@ __global__ __launch_bounds__(kWbThreads) void wb_rows(KernelArgs a) {
   for (int q = t; q < nk; q += T) {
     const int b0 = ko[q], b1 = ko[q + 1];
     if (b0 < 0 || b0 > b1 || b1 > nkl) continue;
+    const int2 e = make_int2(nc + q, (int)row_info(b0, b1 - b0));
     for (int j = b0; j < b1; ++j) {
       const int v = kl[j];
       if ((j > b0 && v == kl[j - 1]) || (unsigned)v >= (unsigned)nv) continue;
       if constexpr (FILL) {
         const unsigned at = (unsigned)atomicAdd(&wo[2 * v + 1], 1);
-        if (at < cap) ww[at] = nc + q;
+        if (at < cap) ww[at] = e;
       } else {
         atomicAdd(&wo[2 * v + 2], 1);
       }
