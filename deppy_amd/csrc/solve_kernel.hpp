@@ -1793,7 +1793,14 @@ struct Group {
   // the round is kept).  The bank's counters are read here and reset at the
   // start of the round after next (run_round), past this round's last barrier.
   __device__ __forceinline__ int finish_round_lds(int crow) {
+#ifdef DP_STAMPS
+    const int64_t tx0 = stamp();
+#endif
     const int cr = g_min(crow);  // the notes, the AtMost flush and the counters are complete
+#ifdef DP_STAMPS
+    const int64_t tx1 = stamp();
+    DP_ACC(30, tx1 - tx0);  // the round's exchange
+#endif
     const int nt = DP_CHK(scal[S_NTB + rb], 0, 2 * (hmask + 1) + 1, 4);
     const bool ovf = scal[S_OVB + rb] != 0;
     const int cvx = scal[S_CVB + rb];
@@ -1830,6 +1837,9 @@ struct Group {
     }
     tlen += nt;
     gsync();
+#ifdef DP_STAMPS
+    DP_ACC(31, stamp() - tx1);  // the commit
+#endif
     return 0;
   }
 
@@ -2026,6 +2036,9 @@ struct Group {
             cnt = (int)w_off[l + 1] - a;
           }
           // flatten: a group-wide prefix sum of the watch-range lengths
+#ifdef DP_STAMPS
+          const int64_t tf0 = stamp();
+#endif
           const int incl = wave_incl_scan(cnt);
           int total = __builtin_amdgcn_readlane(incl, 63), before = 0;
 #ifdef DP_STAMPS
@@ -2042,13 +2055,24 @@ struct Group {
             }
           }
           if (total <= WBUF) {
+#ifdef DP_STAMPS
+            const int64_t tf1 = stamp();
+            if constexpr (NW > 1) DP_ACC(27, tf1 - tf0);  // ranges: scan + exchange
+#endif
             // every frontier literal writes its watch range into the list
             for (int k = 0, at = before + incl - cnt; k < cnt; ++k) wbuf[at + k] = enc(a + k);
             gsync();
+#ifdef DP_STAMPS
+            const int64_t tf2 = stamp();
+            if constexpr (NW > 1) DP_ACC(28, tf2 - tf1);  // the work list
+#endif
             for (int t0 = 0; t0 < total; t0 += NT) {
               make_room(crow, ncq);
               visit_at(t0 + tid < total ? DP_CHK((int)wbuf[t0 + tid], 0, nwatch, 12) : -1, crow, ncq);
             }
+#ifdef DP_STAMPS
+            if constexpr (NW > 1) DP_ACC(29, stamp() - tf2);  // the visits
+#endif
             // wbuf is reused by the next chunk; after the last one the
             // AtMost flush's barrier (several wavefronts) comes first
             if (NW == 1 || b + NT < hi) gsync();

@@ -21,7 +21,7 @@ EXTRA = {16: "search_solve", 17: "pop_guess", 18: "pushes", 19: "visit_1lit", 20
          22: "learned", 23: "n_watch_1lit", 24: "n_front_flat", 25: "n_learned_rows", 26: "n_cards",
          27: "init_stage", 28: "init_validate", 29: "init_build",
          32: "first_violated", 33: "analyze", 34: "n_first_violated", 35: "truncate", 36: "save_model",
-         37: "push_pre", 38: "n_analyze", 39: "search_loop", 40: "loop_gap", 41: "lds_table_redo", 42: "n_flat_entries", 48: "build_count", 49: "build_scan", 50: "build_fill"}
+         37: "push_pre", 38: "n_analyze", 39: "search_loop", 40: "loop_gap", 41: "lds_table_redo", 42: "n_flat_entries", 43: "mw_flat_ranges", 44: "mw_flat_wbuf", 45: "mw_flat_visits", 46: "lds_round_exchange", 47: "lds_round_commit", 48: "build_count", 49: "build_scan", 50: "build_fill"}
 L = _lib.lib()
 L.dp_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _lib.c_i64p]
 config = int(sys.argv[1]) if len(sys.argv) > 1 else 2
