@@ -687,3 +687,38 @@ def test_olm_scale_device_lists_malformed():
     for p in (1, 3):
         assert g["status"][p] == -2 and g["flags"][p] == 512, p
     assert compare_results(g, ref, n, only=[0, 2, 4, 5]) == []
+
+
+def long_row_catalog(n_vars, width, seed):
+    """chain_catalog plus rows too long for a watch entry's packed range
+    (layout.hpp row_info: 255 positions or more): one required variable
+    depending on `width` candidates (a clause row of width + 1 literals) and
+    an AtMost(1) over the same candidates (an AtMost row of `width`)."""
+    base = chain_catalog(n_vars - 2, seed)
+    cands = [str(v.Identifier()) for v in base[:width]]
+    return base + [V("wide-req", sat.Mandatory(), sat.Dependency(*cands)),
+                   V("wide-uniq", sat.AtMost(1, *cands))]
+
+
+@pytest.mark.parametrize("n_vars", [600, 2400], ids=["in_kernel_lists", "device_passes"])
+@pytest.mark.parametrize("flags", [_lib.OPT_FORCE_GROUP, _lib.OPT_FORCE_MID], ids=["split", "split4"])
+def test_multiwave_long_rows_bit_exact(n_vars, flags):
+    """Multi-wave watch entries carry their row's literal range, except rows
+    of 255 or more positions, which keep ROW_INFO_NONE and are read through
+    their offsets (clause rows in a visit and Solve()'s scan, AtMost rows in
+    the flush).  Catalogs with a 300-literal dependency row and a 299-wide
+    AtMost row, with lists built by the solving workgroup (600 variables)
+    and by the grid-wide passes (2400): bit-exact with the oracle."""
+    probs = [long_row_catalog(n_vars, 299, 11 + k) for k in range(3)]
+    # plain int32 records, page-locked: copied as they lie, lists built on the device
+    lw = _lib.Lowered(sat.encode_inputs(probs), pinned=True)
+    assert [int(lw.record(p)[13]) for p in range(3)] == [0, 0, 0]  # DP_FMT_I32
+    c = _lib.Context(0, 1, flags=flags)
+    try:
+        g = c.submit(lw.rec_off, lw.rec).wait()
+        assert c.stats(reset=True)["direct_chunks"] > 0
+    finally:
+        c.close()
+    o = oracle.solve_batch(lw.rec_off, lw.rec, 0, 3)
+    assert compare_results(g, o, 3) == []
+    assert (g["status"] != -2).all()
