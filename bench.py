@@ -386,6 +386,7 @@ def main():
         "records_pinned": bool(lw.pinned),
         "classes": class_mix(res) if res is not None else None,
         "deterministic": bool(deterministic),
+        "build": _lib.build_info(),
         "host_lowering_res_per_s": round(n / t_lower, 1),
         "host_lowering_note": "dp_lower_into (packed 16-bit records, storage reused) on the host pool; not in value",
     }

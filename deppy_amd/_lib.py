@@ -91,7 +91,7 @@ EXPORTS = [
     "dp_launch", "dp_wait", "dp_download", "dp_resident_free", "dp_last_kernel_ms", "dp_gen_catalogs", "dp_gen_wire",
     "dp_gen_free", "dp_upload_traced", "dp_download_trace", "dp_solve_traced", "dp_lowered_errors",
     "dp_device_bytes", "dp_lower_into", "dp_lowered_new", "dp_lowered_exact_count", "dp_lowered_pinned", "dp_rec_widen", "dp_submit", "dp_job_wait", "dp_get_stats", "dp_stage_roundtrip",
-    "dp_stitch_selftest", "dp_partition",
+    "dp_stitch_selftest", "dp_partition", "dp_build_info",
 ]
 
 
@@ -138,6 +138,32 @@ class Result(ctypes.Structure):
 _lib = None
 
 
+def build_info(L=None) -> str:
+    """The library's dp_build_info string ("sources=<digest> arch=gfx950"),
+    or "" for a library without it (an older measurement variant)."""
+    L = L or lib()
+    if not hasattr(L, "dp_build_info"):
+        return ""
+    L.dp_build_info.restype = ctypes.c_char_p
+    return L.dp_build_info().decode()
+
+
+def _check_provenance(L) -> None:
+    """The product library must be the one the tree's sources make: its
+    embedded digest (build.py sources_digest) against the digest of the
+    sources it runs beside.  Measurement variants (DEPPY_VARIANT_LIB, the
+    stamps build) are other revisions or flags by design and are not
+    checked."""
+    if LIB_PATH != os.path.join(HERE, "libdeppy_hip.so"):
+        return
+    from deppy_amd import build as _build  # (sources only; nothing is compiled here)
+    want = _build.sources_digest()
+    got = build_info(L)
+    if ("sources=%s " % want) not in got + " ":
+        raise RuntimeError("deppy_amd: %s was built from other sources (%s; this tree: sources=%s); run "
+                           "__graft_entry__.build() (python -m deppy_amd.build)" % (LIB_PATH, got or "no build info", want))
+
+
 def lib():
     global _lib
     if _lib is not None:
@@ -146,6 +172,7 @@ def lib():
         raise RuntimeError("deppy_amd: %s is missing; run __graft_entry__.build() "
                            "(python deppy_amd/build.py)" % LIB_PATH)
     L = ctypes.CDLL(LIB_PATH)
+    _check_provenance(L)
     vp = ctypes.c_void_p
     L.dp_rec_validate.argtypes = [c_i32p, ctypes.c_int64]
     L.dp_rec_widen.argtypes = [c_i32p, ctypes.c_int64, c_i32p]

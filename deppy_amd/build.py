@@ -2,6 +2,7 @@
 .so travels with the repo snapshot to the GPU box)."""
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -19,6 +20,26 @@ SOURCES = ["solve_lds.hip", "solve_lds_dense.hip", "solve_split.hip", "solve_spl
            "lower.cpp", "gen.cpp"]
 FLAGS = ["-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function",
          "--offload-arch=" + ARCH, "-I" + os.path.join(HERE, "..", "include")]
+
+
+def _headers() -> list[str]:
+    hs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h")))
+    return hs + [os.path.join(HERE, "..", "include", "deppy_hip.h")]
+
+
+def sources_digest(extra: list[str] | None = None) -> str:
+    """sha256 (first 16 hex digits) of every source and header the library is
+    compiled from and of the compile flags.  The library carries it
+    (dp_build_info), and the binding refuses a product library whose digest
+    is not the tree's: the .so that runs is the one these sources make."""
+    h = hashlib.sha256()
+    for f in [os.path.join(CSRC, x) for x in SOURCES] + _headers():
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    h.update(" ".join(FLAGS[:-1] + (extra or [])).encode())  # (the include path is the tree's own)
+    return h.hexdigest()[:16]
 
 
 def _needs(target: str, deps: list[str]) -> bool:
@@ -41,13 +62,15 @@ def build(verbose: bool = False, extra: list[str] | None = None, stamps: bool = 
 
 def _build(verbose, extra, OBJ, LIB) -> str:
     os.makedirs(OBJ, exist_ok=True)
-    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h"))]
-    headers.append(os.path.join(HERE, "..", "include", "deppy_hip.h"))
+    headers = _headers()
+    digest = sources_digest(extra)
+    stamp = os.path.join(OBJ, "digest")
+    stale = not os.path.exists(stamp) or open(stamp).read().strip() != digest
     jobs = []
     for src in SOURCES:
         s = os.path.join(CSRC, src)
         o = os.path.join(OBJ, src + ".o")
-        if _needs(o, [s] + headers) or extra:
+        if stale or _needs(o, [s] + headers) or extra:
             lang = ["-x", "hip"] if src.endswith(".hip") or src in ("runtime.cpp", "solve_launch.cpp") else []
             jobs.append([HIPCC] + FLAGS + (extra or []) + lang + ["-c", s, "-o", o])
     def run(cmd):
@@ -58,7 +81,14 @@ def _build(verbose, extra, OBJ, LIB) -> str:
         list(ex.map(run, jobs))
     objs = [os.path.join(OBJ, s + ".o") for s in SOURCES]
     if _needs(LIB, objs) or jobs:
-        run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs + ["-lpthread"])
+        # the digest, compiled into the library (dp_build_info)
+        info = os.path.join(OBJ, "build_info.cpp")
+        with open(info, "w") as f:
+            f.write('extern "C" const char* dp_build_info(void) { return "sources=%s arch=%s"; }\n' % (digest, ARCH))
+        run([HIPCC] + FLAGS + ["-c", info, "-o", info + ".o"])
+        run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs + [info + ".o", "-lpthread"])
+    with open(stamp, "w") as f:
+        f.write(digest + "\n")
     return LIB
 
 

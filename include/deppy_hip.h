@@ -505,6 +505,13 @@ dp_gen* dp_gen_catalogs(int32_t config, int32_t n_problems, uint64_t base_seed);
 const dp_wire* dp_gen_wire(const dp_gen* g);
 void dp_gen_free(dp_gen* g);
 
+/* Build provenance: "sources=<digest> arch=gfx950", the digest (sha256,
+ * 16 hex digits) of every source, header and compile flag the library was
+ * built from (deppy_amd/build.py sources_digest).  No reference counterpart:
+ * the binding compares it with the tree it runs from and refuses a stale
+ * library. */
+const char* dp_build_info(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -25,6 +25,17 @@ def test_exports_match_header():
         assert hasattr(L, name), name
 
 
+def test_library_built_from_this_tree():
+    """Build provenance: the library carries the digest of the sources,
+    headers and flags it was compiled from (dp_build_info), equal to this
+    tree's; a library whose digest differs is refused at load."""
+    from deppy_amd import build
+    info = _lib.build_info()
+    assert info == "sources=%s arch=gfx950" % build.sources_digest(), info
+    # a different tree (one more flag) would not match: the binding's check is live
+    assert build.sources_digest(["-DDP_STAMPS"]) != build.sources_digest()
+
+
 def variables_of(fixture_vars):
     return [sat_var(v) for v in fixture_vars]
 
