@@ -108,7 +108,7 @@ def test_golden_records_bit_exact(ctx):
 # ---------------------------------------------------------------------------
 # seeded synthetic batches: bit-exact against the oracle
 # ---------------------------------------------------------------------------
-@pytest.mark.parametrize("config,n,seed", [(2, 3000, 11), (3, 8000, 12), (5, 300, 13)])
+@pytest.mark.parametrize("config,n,seed", [(2, 3000, 11), (3, 8000, 12), (5, 300, 13), (6, 3000, 14)])
 def test_generated_bit_exact(ctx, config, n, seed):
     lw = lowered_config(config, n, seed)
     g = ctx.solve(lw.rec_off, lw.rec)
@@ -354,9 +354,9 @@ def test_malformed_16bit_records_found_by_the_kernel(pinned):
     assert compare_results(g, ref, lw.n, only=ok) == []
 
 
-@pytest.mark.parametrize("config,n,seed,flags", [(2, 3000, 101, 0), (3, 9000, 102, 0), (5, 300, 103, 0),
+@pytest.mark.parametrize("config,n,seed,flags", [(2, 3000, 101, 0), (3, 9000, 102, 0), (5, 300, 103, 0), (6, 3000, 104, 0),
                                                  (2, 200, 104, _lib.OPT_FORCE_GROUP)],
-                         ids=["c2", "c3", "c5", "c2-group"])
+                         ids=["c2", "c3", "c5", "c6", "c2-group"])
 def test_packed_records_bit_exact(config, n, seed, flags):
     """Packed records (dp_lower_into DP_LOWER_PACKED: DP_FMT_P16D), copied to the device
     as they lie and decoded by the kernel (or widened on the host for a
