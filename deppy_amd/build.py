@@ -65,12 +65,14 @@ def _build(verbose, extra, OBJ, LIB) -> str:
     headers = _headers()
     digest = sources_digest(extra)
     stamp = os.path.join(OBJ, "digest")
+    # objects follow their sources' mtimes; a digest change (sources or
+    # flags) relinks, so the embedded digest is always the tree's
     stale = not os.path.exists(stamp) or open(stamp).read().strip() != digest
     jobs = []
     for src in SOURCES:
         s = os.path.join(CSRC, src)
         o = os.path.join(OBJ, src + ".o")
-        if stale or _needs(o, [s] + headers) or extra:
+        if _needs(o, [s] + headers) or extra:
             lang = ["-x", "hip"] if src.endswith(".hip") or src in ("runtime.cpp", "solve_launch.cpp") else []
             jobs.append([HIPCC] + FLAGS + (extra or []) + lang + ["-c", s, "-o", o])
     def run(cmd):
@@ -80,7 +82,7 @@ def _build(verbose, extra, OBJ, LIB) -> str:
     with ThreadPoolExecutor(max_workers=8) as ex:
         list(ex.map(run, jobs))
     objs = [os.path.join(OBJ, s + ".o") for s in SOURCES]
-    if _needs(LIB, objs) or jobs:
+    if stale or _needs(LIB, objs) or jobs:
         # the digest, compiled into the library (dp_build_info)
         info = os.path.join(OBJ, "build_info.cpp")
         with open(info, "w") as f:
