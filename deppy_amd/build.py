@@ -42,6 +42,16 @@ def sources_digest(extra: list[str] | None = None) -> str:
     return h.hexdigest()[:16]
 
 
+def _file_digest(paths: list[str], extra: list[str] | None) -> str:
+    h = hashlib.sha256()
+    for f in paths:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    h.update(" ".join(FLAGS[:-1] + (extra or [])).encode())
+    return h.hexdigest()[:16]
+
+
 def _needs(target: str, deps: list[str]) -> bool:
     if not os.path.exists(target):
         return True
@@ -72,15 +82,28 @@ def _build(verbose, extra, OBJ, LIB) -> str:
     for src in SOURCES:
         s = os.path.join(CSRC, src)
         o = os.path.join(OBJ, src + ".o")
-        if _needs(o, [s] + headers) or extra:
+        # an object is rebuilt when its inputs' contents differ from the ones
+        # it was compiled from (not only when they are newer)
+        od = _file_digest([s] + headers, extra)
+        dfile = o + ".digest"
+        same = os.path.exists(dfile) and open(dfile).read().strip() == od
+        if not same or _needs(o, [s] + headers) or extra:
             lang = ["-x", "hip"] if src.endswith(".hip") or src in ("runtime.cpp", "solve_launch.cpp") else []
-            jobs.append([HIPCC] + FLAGS + (extra or []) + lang + ["-c", s, "-o", o])
+            jobs.append(([HIPCC] + FLAGS + (extra or []) + lang + ["-c", s, "-o", o], dfile, od))
     def run(cmd):
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
+
+    def compile_one(job):
+        cmd, dfile, od = job
+        if os.path.exists(dfile):
+            os.remove(dfile)  # (a failed or interrupted compile leaves no digest)
+        run(cmd)
+        with open(dfile, "w") as f:
+            f.write(od + "\n")
     with ThreadPoolExecutor(max_workers=8) as ex:
-        list(ex.map(run, jobs))
+        list(ex.map(compile_one, jobs))
     objs = [os.path.join(OBJ, s + ".o") for s in SOURCES]
     if stale or _needs(LIB, objs) or jobs:
         # the digest, compiled into the library (dp_build_info)
