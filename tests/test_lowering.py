@@ -36,6 +36,16 @@ def test_library_built_from_this_tree():
     assert build.sources_digest(["-DDP_STAMPS"]) != build.sources_digest()
 
 
+def test_stale_library_is_refused(monkeypatch):
+    """A product library whose embedded digest is not the tree's raises at
+    load instead of running (the sources changed since it was built)."""
+    from deppy_amd import build
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    monkeypatch.setattr(build, "sources_digest", lambda extra=None: "0123456789abcdef")
+    with pytest.raises(RuntimeError, match="built from other sources"):
+        _lib._check_provenance(L)
+
+
 def variables_of(fixture_vars):
     return [sat_var(v) for v in fixture_vars]
 
