@@ -586,6 +586,7 @@ struct Group {
 #endif
     cap = L.cap; lcap = L.lcap;
     tlen = qhead = 0;
+    pre_lo = -1;
     steps = 0;
     vis = 0;
     sbank = 0;
@@ -2003,6 +2004,8 @@ struct Group {
       const int64_t t0 = stamp();
 #endif
       int ncq = 0;
+      const int hint = pre_lo;  // (valid for this round only)
+      pre_lo = -1;
       if constexpr (TWLL) {
         if (twl_on) {
           frontier_twl(lo, hi, crow, ncq, front);
@@ -2016,8 +2019,13 @@ struct Group {
         }
       }
       if (hi - lo == 1) {  // one new literal: threads over its watch list
-        const int l = DP_CHK(front(lo), 0, 2 * nv, 10);
-        const int a = w_off[l], e = w_off[l + 1];
+        int a, e;
+        if (NW == 1 && lo == hint) {
+          a = pre_a; e = pre_e;
+        } else {
+          const int l = DP_CHK(front(lo), 0, 2 * nv, 10);
+          a = w_off[l]; e = w_off[l + 1];
+        }
         for (int k0 = a; k0 < e; k0 += NT) {
           make_room(crow, ncq);
           visit_at(k0 + tid < e ? k0 + tid : -1, crow, ncq);
@@ -2198,11 +2206,13 @@ struct Group {
   }
 
   // gini Assume(m) + Test() (search.go:75-76)
-  __device__ __forceinline__ int test_assume(int l) {
+  // (xv: val[l >> 1] when the caller has it already; wa, we: l's watch range)
+  __device__ __forceinline__ int test_assume(int l, int xv = 2, int wa = 0, int we = -1) {
     ++steps;
-    const int x = lit_val(l);
+    const int x = xv == 2 ? lit_val(l) : ((l & 1) ? -xv : xv);
     if (x > 0) return propagate();
     if (x < 0) { ck = CK_ASSUME; c_var = l >> 1; return -1; }
+    if (NW == 1 && we >= 0) { pre_lo = tlen; pre_a = wa; pre_e = we; }
     assign_one(l, R_DEC, -1);
     return propagate();
   }
@@ -2502,6 +2512,9 @@ struct Group {
   // search.Do (search.go:158-203)
   // ------------------------------------------------------------------
   int dq_head, dq_n, ng, result;
+  // One wavefront: a guess's watch range, loaded with its other reads, for
+  // the round whose frontier is the guess alone (trail[pre_lo])
+  int pre_lo, pre_a, pre_e;
   bool class_b, solve_unsat, last_solve;
   bool final_from_solve;  // the search's last failure came from Solve() (else Test/Untest)
 
@@ -2546,19 +2559,50 @@ struct Group {
     const int list = DP_CHK((int)dq[2 * dq_head], 0, nch + nv, 17), idx = DP_CHK((int)dq[2 * dq_head + 1], 0, nv + 1, 18);
     dq_head = dq_head + 1 == cap ? 0 : dq_head + 1;
     --dq_n;
-    const int len = list_len(list);
-    int m = idx < len ? list_at(list, idx) : -1;
+    // The list's entries are src[base + i] >> sh, i < len (list_len /
+    // list_at with the list resolved once), and everything that depends on
+    // the guessed variable is loaded together: the dependent LDS round trips
+    // of a push are the list's row, its offsets, its entries, then their
+    // inS words with m's child rows and value.
+    const bool single = list >= nch;  // an anchor's singleton list
+    int len = 1, base = 0, sh = 0;
+    const IX* src = clause_lits;
+    if (!single) {
+      if (rowref) {
+        const int r = rowref[list];
+        base = (int)clause_off[r] + 1;
+        len = (int)clause_off[r + 1] - base;
+        sh = 1;
+      } else {
+        base = choice_off[list];
+        len = (int)choice_off[list + 1] - base;
+        src = choice_lits;
+      }
+    }
+    auto entry = [&](int i) { return single ? list - nch : (int)src[base + i] >> sh; };
+    int m = idx < len ? entry(idx) : -1;
+    const int mc = m >= 0 ? m : 0;
+    const int c0 = var_choice_off[mc], c1 = var_choice_off[mc + 1], xm = val[mc];
+    int wa = 0, we = 0;
+    if constexpr (NW == 1) { wa = w_off[2 * mc]; we = w_off[2 * mc + 1]; }
     bool any = false;
-    for (int i = tid; i < len; i += NT) any |= getb(inS, list_at(list, i));
+    for (int i = tid; i < len; i += NT) any |= getb(inS, entry(i));
     const bool skip = g_any(any);
     if (skip) m = -1;
     else if (idx >= len) class_b = true;  // exhausted choice
-    if (m >= 0)  // its children: one choice per choice row (pop_guess recounts them)
-      for (int r = var_choice_off[m]; r < (int)var_choice_off[m + 1]; ++r) dq_push_back(r, 0);
+    // its children: one choice per choice row (pop_guess recounts them),
+    // appended in row order, a thread per row
+    const int nchild = m >= 0 ? c1 - c0 : 0;
+    for (int k = tid; k < nchild; k += NT) {
+      int at = dq_head + dq_n + k;
+      if (at >= cap) at -= cap;
+      dq[2 * at] = enc(c0 + k); dq[2 * at + 1] = enc(0);
+    }
+    dq_n += nchild;
     if (tid == 0) {
       IX* g = stk + 3 * ng;
       g[0] = enc(list); g[1] = enc(idx | (skip ? G_SKIP : 0)); g[2] = enc(tlen);
-      if (m >= 0) inS[m >> 5] |= 1u << (m & 31);
+      if (m >= 0) atomicOr(&inS[m >> 5], 1u << (m & 31));
     }
     ++ng;
     gsync();
@@ -2567,7 +2611,7 @@ struct Group {
 #ifdef DP_STAMPS
     DP_ACC(21, stamp() - tpg);
 #endif
-    result = test_assume(2 * m);
+    result = test_assume(2 * m, xm, wa, we);
     last_solve = false;
   }
 
