@@ -2623,7 +2623,21 @@ struct Group {
     const int list = DP_CHK((int)g[0], 0, nch + nv, 19), idxf = (int)g[1],
               mark = DP_CHK((int)g[2], 0, nv + 1, 23);
     const int idx = DP_CHK(idxf & ~G_SKIP, 0, nv + 1, 20);
-    const int m = DP_CHK(guess_m(list, idxf), -1, nv, 21);
+    // guess_m with the list resolved once (as in push_guess)
+    int m = -1;
+    if (!(idxf & G_SKIP)) {
+      if (list >= nch) {
+        m = idx < 1 ? list - nch : -1;
+      } else if (rowref) {
+        const int r = rowref[list];
+        const int a = (int)clause_off[r] + 1, len = (int)clause_off[r + 1] - a;
+        if (idx < len) m = (int)clause_lits[a + idx] >> 1;
+      } else {
+        const int a = choice_off[list], len = (int)choice_off[list + 1] - a;
+        if (idx < len) m = choice_lits[a + idx];
+      }
+    }
+    m = DP_CHK(m, -1, nv, 21);
     const int children = m >= 0 ? (int)var_choice_off[m + 1] - (int)var_choice_off[m] : 0;
     gsync();
     if (m >= 0) {
