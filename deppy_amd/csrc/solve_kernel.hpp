@@ -2020,7 +2020,7 @@ struct Group {
       }
       if (hi - lo == 1) {  // one new literal: threads over its watch list
         int a, e;
-        if (NW == 1 && lo == hint) {
+        if (lo == hint) {
           a = pre_a; e = pre_e;
         } else {
           const int l = DP_CHK(front(lo), 0, 2 * nv, 10);
@@ -2212,7 +2212,7 @@ struct Group {
     const int x = xv == 2 ? lit_val(l) : ((l & 1) ? -xv : xv);
     if (x > 0) return propagate();
     if (x < 0) { ck = CK_ASSUME; c_var = l >> 1; return -1; }
-    if (NW == 1 && we >= 0) { pre_lo = tlen; pre_a = wa; pre_e = we; }
+    if (we >= 0) { pre_lo = tlen; pre_a = wa; pre_e = we; }
     assign_one(l, R_DEC, -1);
     return propagate();
   }
@@ -2512,8 +2512,8 @@ struct Group {
   // search.Do (search.go:158-203)
   // ------------------------------------------------------------------
   int dq_head, dq_n, ng, result;
-  // One wavefront: a guess's watch range, loaded with its other reads, for
-  // the round whose frontier is the guess alone (trail[pre_lo])
+  // A guess's watch range, loaded with its other reads, for the round whose
+  // frontier is the guess alone (trail[pre_lo])
   int pre_lo, pre_a, pre_e;
   bool class_b, solve_unsat, last_solve;
   bool final_from_solve;  // the search's last failure came from Solve() (else Test/Untest)
@@ -2583,8 +2583,7 @@ struct Group {
     int m = idx < len ? entry(idx) : -1;
     const int mc = m >= 0 ? m : 0;
     const int c0 = var_choice_off[mc], c1 = var_choice_off[mc + 1], xm = val[mc];
-    int wa = 0, we = 0;
-    if constexpr (NW == 1) { wa = w_off[2 * mc]; we = w_off[2 * mc + 1]; }
+    const int wa = w_off[2 * mc], we = w_off[2 * mc + 1];
     bool any = false;
     for (int i = tid; i < len; i += NT) any |= getb(inS, entry(i));
     const bool skip = g_any(any);
