@@ -30,7 +30,12 @@ GPU.  Problems are independent (SURVEY.md §8(e)): no data-path collective;
 torch.distributed carries only the barrier and the max-over-ranks of the
 timing.  --scaling weak (default): every rank solves its own batch.
 --scaling strong: the config's total (config 3: 1,000,000 catalogs) is split
-across the ranks.
+across the ranks.  The topology the cgo shim ships is one process driving
+every GPU (dp_create(n_devices=N)): `--inproc` measures that
+instead (one process, N devices, N x the per-GPU batch), and a torchrun run
+with N > 1 ranks also measures it after its own timed region (rank 0 alone
+over all N GPUs while the other ranks wait), as `inproc` in the line, with the
+chunks each device's submitting thread ran.
 
 `roofline.achieved` = algorithmic bytes of a chunk (staged records + outputs,
 DESIGN.md §4.2) / the chunk's solve-kernel device time (HIP events on its
@@ -92,7 +97,7 @@ def cpu_share() -> dict:
 def maybe_relaunch(args) -> None:
     """--gpus N > 1 without torchrun: run this script under
     torch.distributed.run (a child process, started before any GPU call)."""
-    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+    if args.gpus <= 1 or args.inproc or "WORLD_SIZE" in os.environ:
         return
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
            "--master-addr", "127.0.0.1", "--master-port", str(29500 + os.getpid() % 1000),
@@ -219,6 +224,46 @@ def lowered_config(config, n, seed, form="packed"):
     return lw, lw32, t_lower, wa
 
 
+def inproc_leg(config, n, nd, seed, steps, warmup, form):
+    """The one-process topology (the cgo shim's): dp_create(n_devices=nd)
+    over GPUs 0..nd-1, one batch of nd * n catalogs per step (n per device,
+    as each rank of the torchrun run solves n), host to host with a job per
+    chunk slot in flight.  Returns the rate and the chunks each device's
+    submitting thread ran."""
+    from deppy_amd import _lib
+    lw, _, _, _ = lowered_config(config, n * nd, seed, form)
+    ctx = _lib.Context(0, nd)
+    try:
+        ctx.stats(reset=True)
+        ctx.submit(lw.rec_off, lw.rec).wait()
+        depth = max(1, ctx.lanes() * nd // max(1, ctx.stats(reset=True)["chunks"]))
+        outs = [_lib.result_arrays(lw.rec_off, lw.rec) for _ in range(depth)]
+
+        def run(k):
+            jobs = []
+            for i in range(k):
+                if len(jobs) == depth:
+                    jobs.pop(0).wait()
+                jobs.append(ctx.submit(lw.rec_off, lw.rec, outs[i % depth]))
+            for j in jobs:
+                j.wait()
+
+        run(max(warmup, 1))
+        ctx.stats(reset=True)
+        t0 = time.perf_counter()
+        run(steps)
+        el = time.perf_counter() - t0
+        per = [int(ctx.device_stats(d)["chunks"]) for d in range(nd)]
+        kms = [round(ctx.device_stats(d)["kernel_ms"] / max(1, steps), 3) for d in range(nd)]
+    finally:
+        ctx.close()
+    return {"n_devices": nd, "value": round(n * nd * steps / el, 1), "ms_per_step": round(el / steps * 1e3, 4),
+            "catalogs_per_step": n * nd, "chunks_per_device": per, "kernel_ms_per_step_per_device": kms,
+            "jobs_in_flight": depth,
+            "note": "one process, dp_create(n_devices=%d) (the cgo shim's topology, INTEGRATION.md): one "
+                    "submitting thread and host pool per device; not value" % nd}
+
+
 def output_bytes(res) -> int:
     """Every output word the kernel writes: a 32-byte result
     record per problem (status, flags, core length and offset, steps, BCP
@@ -255,6 +300,11 @@ def same_results(a, b) -> bool:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--inproc", action="store_true",
+                    help="one process drives the N GPUs (dp_create(n_devices=N), the cgo shim's topology) "
+                         "instead of one torchrun rank per GPU")
+    ap.add_argument("--no-inproc-leg", action="store_true",
+                    help="torchrun runs with N > 1: skip the one-process leg after the timed region")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--config", type=int, default=2)
@@ -295,15 +345,16 @@ def main():
     if world != args.gpus:
         raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     wl = WORKLOADS[args.config]
+    nd = args.gpus if args.inproc else 1  # devices this process drives
     if args.scaling == "weak":
-        n = args.problems or wl[0]
+        n = (args.problems or wl[0]) * nd
         first = shard.shard_seed(args.seed, rank, n)
     else:
         total = args.problems or wl[1]
         lo, hi = shard.strong_range(total, rank, world)
         n, first = hi - lo, args.seed + lo
     lw, lw32, t_lower, wa = lowered_config(args.config, n, first, args.record_form)
-    ctx = _lib.Context(local, 1, flags=args.flags)
+    ctx = _lib.Context(0 if nd > 1 else local, nd, flags=args.flags)
     global LANES
     LANES = ctx.lanes()
 
@@ -330,6 +381,7 @@ def main():
     if args.kernel_only:  # profiling: only the device-resident leg below
         args.steps = 1
         st, elapsed, res, deterministic = ctx.stats(), float("inf"), None, None
+        per_device = None
     else:
         run_steps(max(args.warmup, 1))
         first_res = ctx.submit(lw.rec_off, lw.rec).wait()  # cold-free single call, for the check
@@ -339,6 +391,7 @@ def main():
         run_steps(args.steps)
         t1 = time.perf_counter()
         g.barrier()
+        per_device = [int(ctx.device_stats(d)["chunks"]) for d in range(nd)]
         st = ctx.stats(reset=True)
         elapsed = g.max(t1 - t0)
         res = ctx.submit(lw.rec_off, lw.rec).wait()
@@ -354,7 +407,7 @@ def main():
         "metric": METRIC,
         "value": round(value, 1),
         "unit": "resolutions/s",
-        "n_gpus": world,
+        "n_gpus": world * nd,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(step_s * 1e3, 4),
@@ -363,8 +416,11 @@ def main():
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic",
-        "config": {"workload": wl[2] % n, "catalogs_per_step_per_gpu": n, "record_forms": record_forms(lw),
-                   "parallelism": "dp%d (host partition)" % world, "seed": args.seed,
+        "config": {"workload": wl[2] % (n // nd), "catalogs_per_step_per_gpu": n // nd,
+                   "record_forms": record_forms(lw),
+                   "parallelism": ("dp%d (host partition; one process, dp_create(n_devices=%d))" % (nd, nd)
+                                   if nd > 1 else "dp%d (host partition; one process per GPU)" % world),
+                   "n_devices_per_process": nd, "chunks_per_device_timed": per_device, "seed": args.seed,
                    "path": "host memory -> host memory (dp_submit/dp_job_wait), %d jobs in flight" % depth},
         "pipeline": {"chunks_per_step": round(chunks / args.steps, 2),
                      "kernel_ms_per_chunk": round(st["kernel_ms"] / chunks, 4),
@@ -543,6 +599,14 @@ def main():
                                               % threads)
         line["verified_bit_exact_vs_oracle"] = bool(ok)
         line["verified_note"] = "GPU on the packed 16-bit records vs oracle on the int32 records, every field incl. cores"
+    if world > 1 and not args.no_inproc_leg and args.scaling == "weak" and not args.kernel_only:
+        # the shipped one-process topology on the same node, after the timed
+        # region: rank 0 drives all N GPUs while the other ranks wait
+        g.barrier()
+        if rank == 0:
+            line["inproc"] = inproc_leg(args.config, n, world, args.seed, args.steps, args.warmup,
+                                        args.record_form)
+        g.barrier()
     if rank == 0:
         print(json.dumps(line), flush=True)
     g.close()

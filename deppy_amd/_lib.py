@@ -70,6 +70,8 @@ OPT_FORCE_GROUP = 1 << 0
 OPT_FORCE_HBM = 1 << 1
 OPT_FORCE_MID = 1 << 2
 OPT_TINY_TABLE = 1 << 3
+OPT_FORCE_LDSG = 1 << 4
+OPT_SHARE_ORDINAL = 1 << 5  # test: every logical device of the context on first_device's GPU
 # dp_flag bits used on the host
 F_TRACE_TRUNCATED = 1 << 8
 if os.environ.get("DEPPY_STAMPS") == "1":  # diagnostic phase-stamp build (scripts/ only)
@@ -91,7 +93,7 @@ EXPORTS = [
     "dp_launch", "dp_wait", "dp_download", "dp_resident_free", "dp_last_kernel_ms", "dp_gen_catalogs", "dp_gen_wire",
     "dp_gen_free", "dp_upload_traced", "dp_download_trace", "dp_solve_traced", "dp_lowered_errors",
     "dp_device_bytes", "dp_lower_into", "dp_lowered_new", "dp_lowered_exact_count", "dp_lowered_pinned", "dp_rec_widen", "dp_submit", "dp_job_wait", "dp_get_stats", "dp_stage_roundtrip",
-    "dp_stitch_selftest", "dp_partition", "dp_build_info",
+    "dp_stitch_selftest", "dp_partition", "dp_build_info", "dp_get_device_stats",
 ]
 
 
@@ -213,6 +215,8 @@ def lib():
     L.dp_submit.argtypes = [vp, ctypes.POINTER(Batch), ctypes.POINTER(Result), ctypes.POINTER(vp)]
     L.dp_job_wait.argtypes = [vp, vp]
     L.dp_get_stats.argtypes = [vp, ctypes.POINTER(Stats), ctypes.c_int32]
+    L.dp_get_device_stats.argtypes = [vp, ctypes.c_int32, ctypes.POINTER(Stats), ctypes.c_int32]
+    L.dp_num_devices.restype = ctypes.c_int32
     L.dp_stage_roundtrip.argtypes = [ctypes.POINTER(Batch), ctypes.c_int32, ctypes.c_int32, ctypes.c_int64,
                                      c_i32p, c_i32p, ctypes.c_int32]
     L.dp_stitch_selftest.argtypes = [ctypes.POINTER(Batch), ctypes.c_int32, ctypes.POINTER(Result)]
@@ -447,6 +451,17 @@ class Context:
     def stats(self, reset: bool = False) -> dict:
         st = Stats()
         lib().dp_get_stats(self.h, ctypes.byref(st), 1 if reset else 0)
+        return {k: getattr(st, k) for k, _ in Stats._fields_}
+
+    def devices(self) -> int:
+        """Logical devices of the context (dp_num_devices)."""
+        return int(lib().dp_num_devices(self.h))
+
+    def device_stats(self, device: int, reset: bool = False) -> dict:
+        """dp_get_device_stats: the share of the pipeline one logical device ran."""
+        st = Stats()
+        if lib().dp_get_device_stats(self.h, device, ctypes.byref(st), 1 if reset else 0) != 0:
+            raise ValueError("dp_get_device_stats: no device %d" % device)
         return {k: getattr(st, k) for k, _ in Stats._fields_}
 
     def last_kernel_ms(self) -> float:

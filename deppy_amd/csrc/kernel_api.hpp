@@ -73,7 +73,8 @@ struct KernelArgs {
 constexpr int kQueueWords = 64;
 
 // Launch one workgroup per problem of order[0..n_blocks) with lds_bytes of
-// LDS: one wavefront (mode M_LDS) or BIG_WAVES wavefronts (M_SPLIT, M_HBM).
+// LDS: one wavefront (mode M_LDS) or a multi-wave workgroup (M_LDSG, M_SPLIT4,
+// M_SPLIT, M_HBM; layout.hpp mode_waves).
 hipError_t launch_solve(const KernelArgs& a, int mode, int n_blocks, int lds_bytes, hipStream_t stream);
 // Before a multi-wave launch (mode M_SPLIT / M_SPLIT4 / M_HBM) of n_items
 // items: the watch lists of its DP_FMT_I32 records above DEV_WATCH_VARS

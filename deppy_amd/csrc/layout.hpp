@@ -37,7 +37,15 @@ constexpr int32_t L_MAX = 64;
 //           (catalogs whose per-variable state exceeds the LDS)
 // M_SPLIT4: M_SPLIT with MID_WAVES wavefronts (catalogs routed off the LDS
 // path for their size, not for overflowing it; runtime.cpp kMidMaxVars)
-enum Mode { M_LDS = 0, M_SPLIT = 1, M_HBM = 2, M_SPLIT4 = 3 };
+// M_LDSG  the M_LDS image and working set, all of it in LDS, solved by one
+//         workgroup of LDSG_WAVES wavefronts: catalogs whose one-wavefront
+//         footprint is above placement.hpp group_above() (a lone wavefront
+//         would leave the CU's other SIMDs idle) but still fits one CU's LDS.
+//         No HBM scratch: every per-literal array, watch list and learned row
+//         is LDS.
+enum Mode { M_LDS = 0, M_SPLIT = 1, M_HBM = 2, M_SPLIT4 = 3, M_LDSG = 4 };
+// The 16-bit LDS image (M_LDS, M_LDSG): record and working set in LDS
+__host__ __device__ constexpr bool mode_n16(int mode) { return mode == M_LDS || mode == M_LDSG; }
 #ifndef DP_BIG_WAVES
 #define DP_BIG_WAVES 8
 #endif
@@ -47,8 +55,12 @@ constexpr int32_t BIG_WAVES = DP_BIG_WAVES;
 #define DP_MID_WAVES 4
 #endif
 constexpr int32_t MID_WAVES = DP_MID_WAVES;
+#ifndef DP_LDSG_WAVES
+#define DP_LDSG_WAVES 4
+#endif
+constexpr int32_t LDSG_WAVES = DP_LDSG_WAVES;
 __host__ __device__ constexpr int32_t mode_waves(int mode) {
-  return mode == M_LDS ? 1 : mode == M_SPLIT4 ? MID_WAVES : BIG_WAVES;
+  return mode == M_LDS ? 1 : mode == M_SPLIT4 ? MID_WAVES : mode == M_LDSG ? LDSG_WAVES : BIG_WAVES;
 }
 // work list of one propagation chunk (rows watched by <= 64*waves frontier literals)
 #ifndef DP_WBUF_LDS
@@ -57,9 +69,11 @@ __host__ __device__ constexpr int32_t mode_waves(int mode) {
 #ifndef DP_CQ_LDS
 #define DP_CQ_LDS 64
 #endif
-__host__ __device__ constexpr int32_t mode_wbuf(int mode) { return mode == M_LDS ? DP_WBUF_LDS : 4096; }
+__host__ __device__ constexpr int32_t mode_wbuf(int mode) {
+  return mode == M_LDS ? DP_WBUF_LDS : mode == M_LDSG ? 1024 : 4096;
+}
 // AtMost rows queued for wave-cooperative evaluation in one round
-__host__ __device__ constexpr int32_t mode_cq(int mode) { return mode == M_LDS ? DP_CQ_LDS : 512; }
+__host__ __device__ constexpr int32_t mode_cq(int mode) { return mode == M_LDS ? DP_CQ_LDS : mode == M_LDSG ? 256 : 512; }
 // M_LDS stores imp (the lowest implying row per literal) in 16 bits, updated
 // by a compare-and-swap, or in 32 bits, updated by atomicMin
 #ifndef DP_IMP16
@@ -77,7 +91,7 @@ constexpr bool IMP16_LDS = DP_IMP16;
 #ifndef DP_2WL
 #define DP_2WL 0
 #endif
-__host__ __device__ constexpr bool mode_2wl(int mode) { return DP_2WL && mode != M_LDS; }
+__host__ __device__ constexpr bool mode_2wl(int mode) { return DP_2WL && !mode_n16(mode); }
 // Two-watched-literal propagation on the one-wavefront path (-DDP_TWL_LDS=1):
 // a clause row of 3..254 literals sits in the watch lists of two of its
 // positions only (Layout::wpos, a byte each); a round that falsifies one of
@@ -105,7 +119,7 @@ constexpr int32_t TWL_MIN_LEN = 3, TWL_MAX_LEN = 254;
 #ifndef DP_ROWSLOT
 #define DP_ROWSLOT 0
 #endif
-__host__ __device__ constexpr bool mode_rowslot(int mode) { return DP_ROWSLOT && mode != M_LDS; }
+__host__ __device__ constexpr bool mode_rowslot(int mode) { return DP_ROWSLOT && !mode_n16(mode); }
 constexpr int32_t ROWSLOT_INLINE = 5;
 
 // wave-shared scalars (S_*), then (multi-wave modes) per-wave reduction slots
@@ -253,7 +267,7 @@ __host__ __device__ inline int64_t staged_words(const int32_t* h, bool narrow) {
 // allocation when the mode places that array in LDS (in_lds below), else into
 // the problem's HBM scratch region.
 struct Layout {
-  int32_t body;      // M_LDS only: the extended record (header dropped), one IX per word;
+  int32_t body;      // M_LDS / M_LDSG only: the extended record (header dropped), one IX per word;
                      // the watch-list build counts on the per-literal arrays (reason..touched)
   int32_t val;       // int8[nv]: 0 unassigned, 1 true, -1 false                  [LDS unless M_HBM]
   int32_t reason;    // IX[nv] implying row; R_DEC / R_EXTRA / a Solve() decision (-3 - index)
@@ -272,7 +286,7 @@ struct Layout {
   int32_t used;      // bits[nid] identities met by a refutation                   [LDS unless M_HBM]
   int32_t en;        // bits[nid] identities enabled (core search)                 [LDS unless M_HBM]
   int32_t en2;       // bits[nid]                                                  [LDS unless M_HBM]
-  int32_t idt;       // (M_LDS) bits[nid] rows -> identities for the outputs (row_of)  [LDS]
+  int32_t idt;       // (M_LDS / M_LDSG) bits[nid] rows -> identities for the outputs (row_of)  [LDS]
   int32_t l_off;     // IX[L_MAX+1] learned rows (rows nrows..)
   int32_t l_lits;    // IX[lcap]
   int32_t dq;        // IX[2*cap] deque of choices (list, idx)
@@ -297,7 +311,7 @@ struct Layout {
   int32_t wend;      // (mode_twl_lds) u16[2nv] live end of each literal's watch list
   int32_t wfi;       // (mode_twl_lds) u8[wbuf] frontier literal of each flattened work-list entry
   int32_t fcur;      // (mode_twl_lds) i32[64] compaction cursor per frontier literal of a chunk
-  int32_t bytes;     // HBM scratch bytes (0 for M_LDS)
+  int32_t bytes;     // HBM scratch bytes (0 for M_LDS / M_LDSG)
   int32_t lds_bytes; // LDS bytes
   int32_t cap, lcap;
 };
@@ -320,16 +334,17 @@ __host__ __device__ inline int32_t round_slots(int32_t nv) {
 
 template <int MODE>
 __host__ __device__ inline Layout layout(const int32_t* h) {
-  using IX = typename std::conditional<MODE == M_LDS, uint16_t, int32_t>::type;
+  constexpr bool N16 = mode_n16(MODE);
+  using IX = typename std::conditional<N16, uint16_t, int32_t>::type;
   Layout L;
   const int32_t nv = h[DP_H_NV], nid = h[DP_H_NID];
   const int32_t nbv = bits_words(nv), nbi = bits_words(nid);
   const int32_t ix = (int32_t)sizeof(IX);
   int32_t og = 0, ol = 0;
   // every array 16-byte aligned; `hot` arrays go to LDS unless M_HBM, the
-  // per-literal arrays to LDS only in M_LDS, the work lists always to LDS
+  // per-literal arrays to LDS only in M_LDS / M_LDSG, the work lists always to LDS
   auto take = [&](int32_t nbytes, int kind) {
-    const bool lds = MODE == M_LDS || kind == 2 || (kind == 1 && (MODE == M_SPLIT || MODE == M_SPLIT4));
+    const bool lds = N16 || kind == 2 || (kind == 1 && (MODE == M_SPLIT || MODE == M_SPLIT4));
     int32_t& o = lds ? ol : og;
     const int32_t at = o;
     o += (nbytes + 15) & ~15;
@@ -343,16 +358,16 @@ __host__ __device__ inline Layout layout(const int32_t* h) {
   // slack.  A packed record's tail is copied to p16_tail_copy (where the
   // watch lists go later) while it is decoded: the region covers that copy.
   int32_t body_bytes = (X.words - DP_H_SIZE + 8) * ix;
-  if (MODE == M_LDS) body_bytes = (lds_body_words(h) + (X.words - h[DP_H_WORDS]) + 8) * ix;
-  if (MODE == M_LDS && (h[DP_H_FMT] == DP_FMT_P16 || h[DP_H_FMT] == DP_FMT_P16D)) {
+  if (N16) body_bytes = (lds_body_words(h) + (X.words - h[DP_H_WORDS]) + 8) * ix;
+  if (N16 && (h[DP_H_FMT] == DP_FMT_P16 || h[DP_H_FMT] == DP_FMT_P16D)) {
     const int32_t need = p16_tail_copy(h) + (int32_t)((p16_tail_bytes(h) + 15) & ~15);
     body_bytes = body_bytes > need ? body_bytes : need;
   }
-  L.body = MODE == M_LDS ? take(body_bytes, COLD) : 0;
+  L.body = N16 ? take(body_bytes, COLD) : 0;
   L.scal = take(mode_nscal(MODE) * 4, WORK);
   L.wbuf = take(mode_wbuf(MODE) * ix, WORK);
   // (multi-wave: each queued row's row_info after the queue, cardq[cq + i])
-  L.cardq = take(mode_cq(MODE) * ix * (MODE == M_LDS ? 1 : 2), WORK);
+  L.cardq = take(mode_cq(MODE) * ix * (N16 ? 1 : 2), WORK);
   // the table shrinks (to 64 slots at least) when the catalog's per-variable
   // state leaves less LDS, so it never moves a catalog off this placement
   L.hc = mode_lds_rounds(MODE) ? round_slots(nv) : 0;
@@ -377,19 +392,19 @@ __host__ __device__ inline Layout layout(const int32_t* h) {
   L.used = take(nbi * 4, HOT);
   L.en = take(nbi * 4, HOT);
   L.en2 = take(nbi * 4, HOT);
-  L.idt = MODE == M_LDS ? take(nbi * 4, HOT) : 0;
+  L.idt = N16 ? take(nbi * 4, HOT) : 0;
   L.reason = take(nv * ix, COLD);
   L.rs = take(nv * ix, COLD);
   L.trail = take(nv * ix, COLD);
   L.touched = take(2 * nv * ix, COLD);
   L.d_mark = take(nv * ix, COLD);
-  L.imp = take(2 * nv * (MODE == M_LDS && IMP16_LDS ? 2 : 4), COLD);
+  L.imp = take(2 * nv * (N16 && IMP16_LDS ? 2 : 4), COLD);
   L.l_off = take((L_MAX + 1) * ix, COLD);
   L.l_lits = take(L.lcap * ix, COLD);
   L.dq = take(2 * L.cap * ix, COLD);
   L.stk = take(3 * L.cap * ix, COLD);
   L.wp = mode_rowslot(MODE) ? take(h[DP_H_NC] * 32, COLD) : mode_2wl(MODE) ? take(h[DP_H_NC] * 8, COLD) : 0;
-  L.wl = MODE != M_LDS && h[DP_H_FMT] == DP_FMT_I32 ? take((2 * nv + 2) * 4 + (h[DP_H_NCL] + h[DP_H_NKL]) * 8, COLD) : 0;
+  L.wl = !N16 && h[DP_H_FMT] == DP_FMT_I32 ? take((2 * nv + 2) * 4 + (h[DP_H_NCL] + h[DP_H_NKL]) * 8, COLD) : 0;
   L.wpos = mode_twl_lds(MODE) ? take(2 * h[DP_H_NC], COLD) : 0;
   L.wend = mode_twl_lds(MODE) ? take(4 * nv, COLD) : 0;
   L.wfi = mode_twl_lds(MODE) ? take(mode_wbuf(MODE), COLD) : 0;

@@ -474,8 +474,9 @@ struct Lowerer {
   // diagnostic DEPPY_HOST_WATCHES=1: multi-wave records above DEV_WATCH_VARS
   // variables carry host-built watch lists (DP_FMT_I32W), as before round 3
   const bool host_watches;
+  const bool ldsg;  // placement.hpp ldsg_env(): mid-size 16-bit records run on M_LDSG
   Lowerer(const dp_wire& wire, bool narrow16, bool packed16, bool host_lists)
-      : w(wire), narrow(narrow16), packed(packed16), host_watches(host_lists) {}
+      : w(wire), narrow(narrow16), packed(packed16), host_watches(host_lists), ldsg(ldsg_env()) {}
 
   // The last record appended to O (int32 words from `base`) in the 16-bit
   // form, in place (word j -> halfword j never overtakes word j).  Every
@@ -489,8 +490,8 @@ struct Lowerer {
     int32_t* r = O.rec.data() + base;
     const int64_t words = r[DP_H_WORDS];
     int64_t phys = words;
-    if (!one_wave(r)) {
-      // a multi-wave problem: its staged form is the int32 record as it is
+    if (!lds_image(r, ldsg)) {
+      // an HBM-read multi-wave problem: its staged form is the int32 record as it is
       // (the device builds its watch lists, layout.hpp DEV_WATCH_VARS)
       if (host_watches && !device_watches(r)) {
         const int64_t ext = 2 * (int64_t)r[DP_H_NV] + 1 + r[DP_H_NCL] + r[DP_H_NKL];
@@ -621,7 +622,7 @@ struct Lowerer {
     hdr[DP_H_NKL] = F.nkl;
     hdr[DP_H_NCHL] = F.nchl;
     hdr[DP_H_WORDS] = dp_rec_layout_of(hdr).words;
-    if (!one_wave(hdr)) return false;  // (fits16 included)
+    if (!lds_image(hdr, ldsg)) return false;  // (fits16 included)
     for (int32_t i = 0; i < F.nc; ++i)
       if (F.clause_off[i + 1] - F.clause_off[i] > 255) return false;
     for (int32_t k = 0; k < F.nk; ++k)

@@ -34,6 +34,22 @@ inline bool one_wave(const int32_t* h) {
   return fits16(h) && (int64_t)layout<M_LDS>(h).lds_bytes <= group_above();
 }
 
+// The all-LDS multi-wave placement (M_LDSG) for 16-bit records past
+// group_above(); DEPPY_LDSG=0 (diagnostic, and tests of the HBM-read
+// multi-wave records) sends them to the HBM-read multi-wave groups as before
+// round 5.  Read once per lowering call and per planned chunk.
+inline bool ldsg_env() {
+  const char* e = std::getenv("DEPPY_LDSG");
+  return !(e && *e == '0');
+}
+// Does the record fit the M_LDSG working set (one CU's LDS)?
+inline bool ldsg_fits(const int32_t* h) { return fits16(h) && (int64_t)layout<M_LDSG>(h).lds_bytes <= kMaxLdsBytes; }
+// Does the record (well formed) run on its 16-bit LDS image, one wavefront
+// (M_LDS) or one multi-wave workgroup (M_LDSG; ldsg: ldsg_env()), without
+// DP_OPT_FORCE_* flags?  The lowering emits such records in a 16-bit form
+// (DP_LOWER_NARROW).
+inline bool lds_image(const int32_t* h, bool ldsg) { return one_wave(h) || (ldsg && ldsg_fits(h)); }
+
 // The watch lists of a multi-wave problem (layout.hpp img_layout), right
 // after its int32 record r: rows in ascending order in every list.  Returns
 // the extended length in words.

@@ -123,7 +123,7 @@ int64_t env_i64(const char* name, int64_t dflt) {
 }
 
 bool forced_of(int32_t opt_flags) {
-  return opt_flags & (DP_OPT_FORCE_GROUP | DP_OPT_FORCE_HBM | DP_OPT_FORCE_MID);
+  return opt_flags & (DP_OPT_FORCE_GROUP | DP_OPT_FORCE_HBM | DP_OPT_FORCE_MID | DP_OPT_FORCE_LDSG);
 }
 
 // Header sanity needed before any layout arithmetic on it: the counts bound
@@ -160,6 +160,7 @@ struct Launch {
 struct Head {
   int8_t place;   // -1 malformed, -2 too large, else the Mode
   int8_t bucket;  // M_LDS: the LDS bucket (ceilings())
+  // (M_LDSG problems are staged like M_LDS ones: `lds` is their M_LDSG footprint)
   bool direct;    // the record is its own staged form (16-bit, 16-byte aligned)
   int32_t lds, inst_words, nid;
   int64_t sw, rec_bytes;
@@ -190,19 +191,38 @@ struct Plan {
   // planning scratch, kept across chunks (no allocation or page fault per
   // chunk once grown)
   std::vector<Head> head;
-  std::vector<int32_t> big[4], cnt, tmp, grp;
+  std::vector<int32_t> big[5], cnt, tmp, grp;
 };
 
-void read_head(Head& H, const int32_t* h, int64_t avail, int32_t opt_flags, bool aligned) {
+void read_head(Head& H, const int32_t* h, int64_t avail, int32_t opt_flags, bool aligned, bool ldsg) {
   H = Head{};
   if (!header_ok(h, avail)) { H.place = -1; return; }
   H.inst_words = bits_words(h[DP_H_NV]);
   H.nid = h[DP_H_NID];
-  // lds_path, with the one-wavefront layout computed once
-  bool nar = false;
-  if (!forced_of(opt_flags) && dp::fits16(h)) {
-    H.lds = layout<M_LDS>(h).lds_bytes;
-    nar = H.lds <= dp::group_above();
+  // lds_path, with the one-wavefront layout computed once; past
+  // group_above(), the all-LDS multi-wave group while the image fits a CU
+  bool nar = false, grp = false;
+  if (dp::fits16(h)) {
+    if (!forced_of(opt_flags)) {
+      H.lds = layout<M_LDS>(h).lds_bytes;
+      nar = H.lds <= dp::group_above();
+    }
+    if (!nar && ((!forced_of(opt_flags) && ldsg) || (opt_flags & DP_OPT_FORCE_LDSG))) {
+      const int32_t g = layout<M_LDSG>(h).lds_bytes;
+      if (g <= kMaxLdsBytes) {
+        grp = true;
+        H.lds = g;
+      }
+    }
+  }
+  if (grp) {
+    // the 16-bit image as for M_LDS, one queued multi-wave launch
+    H.sw = staged_words(h, true);
+    H.rec_bytes = dp_fmt_packed(h[DP_H_FMT]) ? 4 * dp_rec_phys_words(h)
+                                             : 4 * DP_H_SIZE + 2 * ((int64_t)h[DP_H_WORDS] - DP_H_SIZE);
+    H.place = M_LDSG;
+    H.direct = aligned && (h[DP_H_FMT] == DP_FMT_U16 || dp_fmt_packed(h[DP_H_FMT]));
+    return;
   }
   H.sw = staged_words(h, nar);
   // algorithmic input bytes (roofline.achieved): the record as the kernel
@@ -257,6 +277,7 @@ void plan_chunk(Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0,
   P.n_direct = 0;
   P.big_base = 0;
   Head* head = P.head.data();
+  const bool ldsg = dp::ldsg_env();
   auto rd = [&](int64_t i) {
     // every header is a cache miss: keep the next ones in flight
     if (i + 8 < n) {
@@ -265,7 +286,7 @@ void plan_chunk(Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0,
       __builtin_prefetch(h8 + 15);
     }
     read_head(head[i], rec + rec_off[p0 + i], rec_off[p0 + i + 1] - rec_off[p0 + i], opt_flags,
-              (rec_off[p0 + i] & 3) == 0);
+              (rec_off[p0 + i] & 3) == 0, ldsg);
   };
   if (pool && n > 256) pool->run(n, std::function<void(int64_t)>(rd), 64);
   else for (int32_t i = 0; i < n; ++i) rd(i);
@@ -281,7 +302,7 @@ void plan_chunk(Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0,
     P.direct[(size_t)i] = d;
     P.n_direct += d;
     P.other_words += d ? 0 : rec_off[p0 + i + 1] - rec_off[p0 + i];
-    P.narrow[(size_t)i] = H.place == M_LDS;
+    P.narrow[(size_t)i] = H.place == M_LDS || H.place == M_LDSG;
     if (H.place == M_LDS) {
       bcount[H.bucket]++;
       bmax[H.bucket] = std::max(bmax[H.bucket], H.lds);
@@ -324,7 +345,7 @@ void plan_chunk(Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0,
     std::copy(P.tmp.begin(), P.tmp.begin() + (int64_t)m, v);
   };
   // multi-wave launches first: the long-running large catalogs start earliest
-  for (int mode : {(int)M_SPLIT4, (int)M_SPLIT, (int)M_HBM}) {
+  for (int mode : {(int)M_LDSG, (int)M_SPLIT4, (int)M_SPLIT, (int)M_HBM}) {
     auto& bg = P.big[(size_t)mode];
     if (bg.empty()) continue;
     lpt(bg.data(), bg.size());
@@ -333,7 +354,10 @@ void plan_chunk(Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0,
     for (int32_t i : bg) {
       const int32_t* h = rec + rec_off[p0 + i];
       L.dev_lists |= h[DP_H_FMT] == DP_FMT_I32 && !dp::device_watches(h);
-      const Layout Y = mode == M_SPLIT ? layout<M_SPLIT>(h) : mode == M_SPLIT4 ? layout<M_SPLIT4>(h) : layout<M_HBM>(h);
+      const Layout Y = mode == M_SPLIT    ? layout<M_SPLIT>(h)
+                       : mode == M_SPLIT4 ? layout<M_SPLIT4>(h)
+                       : mode == M_LDSG   ? layout<M_LDSG>(h)
+                                          : layout<M_HBM>(h);
       mx = std::max(mx, Y.lds_bytes);
       if (P.scratch_words == 0) P.scratch_words = dp::kQueueWords;  // the launches' queues first
       P.scratch_off.push_back(P.scratch_words);
@@ -1420,14 +1444,16 @@ dp_ctx* dp_create(const dp_opts* opts) {
   }
   int first = opts ? opts->first_device : 0;
   int cnt = opts && opts->n_devices > 0 ? opts->n_devices : n - first;
-  if (first < 0 || cnt <= 0 || first + cnt > n) {
+  // (test) every logical device on first_device's GPU
+  const bool share = opts && (opts->flags & DP_OPT_SHARE_ORDINAL) && opts->n_devices > 0;
+  if (first < 0 || cnt <= 0 || (share ? first >= n || cnt > 8 : first + cnt > n)) {
     dp::set_global_error("dp_create: device range out of bounds");
     return nullptr;
   }
   auto* ctx = new dp_ctx;
   for (int i = 0; i < cnt; ++i) ctx->dev.emplace_back();
   for (int i = 0; i < cnt; ++i) {
-    const int d = first + i;
+    const int d = share ? first : first + i;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, d) != hipSuccess || std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
       dp::set_global_error(std::string("dp_create: device ") + std::to_string(d) + " is not gfx950 (" +
@@ -1626,6 +1652,15 @@ int dp_solve(dp_ctx* ctx, const dp_batch* b, dp_result* res) {
   dp_job* job = nullptr;
   if (dp_submit(ctx, b, res, &job)) return -1;
   return dp_job_wait(ctx, job);
+}
+
+int dp_get_device_stats(dp_ctx* ctx, int32_t device, dp_stats* out, int32_t reset) {
+  if (!ctx || !out || device < 0 || device >= (int32_t)ctx->dev.size()) return -1;
+  Device& D = ctx->dev[(size_t)device];
+  std::lock_guard<std::mutex> dl(D.smu);
+  *out = D.st;
+  if (reset) D.st = dp_stats{};
+  return 0;
 }
 
 int dp_get_stats(dp_ctx* ctx, dp_stats* out, int32_t reset) {

@@ -165,7 +165,9 @@ namespace {
 // VGPRs (an LDS counter per lane: 9).  The unbounded build counts them.
 template <int MODE, int MINW = 1>
 struct Group {
-  using IX = typename std::conditional<MODE == M_LDS, uint16_t, int32_t>::type;
+  // the 16-bit LDS image, the whole working set in LDS (M_LDS, M_LDSG)
+  static constexpr bool N16 = mode_n16(MODE);
+  using IX = typename std::conditional<N16, uint16_t, int32_t>::type;
   static constexpr bool NO_VIS = MODE == M_LDS && MINW > 1;
   static constexpr int NW = mode_waves(MODE);  // wavefronts per problem
   static constexpr int NT = 64 * NW;           // threads per problem
@@ -175,17 +177,17 @@ struct Group {
 
   // the lowest implying row per literal: 16-bit in LDS, 32-bit (global
   // atomics) in the multi-wave modes; IMP_NONE = no implication this round
-  static constexpr bool IMP16 = MODE == M_LDS && IMP16_LDS;
+  static constexpr bool IMP16 = N16 && IMP16_LDS;
   using IMP = typename std::conditional<IMP16, uint16_t, uint32_t>::type;
   static constexpr uint32_t IMP_NONE = IMP16 ? 0xffffu : (uint32_t)INF;
   // guess-stack flag: the choice was already satisfied by a guess (m = none)
-  static constexpr int G_SKIP = MODE == M_LDS ? 0x8000 : 0x40000000;
+  static constexpr int G_SKIP = N16 ? 0x8000 : 0x40000000;
 
   // IX <-> int for the signed values: reasons R_DEC (-1), R_EXTRA (-2) and
   // Solve() decision d (-3 - d); in 16 bits every value from dthr up is one of
   // them (fits16 keeps rows below and decisions above)
   __device__ __forceinline__ int dec(IX x) const {
-    if constexpr (MODE != M_LDS) return x;
+    if constexpr (!N16) return x;
     else return (int)x >= dthr ? (int)x - 0x10000 : (int)x;
   }
   __device__ __forceinline__ static IX enc(int x) { return (IX)x; }
@@ -195,7 +197,7 @@ struct Group {
   // load from another wavefront of the workgroup can hit a stale L1 line.
   // LDS words need no such care.
   __device__ __forceinline__ static uint32_t ld_imp(const IMP* p) {
-    if constexpr (MODE == M_LDS) return *p;
+    if constexpr (N16) return *p;
     else return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __device__ __forceinline__ static uint32_t ld_bits(const uint32_t* p) {
@@ -462,6 +464,9 @@ struct Group {
     const Layout L = layout<MODE>(h);
     const dp_rec_layout R = rec_layout(h);
     const ImgLayout X = img_layout(h);
+    // the group primitives' LDS words first (the decode's g_any uses them)
+    scal = reinterpret_cast<int32_t*>(lds + L.scal);
+    sbank = 0;
     ncl = h[DP_H_NCL]; nkl = h[DP_H_NKL]; nchl = h[DP_H_NCHL];
     nv = h[DP_H_NV]; nc = h[DP_H_NC]; nk = h[DP_H_NK]; nid = h[DP_H_NID]; na = h[DP_H_NA];
     nch = h[DP_H_NCH];
@@ -471,7 +476,7 @@ struct Group {
     bool packed = false;
     rowref = nullptr;
     rowspace = false;
-    if constexpr (MODE == M_LDS) {
+    if constexpr (N16) {
       // The record -> LDS, as it is: the host stages one-wavefront records in
       // a 16-bit form (DP_FMT_U16, or DP_FMT_P16 whose tail is decoded below),
       // 16-byte aligned and padded to 4 words.
@@ -483,19 +488,19 @@ struct Group {
       const int groups = packed ? (int)((p16_tail_at(h) + p16_tail_bytes(h) + 15) >> 4)
                                 : (h[DP_H_WORDS] - DP_H_SIZE + 7) >> 3;
       if (L.body == 0 && ((groups + 63) >> 6) * 1024 <= L.lds_bytes) {
-        // LDS-DMA, every 1 KiB piece in flight at once (lanes past the image
-        // re-read its last piece into LDS the later arrays own; they are
-        // initialised after this)
-        for (int c = 0; c < groups; c += 64) {
+        // LDS-DMA, every 1 KiB piece in flight at once, wavefront w taking
+        // pieces w, w + NW, ... (lanes past the image re-read its last piece
+        // into LDS the later arrays own; they are initialised after this)
+        for (int c = 64 * wid; c < groups; c += NT) {
           const int i = min(c + lane, groups - 1);
           __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src + i),
                                            (__attribute__((address_space(3))) void*)(lds + 16 * c), 16, 0, 0);
         }
         __builtin_amdgcn_s_waitcnt(0);
-        wsync();
+        gsync();
       } else {
         for (int i = tid; i < groups; i += NT) reinterpret_cast<int4*>(b)[i] = src[i];
-        wsync();
+        gsync();
       }
       body = b;
       if (packed) {
@@ -518,9 +523,13 @@ struct Group {
         idmask = reinterpret_cast<const uint32_t*>(q); q += 2 * nbi;
         idpc = reinterpret_cast<const uint16_t*>(q);   q += nbi + 1;
         rowspace = true;
-        if (!unpack16(reinterpret_cast<const char*>(b) + p16_tail_at(h), (int)p16_tail_bytes(h), derived,
-                      lds + L.reason, reinterpret_cast<uint8_t*>(b) + p16_tail_copy(h)))
-          return false;
+        // (one wavefront decodes; with several, the others wait at g_any's barrier)
+        bool ok = true;
+        if (wid == 0)
+          ok = unpack16(reinterpret_cast<const char*>(b) + p16_tail_at(h), (int)p16_tail_bytes(h), derived,
+                        lds + L.reason, reinterpret_cast<uint8_t*>(b) + p16_tail_copy(h));
+        if constexpr (NW > 1) ok = !g_any(!ok);
+        if (!ok) return false;
       }
     } else {
       body = reinterpret_cast<const IX*>(grec + DP_H_SIZE);  // read in place (read-only)
@@ -534,8 +543,8 @@ struct Group {
     }
     nwatch = h[DP_H_NCL] + h[DP_H_NKL];
     dthr = nrows + L_MAX;
-    char* hot = MODE == M_HBM ? hbm : lds;   // val and the bitsets
-    char* cold = MODE == M_LDS ? lds : hbm;  // per-literal arrays
+    char* hot = MODE == M_HBM ? hbm : lds;  // val and the bitsets
+    char* cold = N16 ? lds : hbm;           // per-literal arrays
     val = reinterpret_cast<int8_t*>(hot + L.val);
     reason = reinterpret_cast<IX*>(cold + L.reason);
     rs = reinterpret_cast<IX*>(cold + L.rs);
@@ -571,7 +580,6 @@ struct Group {
     stk = reinterpret_cast<IX*>(cold + L.stk);
     wbuf = reinterpret_cast<IX*>(lds + L.wbuf);
     cardq = reinterpret_cast<IX*>(lds + L.cardq);
-    scal = reinterpret_cast<int32_t*>(lds + L.scal);
     hkey = reinterpret_cast<int32_t*>(lds + L.hkey);
     hrp = reinterpret_cast<uint32_t*>(lds + L.hrp);
     hrn = reinterpret_cast<uint32_t*>(lds + L.hrn);
@@ -589,7 +597,6 @@ struct Group {
     pre_lo = -1;
     steps = 0;
     vis = 0;
-    sbank = 0;
     budget_hit = false;
     ck = CK_NONE; c_row = c_var = c_rp = c_rn = 0;
     collect_guess = false;
@@ -608,9 +615,9 @@ struct Group {
     const int64_t ti1 = stamp();
     sub[0] = ti1 - ti0;
 #endif
-    if constexpr (MODE == M_LDS)
+    if constexpr (N16)
       if ((h[DP_H_FMT] == DP_FMT_U16 || packed) && !valid_record(body, packed, h[DP_H_FMT] == DP_FMT_P16D)) return false;
-    if constexpr (MODE != M_LDS)
+    if constexpr (!N16)
       if ((h[DP_H_FMT] == DP_FMT_I32W || h[DP_H_FMT] == DP_FMT_I32) && !valid_wide(R, X, h[DP_H_FMT] == DP_FMT_I32W))
         return false;
 #ifdef DP_STAMPS
@@ -618,8 +625,8 @@ struct Group {
     sub[1] = ti2 - ti1;
 #endif
     // the watch lists follow the record (M_LDS) or live in the problem's
-    // scratch; M_LDS counts on the per-literal arrays, initialised below
-    if constexpr (MODE == M_LDS) {
+    // scratch; M_LDS / M_LDSG count on the per-literal arrays, initialised below
+    if constexpr (N16) {
       IX* wo = const_cast<IX*>(body) + lds_body_words(h);  // right after the decoded arrays
       build_watches(wo, wo + 2 * nv + 1, reinterpret_cast<uint32_t*>(lds + L.reason));
       w_off = wo; w = wo + 2 * nv + 1;
@@ -638,7 +645,7 @@ struct Group {
     sub[2] = stamp() - ti2;
 #endif
 
-    if constexpr (MODE == M_LDS) {
+    if constexpr (N16) {
       for (int v = tid; v < nv; v += NT) val[v] = 0;
     } else {
       for (int v = tid; v < (nv + 3) / 4; v += NT) reinterpret_cast<uint32_t*>(val)[v] = 0;
@@ -678,7 +685,7 @@ struct Group {
   // host checked every other staged form (DP_FMT_U16_CHECKED, DP_FMT_I32).
   // Array by array, two 16-bit words per LDS load.  Group-uniform result.
   __device__ __forceinline__ bool valid_record(const IX* base, bool packed, bool derived) {
-    static_assert(MODE == M_LDS, "16-bit records run one wavefront per problem");
+    static_assert(N16, "16-bit records run on the LDS image");
     // (base: the body's start, 16-byte aligned; arrays anywhere after it)
     const uint32_t* b32 = reinterpret_cast<const uint32_t*>(base);
     bool bad = false;
@@ -763,7 +770,7 @@ struct Group {
   // positions one run; w_off from 0, non-decreasing, within w; every listed
   // row a row.  Group-uniform result.
   __device__ __forceinline__ bool valid_wide(const dp_rec_layout& R, const ImgLayout& X, bool watches) {
-    static_assert(MODE != M_LDS, "the int32 form runs on multi-wave groups");
+    static_assert(!N16, "the int32 form runs on the HBM-read multi-wave groups");
     const int32_t* r = reinterpret_cast<const int32_t*>(clause_off) - R.clause_off;  // the record
     bool bad = false;
     // VU independent loads per thread and step, so a thread has that many in
@@ -845,7 +852,7 @@ struct Group {
   // `scratch` (the per-literal arrays' LDS, not yet in use) for the
   // dependency rows by rank, each list's row and the per-subject counts.
   __device__ __forceinline__ bool unpack16(const char* tail, int tb, bool derived, char* scratch, uint8_t* tcopy) {
-    static_assert(MODE == M_LDS, "16-bit records run one wavefront per problem");
+    static_assert(N16, "16-bit records run on the LDS image");
     {
       uint4 r = make_uint4(0u, 0u, 0u, 0u);
       if (16 * lane < tb) r = *reinterpret_cast<const uint4*>(tail + 16 * lane);
@@ -907,7 +914,7 @@ struct Group {
     IX* rowk = const_cast<IX*>(rowref);                      // [nch] each list's row (kept)
     uint32_t* cnt = reinterpret_cast<uint32_t*>(scratch + ((2 * nch + 15) & ~15));  // [nv + 1]
     IX* vco = const_cast<IX*>(var_choice_off);
-    for (int i = tid; i <= nv; i += NT) cnt[i] = 0u;
+    for (int i = lane; i <= nv; i += 64) cnt[i] = 0u;  // (one wavefront runs the decode)
     bool bad = false;
     int nd = 0;  // dependency rows
     for (int c = 0; c < nc; c += 64) {
@@ -999,7 +1006,7 @@ struct Group {
   // build_watches.  Ends with a draining barrier: every wavefront reads the
   // lists after it.
   __device__ __forceinline__ void build_watches_wide(IX* wo, int2* ww, uint32_t* cnt) {
-    static_assert(MODE != M_LDS, "one-wavefront problems build theirs in LDS");
+    static_assert(!N16, "LDS-image problems build theirs in LDS");
     const int n2 = 2 * nv + 1;
     for (int i = tid; i < n2; i += NT) cnt[i] = 0u;
     gsync();
@@ -1046,13 +1053,13 @@ struct Group {
   // OLM scale the counters live in HBM and the in-kernel build was
   // latency-bound, 4.7M cycles a catalog.)
   __device__ __forceinline__ void build_watches(IX* wo, IX* ww, uint32_t* cnt) {
-    static_assert(MODE == M_LDS, "the multi-wave modes read host-built watch lists");
+    static_assert(N16, "the HBM-read multi-wave modes build theirs in scratch");
     const int n2 = 2 * nv + 1;
 #ifdef DP_STAMPS
     const int64_t tb0 = stamp();
 #endif
     for (int i = tid; i < n2; i += NT) cnt[i] = 0u;
-    wsync();
+    gsync();
     // four positions per lane per step: the loads first, then the atomics
     // (one LDS round trip per step instead of one per position)
     for (int j0 = 0; j0 < ncl; j0 += 4 * NT) {
@@ -1078,16 +1085,16 @@ struct Group {
           if (j0 + i < b && v[i + 1] != v[i]) atomicAdd(&cnt[2 * v[i + 1] + 1], 1u);
       }
     }
-    wsync();
+    gsync();
 #ifdef DP_STAMPS
     const int64_t tb1 = stamp();
     sub[3] = tb1 - tb0;
 #endif
     // eight consecutive counters per lane (independent loads), their sum
     // scanned across the wave by DPP, then each lane's running prefix: one
-    // scan per 512 counters (a config-2 catalog has ~480)
+    // scan per 512 counters (a config-2 catalog has ~480); wavefront 0 scans
     int carry = 0;
-    for (int b = 0; b < n2; b += 8 * NT) {
+    for (int b = 0; b < (wid == 0 ? n2 : 0); b += 8 * 64) {
       const int i0 = b + 8 * lane;
       int x[8];
 #pragma unroll
@@ -1104,7 +1111,7 @@ struct Group {
       }
       carry += __builtin_amdgcn_readlane(incl, 63);
     }
-    wsync();
+    gsync();
 #ifdef DP_STAMPS
     const int64_t tb2 = stamp();
     sub[4] = tb2 - tb1;
@@ -1138,10 +1145,10 @@ struct Group {
           if (j0 + i < b && v[i + 1] != v[i]) ww[atomicAdd(&cnt[2 * v[i + 1]], 1u)] = enc(nc + k);
       }
     }
-    wsync();
+    gsync();
     if constexpr (TWLL) {  // the cursors end where each list's entries end
       for (int l = tid; l < 2 * nv; l += NT) wend16[l] = (uint16_t)cnt[l];
-      wsync();
+      gsync();
     }
 #ifdef DP_STAMPS
     sub[5] = stamp() - tb2;
@@ -1157,7 +1164,7 @@ struct Group {
   __device__ __forceinline__ bool row_on(int r) const { return !enabled || getb(enabled, row_key(r)); }
   // watch entry j: {row, row_info} (w8), or {row, ROW_INFO_NONE}
   __device__ __forceinline__ int2 went(int j) const {
-    if constexpr (MODE != M_LDS) {
+    if constexpr (!N16) {
       if (w8) return w8[j];
     }
     return make_int2((int)w[j], (int)ROW_INFO_NONE);
@@ -1422,7 +1429,7 @@ struct Group {
         return eval_clause_twl(r, clause_off[r], clause_off[r + 1], crow);
       }
     }
-    if constexpr (MODE != M_LDS) {
+    if constexpr (!N16) {
       if (r < nc && info != ROW_INFO_NONE) {
         const int a = (int)(info >> 8);
         return eval_clause(r, clause_lits, a, a + (int)(info & 255u), crow);
@@ -1501,7 +1508,7 @@ struct Group {
       }
       if (card && pos < CQ) {
         cardq[pos] = enc(r);
-        cardq[CQ + pos] = (IX)info;  // (IX = int32 here)
+        if constexpr (!N16) cardq[CQ + pos] = (IX)info;  // (IX = int32 here; M_LDSG entries carry no range)
       } else if (card) card_serial(r, crow);  // queue full: evaluate in-lane
       else if (ok) {
         const int ul = clause_unit(r, crow, info);
@@ -1702,7 +1709,7 @@ struct Group {
     for (int q = q0; q < ncq; q += qs) {
       const int r = DP_CHK((int)cardq[q], nc, nrows, 3), k = r - nc;
       int a, len;
-      const uint32_t info = NW > 1 ? (uint32_t)cardq[CQ + q] : ROW_INFO_NONE;
+      const uint32_t info = NW > 1 && !N16 ? (uint32_t)cardq[CQ + q] : ROW_INFO_NONE;
       if (info != ROW_INFO_NONE) {  // the range from the row's watch entry
         a = (int)(info >> 8);
         len = (int)(info & 255u);
@@ -2310,7 +2317,7 @@ struct Group {
   __device__ __forceinline__ bool violated(int c, int& fu, uint32_t info = ROW_INFO_NONE) const {
     fu = -1;
     int ja, jb;
-    if (MODE != M_LDS && info != ROW_INFO_NONE) {
+    if (!N16 && info != ROW_INFO_NONE) {
       ja = (int)(info >> 8);
       jb = ja + (int)(info & 255u);
     } else {
@@ -2795,8 +2802,8 @@ struct Group {
     for (int b = 0; b < nid; b += NT) {
       const int id = b + tid;
       const uint64_t m = __ballot(id < nid && getb(src, row_of(id)));
-      const int wd = b >> 5;
-      if (lane == 0) {
+      const int wd = (b + 64 * wid) >> 5;
+      if (lane == 0 && wd < nbi) {
         idt[wd] = (uint32_t)m;
         if (wd + 1 < nbi) idt[wd + 1] = (uint32_t)(m >> 32);
       }
@@ -3042,7 +3049,7 @@ __device__ __forceinline__ void solve_item(const KernelArgs& a, int k, int4* lds
   const int pid = it.pid;
   const int32_t* grec = a.rec + it.rec_off;
   Group<MODE, MINW> W;
-  char* hbm = MODE == M_LDS ? nullptr : reinterpret_cast<char*>(a.scratch + a.scratch_off[k]);
+  char* hbm = mode_n16(MODE) ? nullptr : reinterpret_cast<char*>(a.scratch + a.scratch_off[k]);
   if (!W.init(reinterpret_cast<char*>(lds4), hbm, grec)) {
     if (threadIdx.x == 0) {  // a malformed record: no solve (dp_rec_validate's verdict)
       put_out(a.out + pid, DP_ERROR, DP_F_MALFORMED, 0, 0, 0, 0);

@@ -11,11 +11,13 @@ hipError_t launch_lds_dense(const KernelArgs&, int, int, hipStream_t);
 hipError_t launch_split(const KernelArgs&, int, int, hipStream_t);
 hipError_t launch_split4(const KernelArgs&, int, int, hipStream_t);
 hipError_t launch_hbm(const KernelArgs&, int, int, hipStream_t);
+hipError_t launch_ldsg(const KernelArgs&, int, int, hipStream_t);
 hipError_t launch_lds_configure(int);
 hipError_t launch_lds_dense_configure(int);
 hipError_t launch_split_configure(int);
 hipError_t launch_split4_configure(int);
 hipError_t launch_hbm_configure(int);
+hipError_t launch_ldsg_configure(int);
 
 // The unbounded one-wavefront build runs 3 waves per SIMD (12 per CU).  A
 // launch whose footprint lets LDS hold more problems than that per CU takes
@@ -35,6 +37,7 @@ hipError_t launch_solve(const KernelArgs& a, int mode, int n_blocks, int lds_byt
   }
   if (mode == M_SPLIT) return launch_split(a, n_blocks, lds_bytes, stream);
   if (mode == M_SPLIT4) return launch_split4(a, n_blocks, lds_bytes, stream);
+  if (mode == M_LDSG) return launch_ldsg(a, n_blocks, lds_bytes, stream);
   return launch_hbm(a, n_blocks, lds_bytes, stream);
 }
 
@@ -44,6 +47,7 @@ hipError_t configure_solve_kernel(int max_lds_bytes) {
   if (e == hipSuccess) e = launch_split_configure(max_lds_bytes);
   if (e == hipSuccess) e = launch_split4_configure(max_lds_bytes);
   if (e == hipSuccess) e = launch_hbm_configure(max_lds_bytes);
+  if (e == hipSuccess) e = launch_ldsg_configure(max_lds_bytes);
   return e;
 }
 

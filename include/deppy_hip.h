@@ -323,15 +323,24 @@ typedef struct dp_opts {
 } dp_opts;
 
 /* Placement overrides (testing and measurement): by default a problem whose
- * working set fits a CU's LDS is solved by one wavefront out of LDS, and a
- * larger one by one multi-wave workgroup (per-variable state in LDS when it
- * fits, else in HBM).  These flags send every problem to a multi-wave path. */
+ * 16-bit working set is small is solved by one wavefront out of LDS, a
+ * mid-size one (up to a CU's LDS) by one multi-wave workgroup out of LDS,
+ * and a larger one by one multi-wave workgroup reading its record from HBM
+ * (per-variable state in LDS when it fits, else in HBM).  These flags send
+ * every problem to one of the multi-wave paths. */
 enum dp_opt_flag {
   DP_OPT_FORCE_GROUP = 1 << 0, /* every problem: multi-wave workgroup */
   DP_OPT_FORCE_HBM = 1 << 1,   /* every problem: multi-wave workgroup, state in HBM */
   DP_OPT_FORCE_MID = 1 << 2,   /* every problem: 4-wave workgroup (the mid-size path) */
-  DP_OPT_TINY_TABLE = 1 << 3   /* test: 4-slot round tables in the multi-wave modes, so rounds
+  DP_OPT_TINY_TABLE = 1 << 3,  /* test: 4-slot round tables in the multi-wave modes, so rounds
                                   overflow them and are redone on the HBM arrays */
+  DP_OPT_FORCE_LDSG = 1 << 4,  /* every problem whose 16-bit image fits a CU's LDS: the
+                                  multi-wave all-LDS workgroup (M_LDSG) */
+  DP_OPT_SHARE_ORDINAL = 1 << 5 /* test: the context's n_devices logical devices all run on
+                                  first_device's GPU (each with its own submitting thread,
+                                  host pool, lanes and streams), so the multi-device
+                                  dispatcher -- chunk cut, per-device workers, dp_partition
+                                  and result stitching -- runs on a one-GPU machine */
 };
 
 typedef struct dp_ctx dp_ctx;
@@ -425,6 +434,11 @@ typedef struct dp_stats {
                         serving loop's steady state makes none               */
 } dp_stats;
 int dp_get_stats(dp_ctx* ctx, dp_stats* out, int32_t reset);
+/* The share of dp_get_stats that logical device `device` (0 .. dp_num_devices
+ * - 1) ran through its submitting thread: its chunks, launches, kernel time
+ * and bytes (the pipeline's per-device split of a batch).  dp_get_stats with
+ * reset also resets these. */
+int dp_get_device_stats(dp_ctx* ctx, int32_t device, dp_stats* out, int32_t reset);
 
 /* Device-resident form (benchmarks, pipelines): the batch is partitioned over
  * the context's devices and copied once; dp_run solves it in place. */

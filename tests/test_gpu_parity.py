@@ -150,6 +150,24 @@ def test_multiwave_paths_bit_exact(config, n, seed, flags):
     assert bad == [], bad[:10]
 
 
+@pytest.mark.parametrize("form", ["i32", "u16", "packed"])
+@pytest.mark.parametrize("config,n,seed", [(2, 300, 141), (5, 150, 142), (3, 500, 143), (6, 300, 144)])
+def test_ldsg_paths_bit_exact(config, n, seed, form):
+    """The all-LDS multi-wave workgroup (M_LDSG, forced by DP_OPT_FORCE_LDSG)
+    on small catalogs, where the oracle is cheap: int32 records narrowed and
+    checked on the host, 16-bit records validated by the kernel, packed
+    records decoded by one wavefront -- every field bit-exact."""
+    lw = lowered_config(config, n, seed, narrow=form != "i32", packed=form == "packed")
+    c = _lib.Context(0, 1, flags=_lib.OPT_FORCE_LDSG)
+    try:
+        g = c.solve(lw.rec_off, lw.rec)
+    finally:
+        c.close()
+    o = oracle.solve_batch(lw.rec_off, lw.rec, 0, 16)
+    bad = compare_results(g, o, n)
+    assert bad == [], bad[:10]
+
+
 @pytest.mark.parametrize("flags", [_lib.OPT_FORCE_MID, _lib.OPT_FORCE_GROUP], ids=["split4", "split"])
 @pytest.mark.parametrize("config,n,seed", [(2, 200, 44), (5, 80, 45)])
 def test_round_table_overflow_bit_exact(config, n, seed, flags):
@@ -272,7 +290,7 @@ def test_jobs_in_flight_small_chunks(monkeypatch):
         assert compare_results(out, ref, b.n) == []
 
 
-@pytest.mark.parametrize("flags", [0, _lib.OPT_FORCE_GROUP], ids=["lds", "group"])
+@pytest.mark.parametrize("flags", [0, _lib.OPT_FORCE_GROUP, _lib.OPT_FORCE_LDSG], ids=["lds", "group", "ldsg"])
 def test_malformed_records_are_per_problem_errors(flags):
     """A malformed record yields DP_ERROR + DP_F_MALFORMED for that problem
     (found while narrowing on the host, or by the kernel's own validation)
@@ -329,8 +347,9 @@ def test_pinned_records_copied_directly(config, n, seed, monkeypatch):
     assert compare_results(g, o, n) == []
 
 
+@pytest.mark.parametrize("flags", [0, _lib.OPT_FORCE_LDSG], ids=["lds", "ldsg"])
 @pytest.mark.parametrize("pinned", [False, True], ids=["staged", "direct"])
-def test_malformed_16bit_records_found_by_the_kernel(pinned):
+def test_malformed_16bit_records_found_by_the_kernel(pinned, flags):
     """16-bit records the host passes through unread are validated by the
     kernel (Group::valid_record): each malformed one is DP_ERROR +
     DP_F_MALFORMED, the rest of the batch is solved bit-exactly."""
@@ -342,7 +361,7 @@ def test_malformed_16bit_records_found_by_the_kernel(pinned):
         if corrupt16(lw.rec_off, rec, p, kind):
             bad.append(p)
     assert len(bad) >= 3
-    c = _lib.Context(0, 1)
+    c = _lib.Context(0, 1, flags=flags)
     try:
         g = c.solve(lw.rec_off, rec)
         assert (c.stats()["direct_chunks"] > 0) == pinned
@@ -377,7 +396,8 @@ def test_packed_records_bit_exact(config, n, seed, flags):
     assert compare_results(gb, o, n) == []
 
 
-def test_malformed_packed_records_found_by_the_kernel():
+@pytest.mark.parametrize("flags", [0, _lib.OPT_FORCE_LDSG], ids=["lds", "ldsg"])
+def test_malformed_packed_records_found_by_the_kernel(flags):
     """Packed records are validated on the device: a wrong identity mask, row
     lengths that do not sum to the total, an out-of-range literal, dependency
     rows that no longer imply the header's choice lists (DP_FMT_P16D) ->
@@ -403,7 +423,7 @@ def test_malformed_packed_records_found_by_the_kernel():
             offs = np.concatenate([[0], np.cumsum(t[tail:tail + nc].astype(np.int64))])
             a = next(a for a, e in zip(offs[:-1], offs[1:]) if e - a >= 2 and u[a] & 1 and not np.any(u[a + 1:e] & 1))
             u[a] ^= 1
-    c = _lib.Context(0, 1)
+    c = _lib.Context(0, 1, flags=flags)
     try:
         g = c.solve(lw.rec_off, rec)
     finally:
@@ -469,6 +489,7 @@ def test_wide_records_direct_and_validated(monkeypatch):
     exact."""
     a = lowered_config(5, 120, 121)
     monkeypatch.setenv("DEPPY_HOST_WATCHES", "1")
+    monkeypatch.setenv("DEPPY_LDSG", "0")  # mid-size catalogs as HBM-read multi-wave records
     b = lowered_config(5, 120, 121, packed=True, pinned=True)
     wide = [p for p in range(b.n) if b.rec[b.rec_off[p] + 13] == 4]
     assert len(wide) >= 3
@@ -559,12 +580,13 @@ def test_config5_full_size_bit_exact(ctx):
     assert (g["status"] == -1).sum() > n // 4
 
 
-def test_plain_int32_multiwave_records_validated_by_the_kernel():
+def test_plain_int32_multiwave_records_validated_by_the_kernel(monkeypatch):
     """Multi-wave records of at most 2048 variables go to the device as plain
     int32 records (DP_FMT_I32) copied as they lie; the kernel checks them
     (valid_wide) before building their watch lists.  A clause literal past
     2nv, decreasing clause offsets and an AtMost variable past nv each give
     DP_ERROR + DP_F_MALFORMED for that problem only; the rest stay exact."""
+    monkeypatch.setenv("DEPPY_LDSG", "0")  # mid-size catalogs as HBM-read multi-wave records
     a = lowered_config(5, 160, 191)
     b = lowered_config(5, 160, 191, packed=True, pinned=True)
     plain = [p for p in range(b.n) if b.rec[b.rec_off[p] + 13] == 0]
@@ -623,12 +645,13 @@ def chain_catalog(n_vars, seed):
 
 @pytest.mark.parametrize("flags", [_lib.OPT_FORCE_GROUP, _lib.OPT_FORCE_MID, _lib.OPT_FORCE_HBM],
                          ids=["split", "split4", "hbm"])
-def test_device_watch_boundary_bit_exact(flags):
+def test_device_watch_boundary_bit_exact(flags, monkeypatch):
     """Catalogs of 2047, 2048 and 2049 variables on the multi-wave paths:
     up to 2048 the solving workgroup builds the watch lists (2nv+1 counters
     in the LDS work area), above it the grid-wide passes before the launch
     do (watch_build.hip).  Bit-exact with the oracle on both sides of the
     boundary."""
+    monkeypatch.setenv("DEPPY_LDSG", "0")  # (else these fit the all-LDS group, as 16-bit records)
     probs = [chain_catalog(nv, 7 + nv) for nv in (2047, 2048, 2049)]
     # page-locked plain int32 records on 16-byte boundaries, as dp_lower_into
     # emits multi-wave records: dp_submit copies them as they lie, so the
@@ -722,3 +745,35 @@ def test_multiwave_long_rows_bit_exact(n_vars, flags):
     o = oracle.solve_batch(lw.rec_off, lw.rec, 0, 3)
     assert compare_results(g, o, 3) == []
     assert (g["status"] != -2).all()
+
+
+@pytest.mark.parametrize("config,n,seed", [(2, 3000, 151), (5, 300, 152)])
+def test_multi_device_dispatcher_bit_exact(config, n, seed):
+    """The one-process multi-device topology the cgo shim ships
+    (dp_create(n_devices=2)): with DP_OPT_SHARE_ORDINAL both
+    logical devices run on GPU 0, so the chunk cut, the per-device submitting
+    threads and host pools, dp_partition of a resident batch and the result
+    stitching run on hardware.  Both devices run chunks, and every field is
+    bit-exact against the oracle on both the host-to-host and the resident
+    path (reference caller: pkg/solver/solver.go:42-47)."""
+    lw = lowered_config(config, n, seed, packed=True, pinned=True)
+    w = lowered_config(config, n, seed)
+    o = oracle.solve_batch(w.rec_off, w.rec, 0, 16)
+    c = _lib.Context(0, 2, flags=_lib.OPT_SHARE_ORDINAL)
+    try:
+        assert c.devices() == 2
+        c.stats(reset=True)
+        g = c.submit(lw.rec_off, lw.rec).wait()
+        per = [c.device_stats(d)["chunks"] for d in range(2)]
+        assert min(per) >= 1, per
+        assert sum(per) == c.stats()["chunks"]
+        r = c.upload(lw.rec_off, lw.rec)
+        try:
+            r.run()
+            gr = r.download()
+        finally:
+            r.free()
+    finally:
+        c.close()
+    assert compare_results(g, o, n) == []
+    assert compare_results(gr, o, n) == []
