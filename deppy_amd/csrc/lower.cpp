@@ -474,7 +474,7 @@ struct Lowerer {
   // diagnostic DEPPY_HOST_WATCHES=1: multi-wave records above DEV_WATCH_VARS
   // variables carry host-built watch lists (DP_FMT_I32W), as before round 3
   const bool host_watches;
-  const bool ldsg;  // placement.hpp ldsg_env(): mid-size 16-bit records run on M_LDSG
+  const int ldsg;  // placement.hpp ldsg_env()
   Lowerer(const dp_wire& wire, bool narrow16, bool packed16, bool host_lists)
       : w(wire), narrow(narrow16), packed(packed16), host_watches(host_lists), ldsg(ldsg_env()) {}
 

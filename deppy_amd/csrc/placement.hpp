@@ -35,20 +35,30 @@ inline bool one_wave(const int32_t* h) {
 }
 
 // The all-LDS multi-wave placement (M_LDSG) for 16-bit records past
-// group_above(); DEPPY_LDSG=0 (diagnostic, and tests of the HBM-read
-// multi-wave records) sends them to the HBM-read multi-wave groups as before
-// round 5.  Read once per lowering call and per planned chunk.
-inline bool ldsg_env() {
+// group_above() that fit one CU's LDS.  Alone, such a catalog solves ~25%
+// faster there than on the HBM-read 4-wave group (config 5's largest
+// catalogs: kernel median 0.127 vs 0.169 ms), but a workgroup holding a
+// whole CU's LDS keeps other launches off that CU: with many in flight,
+// config 5 runs 705-718k res/s host to host against 877-917k on the 4-wave
+// groups, which share CUs (profiles/r05_ldsg_ab.txt).  So the pipeline
+// places them on M_LDSG only when a chunk holds at most kLdsgMaxProblems of
+// them (a latency-bound chunk: each gets a CU), else on M_SPLIT4.
+// DEPPY_LDSG (diagnostic, and tests of the HBM-read multi-wave records):
+// 0 never, 1 always, unset/2 that rule.  Read once per lowering call and per
+// planned chunk.
+constexpr int32_t kLdsgMaxProblems = 256;  // MI355X CUs
+enum { LDSG_NEVER = 0, LDSG_ALWAYS = 1, LDSG_AUTO = 2 };
+inline int ldsg_env() {
   const char* e = std::getenv("DEPPY_LDSG");
-  return !(e && *e == '0');
+  return e && *e == '0' ? LDSG_NEVER : e && *e == '1' ? LDSG_ALWAYS : LDSG_AUTO;
 }
 // Does the record fit the M_LDSG working set (one CU's LDS)?
 inline bool ldsg_fits(const int32_t* h) { return fits16(h) && (int64_t)layout<M_LDSG>(h).lds_bytes <= kMaxLdsBytes; }
-// Does the record (well formed) run on its 16-bit LDS image, one wavefront
-// (M_LDS) or one multi-wave workgroup (M_LDSG; ldsg: ldsg_env()), without
-// DP_OPT_FORCE_* flags?  The lowering emits such records in a 16-bit form
-// (DP_LOWER_NARROW).
-inline bool lds_image(const int32_t* h, bool ldsg) { return one_wave(h) || (ldsg && ldsg_fits(h)); }
+// Does the lowering emit the record in a 16-bit form (DP_LOWER_NARROW)?
+// When it runs on one wavefront (M_LDS), or under DEPPY_LDSG=1 on M_LDSG; the
+// mid-size ones stay int32 otherwise (the pipeline narrows them itself for
+// an M_LDSG chunk).
+inline bool lds_image(const int32_t* h, int ldsg) { return one_wave(h) || (ldsg == LDSG_ALWAYS && ldsg_fits(h)); }
 
 // The watch lists of a multi-wave problem (layout.hpp img_layout), right
 // after its int32 record r: rows in ascending order in every list.  Returns

@@ -159,6 +159,7 @@ struct Launch {
 // chunk sit a record apart and every one is a cache miss).
 struct Head {
   int8_t place;   // -1 malformed, -2 too large, else the Mode
+  bool ldsg_ok;   // a mid-size 16-bit-able record the chunk may place on M_LDSG (plan_chunk)
   int8_t bucket;  // M_LDS: the LDS bucket (ceilings())
   // (M_LDSG problems are staged like M_LDS ones: `lds` is their M_LDSG footprint)
   bool direct;    // the record is its own staged form (16-bit, 16-byte aligned)
@@ -194,35 +195,38 @@ struct Plan {
   std::vector<int32_t> big[5], cnt, tmp, grp;
 };
 
-void read_head(Head& H, const int32_t* h, int64_t avail, int32_t opt_flags, bool aligned, bool ldsg) {
+// A mid-size record moved onto M_LDSG: staged (or copied) in 16-bit form.
+void place_ldsg(Head& H, const int32_t* h, bool aligned) {
+  H.lds = layout<M_LDSG>(h).lds_bytes;
+  H.sw = staged_words(h, true);
+  H.rec_bytes = dp_fmt_packed(h[DP_H_FMT]) ? 4 * dp_rec_phys_words(h)
+                                           : 4 * DP_H_SIZE + 2 * ((int64_t)h[DP_H_WORDS] - DP_H_SIZE);
+  H.place = M_LDSG;
+  H.direct = aligned && (h[DP_H_FMT] == DP_FMT_U16 || dp_fmt_packed(h[DP_H_FMT]));
+}
+
+void read_head(Head& H, const int32_t* h, int64_t avail, int32_t opt_flags, bool aligned) {
   H = Head{};
   if (!header_ok(h, avail)) { H.place = -1; return; }
   H.inst_words = bits_words(h[DP_H_NV]);
   H.nid = h[DP_H_NID];
   // lds_path, with the one-wavefront layout computed once; past
-  // group_above(), the all-LDS multi-wave group while the image fits a CU
-  bool nar = false, grp = false;
+  // group_above(), a record whose 16-bit image fits a CU may go to the
+  // all-LDS multi-wave group (ldsg_ok: plan_chunk decides per chunk;
+  // DP_OPT_FORCE_LDSG: always)
+  bool nar = false;
   if (dp::fits16(h)) {
     if (!forced_of(opt_flags)) {
       H.lds = layout<M_LDS>(h).lds_bytes;
       nar = H.lds <= dp::group_above();
     }
-    if (!nar && ((!forced_of(opt_flags) && ldsg) || (opt_flags & DP_OPT_FORCE_LDSG))) {
-      const int32_t g = layout<M_LDSG>(h).lds_bytes;
-      if (g <= kMaxLdsBytes) {
-        grp = true;
-        H.lds = g;
+    if (!nar && (!forced_of(opt_flags) || (opt_flags & DP_OPT_FORCE_LDSG)) && dp::ldsg_fits(h)) {
+      if (opt_flags & DP_OPT_FORCE_LDSG) {
+        place_ldsg(H, h, aligned);
+        return;
       }
+      H.ldsg_ok = true;
     }
-  }
-  if (grp) {
-    // the 16-bit image as for M_LDS, one queued multi-wave launch
-    H.sw = staged_words(h, true);
-    H.rec_bytes = dp_fmt_packed(h[DP_H_FMT]) ? 4 * dp_rec_phys_words(h)
-                                             : 4 * DP_H_SIZE + 2 * ((int64_t)h[DP_H_WORDS] - DP_H_SIZE);
-    H.place = M_LDSG;
-    H.direct = aligned && (h[DP_H_FMT] == DP_FMT_U16 || dp_fmt_packed(h[DP_H_FMT]));
-    return;
   }
   H.sw = staged_words(h, nar);
   // algorithmic input bytes (roofline.achieved): the record as the kernel
@@ -277,7 +281,6 @@ void plan_chunk(Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0,
   P.n_direct = 0;
   P.big_base = 0;
   Head* head = P.head.data();
-  const bool ldsg = dp::ldsg_env();
   auto rd = [&](int64_t i) {
     // every header is a cache miss: keep the next ones in flight
     if (i + 8 < n) {
@@ -286,10 +289,20 @@ void plan_chunk(Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0,
       __builtin_prefetch(h8 + 15);
     }
     read_head(head[i], rec + rec_off[p0 + i], rec_off[p0 + i + 1] - rec_off[p0 + i], opt_flags,
-              (rec_off[p0 + i] & 3) == 0, ldsg);
+              (rec_off[p0 + i] & 3) == 0);
   };
   if (pool && n > 256) pool->run(n, std::function<void(int64_t)>(rd), 64);
   else for (int32_t i = 0; i < n; ++i) rd(i);
+  // mid-size catalogs onto the all-LDS group when the chunk holds few of
+  // them (placement.hpp kLdsgMaxProblems), else the HBM-read 4-wave groups
+  {
+    const int lm = dp::ldsg_env();
+    int32_t n_ok = 0;
+    for (int32_t i = 0; i < n; ++i) n_ok += head[i].ldsg_ok;
+    if (n_ok > 0 && (lm == dp::LDSG_ALWAYS || (lm == dp::LDSG_AUTO && n_ok <= dp::kLdsgMaxProblems)))
+      for (int32_t i = 0; i < n; ++i)
+        if (head[i].ldsg_ok) place_ldsg(head[i], rec + rec_off[p0 + i], (rec_off[p0 + i] & 3) == 0);
+  }
   // one pass: offsets, totals and per-bucket counts / LDS maxima
   for (auto& v : P.big) v.clear();
   int32_t bcount[kNBuckets] = {}, bmax[kNBuckets] = {};

@@ -14,7 +14,7 @@ int main(int argc, char** argv) {
   dp::Pool pool(nt);
   auto secs = [](auto t0) { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
   std::vector<dp::Head> hd((size_t)n);
-  auto rd = [&](int64_t i) { dp::read_head(hd[(size_t)i], rec + ro[i], ro[i + 1] - ro[i], 0, true, true); };
+  auto rd = [&](int64_t i) { dp::read_head(hd[(size_t)i], rec + ro[i], ro[i + 1] - ro[i], 0, true); };
   auto t0 = std::chrono::steady_clock::now();
   for (int r = 0; r < reps; ++r) pool.run(n, std::function<void(int64_t)>(rd), 64);
   const double th = secs(t0);
