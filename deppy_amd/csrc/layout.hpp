@@ -240,6 +240,20 @@ __host__ __device__ inline uint32_t row_info(int32_t a, int32_t len) {
   return a >= 0 && a < (1 << 24) && len >= 0 && len < 255 ? ((uint32_t)a << 8) | (uint32_t)len : ROW_INFO_NONE;
 }
 
+// Bytes per entry of the watch lists the device builds for a multi-wave
+// record (Layout::wl): 2 (the row id alone) when every row id fits 16 bits,
+// else 8 ({row, row_info(row)}, the row's literal range carried in the
+// entry).  The 2-byte entries cost a visit one more dependent read (the
+// row's offsets) but shrink an OLM-scale catalog's lists from ~2.1 MB to
+// ~0.5 MB, so its whole BCP working set (offsets, entries, row literals)
+// fits one XCD's 4 MB L2.  -DDP_WENT=8 keeps the 8-byte entries (A/B).
+#ifndef DP_WENT
+#define DP_WENT 2
+#endif
+__host__ __device__ inline int32_t went_bytes(const int32_t* h) {
+  return DP_WENT == 2 && (int64_t)h[DP_H_NC] + h[DP_H_NK] <= 65535 ? 2 : 8;
+}
+
 struct ImgLayout {
   int32_t w_off, w, words;
 };
@@ -286,6 +300,7 @@ struct Layout {
   int32_t used;      // bits[nid] identities met by a refutation                   [LDS unless M_HBM]
   int32_t en;        // bits[nid] identities enabled (core search)                 [LDS unless M_HBM]
   int32_t en2;       // bits[nid]                                                  [LDS unless M_HBM]
+  int32_t crit;      // bits[nid] identities proven necessary by a core's model rotation [LDS unless M_HBM]
   int32_t idt;       // (M_LDS / M_LDSG) bits[nid] rows -> identities for the outputs (row_of)  [LDS]
   int32_t l_off;     // IX[L_MAX+1] learned rows (rows nrows..)
   int32_t l_lits;    // IX[lcap]
@@ -306,7 +321,7 @@ struct Layout {
   int32_t wp;        // (mode_rowslot) i32[8][nc] row slots {watch x, watch y, len, l0 | offset, l1..l4};
                      // else (mode_2wl) u64[nc] the two literals clause row r watches, low word first
   int32_t wl;        // multi-wave, DP_FMT_I32 records: device-built w_off[2nv+2], then
-                     // int2[ncl+nkl] entries {row, row_info} (8-byte aligned)  [HBM, last]
+                     // [ncl+nkl] entries: u16 rows, or int2 {row, row_info} (went_bytes)  [HBM]
   int32_t wpos;      // (mode_twl_lds) u8[2nc] watched positions of each clause row
   int32_t wend;      // (mode_twl_lds) u16[2nv] live end of each literal's watch list
   int32_t wfi;       // (mode_twl_lds) u8[wbuf] frontier literal of each flattened work-list entry
@@ -392,6 +407,7 @@ __host__ __device__ inline Layout layout(const int32_t* h) {
   L.used = take(nbi * 4, HOT);
   L.en = take(nbi * 4, HOT);
   L.en2 = take(nbi * 4, HOT);
+  L.crit = take(nbi * 4, HOT);
   L.idt = N16 ? take(nbi * 4, HOT) : 0;
   L.reason = take(nv * ix, COLD);
   L.rs = take(nv * ix, COLD);
@@ -404,7 +420,8 @@ __host__ __device__ inline Layout layout(const int32_t* h) {
   L.dq = take(2 * L.cap * ix, COLD);
   L.stk = take(3 * L.cap * ix, COLD);
   L.wp = mode_rowslot(MODE) ? take(h[DP_H_NC] * 32, COLD) : mode_2wl(MODE) ? take(h[DP_H_NC] * 8, COLD) : 0;
-  L.wl = !N16 && h[DP_H_FMT] == DP_FMT_I32 ? take((2 * nv + 2) * 4 + (h[DP_H_NCL] + h[DP_H_NKL]) * 8, COLD) : 0;
+  L.wl = !N16 && h[DP_H_FMT] == DP_FMT_I32
+             ? take((2 * nv + 2) * 4 + (h[DP_H_NCL] + h[DP_H_NKL]) * went_bytes(h), COLD) : 0;
   L.wpos = mode_twl_lds(MODE) ? take(2 * h[DP_H_NC], COLD) : 0;
   L.wend = mode_twl_lds(MODE) ? take(4 * nv, COLD) : 0;
   L.wfi = mode_twl_lds(MODE) ? take(mode_wbuf(MODE), COLD) : 0;

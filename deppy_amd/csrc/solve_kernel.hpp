@@ -239,6 +239,7 @@ struct Group {
   // reading its offsets (one dependent HBM read less per row; w is unused).
   // nullptr: 4-byte row entries in w.
   const int2* w8;
+  const uint16_t* w16;  // 2-byte entries (layout.hpp went_bytes): the row alone
   int nwatch, dthr;
   // BCP-visited bytes (this thread): the watch entries, row offsets, row
   // literals and their values that propagation reads
@@ -275,7 +276,7 @@ struct Group {
   __device__ __forceinline__ bool twl_dyn(int len) const {
     return TWLL && twl_on && len >= TWL_MIN_LEN && len <= TWL_MAX_LEN;
   }
-  uint32_t *d_flip, *inS, *extra, *seen, *model, *used, *en, *en2, *dset, *fg;
+  uint32_t *d_flip, *inS, *extra, *seen, *model, *used, *en, *en2, *crit, *dset, *fg;
   IX *wbuf, *cardq;
   int32_t* scal;
   // LDS round state (mode_lds_rounds; layout.hpp Layout::hkey..fr)
@@ -554,6 +555,7 @@ struct Group {
     imp = reinterpret_cast<IMP*>(cold + L.imp);
     wpair = reinterpret_cast<uint64_t*>(cold + L.wp);
     w8 = nullptr;
+    w16 = nullptr;
     sweep = false;
     twl_on = false;
     if constexpr (TWLL) {
@@ -573,6 +575,7 @@ struct Group {
     used = reinterpret_cast<uint32_t*>(hot + L.used);
     en = reinterpret_cast<uint32_t*>(hot + L.en);
     en2 = reinterpret_cast<uint32_t*>(hot + L.en2);
+    crit = reinterpret_cast<uint32_t*>(hot + L.crit);
     idt = reinterpret_cast<uint32_t*>(lds + L.idt);
     l_off = reinterpret_cast<IX*>(cold + L.l_off);
     l_lits = reinterpret_cast<IX*>(cold + L.l_lits);
@@ -633,10 +636,12 @@ struct Group {
     } else {
       if (h[DP_H_FMT] == DP_FMT_I32) {  // plain int32 record: the lists in scratch (layout.hpp wl)
         IX* wo = reinterpret_cast<IX*>(hbm + L.wl);
-        int2* we = reinterpret_cast<int2*>(wo + 2 * nv + 2);
-        if (device_watches(h)) build_watches_wide(wo, we, reinterpret_cast<uint32_t*>(lds + L.wbuf));
+        const bool e2 = went_bytes(h) == 2;
+        if (device_watches(h)) build_watches_wide(wo, wo + 2 * nv + 2, e2, reinterpret_cast<uint32_t*>(lds + L.wbuf));
         // (else built by the passes before this launch, watch_build.hip)
-        w_off = wo; w = nullptr; w8 = we;
+        w_off = wo; w = nullptr;
+        if (e2) w16 = reinterpret_cast<const uint16_t*>(wo + 2 * nv + 2);
+        else w8 = reinterpret_cast<const int2*>(wo + 2 * nv + 2);
       } else {
         w_off = rv(X.w_off); w = rv(X.w);  // host-built, staged after the record
       }
@@ -1005,7 +1010,7 @@ struct Group {
   // cursors.  Row order within a list is left to the atomics, as in
   // build_watches.  Ends with a draining barrier: every wavefront reads the
   // lists after it.
-  __device__ __forceinline__ void build_watches_wide(IX* wo, int2* ww, uint32_t* cnt) {
+  __device__ __forceinline__ void build_watches_wide(IX* wo, IX* wlist, bool e2, uint32_t* cnt) {
     static_assert(!N16, "LDS-image problems build theirs in LDS");
     const int n2 = 2 * nv + 1;
     for (int i = tid; i < n2; i += NT) cnt[i] = 0u;
@@ -1026,16 +1031,20 @@ struct Group {
       }
     }
     gsync();
+    int2* ww = reinterpret_cast<int2*>(wlist);
+    uint16_t* w2 = reinterpret_cast<uint16_t*>(wlist);
+    auto put = [&](uint32_t at, int row, int a, int len) {
+      if (e2) w2[at] = (uint16_t)row;
+      else ww[at] = make_int2(row, (int)row_info(a, len));
+    };
     for (int r = tid; r < nc; r += NT) {
       const int a = clause_off[r], b = clause_off[r + 1];
-      const int2 e = make_int2(r, (int)row_info(a, b - a));
-      for (int j = a; j < b; ++j) ww[atomicAdd(&cnt[(int)clause_lits[j] ^ 1], 1u)] = e;
+      for (int j = a; j < b; ++j) put(atomicAdd(&cnt[(int)clause_lits[j] ^ 1], 1u), r, a, b - a);
     }
     for (int k = tid; k < nk; k += NT) {
       const int a = card_off[k], b = card_off[k + 1];
-      const int2 e = make_int2(nc + k, (int)row_info(a, b - a));
       for (int j = a; j < b; ++j)
-        if (j == a || card_lits[j] != card_lits[j - 1]) ww[atomicAdd(&cnt[2 * (int)card_lits[j]], 1u)] = e;
+        if (j == a || card_lits[j] != card_lits[j - 1]) put(atomicAdd(&cnt[2 * (int)card_lits[j]], 1u), nc + k, a, b - a);
     }
     bar();  // (drains the lists' stores)
   }
@@ -1165,6 +1174,7 @@ struct Group {
   // watch entry j: {row, row_info} (w8), or {row, ROW_INFO_NONE}
   __device__ __forceinline__ int2 went(int j) const {
     if constexpr (!N16) {
+      if (w16) return make_int2((int)w16[j], (int)ROW_INFO_NONE);
       if (w8) return w8[j];
     }
     return make_int2((int)w[j], (int)ROW_INFO_NONE);
@@ -2885,6 +2895,122 @@ struct Group {
     return r;
   }
 
+  // ---- recursive model rotation (oracle: rotate) ----
+  // A refutation of K \ {c} that finds a model proves c necessary; flipping
+  // one variable of c's row in that model and leaving exactly one other key
+  // c' of K violated proves c' necessary too, without a refutation, and the
+  // walk continues from that model.  Keys owning exactly one row only; depth
+  // first over the row's positions in order; frames below the top in the
+  // round work list (wbuf, free outside rounds), at most ROT_DEPTH.  The
+  // working model is `extra` (free when the solve is UNSAT), K is `en`.
+  static constexpr int ROT_DEPTH = 32;
+  static_assert(3 * ROT_DEPTH <= WBUF, "rotation frames fit the work list");
+  // Is row r violated by the working model?
+  __device__ __forceinline__ bool row_viol_m(int r) const {
+    if (r < nc) {
+      for (int j = clause_off[r]; j < (int)clause_off[r + 1]; ++j) {
+        const int l = clause_lits[j];
+        if ((int)getb(extra, l >> 1) != (l & 1)) return false;  // a true literal
+      }
+      return true;
+    }
+    const int k = r - nc;
+    int cnt = 0;
+    for (int j = card_off[k]; j < (int)card_off[k + 1]; ++j) cnt += (int)getb(extra, card_lits[j]);
+    return cnt > (int)card_bound[k];
+  }
+  // the one row of key c, or -1 (none or several; packed records: the row)
+  __device__ __forceinline__ int single_row_of(int c) {
+    if (rowspace) return c;
+    int n = 0, first = INF;
+    for (int r0 = 0; r0 < nrows; r0 += NT) {
+      const int r = r0 + tid;
+      if (r < nrows && row_ident(r) == c) { ++n; first = min(first, r); }
+    }
+    n = g_sum(n);
+    first = g_min(first);
+    return n == 1 ? first : -1;
+  }
+  // the variable at position t of row r, or -1 past its end
+  __device__ __forceinline__ int row_var(int r, int t) const {
+    const int a = r < nc ? (int)clause_off[r] : (int)card_off[r - nc];
+    const int b = r < nc ? (int)clause_off[r + 1] : (int)card_off[r - nc + 1];
+    if (a + t >= b) return -1;
+    return r < nc ? (int)clause_lits[a + t] >> 1 : (int)card_lits[a + t];
+  }
+  __device__ __forceinline__ bool row_has(int r, int v) const {
+    for (int t = 0;; ++t) {
+      const int x = row_var(r, t);
+      if (x < 0) return false;
+      if (x == v) return true;
+    }
+  }
+  __device__ __forceinline__ void flip_m(int v) {
+    gsync();
+    if (tid == 0) extra[v >> 5] ^= 1u << (v & 31);
+    gsync();
+  }
+  // The one key of K violated among the rows holding v, or -1 (none or
+  // several): the rows in v's two watch lists (every clause holding v or ~v,
+  // every AtMost row holding v), or a scan of all rows when the lists are
+  // two-watched.
+  __device__ __forceinline__ int viol_key(int v) {
+    int lo = INF, hi = -1;
+    auto one = [&](int r) {
+      if (r < 0 || r >= nrows) return;
+      const int k = row_key(r);
+      if (!getb(en, k) || !row_viol_m(r)) return;
+      lo = min(lo, k);
+      hi = max(hi, k);
+    };
+    if (TWLL && twl_on) {
+      for (int r0 = 0; r0 < nrows; r0 += NT) {
+        const int r = r0 + tid;
+        if (r < nrows && row_has(r, v)) one(r);
+      }
+    } else {
+      const int a = w_off[2 * v], b = w_off[2 * v + 2];
+      for (int j0 = a; j0 < b; j0 += NT) {
+        const int j = j0 + tid;
+        if (j < b) one(went(j).x);
+      }
+    }
+    lo = g_min(lo);
+    hi = -g_min(-hi);
+    return lo == hi ? lo : -1;
+  }
+  __device__ __forceinline__ void rotate(int c0) {
+    int r = single_row_of(c0);
+    if (r < 0) return;
+    int c = c0, t = 0, d = 1;
+    IX* st = wbuf;  // frames 0 .. d-2 as (key, row, next position); the top in registers
+    for (;;) {
+      const int v = row_var(r, t);
+      if (v < 0) {  // the frame is done: back to its parent, undoing the flip that opened it
+        if (--d == 0) break;
+        gsync();
+        c = st[3 * (d - 1)]; r = st[3 * (d - 1) + 1]; t = st[3 * (d - 1) + 2];
+        flip_m(row_var(r, t - 1));
+        continue;
+      }
+      ++t;
+      flip_m(v);
+      const int k = viol_key(v);
+      bool opened = false;
+      if (k >= 0 && k != c && !getb(crit, k)) {
+        if (tid == 0) crit[k >> 5] |= 1u << (k & 31);
+        const int rn = single_row_of(k);
+        if (d < ROT_DEPTH && rn >= 0) {  // continue from this model (v stays flipped)
+          if (tid == 0) { st[3 * (d - 1)] = enc(c); st[3 * (d - 1) + 1] = enc(r); st[3 * (d - 1) + 2] = enc(t); }
+          c = k; r = rn; t = 0; ++d;
+          opened = true;
+        }
+      }
+      if (!opened) flip_m(v);
+    }
+    gsync();
+  }
+
   // thread 0's x in every thread
   __device__ __forceinline__ int g_bcast0(int x) {
     if constexpr (NW == 1) {
@@ -2904,17 +3030,20 @@ struct Group {
     // base conflict, or the search's union), an unsatisfiable set: no fresh
     // refutation of the whole catalog (oracle: core_extract)
     copy_bits(en, used, nid);
+    fill_bits(crit, nid, false);
     int any = 0;
     for (int i = tid; i < nbi; i += NT) any |= en[i] != 0u;
     int r = g_any(any) ? RS_UNSAT : RS_BUDGET;
     if (r == RS_UNSAT) {
       // identities in ascending order (rowspace: through their rows, with
-      // the set mirrored over identities in idt for the empty-word skip)
+      // the set mirrored over identities in idt for the empty-word skip);
+      // one proven necessary by a model (crit) stays without a refutation
       const uint32_t* ids = to_idents(en);
       for (int id = 0; id < nid; ++id) {
         if ((id & 31) == 0 && ids[id >> 5] == 0) { id += 31; continue; }  // empty word
         if (!getb(ids, id)) continue;
         const int key = rowspace ? row_of(id) : id;
+        if (getb(crit, key)) continue;
         copy_bits(en2, en, nid);
         if (tid == 0) en2[key >> 5] &= ~(1u << (key & 31));
         gsync();
@@ -2925,6 +3054,10 @@ struct Group {
         } else if (r == RS_BUDGET) {
           flags |= DP_F_CORE_BUDGET;
           break;
+        } else {  // a model of K \ {key}: key is necessary, and the model's rotations find others
+          if (tid == 0) crit[key >> 5] |= 1u << (key & 31);
+          copy_bits(extra, model, nv);
+          rotate(key);
         }
       }
       int c = 0;

@@ -11,9 +11,9 @@
 //          positive l the AtMost rows holding var(l), once per distinct
 //          variable; the same rows as build_watches_host),
 //   scan   the counts into list offsets (one workgroup per record),
-//   fill   the lists through the offsets as cursors: 8-byte entries {row,
-//          row_info(row)} (layout.hpp), so a round reads a row's literals
-//          straight from its entry.
+//   fill   the lists through the offsets as cursors: 2-byte entries (the
+//          row) when every row id fits 16 bits, else 8-byte entries {row,
+//          row_info(row)} (layout.hpp went_bytes).
 // Counts go to wo[l + 2] and cursors run on wo[l + 1], so when the fill ends
 // wo[l] is the start of list l (wo[2nv] their total) with no pass to shift
 // the offsets back.  Row order within a list is left to the atomics, as in
@@ -37,8 +37,9 @@ constexpr int kScanThreads = 1024;  // one scan workgroup per record
 
 struct WbRec {
   const int32_t* h;
-  int32_t* wo;  // [2nv + 2] counters / offsets, then the lists: int2[ncl + nkl] {row, row_info}
+  int32_t* wo;  // [2nv + 2] counters / offsets, then the lists: [ncl + nkl] u16 rows or int2 {row, row_info}
   dp_rec_layout R;
+  bool e2;      // 2-byte entries (layout.hpp went_bytes)
 };
 
 // Item k of the launch, when its lists are built by these passes.
@@ -48,6 +49,7 @@ __device__ __forceinline__ bool wb_rec(const KernelArgs& a, int k, WbRec& x) {
   if (h[DP_H_FMT] != DP_FMT_I32 || device_watches(h)) return false;
   x.h = h;
   x.R = rec_layout(h);
+  x.e2 = went_bytes(h) == 2;
   x.wo = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(a.scratch + a.scratch_off[k]) + layout<MODE>(h).wl);
   return true;
 }
@@ -77,7 +79,13 @@ __global__ __launch_bounds__(kWbThreads) void wb_rows(KernelArgs a) {
   const int32_t* kl = h + x.R.card_lits;
   int32_t* wo = x.wo;
   int2* ww = reinterpret_cast<int2*>(wo + 2 * nv + 2);
+  uint16_t* w2 = reinterpret_cast<uint16_t*>(wo + 2 * nv + 2);
   const unsigned cap = (unsigned)(ncl + nkl), nl = (unsigned)(2 * nv);
+  auto put = [&](unsigned at, int2 e) {
+    if (at >= cap) return;
+    if (x.e2) w2[at] = (uint16_t)e.x;
+    else ww[at] = e;
+  };
   const int t = s * kWbThreads + (int)threadIdx.x, T = kWbSlices * kWbThreads;
   for (int r = t; r < nc; r += T) {
     const int b0 = co[r], b1 = co[r + 1];
@@ -87,8 +95,7 @@ __global__ __launch_bounds__(kWbThreads) void wb_rows(KernelArgs a) {
       const int l = cl[j] ^ 1;  // the literal whose assignment falsifies position j
       if ((unsigned)l >= nl) continue;
       if constexpr (FILL) {
-        const unsigned at = (unsigned)atomicAdd(&wo[l + 1], 1);
-        if (at < cap) ww[at] = e;
+        put((unsigned)atomicAdd(&wo[l + 1], 1), e);
       } else {
         atomicAdd(&wo[l + 2], 1);
       }
@@ -102,8 +109,7 @@ __global__ __launch_bounds__(kWbThreads) void wb_rows(KernelArgs a) {
       const int v = kl[j];
       if ((j > b0 && v == kl[j - 1]) || (unsigned)v >= (unsigned)nv) continue;
       if constexpr (FILL) {
-        const unsigned at = (unsigned)atomicAdd(&wo[2 * v + 1], 1);
-        if (at < cap) ww[at] = e;
+        put((unsigned)atomicAdd(&wo[2 * v + 1], 1), e);
       } else {
         atomicAdd(&wo[2 * v + 2], 1);
       }

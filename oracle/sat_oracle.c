@@ -971,10 +971,131 @@ static int refute(st_t* s, const uint8_t* en) {
   return r;
 }
 
+/* Recursive model rotation (Marques-Silva & Lynce's MUS technique), the walk
+ * the kernel makes (solve_kernel.hpp Group::rotate).  A refutation of K \ {c}
+ * that finds a model m proves c necessary: m satisfies every identity of K
+ * but c.  Flipping one variable of c's row in m and leaving exactly one
+ * other identity c' of K violated proves c' necessary the same way, without
+ * a refutation; the walk continues from that model.  Only identities that
+ * own exactly one row are rotated (their row holds every flipped variable,
+ * so the rows that can change are the flipped variable's occurrences).
+ * Depth first, positions of the row in order, an explicit stack of at most
+ * ROT_DEPTH frames (a necessary identity found below it is marked, not
+ * explored).  Criticality only grows as K shrinks (a subset of a satisfiable
+ * set is satisfiable), so the deletion pass below ends on the same core as
+ * without rotation; only the refutations it skips (and their steps) go. */
+enum { ROT_DEPTH = 32 };
+
+static int mval(const uint32_t* m, int v) { return (int)((m[v >> 5] >> (v & 31)) & 1u); }
+
+/* Is row r violated by the total assignment m? */
+static int row_violated(const prob_t* p, const uint32_t* m, int r) {
+  if (r < p->nc) {
+    for (int j = p->clause_off[r]; j < p->clause_off[r + 1]; ++j) {
+      const int l = p->clause_lits[j];
+      if (mval(m, l >> 1) != (l & 1)) return 0; /* a true literal */
+    }
+    return 1;
+  }
+  const int k = r - p->nc;
+  int cnt = 0;
+  for (int j = p->card_off[k]; j < p->card_off[k + 1]; ++j) cnt += mval(m, p->card_lits[j]);
+  return cnt > p->card_bound[k];
+}
+
+/* The single row of identity c, or -1 (none, or several). */
+static int single_row(const prob_t* p, int c) {
+  int row = -1, n = 0;
+  for (int r = 0; r < p->nrows; ++r)
+    if (row_ident(p, r) == c && n++ == 0) row = r;
+  return n == 1 ? row : -1;
+}
+
+typedef struct {
+  int32_t *off, *rows; /* rows holding variable v: rows[off[v] .. off[v + 1]) */
+} occ_t;
+
+static void occ_build(const prob_t* p, occ_t* o) {
+  o->off = xcalloc((size_t)p->nv + 1, sizeof(int32_t));
+  int32_t* last = xcalloc((size_t)p->nv, sizeof(int32_t));
+  for (int v = 0; v < p->nv; ++v) last[v] = -1;
+  for (int pass = 0; pass < 2; ++pass) {
+    for (int v = 0; v < p->nv; ++v) last[v] = -1;
+    for (int r = 0; r < p->nrows; ++r) {
+      const int a = r < p->nc ? p->clause_off[r] : p->card_off[r - p->nc];
+      const int b = r < p->nc ? p->clause_off[r + 1] : p->card_off[r - p->nc + 1];
+      for (int j = a; j < b; ++j) {
+        const int v = r < p->nc ? p->clause_lits[j] >> 1 : p->card_lits[j];
+        if (last[v] == r) continue;
+        last[v] = r;
+        if (pass == 0) o->off[v + 1]++;
+        else o->rows[o->off[v]++] = r;
+      }
+    }
+    if (pass == 0) {
+      for (int v = 0; v < p->nv; ++v) o->off[v + 1] += o->off[v];
+      o->rows = xcalloc((size_t)o->off[p->nv], sizeof(int32_t));
+    } else {
+      for (int v = p->nv; v > 0; --v) o->off[v] = o->off[v - 1];
+      o->off[0] = 0;
+    }
+  }
+  free(last);
+}
+
+/* m (a model of K \ {c0}) rotated from identity c0; crit marks the
+ * identities proven necessary. */
+static void rotate(const prob_t* p, const occ_t* o, uint32_t* m, int c0, const uint8_t* K, uint8_t* crit) {
+  int fc[ROT_DEPTH], fr[ROT_DEPTH], ft[ROT_DEPTH], d = 0;
+  const int r0 = single_row(p, c0);
+  if (r0 < 0) return;
+  fc[0] = c0; fr[0] = r0; ft[0] = 0; d = 1;
+  while (d > 0) {
+    const int r = fr[d - 1], t = ft[d - 1];
+    const int a = r < p->nc ? p->clause_off[r] : p->card_off[r - p->nc];
+    const int b = r < p->nc ? p->clause_off[r + 1] : p->card_off[r - p->nc + 1];
+    if (a + t >= b) { /* frame done: undo the flip that opened it */
+      if (--d > 0) {
+        const int pr = fr[d - 1], pj = (pr < p->nc ? p->clause_off[pr] : p->card_off[pr - p->nc]) + ft[d - 1] - 1;
+        const int pv = pr < p->nc ? p->clause_lits[pj] >> 1 : p->card_lits[pj];
+        m[pv >> 5] ^= 1u << (pv & 31);
+      }
+      continue;
+    }
+    ft[d - 1] = t + 1;
+    const int v = r < p->nc ? p->clause_lits[a + t] >> 1 : p->card_lits[a + t];
+    m[v >> 5] ^= 1u << (v & 31);
+    /* the violated identities of K among the rows holding v (the others
+     * keep their values): exactly one, not the frame's own? */
+    int lo = INT32_MAX, hi = -1;
+    for (int q = o->off[v]; q < o->off[v + 1]; ++q) {
+      const int rr = o->rows[q], id = row_ident(p, rr);
+      if (!K[id] || !row_violated(p, m, rr)) continue;
+      lo = id < lo ? id : lo;
+      hi = id > hi ? id : hi;
+    }
+    const int c = fc[d - 1];
+    int opened = 0;
+    if (lo == hi && lo != c && !crit[lo]) {
+      crit[lo] = 1;
+      const int rn = single_row(p, lo);
+      if (d < ROT_DEPTH && rn >= 0) { /* continue from this model (v stays flipped) */
+        fc[d] = lo; fr[d] = rn; ft[d] = 0; ++d;
+        opened = 1;
+      }
+    }
+    if (!opened) m[v >> 5] ^= 1u << (v & 31);
+  }
+}
+
 static int core_extract(st_t* s, int32_t* core, int32_t* flags) {
   int nid = s->p.nid, len = 0;
   uint8_t* K = xcalloc((size_t)nid, 1);
   uint8_t* K2 = xcalloc((size_t)nid, 1);
+  uint8_t* crit = xcalloc((size_t)nid, 1);
+  const int nw = (s->p.nv + 31) / 32;
+  uint32_t* m = xcalloc((size_t)nw + 1, 4);
+  occ_t occ = {NULL, NULL};
   int64_t saved_steps = s->steps;
   s->steps = 0; /* the explanation has its own budget */
   /* start from the identities of the solve's own refutation (used[]: the
@@ -986,12 +1107,18 @@ static int core_extract(st_t* s, int32_t* core, int32_t* flags) {
   int r = any ? R_UNSAT : R_BUDGET;
   if (r == R_UNSAT) {
     for (int id = 0; id < nid; ++id) {
-      if (!K[id]) continue;
+      if (!K[id] || crit[id]) continue; /* (a necessary identity stays) */
       memcpy(K2, K, (size_t)nid);
       K2[id] = 0;
       r = refute(s, K2);
       if (r == R_UNSAT) memcpy(K, s->used, (size_t)nid);
       else if (r == R_BUDGET) { *flags |= DP_F_CORE_BUDGET; break; }
+      else { /* a model of K \ {id}: id is necessary, and rotation finds others */
+        crit[id] = 1;
+        if (!occ.off) occ_build(&s->p, &occ);
+        memcpy(m, s->model, (size_t)nw * 4);
+        rotate(&s->p, &occ, m, id, K, crit);
+      }
     }
     for (int id = 0; id < nid; ++id)
       if (K[id]) core[len++] = id;
@@ -1002,6 +1129,10 @@ static int core_extract(st_t* s, int32_t* core, int32_t* flags) {
   s->steps += saved_steps;
   free(K);
   free(K2);
+  free(crit);
+  free(m);
+  free(occ.off);
+  free(occ.rows);
   return len;
 }
 
