@@ -524,12 +524,21 @@ struct Group {
         idmask = reinterpret_cast<const uint32_t*>(q); q += 2 * nbi;
         idpc = reinterpret_cast<const uint16_t*>(q);   q += nbi + 1;
         rowspace = true;
-        // (one wavefront decodes; with several, the others wait at g_any's barrier)
-        bool ok = true;
-        if (wid == 0)
-          ok = unpack16(reinterpret_cast<const char*>(b) + p16_tail_at(h), (int)p16_tail_bytes(h), derived,
-                        lds + L.reason, reinterpret_cast<uint8_t*>(b) + p16_tail_copy(h));
-        if constexpr (NW > 1) ok = !g_any(!ok);
+        // (one wavefront decodes; with several, the others wait at g_any's
+        // barrier.  The one-wavefront build calls it unconditionally: the
+        // call under a branch took its VGPRs from 161 to 202.)
+        auto decode = [&] {
+          return unpack16(reinterpret_cast<const char*>(b) + p16_tail_at(h), (int)p16_tail_bytes(h), derived,
+                          lds + L.reason, reinterpret_cast<uint8_t*>(b) + p16_tail_copy(h));
+        };
+        bool ok;
+        if constexpr (NW == 1) {
+          ok = decode();
+        } else {
+          ok = true;
+          if (wid == 0) ok = decode();
+          ok = !g_any(!ok);
+        }
         if (!ok) return false;
       }
     } else {
@@ -2998,6 +3007,8 @@ struct Group {
       const int k = viol_key(v);
       bool opened = false;
       if (k >= 0 && k != c && !getb(crit, k)) {
+        // (several wavefronts: every one has read crit before thread 0 sets the bit)
+        if constexpr (NW > 1) bar();
         if (tid == 0) crit[k >> 5] |= 1u << (k & 31);
         const int rn = single_row_of(k);
         if (d < ROT_DEPTH && rn >= 0) {  // continue from this model (v stays flipped)
