@@ -171,8 +171,14 @@ def issue_roofline(sq_json, config, res_per_s):
     kernel-only rate, against the VALU and SALU issue peaks."""
     if not sq_json or not os.path.exists(sq_json) or not res_per_s:
         return None
+    from deppy_amd import _lib
     with open(sq_json) as f:
-        d = json.load(f).get(str(config))
+        j = json.load(f)
+    if j.get("build") != _lib.build_info():
+        # counters of another build: not this kernel's issue rate
+        return {"stale": True, "source": os.path.relpath(sq_json, ROOT), "counters_build": j.get("build"),
+                "note": "the SQ counters on file are not this library's (build digest differs): not reported"}
+    d = j.get(str(config))
     if not d:
         return None
     pw = d["per_wave"]

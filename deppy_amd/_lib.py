@@ -61,7 +61,9 @@ def _plan_hw_queues() -> None:
         warnings.warn("deppy_amd: HIP was initialised before the binding was imported, with %d hardware "
                       "queues; the pipeline runs %d lane streams per device (import deppy_amd first for 8)"
                       % (q, q), RuntimeWarning, stacklevel=3)
-    os.environ["DEPPY_HW_QUEUES"] = str(q)
+    # "q@s": HIP runs q queues, known while GPU_MAX_HW_QUEUES reads s (a child
+    # process started with another setting sizes its streams from its own)
+    os.environ["DEPPY_HW_QUEUES"] = "%d@%s" % (q, os.environ.get("GPU_MAX_HW_QUEUES", ""))
 
 
 _plan_hw_queues()
@@ -159,7 +161,11 @@ def _check_provenance(L) -> None:
     if LIB_PATH != os.path.join(HERE, "libdeppy_hip.so"):
         return
     from deppy_amd import build as _build  # (sources only; nothing is compiled here)
-    want = _build.sources_digest()
+    try:
+        want = _build.sources_digest()
+    except OSError as e:
+        raise RuntimeError("deppy_amd: cannot check that %s was built from this tree: its sources are not "
+                           "readable (%s); deploy deppy_amd/csrc and include/ beside the library" % (LIB_PATH, e)) from e
     got = build_info(L)
     if ("sources=%s " % want) not in got + " ":
         raise RuntimeError("deppy_amd: %s was built from other sources (%s; this tree: sources=%s); run "

@@ -62,6 +62,10 @@ def _needs(target: str, deps: list[str]) -> bool:
 def build(verbose: bool = False, extra: list[str] | None = None, stamps: bool = False,
           tag: str = "") -> str:
     global OBJ, LIB
+    if extra and not stamps and not tag:
+        # the product library is the tree's sources with the tree's flags (the
+        # binding checks its digest); other flags make a tagged variant
+        raise ValueError("build(extra=...) makes a measurement variant: give it a tag")
     if stamps:
         extra = (extra or []) + ["-DDP_STAMPS"]
         obj, lib = OBJ + "_stamps" + tag, STAMPS_LIB.replace(".so", tag + ".so")

@@ -1439,7 +1439,14 @@ void cut_chunks(const dp_ctx* ctx, const dp_job* job, std::vector<std::pair<int3
 // differs from the setting when something initialised HIP first.  Without
 // the binding the setting is the best guess.  DEPPY_STREAMS overrides (A/B).
 int lane_streams() {
-  const int64_t hwq = env_i64("DEPPY_HW_QUEUES", env_i64("GPU_MAX_HW_QUEUES", kStreams));
+  // DEPPY_HW_QUEUES = "q@s": q queues, valid while GPU_MAX_HW_QUEUES still
+  // reads s (a child process that inherited it with another setting uses its own)
+  int64_t hwq = env_i64("GPU_MAX_HW_QUEUES", kStreams);
+  if (const char* e = std::getenv("DEPPY_HW_QUEUES")) {
+    const char* at = std::strchr(e, '@');
+    const char* g = std::getenv("GPU_MAX_HW_QUEUES");
+    if (!at || std::strcmp(at + 1, g ? g : "") == 0) hwq = std::atoll(e);
+  }
   return (int)std::min<int64_t>(kMaxStreams,
                                 std::max<int64_t>(1, env_i64("DEPPY_STREAMS", std::min<int64_t>(hwq, 8))));
 }

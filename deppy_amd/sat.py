@@ -444,18 +444,30 @@ def _replay_trace(tracer: Tracer, variables: list, lw, p: int, res: dict, j: int
 
 
 # Lowering storage reused by solve_wire, per calling thread: the records of
-# the last batch (page-locked, packed) stay valid until that thread's next call.
+# the last batch (page-locked, packed) stay valid until that thread's next
+# call.  The page-locked storage stays pinned at the size of the thread's
+# largest batch until the thread exits or calls release_lowering().  A call
+# made while the thread's SolveBatch is still mapping results (a Tracer that
+# solves from Trace) lowers into fresh storage, so the outer batch's
+# identities and errors are not overwritten.
 _lowering = threading.local()
 LOWER_FLAGS = dict(narrow=True, packed=True, pinned=True)  # DP_LOWER_NARROW | PACKED | PINNED
 
 
 def _reused_lowered(wire: _lib.WireArrays) -> _lib.Lowered:
+    if getattr(_lowering, "busy", 0) > 1:  # a SolveBatch inside this thread's SolveBatch
+        return _lib.Lowered(wire, **LOWER_FLAGS)
     lw = getattr(_lowering, "lw", None)
     if lw is None:
         lw = _lowering.lw = _lib.Lowered(wire, **LOWER_FLAGS)
     else:
         lw.relower(wire)
     return lw
+
+
+def release_lowering() -> None:
+    """Free this thread's reused lowering storage (page-locked memory)."""
+    _lowering.lw = None
 
 
 def solve_wire(wire: _lib.WireArrays, context: Optional[_lib.Context] = None, trace_cap: int = 0):
@@ -489,6 +501,14 @@ def SolveBatch(inputs: Sequence[Sequence[Variable]], tracer: Optional[Tracer] = 
     out: list = [None] * len(inputs)
     if not inputs:
         return out
+    _lowering.busy = getattr(_lowering, "busy", 0) + 1
+    try:
+        return _solve_batch(inputs, tracer, traced, context, out)
+    finally:
+        _lowering.busy -= 1
+
+
+def _solve_batch(inputs, tracer, traced, context, out) -> list:
     lw, res = solve_wire(encode_inputs(inputs), context, TRACE_CAP if traced else 0)
     retraced = {}
     if traced:

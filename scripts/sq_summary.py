@@ -32,4 +32,8 @@ for d in sorted(glob.glob(root + "/c*_a")):
         "active_lds_frac": round(agg["SQ_ACTIVE_INST_LDS"] / wc, 3),
         "wait_inst_lds_frac": round(agg["SQ_WAIT_INST_LDS"] / wc, 3),
     }
+# the library the counters came from (bench.py uses them only for that build)
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
+from deppy_amd import _lib  # noqa: E402
+out["build"] = _lib.build_info()
 print(json.dumps(out, indent=1))

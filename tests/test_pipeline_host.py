@@ -300,4 +300,6 @@ def test_hw_queue_plan():
     assert plan("8", True) == (None, 8)
     assert plan("junk", True) == (None, 4)
     import os
-    assert os.environ["DEPPY_HW_QUEUES"] == str(int(os.environ.get("GPU_MAX_HW_QUEUES", "4")))
+    q, at = os.environ["DEPPY_HW_QUEUES"].split("@")
+    assert q == str(int(os.environ.get("GPU_MAX_HW_QUEUES", "4")))
+    assert at == os.environ.get("GPU_MAX_HW_QUEUES", "")

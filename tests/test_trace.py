@@ -62,14 +62,20 @@ def test_oracle_trace_truncation_is_clean():
 # GPU: the kernel's event stream equals the oracle's
 # ---------------------------------------------------------------------------
 @pytest.mark.gpu
-@pytest.mark.parametrize("flags", [0, _lib.OPT_FORCE_GROUP, _lib.OPT_FORCE_HBM],
-                         ids=["lds", "split", "hbm"])
+@pytest.mark.parametrize("packed", [False, True], ids=["i32", "packed"])
+@pytest.mark.parametrize("flags", [0, _lib.OPT_FORCE_GROUP, _lib.OPT_FORCE_HBM, _lib.OPT_FORCE_LDSG],
+                         ids=["lds", "split", "hbm", "ldsg"])
 @pytest.mark.parametrize("config,n,seed,cap", [(2, 400, 51, CAP), (5, 100, 52, CAP), (5, 100, 53, 24)])
-def test_gpu_trace_bit_exact(config, n, seed, cap, flags):
+def test_gpu_trace_bit_exact(config, n, seed, cap, flags, packed):
+    """The kernel's trace equals the oracle's in every placement, from int32
+    records and from packed ones (DP_FMT_P16D: the one-wavefront and M_LDSG
+    kernels keep their bitsets over rows and map them back to identities for
+    the trace, solve_kernel.hpp to_idents), the cap=24 truncation included."""
     lw = lowered_config(config, n, seed)
+    src = lowered_config(config, n, seed, packed=True, pinned=True) if packed else lw
     c = _lib.Context(0, 1, flags=flags)
     try:
-        g = c.solve(lw.rec_off, lw.rec, cap)
+        g = c.solve(src.rec_off, src.rec, cap)
     finally:
         c.close()
     o = oracle.solve_batch(lw.rec_off, lw.rec, 0, 16, trace_cap=cap)
@@ -136,3 +142,30 @@ def test_gpu_tracer_events_match_oracle_through_api():
                 conf.append(str(sat.AppliedConstraint(var, var.Constraints()[int(lw.ident_con[i0 + i])])))
             expect.append(([str(variables[v].Identifier()) for v in vs], conf))
         assert t.events == expect, p
+
+
+@pytest.mark.gpu
+def test_tracer_that_solves_inside_trace():
+    """A Tracer whose Trace calls SolveBatch on the same thread: the nested
+    call lowers into its own storage, so the outer batch's cores and trace
+    still map to its own identities (sat.py _reused_lowered)."""
+    w = _lib.generate(5, 30, 71)
+    inputs = [fixtures.wire_problem_variables(w, p) for p in range(30)]
+    plain = sat.SolveBatch(inputs)
+
+    class Nested(sat.Tracer):
+        def __init__(self):
+            self.n = 0
+
+        def Trace(self, pos):
+            self.n += 1
+            sat.SolveBatch(inputs[:3])  # another batch lowered while the outer one is mapped
+
+    t = Nested()
+    traced = sat.SolveBatch(inputs, tracer=t)
+    assert t.n > 0
+    for (ia, ea), (ib, eb) in zip(plain, traced):
+        assert (ia is None) == (ib is None)
+        if ia is not None:
+            assert [v.Identifier() for v in ia] == [v.Identifier() for v in ib]
+        assert type(ea) is type(eb) and str(ea) == str(eb)
