@@ -241,14 +241,17 @@ __host__ __device__ inline uint32_t row_info(int32_t a, int32_t len) {
 }
 
 // Bytes per entry of the watch lists the device builds for a multi-wave
-// record (Layout::wl): 2 (the row id alone) when every row id fits 16 bits,
-// else 8 ({row, row_info(row)}, the row's literal range carried in the
-// entry).  The 2-byte entries cost a visit one more dependent read (the
-// row's offsets) but shrink an OLM-scale catalog's lists from ~2.1 MB to
-// ~0.5 MB, so its whole BCP working set (offsets, entries, row literals)
-// fits one XCD's 4 MB L2.  -DDP_WENT=8 keeps the 8-byte entries (A/B).
+// record (Layout::wl): 8 ({row, row_info(row)}, the row's literal range
+// carried in the entry), or with -DDP_WENT=2 (A/B) the row id alone when
+// every row id fits 16 bits.  The 2-byte entries shrink an OLM-scale
+// catalog's lists from ~2.1 MB to ~0.5 MB so its BCP working set fits one
+// XCD's 4 MB L2, at one more dependent read a visit (the row's offsets).
+// Measured (round 5, bit-exact): one config-4 catalog alone L2 hit rate
+// 69.7% -> 79.3%, but the 20-catalog kernel median 7.79-7.85 -> 7.85-7.94
+// ms and the 256-catalog batch unchanged (11.77k vs 11.82k res/s), with
+// more write requests (profiles/r05_c4_went_ab.txt).  8 stays.
 #ifndef DP_WENT
-#define DP_WENT 2
+#define DP_WENT 8
 #endif
 __host__ __device__ inline int32_t went_bytes(const int32_t* h) {
   return DP_WENT == 2 && (int64_t)h[DP_H_NC] + h[DP_H_NK] <= 65535 ? 2 : 8;
