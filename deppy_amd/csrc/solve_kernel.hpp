@@ -1496,10 +1496,12 @@ struct Group {
 
   // A watched row reached in a round: clause rows are evaluated by the thread
   // that reached them; AtMost rows are queued (ballot compaction) and later
-  // evaluated by a whole wavefront, one row at a time (flush_cards).  Call
-  // from wave-converged code: every active lane passes its row (or -1).
-  // ncq counts the queue in the one-wavefront mode (a register); with several
-  // wavefronts the queue length is the LDS counter S_NK.
+  // evaluated by the whole wavefront that queued them, one row at a time
+  // (flush_cards).  Call from wave-converged code: every active lane passes
+  // its row (or -1).  Each wavefront owns a segment of CQ / NW queue entries
+  // (multi-wave: and their row_info after the queue) and counts it in ncq (a
+  // register), so queueing and flushing need no barrier between wavefronts.
+  static constexpr int CQW = CQ / NW;
   __device__ __forceinline__ void visit(int r, int& crow, int& ncq, uint32_t info = ROW_INFO_NONE) {
     DP_VIS_ADD(r >= 0 ? sizeof(IX) : 0);  // the watch entry
     const bool ok = r >= 0 && row_on(r);
@@ -1509,30 +1511,18 @@ struct Group {
       if (card) cardq[ncq + __popcll(m & lanemask_lt())] = enc(r);
       note_all(ok && !card ? clause_unit(r, crow, info) : -1, r);
       ncq += __popcll(m);
-    } else if constexpr (NW == 1) {
-      const bool q = ncq + __popcll(m) <= CQ;  // queue full: evaluate in-lane
-      if (card && q) cardq[ncq + __popcll(m & lanemask_lt())] = enc(r);
-      else if (card) card_serial(r, crow);
+    } else {
+      const bool q = ncq + __popcll(m) <= CQW;  // queue full: evaluate in-lane
+      const int pos = wid * CQW + ncq + __popcll(m & lanemask_lt());
+      if (card && q) {
+        cardq[pos] = enc(r);
+        if constexpr (NW > 1 && !N16) cardq[CQ + pos] = (IX)info;  // (IX = int32 here; M_LDSG entries carry no range)
+      } else if (card) card_serial(r, crow);
       else if (ok) {
         const int ul = clause_unit(r, crow, info);
         if (ul >= 0) note(ul, r);
       }
       if (q) ncq += __popcll(m);
-    } else {
-      int pos = CQ;
-      if (m) {
-        int b = 0;
-        if (lane == 0) b = atomicAdd(&scal[S_NK], __popcll(m));
-        pos = __shfl(b, 0) + __popcll(m & lanemask_lt());
-      }
-      if (card && pos < CQ) {
-        cardq[pos] = enc(r);
-        if constexpr (!N16) cardq[CQ + pos] = (IX)info;  // (IX = int32 here; M_LDSG entries carry no range)
-      } else if (card) card_serial(r, crow);  // queue full: evaluate in-lane
-      else if (ok) {
-        const int ul = clause_unit(r, crow, info);
-        if (ul >= 0) note(ul, r);
-      }
     }
   }
 
@@ -1714,18 +1704,11 @@ struct Group {
   // AtMost rows, one at a time per wavefront, lanes over positions (oracle:
   // eval_row): counts by ballot; a variable listed m times is a run of m
   // positions, forced false when the count plus m exceeds the bound.
+  // (each wavefront its own queue segment: no barrier)
   __device__ __forceinline__ void flush_cards(int& crow, int ncq) {
-    int q0, qs;
-    if constexpr (NW == 1) {
-      if (ncq == 0) return;
-      wsync();
-      q0 = 0; qs = 1;
-    } else {
-      bar();
-      ncq = min(scal[S_NK], CQ);
-      q0 = wid; qs = NW;
-    }
-    for (int q = q0; q < ncq; q += qs) {
+    if (ncq == 0) return;
+    wsync();
+    for (int q = wid * CQW; q < wid * CQW + ncq; ++q) {
       const int r = DP_CHK((int)cardq[q], nc, nrows, 3), k = r - nc;
       int a, len;
       const uint32_t info = NW > 1 && !N16 ? (uint32_t)cardq[CQ + q] : ROW_INFO_NONE;
@@ -1831,7 +1814,6 @@ struct Group {
     const int nt = DP_CHK(scal[S_NTB + rb], 0, 2 * (hmask + 1) + 1, 4);
     const bool ovf = scal[S_OVB + rb] != 0;
     const int cvx = scal[S_CVB + rb];
-    if (tid == 0) scal[S_NK] = 0;  // the AtMost queue was flushed (read before the exchange)
     if (ovf) {
       clear_slots(nt);
       return 2;
@@ -1878,9 +1860,6 @@ struct Group {
     }
     gsync();
     const int nt = DP_CHK(scal[S_NTOUCHED], 0, 2 * nv + 1, 4);
-    if constexpr (NW > 1) {
-      if (tid == 0) scal[S_NK] = 0;  // the AtMost queue was flushed
-    }
     if (g_any(crow != INF)) {
       c_row = g_min(crow);
       clear_touched(nt);
@@ -2061,6 +2040,14 @@ struct Group {
         DP_ACC(12, e - a);
 #endif
       } else {
+        // Flattened: each wavefront takes 64 frontier literals of the chunk,
+        // scans their watch-range lengths by DPP and visits the concatenated
+        // entries 64 at a time from its own segment of the work list, with
+        // no barrier between wavefronts (the round's exchange follows the
+        // AtMost flush).  A wavefront whose entries overflow its segment
+        // walks its literals' lists one at a time.
+        constexpr int SEGW = WBUF / NW;
+        IX* wb = wbuf + wid * SEGW;
         for (int b = lo; b < hi; b += NT) {
           const int i = b + tid;
           int cnt = 0, a = 0;
@@ -2069,56 +2056,43 @@ struct Group {
             a = w_off[l];
             cnt = (int)w_off[l + 1] - a;
           }
-          // flatten: a group-wide prefix sum of the watch-range lengths
 #ifdef DP_STAMPS
           const int64_t tf0 = stamp();
 #endif
           const int incl = wave_incl_scan(cnt);
-          int total = __builtin_amdgcn_readlane(incl, 63), before = 0;
+          const int total = __builtin_amdgcn_readlane(incl, 63);  // this wavefront's entries
 #ifdef DP_STAMPS
           if constexpr (NW == 1) DP_ACC(26, total);  // watch entries a flattened chunk visits
 #endif
-          if constexpr (NW > 1) {
-            const int32_t* sl = exchange(incl, lane == 63);
-            total = 0;
-#pragma unroll
-            for (int q = 0; q < NW; ++q) {
-              const int c = sl[q];
-              before += q < wid ? c : 0;
-              total += c;
-            }
-          }
-          if (total <= WBUF) {
+          if (total <= SEGW) {
 #ifdef DP_STAMPS
             const int64_t tf1 = stamp();
-            if constexpr (NW > 1) DP_ACC(27, tf1 - tf0);  // ranges: scan + exchange
+            if constexpr (NW > 1) DP_ACC(27, tf1 - tf0);  // ranges: scan
 #endif
-            // every frontier literal writes its watch range into the list
-            for (int k = 0, at = before + incl - cnt; k < cnt; ++k) wbuf[at + k] = enc(a + k);
-            gsync();
+            // every frontier literal writes its watch range into the segment
+            for (int k = 0, at = incl - cnt; k < cnt; ++k) wb[at + k] = enc(a + k);
+            wsync();
 #ifdef DP_STAMPS
             const int64_t tf2 = stamp();
             if constexpr (NW > 1) DP_ACC(28, tf2 - tf1);  // the work list
 #endif
-            for (int t0 = 0; t0 < total; t0 += NT) {
+            for (int t0 = 0; t0 < total; t0 += 64) {
               make_room(crow, ncq);
-              visit_at(t0 + tid < total ? DP_CHK((int)wbuf[t0 + tid], 0, nwatch, 12) : -1, crow, ncq);
+              visit_at(t0 + lane < total ? DP_CHK((int)wb[t0 + lane], 0, nwatch, 12) : -1, crow, ncq);
             }
 #ifdef DP_STAMPS
             if constexpr (NW > 1) DP_ACC(29, stamp() - tf2);  // the visits
 #endif
-            // wbuf is reused by the next chunk; after the last one the
-            // AtMost flush's barrier (several wavefronts) comes first
-            if (NW == 1 || b + NT < hi) gsync();
+            wsync();  // (the segment is rewritten by the next chunk)
           } else {
-            // a very large chunk: one frontier literal at a time
-            const int n = min(NT, hi - b);
+            // a very large chunk: this wavefront's literals one at a time
+            const int f0 = b + 64 * wid, n = max(0, min(64, hi - f0));
             for (int e = 0; e < n; ++e) {
-              const int l = front(b + e);
+              const int l = front(f0 + e);
               const int a2 = w_off[l], e2 = w_off[l + 1];
-              for (int k0 = a2; k0 < e2; k0 += NT) {
+              for (int k0 = a2; k0 < e2; k0 += 64) {
                 make_room(crow, ncq);
-                visit_at(k0 + tid < e2 ? k0 + tid : -1, crow, ncq);
+                visit_at(k0 + lane < e2 ? k0 + lane : -1, crow, ncq);
               }
             }
           }
@@ -2130,7 +2104,7 @@ struct Group {
       }
 #ifdef DP_STAMPS
       const int64_t tf = stamp();
-      DP_ACC(15, NW == 1 ? ncq : min(scal[S_NK], CQ));
+      DP_ACC(15, ncq);  // (multi-wave: wavefront 0's queue)
       flush_cards(crow, ncq);
       const int64_t tq = stamp();
       DP_ACC(10, tq - tf);
