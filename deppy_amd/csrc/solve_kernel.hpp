@@ -1963,8 +1963,15 @@ struct Group {
       const bool ring = LR && hi - lo <= hmask + 1;
       if constexpr (LR)
         if (!ring) bar();
-      auto front = [&](int i) { return LR && ring ? (int)fr[i & hmask] : (int)trail[i]; };
-      if (run_round([&](int& crow) { visit_frontier(lo, hi, crow, front); }) < 0) return -1;
+      // (two instantiations: one accessor choosing between the LDS ring and
+      // the trail in HBM compiled to flat loads, which wait on both the
+      // vector-memory and the LDS counters, in every round's frontier read)
+      int rr;
+      if (LR && ring)
+        rr = run_round([&](int& crow) { visit_frontier(lo, hi, crow, [&](int i) { return (int)fr[i & hmask]; }); });
+      else
+        rr = run_round([&](int& crow) { visit_frontier(lo, hi, crow, [&](int i) { return (int)trail[i]; }); });
+      if (rr < 0) return -1;
 #ifdef DP_STAMPS
       DP_ACC(0, stamp() - t0);
 #endif
