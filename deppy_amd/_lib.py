@@ -266,6 +266,21 @@ class WireArrays:
                       str_bytes=np.frombuffer(bytes(str_bytes) + b"\0", np.uint8))
         self.interned = interned
 
+    @property
+    def n_problems(self) -> int:
+        return len(self.a["prob_var_off"]) - 1
+
+    def slice(self, p0: int, p1: int) -> "WireArrays":
+        """Problems [p0, p1) as a wire batch of their own, without a copy: the
+        offsets are absolute (include/deppy_hip.h dp_wire), so the range's
+        prob_var_off is a view into this batch's and every other array is
+        shared."""
+        w = WireArrays.__new__(WireArrays)
+        w.a = dict(self.a)
+        w.a["prob_var_off"] = self.a["prob_var_off"][p0:p1 + 1]
+        w.interned = self.interned
+        return w
+
     def struct(self) -> Wire:
         a = self.a
         # keep one extra element so empty arrays still have a valid pointer

@@ -1257,16 +1257,19 @@ extern "C" {
 const char* dp_last_global_error(void) { return dp::g_err.c_str(); }
 
 // The batch-level shape of a wire batch (serial, O(problems)); each problem's
-// own arrays are checked by problem_ok on the lowering threads.
+// own arrays are checked by problem_ok on the lowering threads.  The offsets
+// are absolute: a batch may be a problem range of a larger one's arrays
+// (prob_var_off pointing into its offsets; include/deppy_hip.h dp_wire).
 static bool wire_ok(const dp_wire* w) {
   if (!w || w->n_problems < 0 || !w->prob_var_off) return false;
   if (w->n_problems == 0) return true;
-  const int64_t nvars = w->prob_var_off[w->n_problems];
-  if (w->prob_var_off[0] != 0) return false;
+  const int64_t v0 = w->prob_var_off[0], nvars = w->prob_var_off[w->n_problems];
+  if (v0 < 0) return false;
   for (int32_t p = 0; p < w->n_problems; ++p)
     if (w->prob_var_off[p + 1] < w->prob_var_off[p]) return false;
-  if (nvars > 0 && (!w->var_id || !w->var_con_off || w->var_con_off[0] != 0)) return false;
-  if (nvars > 0 && w->var_con_off[nvars] > 0 && (!w->con_kind || !w->con_arg_off || w->con_arg_off[0] != 0))
+  if (nvars > v0 && (!w->var_id || !w->var_con_off || w->var_con_off[v0] < 0)) return false;
+  if (nvars > v0 && w->var_con_off[nvars] > w->var_con_off[v0] &&
+      (!w->con_kind || !w->con_arg_off || w->con_arg_off[w->var_con_off[v0]] < 0))
     return false;
   return true;
 }
@@ -1315,7 +1318,9 @@ int dp_lower_into(const dp_wire* wire, int32_t flags, dp_lowered* lw) {
   dp::Pool& pool = dp::host_pool();
   int nt = pool.size();
   // threads by work (constraint arguments), chunks small enough to balance
-  const int64_t work = P ? wire->con_arg_off[wire->var_con_off[wire->prob_var_off[P]]] : 0;
+  const int64_t work = P ? wire->con_arg_off[wire->var_con_off[wire->prob_var_off[P]]] -
+                               wire->con_arg_off[wire->var_con_off[wire->prob_var_off[0]]]
+                         : 0;
   if (work < 200000) nt = 1;
   const int32_t chunk = (int32_t)std::max<int64_t>(1, std::min<int64_t>(64, P / (8 * (int64_t)nt)));
   const int32_t nchunks = (P + chunk - 1) / chunk;

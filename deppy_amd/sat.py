@@ -468,6 +468,13 @@ def _reused_lowered(wire: _lib.WireArrays) -> _lib.Lowered:
 def release_lowering() -> None:
     """Free this thread's reused lowering storage (page-locked memory)."""
     _lowering.lw = None
+    _lowering.pipe = None
+
+
+# A batch of at least 2 * SUB_BATCH problems is lowered and solved in
+# sub-batches of SUB_BATCH, pipelined: the host pool lowers sub-batch i + 1
+# while the GPU solves sub-batch i (solve_wire).
+SUB_BATCH = 4096
 
 
 def solve_wire(wire: _lib.WireArrays, context: Optional[_lib.Context] = None, trace_cap: int = 0):
@@ -477,14 +484,83 @@ def solve_wire(wire: _lib.WireArrays, context: Optional[_lib.Context] = None, tr
     dp_job_wait; up to 16 catalogs on the latency path).  The records are the
     form the GPU reads and are DMA'd without staging (the bench's `value` and
     `end_to_end` legs time the same records).  Problems the lowering rejected
-    keep an empty record, solved as nothing and reported from lw.err.
+    keep an empty record, solved as nothing and reported from lw.err.  A
+    large untraced batch goes through _solve_pipelined (the same records,
+    lowered and solved in overlapping sub-batches).
     Returns (lowered, results); both stay valid until this thread's next
     call.  trace_cap > 0 solves through the traced device-resident form."""
+    if trace_cap <= 0 and wire.n_problems >= 2 * SUB_BATCH:
+        return _solve_pipelined(wire, context)
     lw = _reused_lowered(wire)
     with (contextlib.nullcontext() if context else _ctx_lock):
         ctx = context or device_context()
         res = ctx.solve(lw.rec_off, lw.rec, trace_cap)
     return lw, res
+
+
+class _Stitched:
+    """The lowering outputs SolveBatch reads (identities, errors), gathered
+    from the sub-batches of a pipelined solve (copies: the sub-batches'
+    storage is reused)."""
+
+    def __init__(self, parts):
+        self.n = sum(x[0] for x in parts)
+        offs = [0]
+        for _, io, _, _, _, _ in parts:
+            offs.append(offs[-1] + int(io[-1]))
+        self.ident_off = np.concatenate([[0]] + [io[1:] + offs[k] for k, (_, io, _, _, _, _) in enumerate(parts)])
+        self.ident_var = np.concatenate([x[2] for x in parts]) if parts else np.zeros(0, np.int32)
+        self.ident_con = np.concatenate([x[3] for x in parts]) if parts else np.zeros(0, np.int32)
+        self.err = np.concatenate([x[4] for x in parts]) if parts else np.zeros(0, np.int32)
+        self.msg = [m for x in parts for m in x[5]]
+
+
+def _stitch_results(rs: list) -> dict:
+    """Per-sub-batch result dicts (result_arrays layout) -> one, in order."""
+    out = {k: np.concatenate([r[k] for r in rs]) for k in ("status", "flags", "core_len", "steps")}
+    for data, off in (("installed", "inst_off"), ("core", "core_off")):
+        parts, offs, at = [], [np.zeros(1, np.int64)], 0
+        for r in rs:
+            o = r[off]
+            parts.append(r[data][:int(o[-1])])
+            offs.append(o[1:] + at)
+            at += int(o[-1])
+        out[data] = np.concatenate(parts) if at else np.zeros(1, rs[0][data].dtype)
+        out[off] = np.concatenate(offs)
+    return out
+
+
+def _solve_pipelined(wire: _lib.WireArrays, context: Optional[_lib.Context]):
+    n = wire.n_problems
+    cuts = list(range(0, n, SUB_BATCH)) + [n]
+    pipe = getattr(_lowering, "pipe", None)
+    if pipe is None or getattr(_lowering, "busy", 0) > 1:
+        pipe = [None, None]
+        if getattr(_lowering, "busy", 0) <= 1:
+            _lowering.pipe = pipe
+    parts, results, jobs = [], [], []
+    with (contextlib.nullcontext() if context else _ctx_lock):
+        ctx = context or device_context()
+
+        def collect():
+            lw, job = jobs.pop(0)
+            results.append(job.wait())
+            parts.append((lw.n, lw.ident_off.copy(), lw.ident_var.copy(), lw.ident_con.copy(), lw.err.copy(),
+                          list(lw.msg)))
+
+        for i in range(len(cuts) - 1):
+            if len(jobs) == 2:
+                collect()  # frees the storage sub-batch i reuses
+            sub = wire.slice(cuts[i], cuts[i + 1])
+            k = i % 2
+            if pipe[k] is None:
+                pipe[k] = _lib.Lowered(sub, **LOWER_FLAGS)
+            else:
+                pipe[k].relower(sub)
+            jobs.append((pipe[k], ctx.submit(pipe[k].rec_off, pipe[k].rec)))
+        while jobs:
+            collect()
+    return _Stitched(parts), _stitch_results(results)
 
 
 def SolveBatch(inputs: Sequence[Sequence[Variable]], tracer: Optional[Tracer] = None,

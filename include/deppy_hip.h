@@ -59,6 +59,10 @@ enum dp_kind {
 /* A batch of independent problems.  Every problem is the []Variable handed to
  * sat.WithInput (solve.go:133).  Identifiers are byte strings in a shared
  * string table; they are compared by bytes within one problem. */
+/* Offsets are absolute indices into the arrays they point into, so a batch
+ * may be a range of problems of a larger batch: prob_var_off pointing at
+ * the range's first offset, every other array the larger batch's own (no
+ * rebasing; prob_var_off[0] is then the range's first variable). */
 typedef struct dp_wire {
   int32_t n_problems;
   const int64_t* prob_var_off; /* [n_problems+1] -> variables          */

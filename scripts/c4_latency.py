@@ -24,7 +24,7 @@ w = _lib.generate(4, m, first)
 wa = _lib.WireArrays(**{k: w[k] for k in ("prob_var_off", "var_id", "var_con_off", "con_kind", "con_n",
                                           "con_arg_off", "con_arg", "str_off")}, str_bytes=w["str_bytes"].tobytes())
 lw = _lib.Lowered(wa)  # int32 records (what config 4 lowers to in any form)
-ctx = _lib.Context(0, 1)
+ctx = _lib.Context(0, 1, flags=int(os.environ.get("DEPPY_C4_FLAGS", "0")))  # (placement A/B: 4 = 4-wave groups)
 rows = []
 for p in range(m):
     one = np.ascontiguousarray(lw.record(p))

@@ -777,3 +777,22 @@ def test_multi_device_dispatcher_bit_exact(config, n, seed):
         c.close()
     assert compare_results(g, o, n) == []
     assert compare_results(gr, o, n) == []
+
+
+def test_pipelined_solve_wire_bit_exact(ctx):
+    """sat.solve_wire on a batch of more than 2 x SUB_BATCH catalogs (the
+    SolveBatch path) lowers and solves it in overlapping sub-batches; every
+    field equals one solve of the whole batch's packed records, and the
+    stitched identities equal the whole lowering's."""
+    from deppy_amd import sat
+    n = 2 * sat.SUB_BATCH + 1234
+    w = _lib.generate(5, n, 171)
+    wa = _lib.WireArrays(**{k: w[k] for k in ("prob_var_off", "var_id", "var_con_off", "con_kind", "con_n",
+                                              "con_arg_off", "con_arg", "str_off")}, str_bytes=w["str_bytes"].tobytes())
+    lw, res = sat.solve_wire(wa, ctx)
+    assert isinstance(lw, sat._Stitched) and lw.n == n
+    whole = _lib.Lowered(wa, narrow=True, packed=True, pinned=True)
+    g = ctx.solve(whole.rec_off, whole.rec)
+    assert compare_results(res, g, n) == []
+    for k in ("ident_off", "ident_var", "ident_con", "err"):
+        np.testing.assert_array_equal(getattr(lw, k), getattr(whole, k))

@@ -303,3 +303,38 @@ def test_hw_queue_plan():
     q, at = os.environ["DEPPY_HW_QUEUES"].split("@")
     assert q == str(int(os.environ.get("GPU_MAX_HW_QUEUES", "4")))
     assert at == os.environ.get("GPU_MAX_HW_QUEUES", "")
+
+
+def test_pipelined_solve_wire_stitching():
+    """sat._solve_pipelined's result stitching (CPU): the per-sub-batch
+    result dicts of a batch cut in three, stitched, equal the whole batch's
+    (the oracle stands in for the device solve here), and the wire slices
+    lower to the same records as the whole batch."""
+    from deppy_amd import sat
+    from oracle import oracle
+    w = _lib.generate(5, 300, 77)
+    wa = _lib.WireArrays(**{k: w[k] for k in ("prob_var_off", "var_id", "var_con_off", "con_kind", "con_n",
+                                              "con_arg_off", "con_arg", "str_off")}, str_bytes=w["str_bytes"].tobytes())
+    whole = _lib.Lowered(wa)
+    full = oracle.solve_batch(whole.rec_off, whole.rec, 0, 4)
+    cuts = [0, 97, 201, 300]
+    subs, parts = [], []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        lw = _lib.Lowered(wa.slice(a, b))
+        np.testing.assert_array_equal(lw.rec, whole.rec[whole.rec_off[a]:whole.rec_off[b]])
+        subs.append(oracle.solve_batch(lw.rec_off, lw.rec, 0, 4))
+        parts.append((lw.n, lw.ident_off.copy(), lw.ident_var.copy(), lw.ident_con.copy(), lw.err.copy(), list(lw.msg)))
+    got = sat._stitch_results(subs)
+    for k in ("status", "flags", "core_len", "steps", "inst_off", "core_off"):
+        np.testing.assert_array_equal(got[k], full[k][:len(got[k])], err_msg=k)
+    n_inst, n_core = int(full["inst_off"][-1]), int(full["core_off"][-1])
+    np.testing.assert_array_equal(got["installed"][:n_inst], full["installed"][:n_inst])
+    for p in range(300):
+        c0, c1 = int(full["core_off"][p]), int(full["core_off"][p]) + int(full["core_len"][p])
+        np.testing.assert_array_equal(got["core"][c0:c1], full["core"][c0:c1])
+    st = sat._Stitched(parts)
+    np.testing.assert_array_equal(st.ident_off, whole.ident_off)
+    np.testing.assert_array_equal(st.ident_var, whole.ident_var)
+    np.testing.assert_array_equal(st.ident_con, whole.ident_con)
+    np.testing.assert_array_equal(st.err, whole.err)
+    assert n_core >= 0
