@@ -2053,12 +2053,17 @@ struct Group {
         // no barrier between wavefronts (the round's exchange follows the
         // AtMost flush).  A wavefront whose entries overflow its segment
         // walks its literals' lists one at a time.
+        // The frontier is dealt evenly: each wavefront takes S <= 64
+        // consecutive literals per step (a frontier of 128 literals gives
+        // each of 8 wavefronts 16, so their ~50 entries are one pass of its
+        // lanes, not three passes of one wavefront's 64 literals).
         constexpr int SEGW = WBUF / NW;
         IX* wb = wbuf + wid * SEGW;
-        for (int b = lo; b < hi; b += NT) {
-          const int i = b + tid;
+        const int S = NW == 1 ? 64 : min(64, (hi - lo + NW - 1) / NW);
+        for (int b = lo; b < hi; b += S * NW) {
+          const int i = b + wid * S + lane;
           int cnt = 0, a = 0;
-          if (i < hi) {
+          if (lane < S && i < hi) {
             const int l = DP_CHK(front(i), 0, 2 * nv, 11);
             a = w_off[l];
             cnt = (int)w_off[l + 1] - a;
@@ -2093,7 +2098,7 @@ struct Group {
             wsync();  // (the segment is rewritten by the next chunk)
           } else {
             // a very large chunk: this wavefront's literals one at a time
-            const int f0 = b + 64 * wid, n = max(0, min(64, hi - f0));
+            const int f0 = b + S * wid, n = max(0, min(S, hi - f0));
             for (int e = 0; e < n; ++e) {
               const int l = front(f0 + e);
               const int a2 = w_off[l], e2 = w_off[l + 1];
