@@ -2,5 +2,5 @@
 #include "solve_kernel.hpp"
 
 namespace dp {
-DP_DEFINE_MODE(M_HBM, 1, launch_hbm)
+DP_DEFINE_MODE(M_HBM, 2, launch_hbm)
 }  // namespace dp

@@ -2,5 +2,5 @@
 #include "solve_kernel.hpp"
 
 namespace dp {
-DP_DEFINE_MODE(M_SPLIT, 1, launch_split)
+DP_DEFINE_MODE(M_SPLIT, 2, launch_split)
 }  // namespace dp

@@ -3,5 +3,5 @@
 #include "solve_kernel.hpp"
 
 namespace dp {
-DP_DEFINE_MODE(M_SPLIT4, 1, launch_split4)
+DP_DEFINE_MODE(M_SPLIT4, 2, launch_split4)
 }  // namespace dp

@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import contextlib
 import io
+import os
 import threading
 import warnings
 from dataclasses import dataclass, field
@@ -471,10 +472,17 @@ def release_lowering() -> None:
     _lowering.pipe = None
 
 
-# A batch of at least 2 * SUB_BATCH problems is lowered and solved in
-# sub-batches of SUB_BATCH, pipelined: the host pool lowers sub-batch i + 1
-# while the GPU solves sub-batch i (solve_wire).
-SUB_BATCH = 4096
+# With SUB_BATCH > 0, a batch of at least 2 * SUB_BATCH problems is lowered
+# and solved in sub-batches of SUB_BATCH, pipelined: the host pool lowers
+# sub-batch i + 1 while the GPU solves sub-batch i (_solve_pipelined).
+# Measured on the box (config 2, 10k catalogs, scripts/pipe_timing.py): the
+# whole batch lowers in 3.8 ms and solves in 2.0 ms (6.3 ms through
+# solve_wire), yet the pipelined path took 8.4 ms with 2048-problem
+# sub-batches, 11.8 ms with 4096 and 6.3 ms with 8192 -- the sub-batches'
+# lowering and solving did not overlap, and each sub-batch pays a launch
+# tail (profiles/r05_pipe_timing.txt).  Off by default (0); the tests run it
+# for parity.  DEPPY_SUB_BATCH sets it.
+SUB_BATCH = int(os.environ.get("DEPPY_SUB_BATCH", "0"))
 
 
 def solve_wire(wire: _lib.WireArrays, context: Optional[_lib.Context] = None, trace_cap: int = 0):
@@ -489,7 +497,7 @@ def solve_wire(wire: _lib.WireArrays, context: Optional[_lib.Context] = None, tr
     lowered and solved in overlapping sub-batches).
     Returns (lowered, results); both stay valid until this thread's next
     call.  trace_cap > 0 solves through the traced device-resident form."""
-    if trace_cap <= 0 and wire.n_problems >= 2 * SUB_BATCH:
+    if trace_cap <= 0 and SUB_BATCH > 0 and wire.n_problems >= 2 * SUB_BATCH:
         return _solve_pipelined(wire, context)
     lw = _reused_lowered(wire)
     with (contextlib.nullcontext() if context else _ctx_lock):

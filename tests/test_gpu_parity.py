@@ -779,12 +779,13 @@ def test_multi_device_dispatcher_bit_exact(config, n, seed):
     assert compare_results(gr, o, n) == []
 
 
-def test_pipelined_solve_wire_bit_exact(ctx):
+def test_pipelined_solve_wire_bit_exact(ctx, monkeypatch):
     """sat.solve_wire on a batch of more than 2 x SUB_BATCH catalogs (the
     SolveBatch path) lowers and solves it in overlapping sub-batches; every
     field equals one solve of the whole batch's packed records, and the
     stitched identities equal the whole lowering's."""
     from deppy_amd import sat
+    monkeypatch.setattr(sat, "SUB_BATCH", 4096)
     n = 2 * sat.SUB_BATCH + 1234
     w = _lib.generate(5, n, 171)
     wa = _lib.WireArrays(**{k: w[k] for k in ("prob_var_off", "var_id", "var_con_off", "con_kind", "con_n",
