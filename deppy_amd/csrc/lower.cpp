@@ -192,9 +192,11 @@ struct FlatMap {
 struct Aig {
   int32_t next_node = 1;
   FlatMap strash;
+  std::vector<uint64_t> fanin;  // gate node 1 + nv + i: its strash key (a << 32 | b)
   void reset(int nv) {
     next_node = 1 + nv;
     strash.reset();
+    fanin.clear();
   }
   static int32_t input(int v) { return 2 * (v + 1); }
   int32_t And(int32_t a, int32_t b) {
@@ -209,6 +211,7 @@ struct Aig {
     if (hit >= 0) return hit;
     int32_t g = 2 * next_node++;
     strash.insert(key, g);
+    fanin.push_back(key);
     return g;
   }
   int32_t Or(int32_t a, int32_t b) { return And(a ^ 1, b ^ 1) ^ 1; }
@@ -319,6 +322,11 @@ struct alignas(128) Work {  // per-thread scratch
   std::vector<int32_t> card_off, card_lits, card_bound, card_id;
   std::vector<int32_t> var_choice_off, choice_off, choice_lits, anchors;
   std::vector<int32_t> ms, sorted, order, mult;
+  // AtMost networks (Lowerer::network_rows): next auxiliary variable, a
+  // gate's cone and the walk's marks
+  int32_t naux = 0;
+  std::vector<int32_t> cone, walk;
+  std::vector<uint8_t> vis;
   std::vector<std::string> errs;
   // fast path (lower_fast): identity keys and the record under construction
   FlatMap fkey;
@@ -710,6 +718,7 @@ struct Lowerer {
     W.clause_off.assign(1, 0); W.clause_lits.clear(); W.clause_id.clear();
     W.card_off.assign(1, 0); W.card_lits.clear(); W.card_bound.clear(); W.card_id.clear();
     W.errs.clear();
+    W.naux = nv;
 
     // pass 2: Apply every constraint (lit_mapping.go:59-74)
     for (int vi = 0; vi < nv; ++vi) {
@@ -787,8 +796,9 @@ struct Lowerer {
       W.var_choice_off.push_back((int32_t)W.choice_off.size() - 1);
       if (anchor) W.anchors.push_back(vi);
     }
+    W.var_choice_off.resize((size_t)W.naux + 1, W.var_choice_off.back());  // auxiliaries: no choices
     const size_t base = O.nrec;
-    emit_record(W, O, nv);
+    emit_record(W, O, W.naux, W.naux > nv ? nv : 0);
     narrow_last(O, base);
   }
 
@@ -1087,10 +1097,12 @@ struct Lowerer {
     return true;
   }
 
+  // CardSort(ms).Leq(n): the network is built before Leq reads it, whatever
+  // n (gini's order, constraints.go:180-186), so an AtMost folded to a
+  // constant still adds its gates to the graph (the nodes later networks
+  // share and number after).
   static int32_t leq(Aig& aig, Work& W, int32_t n) {
     const int N = (int)W.ms.size();
-    if (n < 0) return kF;
-    if (n >= N) return kT;
     int p = 1;
     while (p < N) p <<= 1;
     W.sorted.assign(W.ms.begin(), W.ms.end());
@@ -1101,6 +1113,8 @@ struct Lowerer {
       W.sorted[(size_t)pr.first] = hi;
       W.sorted[(size_t)pr.second] = lo;
     }
+    if (n < 0) return kF;
+    if (n >= N) return kT;
     return W.sorted[(size_t)n] ^ 1;
   }
 
@@ -1147,6 +1161,10 @@ struct Lowerer {
         if (j == W.order.size()) { W.order.push_back(v); W.mult.push_back(0); }
         W.mult[j]++;
       }
+      if ((int64_t)W.order.size() < a1 - a0) {  // a variable listed more than once
+        network_rows(W, m, nv, ident);
+        return;
+      }
       for (size_t j = 0; j < W.order.size(); ++j)
         for (int t = 0; t < W.mult[j]; ++t) W.card_lits.push_back(W.order[j]);
       W.card_off.push_back((int32_t)W.card_lits.size());
@@ -1167,7 +1185,55 @@ struct Lowerer {
     O.msg.push_back(msg);
   }
 
-  static void emit_record(Work& W, Out& O, int nv) {
+  // AtMost(n; ids) listing a variable more than once: the rows of gini's own
+  // encoding, CardSort(ms).Leq(n) (constraints.go:180-186), because unit
+  // propagation over a counting row is strictly stronger there (DESIGN.md
+  // §3.1).  Every And gate in the cone of m becomes an auxiliary variable
+  // (after the input's variables, in ascending node order) with its three
+  // Tseitin rows (~g a) (~g b) (g ~a ~b); then the unit row (m).  Every row
+  // carries the AtMost's identity (oracle/lower_ref.py _network_rows).
+  static void network_rows(Work& W, int32_t m, int nv, int32_t ident) {
+    const Aig& aig = W.aig;
+    const int32_t first = nv + 1;  // the first gate's node
+    W.vis.assign((size_t)(aig.next_node - first), 0);
+    W.cone.clear();
+    W.walk.assign(1, m >> 1);
+    while (!W.walk.empty()) {
+      const int32_t node = W.walk.back();
+      W.walk.pop_back();
+      if (node < first || W.vis[(size_t)(node - first)]) continue;
+      W.vis[(size_t)(node - first)] = 1;
+      W.cone.push_back(node);
+      const uint64_t key = aig.fanin[(size_t)(node - first)];
+      W.walk.push_back((int32_t)(key >> 32) >> 1);
+      W.walk.push_back((int32_t)(uint32_t)key >> 1);
+    }
+    std::sort(W.cone.begin(), W.cone.end());
+    const int32_t base = W.naux;
+    W.naux += (int32_t)W.cone.size();
+    auto lit = [&](int32_t x) -> int32_t {  // AIG literal -> record literal
+      const int32_t node = x >> 1;
+      const int32_t v = node < first ? node - 1
+                                     : base + (int32_t)(std::lower_bound(W.cone.begin(), W.cone.end(), node) -
+                                                        W.cone.begin());
+      return 2 * v + (x & 1);
+    };
+    auto row = [&](std::initializer_list<int32_t> ls) {
+      for (int32_t l : ls) W.clause_lits.push_back(l);
+      W.clause_off.push_back((int32_t)W.clause_lits.size());
+      W.clause_id.push_back(ident);
+    };
+    for (const int32_t node : W.cone) {
+      const uint64_t key = aig.fanin[(size_t)(node - first)];
+      const int32_t g = lit(2 * node), a = lit((int32_t)(key >> 32)), b = lit((int32_t)(uint32_t)key);
+      row({g ^ 1, a});
+      row({g ^ 1, b});
+      row({g, a ^ 1, b ^ 1});
+    }
+    row({lit(m)});
+  }
+
+  static void emit_record(Work& W, Out& O, int nv, int nvu = 0) {
     const int32_t nc = (int32_t)W.clause_id.size(), nk = (int32_t)W.card_id.size();
     const int32_t nch = (int32_t)W.choice_off.size() - 1;
     int32_t hdr[DP_H_SIZE] = {0};
@@ -1181,6 +1247,7 @@ struct Lowerer {
     hdr[DP_H_NCL] = (int32_t)W.clause_lits.size();
     hdr[DP_H_NKL] = (int32_t)W.card_lits.size();
     hdr[DP_H_NCHL] = (int32_t)W.choice_lits.size();
+    hdr[DP_H_NVU] = nvu;
     dp_rec_layout L = dp_rec_layout_of(hdr);
     hdr[DP_H_WORDS] = L.words;
     size_t base = O.nrec;
@@ -1549,6 +1616,7 @@ int dp_rec_validate(const int32_t* rec, int64_t words) {
   if (L.words != rec[DP_H_WORDS] || L.words > words) return -4;
   const int32_t nv = rec[DP_H_NV], nc = rec[DP_H_NC], nk = rec[DP_H_NK], nch = rec[DP_H_NCH];
   const int32_t nid = rec[DP_H_NID];
+  if (rec[DP_H_NVU] < 0 || rec[DP_H_NVU] > nv) return -21;
   std::vector<int32_t> run_starts;
   auto mono = [&](int32_t off, int32_t n, int32_t total) {
     if (rec[off] != 0 || rec[off + n] != total) return false;

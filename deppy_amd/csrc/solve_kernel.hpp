@@ -3075,10 +3075,17 @@ struct Group {
   // ------------------------------------------------------------------
   // SAT epilogue, solve.go:86-110 (oracle: epilogue)
   // ------------------------------------------------------------------
-  __device__ __forceinline__ int epilogue(int32_t& flags, uint32_t* __restrict__ out) {
+  // The extras, the fixed variables and the installed set are the input's
+  // variables 0..nvu-1 only (litMap.Variables, solve.go:88-96): an AtMost
+  // network's gates (DP_H_NVU) stay free.
+  __device__ __forceinline__ int epilogue(int32_t& flags, uint32_t* __restrict__ out, int nvu) {
+    auto ubits = [&](int i) -> uint32_t {
+      const int r = nvu - 32 * i;
+      return r >= 32 ? ~0u : r <= 0 ? 0u : (1u << r) - 1u;
+    };
     int ne = 0;
     for (int i = tid; i < nbv; i += NT) {
-      const uint32_t x = model[i] & ~inS[i];
+      const uint32_t x = model[i] & ~inS[i] & ubits(i);
       extra[i] = x;
       ne += __popc(x);
     }
@@ -3097,7 +3104,7 @@ struct Group {
       const int v = b + tid;
       bool f = false;
       int l = 0;
-      if (v < nv && !getb(extra, v)) {
+      if (v < nvu && !getb(extra, v)) {
         const int want = getb(inS, v) ? 1 : -1;
         if (val[v] == -want) bad = true;
         if (val[v] == 0) { f = true; l = 2 * v + (want < 0 ? 1 : 0); }
@@ -3125,7 +3132,7 @@ struct Group {
       const int r = dpll();
       if (r == RS_SAT) {
         extra_mode = false;
-        for (int i = tid; i < nbv; i += NT) out[i] = model[i];
+        for (int i = tid; i < nbv; i += NT) out[i] = model[i] & ubits(i);
         return DP_SAT;
       }
       if (r == RS_BUDGET) { extra_mode = false; return DP_INCOMPLETE; }
@@ -3165,6 +3172,12 @@ __device__ __forceinline__ void put_out(ProblemOut* o, int status, int32_t flags
   uint4* p = reinterpret_cast<uint4*>(o);
   p[0] = x;
   p[1] = y;
+}
+
+// The input's variable count (DP_H_NVU; 0: every variable is the input's).
+__device__ __forceinline__ int nvu_of(const int32_t* grec, int nv) {
+  const int u = grec[DP_H_NVU];
+  return u > 0 && u < nv ? u : nv;
 }
 
 // Item k of the launch: one problem, start to finish.
@@ -3215,7 +3228,7 @@ __device__ __forceinline__ void solve_item(const KernelArgs& a, int k, int4* lds
   } else if (base == 1) {
     flags |= DP_F_SEARCH_SKIPPED;
     W.save_model();
-    status = W.epilogue(flags, inst);
+    status = W.epilogue(flags, inst, nvu_of(grec, W.nv));
   } else {
     const int r = W.search();
     DP_STAMP(3);
@@ -3228,7 +3241,7 @@ __device__ __forceinline__ void solve_item(const KernelArgs& a, int k, int4* lds
       status = DP_UNSAT;
       if (!W.final_from_solve) W.analyze();  // the final root conflict (an Untest)
     } else {
-      status = W.epilogue(flags, inst);
+      status = W.epilogue(flags, inst, nvu_of(grec, W.nv));
       if (status == DP_INCOMPLETE) flags |= DP_F_BUDGET;
     }
   }

@@ -125,6 +125,12 @@ enum dp_rec_header {
   DP_H_NKL = 8,
   DP_H_NCHL = 9,
   DP_H_WORDS = 10, /* total record length in int32 words, header included */
+  /* 0, or the input's variable count when nv also counts auxiliary variables
+   * nvu..nv-1: the gates of an AtMost that lists a variable more than once,
+   * lowered as gini's sorting network (constraints.go:180-186) with its
+   * Tseitin rows.  They have no choices, are never installed and are never
+   * SAT-epilogue extras; 0 < nvu <= nv. */
+  DP_H_NVU = 11,
   DP_H_SIZE = 16
 };
 

@@ -186,6 +186,7 @@ def lower_problem(variables) -> Lowered:
     ident_owner: list[list[int]] = []
     clauses: list[tuple[list[int], int]] = []
     cards: list[tuple[list[int], int, int]] = []
+    aux: list[int] = [nv]  # next auxiliary variable (AtMost network gates)
 
     # pass 2, lit_mapping.go:59-74
     for vi, (vid, cons) in enumerate(variables):
@@ -229,7 +230,7 @@ def lower_problem(variables) -> Lowered:
                 ident = len(ident_owner)
                 key_ident[m] = ident
                 ident_owner.append([vi, ci])
-                _emit_rows(m, nv, kind, s, n, args, index, ident, clauses, cards)
+                _emit_rows(m, nv, kind, s, n, args, index, ident, clauses, cards, aig, aux)
             else:
                 ident_owner[ident] = [vi, ci]  # last writer wins, lit_mapping.go:69-72
     if errs:
@@ -249,12 +250,49 @@ def lower_problem(variables) -> Lowered:
         var_choice_off.append(len(choice_off) - 1)
         if any(kind == MANDATORY for kind, _, _ in cons):
             anchors.append(vi)
-    rec = build_record(nv, clauses, cards, var_choice_off, choice_off, choice_lits, anchors,
-                       len(ident_owner))
+    var_choice_off += [var_choice_off[-1]] * (aux[0] - nv)  # auxiliary variables: no choices
+    rec = build_record(aux[0], clauses, cards, var_choice_off, choice_off, choice_lits, anchors,
+                       len(ident_owner), nv if aux[0] > nv else 0)
     return Lowered(rec, [o[0] for o in ident_owner], [o[1] for o in ident_owner])
 
 
-def _emit_rows(m, nv, kind, s, n, args, index, ident, clauses, cards):
+def _network_rows(m, nv, aig, ident, clauses, aux):
+    """AtMost(n; ids) with an id listed more than once: the rows of the
+    reference's own encoding, CardSort(ms).Leq(n) (constraints.go:180-186).
+    Every And gate in the cone of the gate literal m gets an auxiliary
+    variable (after the input's variables, in ascending node order) and its
+    three Tseitin clauses [~g a] [~g b] [g ~a ~b]; then the unit [m].  Unit
+    propagation over them derives exactly what gini's does over the gates
+    (the counting row is strictly stronger with repeated ids, DESIGN.md
+    §3.1).  Every row carries the AtMost's identity."""
+    rev = {g: ab for ab, g in aig.strash.items()}
+    cone, todo = set(), [m & ~1]
+    while todo:
+        g = todo.pop()
+        if g in cone or g not in rev:
+            continue
+        cone.add(g)
+        a, b = rev[g]
+        todo += [a & ~1, b & ~1]
+    var = {}
+    for g in sorted(cone):
+        var[g] = aux[0]
+        aux[0] += 1
+
+    def lit(x):  # AIG literal -> record literal (inputs: 2 * (node - 1))
+        node = x >> 1
+        v = node - 1 if 1 <= node <= nv else var[x & ~1]
+        return 2 * v + (x & 1)
+
+    for g in sorted(cone):
+        a, b = rev[g]
+        clauses.append(([lit(g) ^ 1, lit(a)], ident))
+        clauses.append(([lit(g) ^ 1, lit(b)], ident))
+        clauses.append(([lit(g), lit(a) ^ 1, lit(b) ^ 1], ident))
+    clauses.append(([lit(m)], ident))
+
+
+def _emit_rows(m, nv, kind, s, n, args, index, ident, clauses, cards, aig=None, aux=None):
     if m == F:
         clauses.append(([], ident))
         return
@@ -282,13 +320,16 @@ def _emit_rows(m, nv, kind, s, n, args, index, ident, clauses, cards):
                 order.append(v)
                 mult[v] = 0
             mult[v] += 1
+        if len(order) < len(args) and aig is not None:  # an id listed more than once
+            _network_rows(m, nv, aig, ident, clauses, aux)
+            return
         pos = [v for v in order for _ in range(mult[v])]
         cards.append((pos, n, ident))
     else:  # Mandatory / Prohibited always lower to an input literal
         raise AssertionError("unexpected gate literal for kind %d" % kind)
 
 
-def build_record(nv, clauses, cards, var_choice_off, choice_off, choice_lits, anchors, nid):
+def build_record(nv, clauses, cards, var_choice_off, choice_off, choice_lits, anchors, nid, nvu=0):
     nc, nk = len(clauses), len(cards)
     clause_off = [0]
     clause_lits: list[int] = []
@@ -304,7 +345,7 @@ def build_record(nv, clauses, cards, var_choice_off, choice_off, choice_lits, an
             + [c[1] for c in cards] + [c[2] for c in cards] + var_choice_off + choice_off
             + choice_lits + anchors)
     hdr = [REC_MAGIC, nv, nc, nk, len(choice_off) - 1, len(anchors), nid, len(clause_lits),
-           len(card_lits), len(choice_lits), 0, 0, 0, 0, 0, 0]
+           len(card_lits), len(choice_lits), 0, nvu, 0, 0, 0, 0]  # [11]: input variables when nv counts auxiliaries
     rec = np.array(hdr + body, dtype=np.int32)
     rec[10] = len(rec)
     return rec

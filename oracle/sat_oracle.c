@@ -45,6 +45,7 @@ enum { CK_NONE = 0, CK_ROW, CK_VAR, CK_ASSUME, CK_EXTRA };
 
 typedef struct {
   int nv, nc, nk, nch, na, nid, nrows;
+  int nvu; /* the input's variables: nvu..nv-1 are an AtMost network's gates (DP_H_NVU) */
   const int32_t *clause_off, *clause_lits, *clause_id;
   const int32_t *card_off, *card_lits, *card_bound, *card_id;
   const int32_t *var_choice_off, *choice_off, *choice_lits, *anchors;
@@ -135,6 +136,7 @@ static void parse(prob_t* p, const int32_t* rec) {
   p->nch = rec[DP_H_NCH];
   p->na = rec[DP_H_NA];
   p->nid = rec[DP_H_NID];
+  p->nvu = rec[DP_H_NVU] > 0 ? rec[DP_H_NVU] : p->nv;
   p->nrows = p->nc + p->nk;
   p->clause_off = rec + L.clause_off;
   p->clause_lits = rec + L.clause_lits;
@@ -1142,8 +1144,12 @@ static int core_extract(st_t* s, int32_t* core, int32_t* flags) {
 
 static int epilogue(st_t* s, int32_t* flags, uint32_t* installed) {
   const prob_t* p = &s->p;
-  int nv = p->nv, ne = 0;
-  int nw = (nv + 31) / 32;
+  /* the extras, the fixed variables and the installed set are the input's
+   * variables only (litMap.Variables, solve.go:88-96); the network's gates
+   * stay free */
+  int nv = p->nvu, ne = 0;
+  int nw = (p->nv + 31) / 32;
+  for (int v = 0; v < p->nv; ++v) s->is_extra[v] = 0;
   for (int v = 0; v < nv; ++v) {
     int mv = (s->model[v >> 5] >> (v & 31)) & 1;
     s->is_extra[v] = (uint8_t)(!s->inS[v] && mv);
@@ -1177,7 +1183,9 @@ static int epilogue(st_t* s, int32_t* flags, uint32_t* installed) {
     int r = dpll(s);
     if (r == R_SAT) {
       s->extra_mode = 0;
-      memcpy(installed, s->model, (size_t)nw * 4);
+      memset(installed, 0, (size_t)nw * 4);
+      for (int v = 0; v < nv; ++v)
+        if ((s->model[v >> 5] >> (v & 31)) & 1) installed[v >> 5] |= 1u << (v & 31);
       return DP_SAT;
     }
     if (r == R_BUDGET) { s->extra_mode = 0; return DP_INCOMPLETE; }

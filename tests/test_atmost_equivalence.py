@@ -149,8 +149,10 @@ def test_network_up_vs_counting_multiplicity(seed):
     the network derives, counting derives too, but counting also forces a
     variable whose multiplicity alone exceeds the room left (cnt + m > n),
     which UP over the network sees only in some network shapes (And(x,x)=x
-    folds some of them).  A known deviation: the generator and
-    catalogs list every id once, where the two are equal (tests above)."""
+    folds some of them).  So the lowering does not give such a row a counting
+    row: it emits the network's Tseitin rows (tests/test_atmost_network.py,
+    DESIGN.md §3.1); the tests above are why a row listing every id once keeps
+    its counting row."""
     rng = np.random.default_rng(100 + seed)
     stronger = 0
     for _ in range(25):
