@@ -336,8 +336,12 @@ struct Layout {
 
 // S_NTB / S_CVB / S_OVB: two banks each (alternate LDS-table rounds) of the
 // round's first-implication count, lowest variable implied both ways (stored
-// as INF - v, 0 none) and table-overflow flag.
-enum Scalar { S_NTOUCHED = 0, S_NWORK = 1, S_NK = 2, S_APP = 3, S_NTB = 4, S_CVB = 6, S_OVB = 8, S_SLOT = 32 };
+// as INF - v, 0 none) and table-overflow flag.  S_POSROWS: the record has
+// auxiliary variables (DP_H_NVU), so clause rows without a negative literal
+// (an AtMost network's (g a b) rows) can be violated by the all-false
+// completion (Group::first_violated scans every row).
+// (M_LDS has slots 0..7 only.)
+enum Scalar { S_NTOUCHED = 0, S_NWORK = 1, S_POSROWS = 2, S_APP = 3, S_NTB = 4, S_CVB = 6, S_OVB = 8, S_SLOT = 32 };
 
 // Multi-wave modes whose per-variable state is in LDS keep a round's state
 // there too (Layout::hkey..fr); M_HBM keeps it in HBM.

@@ -671,7 +671,10 @@ struct Group {
       d_flip[i] = 0; inS[i] = 0; extra[i] = 0; seen[i] = 0; model[i] = 0; dset[i] = 0; fg[i] = 0;
     }
     for (int i = tid; i < mode_nscal(MODE); i += NT) scal[i] = 0;
-    if (tid == 0) l_off[0] = 0;
+    if (tid == 0) {  // (after the zeroing in program order: both are wavefront 0's stores)
+      l_off[0] = 0;
+      scal[S_POSROWS] = h[DP_H_NVU] > 0;
+    }
     if constexpr (TWL || RSLOT)  // every row watches its first two literals (nothing is assigned yet)
       for (int r = tid; r < nc; r += NT) {
         const int a = clause_off[r], b = clause_off[r + 1], len = b - a;
@@ -2345,9 +2348,11 @@ struct Group {
   // The lowest clause row the all-false completion violates -> its first
   // unassigned positive literal (the decision), or -1.  Such a row has a
   // positive literal but no true one, and every negative literal on a true
-  // variable, so it is in the watch list of some true positive literal:
-  // threads scan the watch lists of the variables assigned true instead of
-  // every clause row (same answer as the oracle's full scan).
+  // variable, so, when it has a negative literal, it is in the watch list of
+  // some variable assigned true: threads scan those lists instead of every
+  // clause row (same answer as the oracle's full scan).  Rows without a
+  // negative literal are units (assigned at the base) except an AtMost
+  // network's (g a b) rows: records with auxiliary variables scan every row.
   __device__ __forceinline__ int first_violated() {
 #ifdef DP_STAMPS
     const int64_t t0 = stamp();
@@ -2361,7 +2366,7 @@ struct Group {
     int best = INF;
     // (two-watched lists no longer hold every row a true literal occurs in:
     // scan the rows)
-    if (nc <= 4 * NT || (TWLL && twl_on)) {
+    if (nc <= 4 * NT || (TWLL && twl_on) || scal[S_POSROWS]) {
       // few rows: every thread scans its rows in ascending order (the
       // oracle's scan, a short dependent chain per thread)
       for (int c = tid; c < nc; c += NT) {
