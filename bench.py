@@ -335,10 +335,10 @@ def main():
                     help="skip the host-to-host leg (profiling runs of the solve kernel)")
     ap.add_argument("--flags", type=int, default=0,
                     help="dp_opts.flags (diagnostic placements: 1 group, 2 HBM, 4 mid groups)")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r04_pmc_traffic.jsonl"),
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r05_pmc_traffic.jsonl"),
                     help="HBM bytes per solve kernel dispatch from separate rocprofv3 --pmc passes; "
                          "used for roofline.traffic when its config/problems match")
-    ap.add_argument("--sq-json", default=os.path.join(ROOT, "profiles", "r04_sq_split.json"),
+    ap.add_argument("--sq-json", default=os.path.join(ROOT, "profiles", "r05_sq_split.json"),
                     help="SQ instruction counts per wave of this build (scripts/pmc_sq_r02.sh + sq_summary.py), "
                          "for roofline.issue")
     args = ap.parse_args()
@@ -527,6 +527,12 @@ def main():
                             "traffic_over_algorithmic": round(traffic / alg, 3) if traffic else None,
                             "issue": issue_roofline(args.sq_json, args.config,
                                                     n * ksteps / tk if tk == tk else None)}
+        # the same bytes at the sustained rate: batches in flight, records resident
+        # (algorithmic bytes per batch / kernel_only.ms_per_step)
+        sus = alg / (tk / ksteps) / 1e9 if tk == tk else None  # (--kernel-only keeps launches serial)
+        line["roofline"]["sustained"] = None if sus is None else {
+            "achieved": round(sus, 3), "frac": round(sus / HBM_PEAK_GBS, 6), "ms_per_batch": round(tk / ksteps * 1e3, 4),
+            "note": "algorithmic bytes / kernel_only.ms_per_step (%d batches in flight)" % kdepth}
 
     if rank == 0 and not args.no_cpu:
         from oracle import oracle  # CPU baseline + checker only
