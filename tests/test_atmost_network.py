@@ -324,3 +324,21 @@ def test_gpu_network_through_sat_api():
                 var = vs[int(lw.ident_var[i0 + i])]
                 want.append(str(sat.AppliedConstraint(var, var.Constraints()[int(lw.ident_con[i0 + i])])))
             assert [str(a) for a in err] == want, p
+
+
+def test_nvu_header_validated():
+    """dp_rec_validate refuses an input-variable count outside 0..nv
+    (DP_H_NVU, include/deppy_hip.h) and accepts the lowering's own."""
+    lw = _lib.Lowered(sat.encode_inputs([FIXED[3]]))
+    r = np.ascontiguousarray(lw.record(0)).copy()
+    L = _lib.lib()
+    nv = int(r[H_NV])
+    assert 0 < int(r[H_NVU]) < nv
+    for bad in (-1, nv + 1):
+        r2 = r.copy()
+        r2[H_NVU] = bad
+        assert L.dp_rec_validate(r2.ctypes.data_as(_lib.c_i32p), len(r2)) == -21
+    for ok in (0, nv):
+        r2 = r.copy()
+        r2[H_NVU] = ok
+        assert L.dp_rec_validate(r2.ctypes.data_as(_lib.c_i32p), len(r2)) == 0
