@@ -656,7 +656,7 @@ bool pinned_range(const void* p, size_t bytes) {
 // Byte layout of a chunk's input region (identical in pinned host memory and
 // on the device, so one copy moves it) and of its output region.
 struct InLayout {
-  size_t img, items, scratch_off, end;
+  size_t img, items, pool_len, scratch_off, end;
 };
 struct OutLayout {
   size_t prob, installed, pool_len, pool, end;
@@ -670,6 +670,7 @@ InLayout in_layout(const Plan& P) {
   size_t o = 0;
   L.img = o;         o = al(o + (size_t)P.img_words * 4);
   L.items = o;       o = al(o + P.order.size() * sizeof(dp::WorkItem));
+  L.pool_len = o;    o = al(o + 4);  // the core pool's counter, zeroed by the chunk's H2D copy
   L.scratch_off = o; o = al(o + P.scratch_off.size() * 8);
   L.end = o;
   return L;
@@ -695,6 +696,7 @@ void fill_in_tables(const Plan& P, const InLayout& L, char* base) {
     const int32_t i = P.order[k];
     it[k] = dp::WorkItem{P.dev_off[(size_t)i], (int32_t)P.inst_off[(size_t)i], i};
   }
+  *reinterpret_cast<int32_t*>(base + L.pool_len) = 0;
   if (!P.scratch_off.empty()) std::memcpy(base + L.scratch_off, P.scratch_off.data(), P.scratch_off.size() * 8);
 }
 
@@ -1291,9 +1293,18 @@ int start_chunk(dp_ctx* ctx, Device& D, Lane& L, dp_job* job, int32_t p0, int32_
   if (cs != L.s || chain) HIP_OK(hipEventRecord(L.copied, cs));
   if (cs != L.s) HIP_OK(hipStreamWaitEvent(L.s, L.copied, 0));
   D.last_copied = chain ? L.copied : nullptr;  // (a chain restarts after an unchained chunk)
-  HIP_OK(hipMemsetAsync(L.d_out.p + L.ol.pool_len, 0, 4, L.s));
   dp::KernelArgs a = kernel_args(il, L.ol, din, dout, reinterpret_cast<int32_t*>(L.scratch.p), ctx->budget);
-  a.core_pool_len = at<int32_t>(L.d_out.p, L.ol.pool_len);
+  static const bool pool_memset = env_i64("DEPPY_POOL_MEMSET", 0) != 0;  // diagnostic: 1 = the fill kernel
+  if (!zc_in && L.zc_out && !pool_memset) {
+    // the pool's counter in the input region, zeroed by the copy above: one
+    // dispatch fewer per chunk (a fill kernel, ~58 us under load in the
+    // r05_final kernel traces); host to host measured the same either way
+    // (profiles/r05_pool_ab.txt)
+    a.core_pool_len = at<int32_t>(din, il.pool_len);
+  } else {  // (the host reads the counter back from the output region)
+    HIP_OK(hipMemsetAsync(L.d_out.p + L.ol.pool_len, 0, 4, L.s));
+    a.core_pool_len = at<int32_t>(L.d_out.p, L.ol.pool_len);
+  }
   a.items = at<dp::WorkItem>(din, il.items);
   HIP_OK(hipEventRecord(L.k0, L.s));
   set_siblings(D, (int)(&L - D.lanes) % D.nstreams, L.spread, ctx->spread);
