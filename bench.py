@@ -106,7 +106,7 @@ def maybe_relaunch(args) -> None:
     sys.exit(subprocess.call(cmd, env=env))
 
 
-FORMS = {0: "I32", 1: "U16", 3: "P16", 4: "I32W", 5: "P16D"}
+FORMS = {0: "I32", 1: "U16", 3: "P16", 4: "I32W", 5: "P16D", 6: "P8D"}
 
 
 def record_forms(lw) -> dict:
@@ -221,7 +221,7 @@ def lowered_config(config, n, seed, form="packed"):
         "prob_var_off", "var_id", "var_con_off", "con_kind", "con_n", "con_arg_off", "con_arg",
         "str_off")}, str_bytes=w["str_bytes"].tobytes())
     lw32 = _lib.Lowered(wa)
-    lw = _lib.Lowered(wa, narrow=form != "i32", pinned=True, packed=form == "packed")
+    lw = _lib.Lowered(wa, narrow=form != "i32", pinned=True, packed=form in ("packed", "p16d"), p8=form != "p16d")
     reps, t0 = 0, time.perf_counter()
     while reps < 3 or time.perf_counter() - t0 < 1.0:
         lw.relower(wa)
@@ -324,9 +324,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--kernel-steps", type=int, default=20,
                     help="steps of the device-resident (kernel-only) secondary figure; 0: skip")
-    ap.add_argument("--record-form", choices=("packed", "u16", "i32"), default="packed",
-                    help="the records the GPU legs are given: dp_lower_into NARROW|PACKED (P16D/P16, default), "
-                         "NARROW (U16) or int32 (staged by the host)")
+    ap.add_argument("--record-form", choices=("packed", "p16d", "u16", "i32"), default="packed",
+                    help="the records the GPU legs are given: dp_lower_into NARROW|PACKED (P8D/P16D/P16, "
+                         "default), NARROW|PACKED|NO_P8 (P16D/P16: A/B), NARROW (U16) or int32 (staged by the host)")
     ap.add_argument("--e2e-steps", type=int, default=10,
                     help="steps of the lowering-inclusive (wire -> results) secondary figure; 0: skip")
     ap.add_argument("--kernel-depth", type=int, default=0,
@@ -424,6 +424,8 @@ def main():
         "data": "synthetic",
         "config": {"workload": wl[2] % (n // nd), "catalogs_per_step_per_gpu": n // nd,
                    "record_forms": record_forms(lw),
+                   "placements": {k: v // max(args.steps, 1) for k, v in st["placed"].items() if v},
+                   "placement_launches": {k: v // max(args.steps, 1) for k, v in st["placed_launches"].items() if v},
                    "parallelism": ("dp%d (host partition; one process, dp_create(n_devices=%d))" % (nd, nd)
                                    if nd > 1 else "dp%d (host partition; one process per GPU)" % world),
                    "n_devices_per_process": nd, "chunks_per_device_timed": per_device, "seed": args.seed,

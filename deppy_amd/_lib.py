@@ -95,7 +95,7 @@ EXPORTS = [
     "dp_launch", "dp_wait", "dp_download", "dp_resident_free", "dp_last_kernel_ms", "dp_gen_catalogs", "dp_gen_wire",
     "dp_gen_free", "dp_upload_traced", "dp_download_trace", "dp_solve_traced", "dp_lowered_errors",
     "dp_device_bytes", "dp_lower_into", "dp_lowered_new", "dp_lowered_exact_count", "dp_lowered_pinned", "dp_rec_widen", "dp_submit", "dp_job_wait", "dp_get_stats", "dp_stage_roundtrip",
-    "dp_stitch_selftest", "dp_partition", "dp_build_info", "dp_get_device_stats",
+    "dp_stitch_selftest", "dp_partition", "dp_build_info", "dp_get_device_stats", "dp_plan_placements",
 ]
 
 
@@ -126,7 +126,19 @@ class Stats(ctypes.Structure):
                 ("kernel_ms", ctypes.c_double), ("h2d_bytes", ctypes.c_int64), ("d2h_bytes", ctypes.c_int64),
                 ("rec_bytes", ctypes.c_int64), ("stage_ms", ctypes.c_double), ("plan_ms", ctypes.c_double), ("wait_ms", ctypes.c_double),
                 ("scatter_ms", ctypes.c_double), ("direct_chunks", ctypes.c_int64),
-                ("bcp_bytes", ctypes.c_int64), ("allocs", ctypes.c_int64)]
+                ("bcp_bytes", ctypes.c_int64), ("allocs", ctypes.c_int64),
+                ("placed", ctypes.c_int64 * 5), ("placed_launches", ctypes.c_int64 * 5)]
+
+# enum dp_place (include/deppy_hip.h), the index of Stats.placed
+PLACES = ["lds", "split", "hbm", "split4", "ldsg"]
+
+
+def _stats_dict(st) -> dict:
+    d = {}
+    for k, _ in Stats._fields_:
+        v = getattr(st, k)
+        d[k] = {PLACES[m]: int(v[m]) for m in range(5)} if k.startswith("placed") else v
+    return d
 
 
 class Batch(ctypes.Structure):
@@ -239,6 +251,7 @@ def lib():
     L.dp_gen_wire.restype = ctypes.POINTER(Wire)
     L.dp_gen_free.argtypes = [vp]
     L.dp_device_bytes.argtypes = [ctypes.POINTER(Batch), ctypes.c_int32, c_i64p, c_i64p]
+    L.dp_plan_placements.argtypes = [ctypes.POINTER(Batch), ctypes.c_int32, c_i8p]
     _lib = L
     return L
 
@@ -352,18 +365,20 @@ class Lowered:
     relower(wire) lowers another batch into the same storage
     (dp_lower_into), invalidating the previous views' contents."""
 
-    def __init__(self, wire: WireArrays, narrow: bool = False, pinned: bool = False, packed: bool = False):
+    def __init__(self, wire: WireArrays, narrow: bool = False, pinned: bool = False, packed: bool = False,
+                 p8: bool = True):
         """narrow: records that fit 16 bits in the DP_FMT_U16 form, each on a
         16-byte boundary (the staged form, DP_LOWER_NARROW); default int32
         records.  pinned: the records in page-locked memory when a GPU is
         present (DP_LOWER_PINNED; with narrow, dp_submit copies them to the
-        device without staging).  packed (with narrow): the DP_FMT_P16 form
-        where it applies (DP_LOWER_PACKED; a fifth fewer bytes)."""
+        device without staging).  packed (with narrow): the packed forms
+        where they apply (DP_LOWER_PACKED: DP_FMT_P8D, DP_FMT_P16D or
+        DP_FMT_P16); p8=False keeps DP_FMT_P16D (DP_LOWER_NO_P8)."""
         L = lib()
         h = ctypes.c_void_p()
         ws = wire.struct()
         self.narrow = narrow
-        self._flags = (1 if narrow else 0) | (2 if pinned else 0) | (4 if packed else 0)
+        self._flags = (1 if narrow else 0) | (2 if pinned else 0) | (4 if packed else 0) | (0 if p8 else 8)
         if self._flags:
             h = ctypes.c_void_p(L.dp_lowered_new())
             if L.dp_lower_into(ctypes.byref(ws), self._flags, h) != 0:
@@ -472,7 +487,7 @@ class Context:
     def stats(self, reset: bool = False) -> dict:
         st = Stats()
         lib().dp_get_stats(self.h, ctypes.byref(st), 1 if reset else 0)
-        return {k: getattr(st, k) for k, _ in Stats._fields_}
+        return _stats_dict(st)
 
     def devices(self) -> int:
         """Logical devices of the context (dp_num_devices)."""
@@ -483,7 +498,7 @@ class Context:
         st = Stats()
         if lib().dp_get_device_stats(self.h, device, ctypes.byref(st), 1 if reset else 0) != 0:
             raise ValueError("dp_get_device_stats: no device %d" % device)
-        return {k: getattr(st, k) for k, _ in Stats._fields_}
+        return _stats_dict(st)
 
     def last_kernel_ms(self) -> float:
         ms = ctypes.c_double()
@@ -616,6 +631,17 @@ def device_bytes(rec_off, rec, flags: int = 0) -> tuple[int, int]:
     if lib().dp_device_bytes(ctypes.byref(_batch(rec_off, rec)), flags, ctypes.byref(rb), ctypes.byref(ib)) != 0:
         raise RuntimeError("dp_device_bytes failed")
     return rb.value, ib.value
+
+
+def plan_placements(rec_off, rec, flags: int = 0) -> np.ndarray:
+    """Per-problem placement dp_submit plans for a batch cut as one chunk
+    (dp_plan_placements: an index into PLACES, or -1 malformed / -2 too large)."""
+    rec_off = np.ascontiguousarray(rec_off, np.int64)
+    rec = np.ascontiguousarray(rec if len(rec) else np.zeros(1, np.int32), np.int32)
+    place = np.zeros(max(len(rec_off) - 1, 1), np.int8)
+    if lib().dp_plan_placements(ctypes.byref(_batch(rec_off, rec)), flags, _p(place, c_i8p)) != 0:
+        raise RuntimeError("dp_plan_placements failed")
+    return place[:len(rec_off) - 1]
 
 
 def stage_roundtrip(rec_off, rec, flags: int = 0, chunk_problems: int = 0, chunk_bytes: int = 0):

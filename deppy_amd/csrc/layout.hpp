@@ -44,6 +44,9 @@ constexpr int32_t L_MAX = 64;
 //         No HBM scratch: every per-literal array, watch list and learned row
 //         is LDS.
 enum Mode { M_LDS = 0, M_SPLIT = 1, M_HBM = 2, M_SPLIT4 = 3, M_LDSG = 4 };
+static_assert((int)M_LDS == DP_PLACE_LDS && (int)M_SPLIT == DP_PLACE_SPLIT && (int)M_HBM == DP_PLACE_HBM &&
+                  (int)M_SPLIT4 == DP_PLACE_SPLIT4 && (int)M_LDSG == DP_PLACE_LDSG,
+              "enum dp_place (include/deppy_hip.h) names the placements");
 // The 16-bit LDS image (M_LDS, M_LDSG): record and working set in LDS
 __host__ __device__ constexpr bool mode_n16(int mode) { return mode == M_LDS || mode == M_LDSG; }
 #ifndef DP_BIG_WAVES
@@ -133,14 +136,18 @@ __host__ __device__ constexpr int32_t mode_nscal(int mode) {
 }
 
 // dp_p16_tail_at / dp_p16_tail_bytes (include/deppy_hip.h) for device code.
+__host__ __device__ inline bool fmt_derived(int32_t fmt) { return fmt == DP_FMT_P16D || fmt == DP_FMT_P8D; }
+__host__ __device__ inline bool fmt_packed(int32_t fmt) { return fmt == DP_FMT_P16 || fmt_derived(fmt); }
 __host__ __device__ inline int64_t p16_tail_at(const int32_t* h) {
-  const int64_t ch = h[DP_H_FMT] == DP_FMT_P16D ? 0 : h[DP_H_NCHL];
+  const int64_t ch = fmt_derived(h[DP_H_FMT]) ? 0 : h[DP_H_NCHL];
   return (2 * ((int64_t)h[DP_H_NCL] + h[DP_H_NKL] + h[DP_H_NK] + ch + h[DP_H_NA]) + 15) & ~(int64_t)15;
 }
 __host__ __device__ inline int64_t p16_tail_bytes(const int32_t* h) {
-  const int64_t vc = h[DP_H_FMT] == DP_FMT_P16D ? 0 : (int64_t)h[DP_H_NV];
+  const int64_t vc = fmt_derived(h[DP_H_FMT]) ? 0 : (int64_t)h[DP_H_NV];
   return (int64_t)h[DP_H_NC] + h[DP_H_NK] + h[DP_H_NCH] + vc + ((int64_t)h[DP_H_NID] + 7) / 8;
 }
+// DP_FMT_P8D: the body's bytes (header word DP_H_P8, bits 8..)
+__host__ __device__ inline int32_t p8_bytes(const int32_t* h) { return (int32_t)((uint32_t)h[DP_H_P8] >> 8); }
 // 16-bit words of a record's body (the arrays after the header) as the
 // one-wavefront kernel decodes it into LDS: the int32 form's, except that
 // DP_FMT_P16D's choice lists stay in the dependency rows they are implied
@@ -156,15 +163,18 @@ __host__ __device__ inline int32_t id_mask_words16(const int32_t* h) {
 }
 __host__ __device__ inline int32_t lds_body_words(const int32_t* h) {
   int32_t b = h[DP_H_WORDS] - DP_H_SIZE;
-  if (h[DP_H_FMT] == DP_FMT_P16 || h[DP_H_FMT] == DP_FMT_P16D)
-    b += id_mask_words16(h) - h[DP_H_NC] - h[DP_H_NK];
-  return h[DP_H_FMT] == DP_FMT_P16D ? b - 1 - h[DP_H_NCHL] : b;
+  if (fmt_packed(h[DP_H_FMT])) b += id_mask_words16(h) - h[DP_H_NC] - h[DP_H_NK];
+  return fmt_derived(h[DP_H_FMT]) ? b - 1 - h[DP_H_NCHL] : b;
 }
 // Byte offset (in the M_LDS body region) of the packed tail's copy while the
 // kernel decodes it: the first 16-byte boundary past the decoded 16-bit
-// arrays (lds_body_words).
+// arrays (lds_body_words).  DP_FMT_P8D: where its record lands (LDS-DMA),
+// its DP_FMT_P16D tail decoded right after it (p8_tail).
 __host__ __device__ inline int32_t p16_tail_copy(const int32_t* h) {
   return (2 * lds_body_words(h) + 15) & ~15;
+}
+__host__ __device__ inline int32_t p8_tail(const int32_t* h) {
+  return p16_tail_copy(h) + ((p8_bytes(h) + 15) & ~15);
 }
 
 // dp_rec_layout_of (include/deppy_hip.h) for host and device code.
@@ -355,7 +365,7 @@ __host__ __device__ inline int32_t round_slots(int32_t nv) {
 }
 
 template <int MODE>
-__host__ __device__ inline Layout layout(const int32_t* h) {
+__host__ __device__ inline Layout layout_hc(const int32_t* h, int32_t hc) {
   constexpr bool N16 = mode_n16(MODE);
   using IX = typename std::conditional<N16, uint16_t, int32_t>::type;
   Layout L;
@@ -381,8 +391,9 @@ __host__ __device__ inline Layout layout(const int32_t* h) {
   // watch lists go later) while it is decoded: the region covers that copy.
   int32_t body_bytes = (X.words - DP_H_SIZE + 8) * ix;
   if (N16) body_bytes = (lds_body_words(h) + (X.words - h[DP_H_WORDS]) + 8) * ix;
-  if (N16 && (h[DP_H_FMT] == DP_FMT_P16 || h[DP_H_FMT] == DP_FMT_P16D)) {
-    const int32_t need = p16_tail_copy(h) + (int32_t)((p16_tail_bytes(h) + 15) & ~15);
+  if (N16 && fmt_packed(h[DP_H_FMT])) {
+    const int32_t tail = h[DP_H_FMT] == DP_FMT_P8D ? p8_tail(h) : p16_tail_copy(h);
+    const int32_t need = tail + (int32_t)((p16_tail_bytes(h) + 15) & ~15);
     body_bytes = body_bytes > need ? body_bytes : need;
   }
   L.body = N16 ? take(body_bytes, COLD) : 0;
@@ -390,14 +401,7 @@ __host__ __device__ inline Layout layout(const int32_t* h) {
   L.wbuf = take(mode_wbuf(MODE) * ix, WORK);
   // (multi-wave: each queued row's row_info after the queue, cardq[cq + i])
   L.cardq = take(mode_cq(MODE) * ix * (N16 ? 1 : 2), WORK);
-  // the table shrinks (to 64 slots at least) when the catalog's per-variable
-  // state leaves less LDS, so it never moves a catalog off this placement
-  L.hc = mode_lds_rounds(MODE) ? round_slots(nv) : 0;
-  if (mode_lds_rounds(MODE)) {
-    auto a16 = [](int32_t x) { return (x + 15) & ~15; };
-    const int32_t rest = ol + a16(nv) + 7 * a16(nbv * 4) + 3 * a16(nbi * 4);  // work lists so far + val + bitsets
-    while (L.hc > 64 && rest + 20 * L.hc > 160 * 1024) L.hc >>= 1;
-  }
+  L.hc = mode_lds_rounds(MODE) ? hc : 0;
   L.hkey = take(L.hc * 4, WORK);
   L.hrp = take(L.hc * 4, WORK);
   L.hrn = take(L.hc * 4, WORK);
@@ -435,6 +439,21 @@ __host__ __device__ inline Layout layout(const int32_t* h) {
   L.fcur = mode_twl_lds(MODE) ? take(64 * 4, COLD) : 0;
   L.bytes = og;
   L.lds_bytes = ol;
+  return L;
+}
+
+// The round table shrinks (to 64 slots at least) when the catalog's
+// per-variable state leaves less LDS, so it never moves a catalog off this
+// placement.  The budget is the layout itself (every array layout_hc takes),
+// not a formula beside it: round 5 added an identity bitset (crit) that a
+// hand-written budget left out, and every OLM-scale catalog fell to M_HBM.
+constexpr int32_t kLdsLimitBytes = 160 * 1024;  // LDS per CU on gfx950
+template <int MODE>
+__host__ __device__ inline Layout layout(const int32_t* h) {
+  if (!mode_lds_rounds(MODE)) return layout_hc<MODE>(h, 0);
+  int32_t hc = round_slots(h[DP_H_NV]);
+  Layout L = layout_hc<MODE>(h, hc);
+  while (hc > 64 && L.lds_bytes > kLdsLimitBytes) L = layout_hc<MODE>(h, hc >>= 1);
   return L;
 }
 

@@ -475,6 +475,116 @@ bool choice_sources(const int32_t* r, const dp_rec_layout& L, uint8_t* src) {
   return row >= nc;  // every dependency row taken
 }
 
+// DP_FMT_P8D (include/deppy_hip.h) -> the DP_FMT_P16D record it encodes,
+// into p16 (header + body, DP_H_P8 cleared).  0, or < 0 when the flags are
+// unknown, the body is shorter than its sections or a src value marked
+// nonzero is zero (dp_rec_widen then checks the DP_FMT_P16D record).
+int p8_to_p16d(const int32_t* rec, int64_t avail, std::vector<int32_t>& p16) {
+  const uint32_t w14 = (uint32_t)rec[DP_H_P8];
+  const int32_t f = (int32_t)(w14 & 0xffu);
+  const int64_t bytes = w14 >> 8;
+  if (f & ~(DP_P8_B1 | DP_P8_HI | DP_P8_NIB)) return -22;
+  if (DP_H_SIZE + (bytes + 3) / 4 > avail) return -4;
+  const dp_p8_layout P = dp_p8_layout_of(rec);
+  const int64_t ncl = rec[DP_H_NCL], nkl = rec[DP_H_NKL], nk = rec[DP_H_NK], na = rec[DP_H_NA];
+  const int64_t nc = rec[DP_H_NC], nch = rec[DP_H_NCH], nid = rec[DP_H_NID];
+  if (P.srcval > bytes) return -22;
+  const uint8_t* b = reinterpret_cast<const uint8_t*>(rec + DP_H_SIZE);
+  auto bit = [&](int64_t at, int64_t j) -> int { return (b[at + (j >> 3)] >> (j & 7)) & 1; };
+  int64_t nz = 0;
+  for (int64_t k = 0; k < nch; ++k) nz += bit(P.srcnz, k);
+  if (dp_p8_body_bytes(rec, nz) > bytes) return -22;
+  int32_t hdr[DP_H_SIZE];
+  std::memcpy(hdr, rec, sizeof hdr);
+  hdr[DP_H_FMT] = DP_FMT_P16D;
+  hdr[DP_H_P8] = 0;
+  const int64_t at = dp_p16_tail_at(hdr), tb = dp_p16_tail_bytes(hdr);
+  p16.assign((size_t)(DP_H_SIZE + (at + tb + 3) / 4), 0);
+  std::memcpy(p16.data(), hdr, sizeof hdr);
+  uint16_t* u = reinterpret_cast<uint16_t*>(p16.data() + DP_H_SIZE);
+  const bool hi = f & DP_P8_HI;
+  auto var = [&](int64_t lo, int64_t hp, int64_t j) -> int { return b[lo + j] | (hi ? bit(hp, j) << 8 : 0); };
+  for (int64_t j = 0; j < ncl; ++j) *u++ = (uint16_t)(2 * var(P.cvar, P.chi, j) + bit(P.neg, j));
+  for (int64_t j = 0; j < nkl; ++j) *u++ = (uint16_t)var(P.kvar, P.khi, j);
+  for (int64_t k = 0; k < nk; ++k) *u++ = (uint16_t)((f & DP_P8_B1) ? 1 : b[P.bound + k]);
+  for (int64_t i = 0; i < na; ++i) *u++ = (uint16_t)var(P.avar, P.ahi, i);
+  uint8_t* t = reinterpret_cast<uint8_t*>(p16.data() + DP_H_SIZE) + at;
+  for (int64_t i = 0; i < nc + nk; ++i)
+    *t++ = (f & DP_P8_NIB) ? (uint8_t)((b[P.lens + (i >> 1)] >> (4 * (i & 1))) & 15) : b[P.lens + i];
+  int64_t q = 0;
+  for (int64_t k = 0; k < nch; ++k) {
+    if (!bit(P.srcnz, k)) { *t++ = 0; continue; }
+    if (b[P.srcval + q] == 0) return -22;
+    *t++ = b[P.srcval + q++];
+  }
+  std::memcpy(t, b + P.srcval + nz, (size_t)((nid + 7) / 8));
+  return 0;
+}
+
+// The DP_FMT_P16D record r in the DP_FMT_P8D form, in place, when it applies
+// (at most DP_P8_MAX_VARS variables, every AtMost bound below 256).  Returns
+// its words as it lies (dp_rec_phys_words), or 0 with r unchanged.
+int64_t pack8(int32_t* r) {
+  if (r[DP_H_FMT] != DP_FMT_P16D || r[DP_H_NV] > DP_P8_MAX_VARS) return 0;
+  const int64_t ncl = r[DP_H_NCL], nkl = r[DP_H_NKL], nk = r[DP_H_NK], na = r[DP_H_NA];
+  const int64_t nc = r[DP_H_NC], nch = r[DP_H_NCH], nid = r[DP_H_NID];
+  const uint16_t* u = reinterpret_cast<const uint16_t*>(r + DP_H_SIZE);
+  const uint16_t *cl = u, *kl = cl + ncl, *kb = kl + nkl, *an = kb + nk;
+  const uint8_t* t = reinterpret_cast<const uint8_t*>(r + DP_H_SIZE) + dp_p16_tail_at(r);
+  const uint8_t *lens = t, *src = t + nc + nk, *mask = src + nch;
+  int32_t f = r[DP_H_NV] > 256 ? DP_P8_HI : 0;
+  bool b1 = true, nib = true;
+  for (int64_t k = 0; k < nk; ++k) {
+    if (kb[k] > 255) return 0;
+    b1 = b1 && kb[k] == 1;
+  }
+  for (int64_t i = 0; i < nc + nk; ++i) nib = nib && lens[i] <= 15;
+  f |= (b1 ? DP_P8_B1 : 0) | (nib ? DP_P8_NIB : 0);
+  int32_t h[DP_H_SIZE];
+  std::memcpy(h, r, sizeof h);
+  h[DP_H_FMT] = DP_FMT_P8D;
+  h[DP_H_P8] = f;
+  const dp_p8_layout P = dp_p8_layout_of(h);
+  int64_t nz = 0;
+  for (int64_t k = 0; k < nch; ++k) nz += src[k] != 0;
+  const int64_t bytes = dp_p8_body_bytes(h, nz);
+  static thread_local std::vector<uint8_t> o;
+  o.assign((size_t)bytes, 0);
+  auto setbit = [&](int64_t at, int64_t j) { o[(size_t)(at + (j >> 3))] |= (uint8_t)(1u << (j & 7)); };
+  for (int64_t j = 0; j < ncl; ++j) {
+    o[(size_t)(P.cvar + j)] = (uint8_t)(cl[j] >> 1);
+    if (cl[j] & 1) setbit(P.neg, j);
+    if ((f & DP_P8_HI) && (cl[j] >> 9)) setbit(P.chi, j);
+  }
+  for (int64_t j = 0; j < nkl; ++j) {
+    o[(size_t)(P.kvar + j)] = (uint8_t)kl[j];
+    if ((f & DP_P8_HI) && (kl[j] >> 8)) setbit(P.khi, j);
+  }
+  for (int64_t i = 0; i < na; ++i) {
+    o[(size_t)(P.avar + i)] = (uint8_t)an[i];
+    if ((f & DP_P8_HI) && (an[i] >> 8)) setbit(P.ahi, i);
+  }
+  if (!b1)
+    for (int64_t k = 0; k < nk; ++k) o[(size_t)(P.bound + k)] = (uint8_t)kb[k];
+  for (int64_t i = 0; i < nc + nk; ++i) {
+    if (nib) o[(size_t)(P.lens + (i >> 1))] |= (uint8_t)(lens[i] << (4 * (i & 1)));
+    else o[(size_t)(P.lens + i)] = lens[i];
+  }
+  int64_t q = 0;
+  for (int64_t k = 0; k < nch; ++k)
+    if (src[k]) {
+      setbit(P.srcnz, k);
+      o[(size_t)(P.srcval + q++)] = src[k];
+    }
+  std::memcpy(o.data() + P.srcval + nz, mask, (size_t)((nid + 7) / 8));
+  h[DP_H_P8] = (int32_t)((uint32_t)f | ((uint32_t)bytes << 8));
+  std::memcpy(r, h, sizeof h);
+  uint8_t* b = reinterpret_cast<uint8_t*>(r + DP_H_SIZE);
+  std::memcpy(b, o.data(), (size_t)bytes);
+  std::memset(b + bytes, 0, (size_t)((4 - bytes % 4) % 4));  // to the last word's end
+  return dp_rec_phys_words(r);
+}
+
 struct Lowerer {
   const dp_wire& w;
   const bool narrow;  // DP_LOWER_NARROW: records that fit 16 bits in the DP_FMT_U16 form
@@ -483,8 +593,9 @@ struct Lowerer {
   // variables carry host-built watch lists (DP_FMT_I32W), as before round 3
   const bool host_watches;
   const int ldsg;  // placement.hpp ldsg_env()
-  Lowerer(const dp_wire& wire, bool narrow16, bool packed16, bool host_lists)
-      : w(wire), narrow(narrow16), packed(packed16), host_watches(host_lists), ldsg(ldsg_env()) {}
+  const bool p8;   // packed records in DP_FMT_P8D where it applies (not DP_LOWER_NO_P8)
+  Lowerer(const dp_wire& wire, bool narrow16, bool packed16, bool host_lists, bool p8d)
+      : w(wire), narrow(narrow16), packed(packed16), host_watches(host_lists), ldsg(ldsg_env()), p8(p8d) {}
 
   // The last record appended to O (int32 words from `base`) in the 16-bit
   // form, in place (word j -> halfword j never overtakes word j).  Every
@@ -510,7 +621,8 @@ struct Lowerer {
         phys = words + ext;
       }
     } else if (packed && pack16(r, src)) {
-      phys = dp_rec_phys_words(r);
+      const int64_t p8w = p8 ? pack8(r) : 0;
+      phys = p8w ? p8w : dp_rec_phys_words(r);
     } else if (dp_rec_fits16(r)) {
       uint16_t* u = reinterpret_cast<uint16_t*>(r + DP_H_SIZE);
       for (int64_t j = 0; j < words - DP_H_SIZE; ++j) u[j] = (uint16_t)r[DP_H_SIZE + j];
@@ -661,7 +773,16 @@ struct Lowerer {
     t += F.nch;
     std::memset(t, 0, (size_t)(reinterpret_cast<uint8_t*>(r + padded) - t));  // mask, then the padding
     for (int32_t k = 0; k < F.nk; ++k) t[F.card_id[k] >> 3] |= (uint8_t)(1u << (F.card_id[k] & 7));
-    O.rec_len.push_back(padded);
+    int64_t len = padded;
+    if (p8) {
+      const int64_t p8w = pack8(r);
+      if (p8w) {  // the record shrank in place: give the rest back
+        len = (p8w + 3) & ~3LL;
+        for (int64_t j = p8w; j < len; ++j) r[j] = 0;
+        O.nrec -= (size_t)(padded - len);
+      }
+    }
+    O.rec_len.push_back(len);
     O.ivar.insert(O.ivar.end(), F.owner_v, F.owner_v + F.nid);
     O.icon.insert(O.icon.end(), F.owner_c, F.owner_c + F.nid);
     O.ident_len.push_back(F.nid);
@@ -1412,7 +1533,7 @@ int dp_lower_into(const dp_wire* wire, int32_t flags, dp_lowered* lw) {
   const char* hw = std::getenv("DEPPY_HOST_WATCHES");
   dp::Lowerer L(*wire, (flags & DP_LOWER_NARROW) != 0,
                 (flags & (DP_LOWER_NARROW | DP_LOWER_PACKED)) == (DP_LOWER_NARROW | DP_LOWER_PACKED),
-                hw && *hw && *hw != '0');
+                hw && *hw && *hw != '0', (flags & DP_LOWER_NO_P8) == 0);
   std::atomic<bool> bad{false};
   auto lower_chunk = [&](int64_t c, int t) {
     dp::Work& W = lw->work[(size_t)t];
@@ -1525,6 +1646,11 @@ int dp_rec_widen(const int32_t* rec, int64_t avail, int32_t* out) {
   const dp_rec_layout L = dp_rec_layout_of(rec);
   if (L.words != rec[DP_H_WORDS] || ((fmt == DP_FMT_U16 || dp_fmt_packed(fmt)) && !dp_rec_fits16(rec))) return -4;
   if (dp_fmt_packed(fmt) && dp_p16_tail_bytes(rec) > DP_P16_TAIL_MAX) return -17;
+  if (fmt == DP_FMT_P8D) {  // its DP_FMT_P16D record, then that one's int32 form
+    static thread_local std::vector<int32_t> p16;
+    const int e = dp::p8_to_p16d(rec, avail, p16);
+    return e ? e : dp_rec_widen(p16.data(), (int64_t)p16.size(), out);
+  }
   if (dp_rec_phys_words(rec) > avail) return -4;
   const int64_t words = rec[DP_H_WORDS];
   std::memcpy(out, rec, 4 * DP_H_SIZE);

@@ -11,7 +11,7 @@
 
 namespace dp {
 
-constexpr int kMaxLdsBytes = 160 * 1024;  // LDS per CU on gfx950
+constexpr int kMaxLdsBytes = kLdsLimitBytes;  // LDS per CU on gfx950
 
 // Problems whose one-wavefront LDS footprint exceeds kGroupAbove run as
 // multi-wave workgroups: at two or one per CU a lone wavefront per problem

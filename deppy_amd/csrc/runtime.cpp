@@ -108,6 +108,11 @@ constexpr int32_t kMidMaxVars = 8192;
 // batch needs no pinned staging room, so the cap is the device image).
 constexpr int32_t kChunkProblems = 65536;
 constexpr int64_t kChunkBytes = 1ll << 30;
+// several devices (cut_chunks): chunks per device for the shared queue to
+// balance, and the smallest such chunk (config 2: 5000-problem chunks ran 3%
+// under whole 10k ones, 2500-problem ones 32%; profiles/r05_chunk_ab.txt)
+constexpr int32_t kChunksPerDevice = 3;
+constexpr int32_t kMinSharedChunk = 4096;
 // D2H of the explanation pool per chunk: this many words per problem are
 // copied with the fixed outputs; a chunk whose cores need more fetches the
 // rest with a second copy.
@@ -939,9 +944,15 @@ struct dp_ctx {
   bool direct = true;  // copy page-locked batches of staged-form records as they are
   int32_t chunk_problems = kChunkProblems;
   int64_t chunk_bytes = kChunkBytes;
+  int32_t min_shared_chunk = kMinSharedChunk;  // (DEPPY_MIN_SHARED_CHUNK: tests of the shared queue)
   int32_t grid_cap = 0;  // test: workgroups of a queued launch (DEPPY_GRID_CAP; 0 = resident maximum)
   bool fast_path = true;  // small dp_solve batches on the latency path (DEPPY_FAST_PATH=0: off)
   bool spread = false;    // DEPPY_SPREAD=1: a chunk's later one-wavefront launches on sibling streams
+  // Several devices: the chunks of every job wait here, the costliest
+  // first, and a device's submitting thread takes the next one whenever it
+  // has a free lane (worker_main), so the devices balance dynamically.
+  std::mutex sqmu;
+  std::deque<Task> sq;
   dp_stats st{};         // the caller-thread paths (resident batches)
   ~dp_ctx() { delete pool; }
 };
@@ -1009,6 +1020,10 @@ void add_stats(dp_stats& a, const dp_stats& b) {
   a.h2d_bytes += b.h2d_bytes; a.d2h_bytes += b.d2h_bytes; a.rec_bytes += b.rec_bytes; a.stage_ms += b.stage_ms;
   a.plan_ms += b.plan_ms; a.wait_ms += b.wait_ms; a.scatter_ms += b.scatter_ms; a.direct_chunks += b.direct_chunks;
   a.bcp_bytes += b.bcp_bytes; a.allocs += b.allocs;
+  for (int m = 0; m < 5; ++m) {
+    a.placed[m] += b.placed[m];
+    a.placed_launches[m] += b.placed_launches[m];
+  }
 }
 void add_device_stats(Device& D, const dp_stats& b) {
   std::lock_guard<std::mutex> lk(D.smu);
@@ -1054,6 +1069,8 @@ int enqueue_launches(dp_ctx* ctx, const Plan& P, const dp::KernelArgs& base, hip
       ++nf;
     }
     st.launches++;
+    st.placed[L.mode] += L.count;
+    st.placed_launches[L.mode]++;
   }
   return 0;
 }
@@ -1363,14 +1380,33 @@ void run_task(dp_ctx* ctx, Device& D, const Task& t) {
 // waiter is blocked on their job, else when their `done` event has fired
 // (polled every 50 us while chunks are in flight).  Exits once stopped and
 // drained.
+// The next chunk of the context's shared queue when this device has a free
+// lane (its oldest lane delivered), so a busy device leaves the queue's
+// chunks to the others.  (Called with D.qmu held: qmu, then sqmu.)
+bool take_shared(dp_ctx* ctx, Device& D, Task& t) {
+  if ((int)D.inflight.size() >= D.nlanes) return false;
+  std::lock_guard<std::mutex> g(ctx->sqmu);
+  if (ctx->sq.empty()) return false;
+  t = ctx->sq.front();
+  ctx->sq.pop_front();
+  return true;
+}
+
 void worker_main(dp_ctx* ctx, Device* Dp) {
   Device& D = *Dp;
   (void)hipSetDevice(D.ordinal);
   std::unique_lock<std::mutex> lk(D.qmu);
   for (;;) {
+    Task t;
     if (!D.q.empty()) {
-      const Task t = D.q.front();
+      t = D.q.front();
       D.q.pop_front();
+      lk.unlock();
+      run_task(ctx, D, t);
+      lk.lock();
+      continue;
+    }
+    if (take_shared(ctx, D, t)) {
       lk.unlock();
       run_task(ctx, D, t);
       lk.lock();
@@ -1389,7 +1425,11 @@ void worker_main(dp_ctx* ctx, Device* Dp) {
       }
       continue;
     }
-    if (D.stop) return;
+    if (D.stop) {
+      std::lock_guard<std::mutex> g(ctx->sqmu);
+      if (ctx->sq.empty()) return;
+      continue;
+    }
     D.qcv.wait(lk);
   }
 }
@@ -1433,7 +1473,12 @@ void cut_chunks(const dp_ctx* ctx, const dp_job* job, std::vector<std::pair<int3
   const int32_t P = job->n;
   const int nd = (int)ctx->dev.size();
   int32_t cp = ctx->chunk_problems;
-  if (nd > 1 && P >= nd) cp = std::min<int32_t>(cp, (P + nd - 1) / nd);
+  // several devices: about kChunksPerDevice chunks each (but not below
+  // kMinSharedChunk problems: a chunk's launches last as long as its slowest
+  // catalog, so small chunks are tail-bound), for the shared queue to balance
+  if (nd > 1 && P >= nd)
+    cp = std::min<int32_t>(cp, std::max<int32_t>((P + kChunksPerDevice * nd - 1) / (kChunksPerDevice * nd),
+                                                 std::min<int32_t>(ctx->min_shared_chunk, (P + nd - 1) / nd)));
   for (int32_t p = 0; p < P;) {
     const int32_t q = next_chunk(job->rec_off, p, P, cp, ctx->chunk_bytes);
     out.emplace_back(p, q - p);
@@ -1524,6 +1569,7 @@ dp_ctx* dp_create(const dp_opts* opts) {
   if (opts) ctx->flags = opts->flags;
   ctx->chunk_problems = (int32_t)std::max<int64_t>(1, env_i64("DEPPY_CHUNK_PROBLEMS", kChunkProblems));
   ctx->chunk_bytes = std::max<int64_t>(1, env_i64("DEPPY_CHUNK_BYTES", kChunkBytes));
+  ctx->min_shared_chunk = (int32_t)std::max<int64_t>(1, env_i64("DEPPY_MIN_SHARED_CHUNK", kMinSharedChunk));
   ctx->zc_in = env_i64("DEPPY_ZC_IN", 0) != 0;   // diagnostic: 1 = kernels read staged records over PCIe
   ctx->zc_out = env_i64("DEPPY_ZC_OUT", 1) != 0; // diagnostic: 0 = D2H copy of every chunk
   ctx->direct = env_i64("DEPPY_DIRECT", 1) != 0; // diagnostic: 0 = stage every chunk
@@ -1619,6 +1665,14 @@ int dp_device_bytes(const dp_batch* b, int32_t opt_flags, int64_t* rec_bytes, in
   return 0;
 }
 
+int dp_plan_placements(const dp_batch* b, int32_t opt_flags, int8_t* place) {
+  if (!b || !place || b->n_problems < 0 || (b->n_problems > 0 && (!b->rec || !b->rec_off))) return -1;
+  Plan P;
+  dp::plan_chunk(P, b->rec, b->rec_off, 0, b->n_problems, opt_flags, nullptr);
+  for (int32_t i = 0; i < b->n_problems; ++i) place[i] = (int8_t)P.head[(size_t)i].place;
+  return 0;
+}
+
 // ---- host-to-host pipeline ----
 
 int dp_submit(dp_ctx* ctx, const dp_batch* b, dp_result* res, dp_job** out) {
@@ -1634,18 +1688,28 @@ int dp_submit(dp_ctx* ctx, const dp_batch* b, dp_result* res, dp_job** out) {
   cut_chunks(ctx, job, chunks);
   job->chunks_left = (int)chunks.size();
   const int nd = (int)ctx->dev.size();
-  int d0;
-  {
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    d0 = ctx->next_dev;
-    ctx->next_dev = (int)((ctx->next_dev + chunks.size()) % (size_t)nd);
-  }
-  for (size_t c = 0; c < chunks.size(); ++c) {
-    Device& D = ctx->dev[(d0 + c) % (size_t)nd];
+  if (nd == 1) {
+    Device& D = ctx->dev[0];
     {
       std::lock_guard<std::mutex> lk(D.qmu);
-      D.q.push_back(Task{job, chunks[c].first, chunks[c].second});
+      for (const auto& c : chunks) D.q.push_back(Task{job, c.first, c.second});
     }
+    D.qcv.notify_one();
+    *out = job;
+    return 0;
+  }
+  // several devices: the shared queue, costliest chunk first (record words,
+  // the cost the plan can see before solving), pulled by whichever device
+  // has a lane free (worker_main take_shared)
+  std::stable_sort(chunks.begin(), chunks.end(), [&](const auto& x, const auto& y) {
+    return b->rec_off[x.first + x.second] - b->rec_off[x.first] > b->rec_off[y.first + y.second] - b->rec_off[y.first];
+  });
+  {
+    std::lock_guard<std::mutex> g(ctx->sqmu);
+    for (const auto& c : chunks) ctx->sq.push_back(Task{job, c.first, c.second});
+  }
+  for (auto& D : ctx->dev) {  // (taking qmu orders the wake-up after a worker's check)
+    { std::lock_guard<std::mutex> lk(D.qmu); }
     D.qcv.notify_one();
   }
   *out = job;

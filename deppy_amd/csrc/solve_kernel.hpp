@@ -484,31 +484,38 @@ struct Group {
       IX* b = reinterpret_cast<IX*>(lds + L.body);
       const int4* src = reinterpret_cast<const int4*>(grec + DP_H_SIZE);
       const int fmt = h[DP_H_FMT];
-      packed = fmt == DP_FMT_P16 || fmt == DP_FMT_P16D;
+      packed = fmt_packed(fmt);
       if (!packed && fmt != DP_FMT_U16 && fmt != DP_FMT_U16_CHECKED) return false;
-      const int groups = packed ? (int)((p16_tail_at(h) + p16_tail_bytes(h) + 15) >> 4)
-                                : (h[DP_H_WORDS] - DP_H_SIZE + 7) >> 3;
-      if (L.body == 0 && ((groups + 63) >> 6) * 1024 <= L.lds_bytes) {
+      // DP_FMT_P8D lands past the arrays it decodes to (p16_tail_copy), the
+      // other forms at the body's start
+      const bool p8 = fmt == DP_FMT_P8D;
+      const int land = p8 ? p16_tail_copy(h) : 0;
+      const int groups = p8 ? (p8_bytes(h) + 15) >> 4
+                            : packed ? (int)((p16_tail_at(h) + p16_tail_bytes(h) + 15) >> 4)
+                                     : (h[DP_H_WORDS] - DP_H_SIZE + 7) >> 3;
+      if (L.body == 0 && land + ((groups + 63) >> 6) * 1024 <= L.lds_bytes) {
         // LDS-DMA, every 1 KiB piece in flight at once, wavefront w taking
         // pieces w, w + NW, ... (lanes past the image re-read its last piece
         // into LDS the later arrays own; they are initialised after this)
         for (int c = 64 * wid; c < groups; c += NT) {
           const int i = min(c + lane, groups - 1);
           __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src + i),
-                                           (__attribute__((address_space(3))) void*)(lds + 16 * c), 16, 0, 0);
+                                           (__attribute__((address_space(3))) void*)(lds + land + 16 * c), 16, 0, 0);
         }
         __builtin_amdgcn_s_waitcnt(0);
         gsync();
       } else {
-        for (int i = tid; i < groups; i += NT) reinterpret_cast<int4*>(b)[i] = src[i];
+        for (int i = tid; i < groups; i += NT) reinterpret_cast<int4*>(reinterpret_cast<char*>(b) + land)[i] = src[i];
         gsync();
       }
       body = b;
       if (packed) {
         // DP_FMT_P16 / DP_FMT_P16D in LDS: the uint16 arrays where they
         // landed, then the offsets arrays and the identities decoded from the
-        // tail (and, DP_FMT_P16D, the choice lists derived after them)
-        const bool derived = fmt == DP_FMT_P16D;
+        // tail (and, DP_FMT_P16D, the choice lists derived after them).
+        // DP_FMT_P8D: its arrays first widened into DP_FMT_P16D's places and
+        // its tail expanded after it (expand8), then decoded the same way.
+        const bool derived = fmt_derived(fmt);
         IX* q = b;
         clause_lits = q; q += ncl;
         card_lits = q;   q += nkl;
@@ -528,8 +535,14 @@ struct Group {
         // barrier.  The one-wavefront build calls it unconditionally: the
         // call under a branch took its VGPRs from 161 to 202.)
         auto decode = [&] {
-          return unpack16(reinterpret_cast<const char*>(b) + p16_tail_at(h), (int)p16_tail_bytes(h), derived,
-                          lds + L.reason, reinterpret_cast<uint8_t*>(b) + p16_tail_copy(h));
+          uint8_t* raw = reinterpret_cast<uint8_t*>(b) + land;
+          uint8_t* ex = reinterpret_cast<uint8_t*>(b) + p8_tail(h);
+          const bool ok8 = !p8 || expand8(raw, h[DP_H_P8] & 0xff, p8_bytes(h), ex);
+          const bool ok16 = unpack16(p8 ? reinterpret_cast<const char*>(ex)
+                                        : reinterpret_cast<const char*>(b) + p16_tail_at(h),
+                                     (int)p16_tail_bytes(h), derived, lds + L.reason,
+                                     p8 ? ex : reinterpret_cast<uint8_t*>(b) + p16_tail_copy(h));
+          return ok8 && ok16;
         };
         bool ok;
         if constexpr (NW == 1) {
@@ -628,7 +641,7 @@ struct Group {
     sub[0] = ti1 - ti0;
 #endif
     if constexpr (N16)
-      if ((h[DP_H_FMT] == DP_FMT_U16 || packed) && !valid_record(body, packed, h[DP_H_FMT] == DP_FMT_P16D)) return false;
+      if ((h[DP_H_FMT] == DP_FMT_U16 || packed) && !valid_record(body, packed, fmt_derived(h[DP_H_FMT]))) return false;
     if constexpr (!N16)
       if ((h[DP_H_FMT] == DP_FMT_I32W || h[DP_H_FMT] == DP_FMT_I32) && !valid_wide(R, X, h[DP_H_FMT] == DP_FMT_I32W))
         return false;
@@ -856,6 +869,55 @@ struct Group {
     return !g_any(bad);
   }
 
+  // DP_FMT_P8D (include/deppy_hip.h; lower.cpp p8_to_p16d) -> DP_FMT_P16D:
+  // the 16-bit arrays at their places (clause_lits .. anchors, set up by
+  // init) from the record's bytes at `raw`, and DP_FMT_P16D's tail (lengths,
+  // list sources, identity mask) at `ex`, for unpack16.  One wavefront.
+  // False when the sections overrun the body's `bytes` or a source marked
+  // nonzero is zero (the rest is unpack16's and valid_record's).
+  __device__ __forceinline__ bool expand8(const uint8_t* raw, int f, int bytes, uint8_t* ex) {
+    static_assert(N16, "16-bit records run on the LDS image");
+    const bool hi = f & DP_P8_HI, nib = f & DP_P8_NIB;
+    const int o_kv = ncl, o_av = ncl + nkl, o_b = o_av + na;
+    const int o_neg = o_b + ((f & DP_P8_B1) ? 0 : nk);
+    const int o_chi = o_neg + ((ncl + 7) >> 3);
+    const int o_khi = o_chi + (hi ? (ncl + 7) >> 3 : 0);
+    const int o_ahi = o_khi + (hi ? (nkl + 7) >> 3 : 0);
+    const int o_len = o_ahi + (hi ? (na + 7) >> 3 : 0);
+    const int o_snz = o_len + (nib ? (nc + nk + 1) >> 1 : nc + nk);
+    const int o_sv = o_snz + ((nch + 7) >> 3);
+    bool bad = o_sv > bytes || (f & ~(DP_P8_B1 | DP_P8_HI | DP_P8_NIB)) != 0;
+    const int lim = bytes > 0 ? bytes - 1 : 0;  // (reads stay inside the landed body)
+    auto byte = [&](int i) -> int { return (int)raw[min(i, lim)]; };
+    auto bit = [&](int at, int j) -> int { return (byte(at + (j >> 3)) >> (j & 7)) & 1; };
+    IX* cl = const_cast<IX*>(clause_lits);
+    IX* kl = const_cast<IX*>(card_lits);
+    IX* kb = const_cast<IX*>(card_bound);
+    IX* an = const_cast<IX*>(anchors);
+    for (int j = lane; j < ncl; j += 64) cl[j] = enc(2 * (byte(j) | (hi ? bit(o_chi, j) << 8 : 0)) + bit(o_neg, j));
+    for (int j = lane; j < nkl; j += 64) kl[j] = enc(byte(o_kv + j) | (hi ? bit(o_khi, j) << 8 : 0));
+    for (int k = lane; k < nk; k += 64) kb[k] = enc((f & DP_P8_B1) ? 1 : byte(o_b + k));
+    for (int i = lane; i < na; i += 64) an[i] = enc(byte(o_av + i) | (hi ? bit(o_ahi, i) << 8 : 0));
+    for (int i = lane; i < nc + nk; i += 64)
+      ex[i] = (uint8_t)(nib ? (byte(o_len + (i >> 1)) >> (4 * (i & 1))) & 15 : byte(o_len + i));
+    const uint64_t lt = lanemask_lt();
+    int q = o_sv;
+    for (int c = 0; c < nch; c += 64) {
+      const int k = c + lane;
+      const bool nz = k < nch && bit(o_snz, k);
+      const uint64_t m = __ballot(nz);
+      const int v = nz ? byte(q + __popcll(m & lt)) : 0;
+      bad |= nz && v == 0;
+      if (k < nch) ex[nc + nk + k] = (uint8_t)v;
+      q += __popcll(m);
+    }
+    const int mb = (nid + 7) >> 3;
+    bad |= q + mb > bytes;
+    for (int i = lane; i < mb; i += 64) ex[nc + nk + nch + i] = (uint8_t)byte(q + i);
+    wsync();
+    return !__ballot(bad);
+  }
+
   // DP_FMT_P16 tail (include/deppy_hip.h) -> the offsets arrays and the row
   // identities, in place after the uint16 arrays.  The tail (at most
   // DP_P16_TAIL_MAX bytes) is first copied to `tcopy` (p16_tail_copy: past
@@ -870,7 +932,7 @@ struct Group {
   // dependency rows by rank, each list's row and the per-subject counts.
   __device__ __forceinline__ bool unpack16(const char* tail, int tb, bool derived, char* scratch, uint8_t* tcopy) {
     static_assert(N16, "16-bit records run on the LDS image");
-    {
+    if (tail != reinterpret_cast<const char*>(tcopy)) {  // (DP_FMT_P8D: expand8 wrote it there)
       uint4 r = make_uint4(0u, 0u, 0u, 0u);
       if (16 * lane < tb) r = *reinterpret_cast<const uint4*>(tail + 16 * lane);
       if (16 * lane < tb) *reinterpret_cast<uint4*>(tcopy + 16 * lane) = r;

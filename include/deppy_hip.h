@@ -214,25 +214,84 @@ static inline dp_rec_layout dp_rec_layout_of(const int32_t* h) {
  * The kernel checks their bounds; that they list exactly those rows is the
  * producer's contract (dp_lower_into builds them). */
 enum { DP_H_FMT = 13 };
-enum { DP_FMT_I32 = 0, DP_FMT_U16 = 1, DP_FMT_P16 = 3, DP_FMT_I32W = 4, DP_FMT_P16D = 5 };
+enum { DP_FMT_I32 = 0, DP_FMT_U16 = 1, DP_FMT_P16 = 3, DP_FMT_I32W = 4, DP_FMT_P16D = 5, DP_FMT_P8D = 6 };
 enum { DP_P16_TAIL_MAX = 1024 };
+
+/* DP_FMT_P8D: DP_FMT_P16D with every variable in 8 bits plus bit planes, for
+ * records of at most 512 variables (dp_lower_into DP_LOWER_PACKED emits it
+ * where it applies; config 2's catalogs cross PCIe in about 45% fewer bytes
+ * than DP_FMT_P16D).  Header word DP_H_P8 holds its flags (bits 0-7) and the
+ * body's byte count (bits 8-31).  After the header,
+ * byte-addressed from the body's start, no padding inside:
+ *   uint8 clause_var[ncl]   the variable of each clause literal, low 8 bits
+ *   uint8 card_var[nkl], anchor_var[na]                     (low 8 bits)
+ *   uint8 card_bound[nk]    absent with DP_P8_B1 (every bound is 1)
+ *   bits  clause_neg[ncl]   bit j (LSB first) set iff clause literal j is negative
+ *   bits  clause_hi[ncl], card_hi[nkl], anchor_hi[na]
+ *                           bit 8 of each variable; present only with DP_P8_HI
+ *   lengths                 clause_len[nc] then card_len[nk], a byte each, or
+ *                           with DP_P8_NIB a nibble each (low nibble first,
+ *                           ceil((nc+nk)/2) bytes)
+ *   bits  src_nz[nch]       bit k set iff DP_FMT_P16D's src[k] != 0
+ *   uint8 src_val[...]      those src[k], in list order
+ *   bits  card_mask[nid]    as DP_FMT_P16's
+ * Each bit array is ceil(n/8) bytes.  A literal is 2 * variable + negative.
+ * The record decodes to exactly DP_FMT_P16D's arrays (dp_rec_widen). */
+enum { DP_H_P8 = 14 };
+enum { DP_P8_B1 = 1, DP_P8_HI = 2, DP_P8_NIB = 4 };
+enum { DP_P8_MAX_VARS = 512 };
+static inline int64_t dp_p8_bits(int64_t n) { return (n + 7) >> 3; }
+/* Byte offsets of DP_FMT_P8D's sections (from the body's start). */
+typedef struct dp_p8_layout {
+  int64_t cvar, kvar, avar, bound, neg, chi, khi, ahi, lens, srcnz, srcval, mask;
+} dp_p8_layout;
+static inline dp_p8_layout dp_p8_layout_of(const int32_t* h) {
+  dp_p8_layout L;
+  const int32_t f = h[DP_H_P8];
+  const int64_t ncl = h[DP_H_NCL], nkl = h[DP_H_NKL], na = h[DP_H_NA], nk = h[DP_H_NK], nc = h[DP_H_NC];
+  int64_t o = 0;
+  L.cvar = o;  o += ncl;
+  L.kvar = o;  o += nkl;
+  L.avar = o;  o += na;
+  L.bound = o; o += (f & DP_P8_B1) ? 0 : nk;
+  L.neg = o;   o += dp_p8_bits(ncl);
+  L.chi = o;   o += (f & DP_P8_HI) ? dp_p8_bits(ncl) : 0;
+  L.khi = o;   o += (f & DP_P8_HI) ? dp_p8_bits(nkl) : 0;
+  L.ahi = o;   o += (f & DP_P8_HI) ? dp_p8_bits(na) : 0;
+  L.lens = o;  o += (f & DP_P8_NIB) ? (nc + nk + 1) / 2 : nc + nk;
+  L.srcnz = o; o += dp_p8_bits(h[DP_H_NCH]);
+  L.srcval = o;
+  L.mask = -1; /* after the src values: their count is the popcount of src_nz */
+  return L;
+}
 
 /* DP_FMT_P16 / DP_FMT_P16D (the packed forms): uint16 words before the
  * padding, byte offset of the lengths (from the body's start), and bytes of
  * lengths plus mask. */
-static inline int dp_fmt_packed(int32_t fmt) { return fmt == DP_FMT_P16 || fmt == DP_FMT_P16D; }
+static inline int dp_fmt_packed(int32_t fmt) { return fmt == DP_FMT_P16 || fmt == DP_FMT_P16D || fmt == DP_FMT_P8D; }
+/* the packed forms whose choice lists are implied by the dependency rows */
+static inline int dp_fmt_derived(int32_t fmt) { return fmt == DP_FMT_P16D || fmt == DP_FMT_P8D; }
 static inline int64_t dp_p16_nu16(const int32_t* h) {
   return (int64_t)h[DP_H_NCL] + h[DP_H_NKL] + h[DP_H_NK] + h[DP_H_NA] +
-         (h[DP_H_FMT] == DP_FMT_P16D ? 0 : h[DP_H_NCHL]);
+         (dp_fmt_derived(h[DP_H_FMT]) ? 0 : h[DP_H_NCHL]);
 }
 static inline int64_t dp_p16_tail_at(const int32_t* h) { return (2 * dp_p16_nu16(h) + 15) & ~(int64_t)15; }
+/* (DP_FMT_P8D: the DP_FMT_P16D tail its sections decode to) */
 static inline int64_t dp_p16_tail_bytes(const int32_t* h) {
   return (int64_t)h[DP_H_NC] + h[DP_H_NK] + h[DP_H_NCH] + ((int64_t)h[DP_H_NID] + 7) / 8 +
-         (h[DP_H_FMT] == DP_FMT_P16D ? 0 : (int64_t)h[DP_H_NV]);
+         (dp_fmt_derived(h[DP_H_FMT]) ? 0 : (int64_t)h[DP_H_NV]);
+}
+/* DP_FMT_P8D body bytes up to the src values (their count is in the body:
+ * the popcount of src_nz), and the whole body given that count. */
+static inline int64_t dp_p8_body_bytes(const int32_t* h, int64_t n_src_val) {
+  return dp_p8_layout_of(h).srcval + n_src_val + dp_p8_bits(h[DP_H_NID]);
 }
 
+/* Words of the record as it lies (for DP_FMT_P8D: header word DP_H_P8's
+ * bits 8.. hold the body's byte count). */
 static inline int64_t dp_rec_phys_words(const int32_t* h) {
   if (h[DP_H_FMT] == DP_FMT_U16) return DP_H_SIZE + ((int64_t)h[DP_H_WORDS] - DP_H_SIZE + 1) / 2;
+  if (h[DP_H_FMT] == DP_FMT_P8D) return DP_H_SIZE + (((int64_t)((uint32_t)h[DP_H_P8] >> 8)) + 3) / 4;
   if (dp_fmt_packed(h[DP_H_FMT])) return DP_H_SIZE + (dp_p16_tail_at(h) + dp_p16_tail_bytes(h) + 3) / 4;
   if (h[DP_H_FMT] == DP_FMT_I32W)
     return (int64_t)h[DP_H_WORDS] + 2 * (int64_t)h[DP_H_NV] + 1 + h[DP_H_NCL] + h[DP_H_NKL];
@@ -282,7 +341,9 @@ int dp_lower(const dp_wire* wire, dp_lowered** out);
  * form for the other 16-bit ones.  With DP_LOWER_NARROW, records of problems
  * solved by multi-wave workgroups (too large for one wavefront's LDS image,
  * or beyond 16 bits) take the DP_FMT_I32W form.  Returns 0 or -1. */
-enum { DP_LOWER_NARROW = 1, DP_LOWER_PINNED = 2, DP_LOWER_PACKED = 4 };
+/* DP_LOWER_PACKED emits DP_FMT_P8D for the DP_FMT_P16D records that allow
+ * it; DP_LOWER_NO_P8 keeps them DP_FMT_P16D (tests, A/B). */
+enum { DP_LOWER_NARROW = 1, DP_LOWER_PINNED = 2, DP_LOWER_PACKED = 4, DP_LOWER_NO_P8 = 8 };
 int dp_lower_into(const dp_wire* wire, int32_t flags, dp_lowered* lw);
 dp_lowered* dp_lowered_new(void); /* an empty result for dp_lower_into */
 void dp_lowered_free(dp_lowered* lw);
@@ -442,6 +503,8 @@ typedef struct dp_stats {
                         buffers, planning storage).  The first chunk of a
                         batch shape grows every lane of its device, so a
                         serving loop's steady state makes none               */
+  int64_t placed[5];          /* problems solved per placement (enum dp_place) */
+  int64_t placed_launches[5]; /* solve kernel launches per placement          */
 } dp_stats;
 int dp_get_stats(dp_ctx* ctx, dp_stats* out, int32_t reset);
 /* The share of dp_get_stats that logical device `device` (0 .. dp_num_devices
@@ -510,6 +573,19 @@ int dp_stage_roundtrip(const dp_batch* b, int32_t opt_flags, int32_t chunk_probl
                        int32_t* out_rec, int32_t* chunk_first, int32_t cap);
 int dp_stitch_selftest(const dp_batch* b, int32_t chunk_problems, dp_result* res);
 int dp_partition(const int64_t* rec_off, int32_t n_problems, int32_t nd, int32_t* cut);
+/*   dp_plan_placements: the placement dp_submit plans for each problem of b
+ *     as one chunk (enum dp_place, or DP_PLACE_MALFORMED / DP_PLACE_TOO_LARGE)
+ *     into place[n_problems].  Returns 0 or -1. */
+enum dp_place {
+  DP_PLACE_LDS = 0,    /* one wavefront, record and working set in LDS          */
+  DP_PLACE_SPLIT = 1,  /* 8-wave workgroup, per-variable and round state in LDS */
+  DP_PLACE_HBM = 2,    /* 8-wave workgroup, working set in HBM                   */
+  DP_PLACE_SPLIT4 = 3, /* 4-wave workgroup, as DP_PLACE_SPLIT                    */
+  DP_PLACE_LDSG = 4,   /* 4-wave workgroup, the one-wavefront image all in LDS   */
+  DP_PLACE_MALFORMED = -1,
+  DP_PLACE_TOO_LARGE = -2
+};
+int dp_plan_placements(const dp_batch* b, int32_t opt_flags, int8_t* place);
 
 /* Device time of the solve kernel(s) of the last waited launch (dp_run,
  * dp_wait, dp_solve), measured with HIP events on its stream (max over devices). */

@@ -136,7 +136,8 @@ static void parse(prob_t* p, const int32_t* rec) {
   p->nch = rec[DP_H_NCH];
   p->na = rec[DP_H_NA];
   p->nid = rec[DP_H_NID];
-  p->nvu = rec[DP_H_NVU] > 0 ? rec[DP_H_NVU] : p->nv;
+  /* (clamped as the kernel's nvu_of: a record with NVU past nv reads no bit past nv) */
+  p->nvu = rec[DP_H_NVU] > 0 && rec[DP_H_NVU] < p->nv ? rec[DP_H_NVU] : p->nv;
   p->nrows = p->nc + p->nk;
   p->clause_off = rec + L.clause_off;
   p->clause_lits = rec + L.clause_lits;
@@ -201,9 +202,73 @@ static void implied_choices(const dp_rec_layout* L, const uint8_t* src, int32_t*
   free(rowk);
 }
 
+/* DP_FMT_P8D (include/deppy_hip.h) into the int32 record o (header copied):
+ * the 8-bit variables with their sign and bit-8 planes, the byte or nibble
+ * lengths, the nonzero list sources and the identity mask, read in the
+ * order the format lists them; then the lists as DP_FMT_P16D's. */
+static int p8_bit(const uint8_t* b, int64_t at, int64_t j) { return (b[at + (j >> 3)] >> (j & 7)) & 1; }
+static void widen_p8(const int32_t* rec, int32_t* o) {
+  const dp_rec_layout L = dp_rec_layout_of(rec);
+  const int32_t f = rec[DP_H_P8] & 0xff;
+  const int32_t ncl = rec[DP_H_NCL], nkl = rec[DP_H_NKL], na = rec[DP_H_NA], nk = rec[DP_H_NK];
+  const int32_t nc = rec[DP_H_NC], nch = rec[DP_H_NCH], nid = rec[DP_H_NID];
+  const uint8_t* b = (const uint8_t*)(rec + DP_H_SIZE);
+  int64_t at = 0;
+  const int64_t cv = at; at += ncl;
+  const int64_t kv = at; at += nkl;
+  const int64_t av = at; at += na;
+  const int64_t kb = at; at += (f & DP_P8_B1) ? 0 : nk;
+  const int64_t neg = at; at += (ncl + 7) / 8;
+  int64_t chi = -1, khi = -1, ahi = -1;
+  if (f & DP_P8_HI) {
+    chi = at; at += (ncl + 7) / 8;
+    khi = at; at += (nkl + 7) / 8;
+    ahi = at; at += (na + 7) / 8;
+  }
+  for (int32_t j = 0; j < ncl; ++j)
+    o[L.clause_lits + j] = 2 * (b[cv + j] + (chi >= 0 ? 256 * p8_bit(b, chi, j) : 0)) + p8_bit(b, neg, j);
+  for (int32_t j = 0; j < nkl; ++j) o[L.card_lits + j] = b[kv + j] + (khi >= 0 ? 256 * p8_bit(b, khi, j) : 0);
+  for (int32_t i = 0; i < na; ++i) o[L.anchors + i] = b[av + i] + (ahi >= 0 ? 256 * p8_bit(b, ahi, i) : 0);
+  for (int32_t k = 0; k < nk; ++k) o[L.card_bound + k] = (f & DP_P8_B1) ? 1 : b[kb + k];
+  const int32_t offs[2] = {L.clause_off, L.card_off}, ns[2] = {nc, nk};
+  int64_t i = 0;
+  for (int a = 0; a < 2; ++a) {
+    o[offs[a]] = 0;
+    for (int32_t j = 0; j < ns[a]; ++j, ++i) {
+      const int len = (f & DP_P8_NIB) ? (b[at + i / 2] >> (4 * (i % 2))) & 15 : b[at + i];
+      o[offs[a] + j + 1] = o[offs[a] + j] + len;
+    }
+  }
+  at += (f & DP_P8_NIB) ? (nc + nk + 1) / 2 : nc + nk;
+  const int64_t snz = at;
+  at += (nch + 7) / 8;
+  uint8_t* src = xcalloc((size_t)nch + 1, 1);
+  for (int32_t k = 0; k < nch; ++k)
+    if (p8_bit(b, snz, k)) src[k] = b[at++];
+  int32_t c0 = 0, c1 = 0;
+  for (int32_t id = 0; id < nid; ++id) {
+    if (p8_bit(b, at, id)) {
+      if (c1 < nk) o[L.card_id + c1++] = id;
+    } else if (c0 < nc) {
+      o[L.clause_id + c0++] = id;
+    }
+  }
+  implied_choices(&L, src, o);
+  free(src);
+}
+
 static const int32_t* widen(const int32_t* rec, int32_t** tmp) {
   *tmp = NULL;
   const int32_t fmt = rec[DP_H_FMT];
+  if (fmt == DP_FMT_P8D) {
+    int32_t* o = xcalloc((size_t)rec[DP_H_WORDS], sizeof(int32_t));
+    memcpy(o, rec, DP_H_SIZE * sizeof(int32_t));
+    o[DP_H_FMT] = DP_FMT_I32;
+    o[DP_H_P8] = 0;
+    widen_p8(rec, o);
+    *tmp = o;
+    return o;
+  }
   if (fmt != DP_FMT_U16 && fmt != DP_FMT_P16 && fmt != DP_FMT_P16D) return rec;
   int32_t w = rec[DP_H_WORDS];
   int32_t* o = xcalloc((size_t)w, sizeof(int32_t));

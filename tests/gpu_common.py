@@ -4,7 +4,7 @@ import numpy as np
 from deppy_amd import _lib
 
 
-def lowered_config(config, n, seed, narrow=False, pinned=False, packed=False):
+def lowered_config(config, n, seed, narrow=False, pinned=False, packed=False, p8=True):
     """Synthetic catalogs (SURVEY §8(d) generator) lowered by dp_lower;
     narrow: records that fit 16 bits in the DP_FMT_U16 form (packed: the
     DP_FMT_P16D / DP_FMT_P16 forms where they apply); pinned: in page-locked memory (with a
@@ -13,7 +13,7 @@ def lowered_config(config, n, seed, narrow=False, pinned=False, packed=False):
     return _lib.Lowered(_lib.WireArrays(**{k: w[k] for k in (
         "prob_var_off", "var_id", "var_con_off", "con_kind", "con_n", "con_arg_off", "con_arg",
         "str_off")}, str_bytes=w["str_bytes"].tobytes()), narrow=narrow or packed, pinned=pinned,
-        packed=packed)
+        packed=packed, p8=p8)
 
 
 def corrupt16(rec_off, rec, p, kind):
@@ -65,10 +65,54 @@ def implied_choices(nv, clause_off, clause_lits, src):
     return vco.astype(np.int32), np.array(co, np.int32), np.array(chl, np.int32)
 
 
+def unpack_p8(r):
+    """The DP_FMT_P16D record a DP_FMT_P8D one encodes (include/deppy_hip.h),
+    restated independently of the library: 8-bit variables with their sign
+    and bit-8 planes, byte or nibble lengths, the nonzero list sources by a
+    bit mask, then the identity mask."""
+    nv, nc, nk, nch, na, nid, ncl, nkl = (int(r[i]) for i in range(1, 9))
+    f = int(r[14]) & 0xff
+    b = r[16:].view(np.uint8)
+    at = 0
+
+    def take(n):
+        nonlocal at
+        x = b[at:at + n]
+        at += n
+        return x
+
+    def bits(n):
+        return np.unpackbits(take((n + 7) // 8), bitorder="little")[:n].astype(np.int32)
+
+    cv, kv, av = take(ncl).astype(np.int32), take(nkl).astype(np.int32), take(na).astype(np.int32)
+    kb = np.ones(nk, np.int32) if f & 1 else take(nk).astype(np.int32)
+    neg = bits(ncl)
+    if f & 2:
+        cv, kv, av = cv + 256 * bits(ncl), kv + 256 * bits(nkl), av + 256 * bits(na)
+    if f & 4:
+        nb = take((nc + nk + 1) // 2)
+        lens = np.stack([nb & 15, nb >> 4], axis=1).reshape(-1)[:nc + nk]
+    else:
+        lens = take(nc + nk)
+    nz = bits(nch).astype(bool)
+    src = np.zeros(nch, np.uint8)
+    src[nz] = take(int(nz.sum()))
+    mask = take((nid + 7) // 8)
+    u16 = np.concatenate([2 * cv + neg, kv, kb, av]).astype(np.uint16).tobytes()
+    u16 += bytes((-len(u16)) % 16)
+    body = u16 + np.asarray(lens, np.uint8).tobytes() + src.tobytes() + mask.tobytes()
+    body += bytes((-len(body)) % 4)
+    head = np.asarray(r[:16], np.int32).copy()
+    head[13], head[14] = 5, 0
+    return np.concatenate([head, np.frombuffer(body, np.int32)])
+
+
 def unpack_p16(r):
-    """The int32 form of one DP_FMT_P16 / DP_FMT_P16D record
-    (include/deppy_hip.h), restated here independently of the library's
-    dp_rec_widen."""
+    """The int32 form of one DP_FMT_P16 / DP_FMT_P16D (or DP_FMT_P8D, through
+    unpack_p8) record (include/deppy_hip.h), restated here independently of
+    the library's dp_rec_widen."""
+    if int(r[13]) == 6:
+        r = unpack_p8(r)
     nv, nc, nk, nch, na, nid, ncl, nkl, nchl, words = (int(r[i]) for i in range(1, 11))
     derived = int(r[13]) == 5
     u = r[16:].view(np.uint16)
@@ -133,7 +177,7 @@ def widen(rec_off, rec):
     parts, offs = [], [0]
     for p in range(len(rec_off) - 1):
         r = rec[rec_off[p]:rec_off[p + 1]]
-        if len(r) and r[13] in (3, 5):
+        if len(r) and r[13] in (3, 5, 6):
             r = unpack_p16(r)
         elif len(r) and r[13] == 1:
             words = int(r[10])
@@ -168,3 +212,59 @@ def compare_results(g, o, n, rec_off=None, rec=None, only=None):
         if cl != o["core_len"][p] or not np.array_equal(g["core"][c0:c0 + cl], o["core"][c0:c0 + cl]):
             bad.append((p, "core"))
     return bad
+
+
+def wide_problems(seed, n, nvs):
+    """Problems of nv variables each (nv drawn from nvs): Dependencies on
+    far-apart candidates, Conflicts, Mandatory anchors, AtMost rows with
+    bounds 1 and 2, and (in every other problem) a Dependency of 20
+    candidates -- so their DP_FMT_P8D records use the bit-8 planes (257..512
+    variables), byte bounds and byte lengths; past 512 variables they stay
+    DP_FMT_P16D."""
+    from deppy_amd import sat
+    from tests.test_lowering import V
+    rng = np.random.default_rng(seed)
+    out = []
+    for q in range(n):
+        nv = int(nvs[q % len(nvs)])
+        names = ["w%d" % i for i in range(nv)]
+        vs = []
+        for i in range(nv):
+            cons = []
+            u = rng.random()
+            if u < 0.05:
+                cons.append(sat.Mandatory())
+            if rng.random() < 0.3:
+                m = int(rng.integers(1, 5))
+                cons.append(sat.Dependency(*[names[j] for j in rng.choice(nv, m, replace=False) if j != i]))
+            if rng.random() < 0.1:
+                j = int(rng.integers(0, nv))
+                if j != i:
+                    cons.append(sat.Conflict(names[j]))
+            if i % 20 == 7:
+                ids = [names[j] for j in rng.choice(nv, int(rng.integers(3, 7)), replace=False)]
+                cons.append(sat.AtMost(int(rng.integers(1, 3)), *ids))
+            if i == 3 and q % 2 == 0:
+                cons.append(sat.Dependency(*[names[j] for j in rng.choice(nv, 20, replace=False) if j != i]))
+            vs.append(V(names[i], *cons))
+        out.append(vs)
+    return out
+
+
+def p8_sections(r):
+    """Byte offsets of a DP_FMT_P8D record's sections (from the body's start;
+    include/deppy_hip.h), and its count of nonzero list sources."""
+    nv, nc, nk, nch, na, nid, ncl, nkl = (int(r[i]) for i in range(1, 9))
+    f = int(r[14]) & 0xff
+    S, at = {}, 0
+    for name, n in (("cvar", ncl), ("kvar", nkl), ("avar", na), ("bound", 0 if f & 1 else nk),
+                    ("neg", (ncl + 7) // 8), ("chi", (ncl + 7) // 8 if f & 2 else 0),
+                    ("khi", (nkl + 7) // 8 if f & 2 else 0), ("ahi", (na + 7) // 8 if f & 2 else 0),
+                    ("lens", (nc + nk + 1) // 2 if f & 4 else nc + nk), ("srcnz", (nch + 7) // 8)):
+        S[name] = at
+        at += n
+    S["srcval"] = at
+    b = np.asarray(r[16:], np.int32).view(np.uint8)
+    S["nz"] = int(np.unpackbits(b[S["srcnz"]:S["srcnz"] + (nch + 7) // 8], bitorder="little")[:nch].sum())
+    S["mask"] = at + S["nz"]
+    return S

@@ -373,15 +373,21 @@ def test_malformed_16bit_records_found_by_the_kernel(pinned, flags):
     assert compare_results(g, ref, lw.n, only=ok) == []
 
 
-@pytest.mark.parametrize("config,n,seed,flags", [(2, 3000, 101, 0), (3, 9000, 102, 0), (5, 300, 103, 0), (6, 3000, 104, 0),
-                                                 (2, 200, 104, _lib.OPT_FORCE_GROUP)],
-                         ids=["c2", "c3", "c5", "c6", "c2-group"])
-def test_packed_records_bit_exact(config, n, seed, flags):
-    """Packed records (dp_lower_into DP_LOWER_PACKED: DP_FMT_P16D), copied to the device
+@pytest.mark.parametrize("config,n,seed,flags,p8", [(2, 3000, 101, 0, True), (3, 9000, 102, 0, True),
+                                                    (5, 300, 103, 0, True), (6, 3000, 104, 0, True),
+                                                    (2, 200, 104, _lib.OPT_FORCE_GROUP, True),
+                                                    (2, 200, 105, _lib.OPT_FORCE_LDSG, True),
+                                                    (2, 3000, 101, 0, False), (5, 300, 103, 0, False)],
+                         ids=["c2", "c3", "c5", "c6", "c2-group", "c2-ldsg", "c2-p16d", "c5-p16d"])
+def test_packed_records_bit_exact(config, n, seed, flags, p8):
+    """Packed records (dp_lower_into DP_LOWER_PACKED: DP_FMT_P8D up to 512
+    variables, else DP_FMT_P16D; p8=False: DP_FMT_P16D), copied to the device
     as they lie and decoded by the kernel (or widened on the host for a
     multi-wave placement), solve exactly like their int32 form and the oracle."""
     a = lowered_config(config, n, seed)
-    b = lowered_config(config, n, seed, packed=True, pinned=True)
+    b = lowered_config(config, n, seed, packed=True, pinned=True, p8=p8)
+    fmts = set(b.rec[b.rec_off[:-1] + 13].tolist())
+    assert (6 in fmts) == (p8 and config != 4), fmts
     c = _lib.Context(0, 1, flags=flags)
     try:
         gb = c.submit(b.rec_off, b.rec).wait()
@@ -402,7 +408,7 @@ def test_malformed_packed_records_found_by_the_kernel(flags):
     lengths that do not sum to the total, an out-of-range literal, dependency
     rows that no longer imply the header's choice lists (DP_FMT_P16D) ->
     DP_ERROR + DP_F_MALFORMED for that problem only."""
-    lw = lowered_config(2, 40, 111, packed=True, pinned=True)
+    lw = lowered_config(2, 40, 111, packed=True, pinned=True, p8=False)
     ref = oracle.solve_batch(lw.rec_off, lw.rec, 0, 16)
     rec = lw.rec
     bad = [5, 12, 27, 33]
@@ -434,6 +440,62 @@ def test_malformed_packed_records_found_by_the_kernel(flags):
     assert compare_results(g, ref, lw.n, only=ok) == []
 
 
+@pytest.mark.parametrize("flags", [0, _lib.OPT_FORCE_LDSG], ids=["lds", "ldsg"])
+def test_malformed_p8_records_found_by_the_kernel(flags):
+    """DP_FMT_P8D records are decoded and validated on the device: an unknown
+    flag bit, a list source marked nonzero that is zero, a variable past nv,
+    row lengths that do not sum to the total -> DP_ERROR + DP_F_MALFORMED for
+    that problem only, the others bit-exact."""
+    from tests.gpu_common import p8_sections
+    lw = lowered_config(2, 60, 112, packed=True, pinned=True)
+    ref = oracle.solve_batch(lw.rec_off, lw.rec, 0, 16)
+    rec = lw.rec
+    cand = [p for p in range(lw.n) if int(rec[lw.rec_off[p] + 1]) < 256 and rec[lw.rec_off[p] + 14] & 4
+            and p8_sections(rec[lw.rec_off[p]:lw.rec_off[p + 1]])["nz"] > 0]
+    bad = cand[:4]
+    assert len(bad) == 4
+    for p, kind in zip(bad, ("flag", "src", "var", "len")):
+        r = rec[lw.rec_off[p]:lw.rec_off[p + 1]]
+        assert r[13] == 6
+        S = p8_sections(r)
+        t = r[16:].view(np.uint8)
+        if kind == "flag":
+            r[14] |= 64
+        elif kind == "src":
+            t[S["srcval"]] = 0
+        elif kind == "var":
+            t[0] = 255
+        else:
+            t[S["lens"]] ^= 1
+    c = _lib.Context(0, 1, flags=flags)
+    try:
+        g = c.solve(lw.rec_off, rec)
+    finally:
+        c.close()
+    ok = [p for p in range(lw.n) if p not in bad]
+    for p in bad:
+        assert g["status"][p] == -2 and g["flags"][p] == 512 and g["core_len"][p] == 0, p
+    assert compare_results(g, ref, lw.n, only=ok) == []
+
+
+def test_p8_wide_variables_bit_exact():
+    """DP_FMT_P8D with the bit-8 planes (257..512 variables), byte bounds and
+    byte lengths, beside DP_FMT_P16D past 512 variables: decoded on the
+    device, bit-exact with the int32 records and the oracle."""
+    from tests.gpu_common import wide_problems
+    wire = sat.encode_inputs(wide_problems(7, 24, [300, 512, 513, 200, 450]))
+    a = _lib.Lowered(wire)
+    b = _lib.Lowered(wire, narrow=True, packed=True, pinned=True)
+    fmts = b.rec[b.rec_off[:-1] + 13]
+    assert (fmts == 6).sum() >= 16 and (fmts == 5).sum() >= 4, fmts
+    c = _lib.Context(0, 1)
+    try:
+        g = c.submit(b.rec_off, b.rec).wait()
+    finally:
+        c.close()
+    assert compare_results(g, oracle.solve_batch(a.rec_off, a.rec, 0, 16), a.n) == []
+
+
 def test_packed_tail_larger_than_watch_room_bit_exact():
     """The kernel copies a packed record's tail past the decoded arrays (where
     the watch lists go later) while it decodes it; layout() grows the body
@@ -448,7 +510,7 @@ def test_packed_tail_larger_than_watch_room_bit_exact():
     a = _lib.Lowered(wire)
     b = _lib.Lowered(wire, narrow=True, packed=True, pinned=True)
     fmts = [int(b.record(p)[13]) for p in range(b.n)]
-    assert fmts[0] == 5 and fmts[1] == 3, fmts
+    assert fmts[0] == 6 and fmts[1] == 3, fmts  # (DP_FMT_P8D: its tail expanded after its bytes)
     for p in range(b.n):  # the tail is larger than the record's watch-list room
         h = b.record(p)
         nv, nc, nk, nch, nid, ncl, nkl = (int(h[i]) for i in (1, 2, 3, 4, 6, 7, 8))
@@ -777,6 +839,34 @@ def test_multi_device_dispatcher_bit_exact(config, n, seed):
         c.close()
     assert compare_results(g, o, n) == []
     assert compare_results(gr, o, n) == []
+
+
+def test_multi_device_shared_queue_bit_exact(monkeypatch):
+    """Several devices pull a job's chunks from the context's shared queue,
+    costliest (most record words) first, whenever a device has a free lane
+    (runtime.cpp take_shared): config 5's mixed sizes cut into six chunks
+    over two logical devices on GPU 0.  Every chunk runs exactly once, both
+    devices run some, the per-device kernel time is reported, and every field
+    is bit-exact against the oracle (reference caller:
+    pkg/solver/solver.go:42-47)."""
+    monkeypatch.setenv("DEPPY_MIN_SHARED_CHUNK", "32")
+    n = 600
+    lw = lowered_config(5, n, 153, packed=True, pinned=True)
+    w = lowered_config(5, n, 153)
+    o = oracle.solve_batch(w.rec_off, w.rec, 0, 16)
+    c = _lib.Context(0, 2, flags=_lib.OPT_SHARE_ORDINAL)
+    try:
+        c.stats(reset=True)
+        g = c.submit(lw.rec_off, lw.rec).wait()
+        per = [c.device_stats(d) for d in range(2)]
+        tot = c.stats()
+    finally:
+        c.close()
+    assert tot["chunks"] == 6 and sum(d["chunks"] for d in per) == 6, (tot["chunks"], per)
+    assert min(d["chunks"] for d in per) >= 1
+    assert sum(d["problems"] for d in per) == n
+    assert all(d["kernel_ms"] > 0 for d in per)
+    assert compare_results(g, o, n) == []
 
 
 def test_pipelined_solve_wire_bit_exact(ctx, monkeypatch):

@@ -195,9 +195,12 @@ def test_packed_lowering_is_the_int32_record(config, n):
     np.testing.assert_array_equal(rec, a.rec)
     fmt = b.rec[b.rec_off[:-1] + 13]
     if config in (2, 3):
-        # the generated catalogs' dependency rows imply their choice lists
-        assert np.all(fmt == 5)
-        assert b.rec_off[-1] < 0.65 * lowered_config(config, n, 17, narrow=True).rec_off[-1]
+        # the generated catalogs' dependency rows imply their choice lists;
+        # DP_FMT_P8D up to 512 variables (all of them: config 2 peaks near 300)
+        assert np.all(fmt == 6)
+        c = lowered_config(config, n, 17, packed=True, p8=False)
+        assert np.all(c.rec[c.rec_off[:-1] + 13] == 5)
+        assert b.rec_off[-1] < 0.67 * c.rec_off[-1], (b.rec_off[-1], c.rec_off[-1])
     assert np.all(b.rec_off % 4 == 0)
     L = _lib.lib()
     for p in range(n):
@@ -206,7 +209,7 @@ def test_packed_lowering_is_the_int32_record(config, n):
         assert L.dp_rec_widen(r.ctypes.data_as(_lib.c_i32p), len(r), out.ctypes.data_as(_lib.c_i32p)) == 0
         np.testing.assert_array_equal(out, a.record(p))
         assert L.dp_rec_validate(r.ctypes.data_as(_lib.c_i32p), len(r)) == 0
-        if r[13] in (3, 5):
+        if r[13] in (3, 5, 6):
             np.testing.assert_array_equal(unpack_p16(r), a.record(p))
 
 
@@ -215,7 +218,7 @@ def test_packed_malformed_is_rejected():
     sum to the row total, an out-of-range literal, dependency rows that no
     longer imply the header's choice lists (DP_FMT_P16D): dp_rec_validate
     rejects each (the kernel checks the same, tests/test_gpu_parity.py)."""
-    b = lowered_config(2, 4, 41, packed=True)
+    b = lowered_config(2, 4, 41, packed=True, p8=False)
     L = _lib.lib()
     r0 = np.ascontiguousarray(b.record(1)).copy()
     assert r0[13] == 5
@@ -338,3 +341,81 @@ def test_pipelined_solve_wire_stitching():
     np.testing.assert_array_equal(st.ident_con, whole.ident_con)
     np.testing.assert_array_equal(st.err, whole.err)
     assert n_core >= 0
+
+
+# ---------------------------------------------------------------------------
+# DP_FMT_P8D: DP_FMT_P16D in 8-bit variables + bit planes
+# ---------------------------------------------------------------------------
+def test_p8_wide_variables_and_flags():
+    """Records of 257..512 variables take DP_FMT_P8D with the bit-8 planes,
+    AtMost bounds of 2 their byte bounds, a 20-candidate Dependency byte
+    lengths; past 512 variables the record stays DP_FMT_P16D.  Every record
+    widens (dp_rec_widen and the restatement) to its int32 record."""
+    from deppy_amd import sat
+    from tests.gpu_common import unpack_p16, wide_problems
+    probs = wide_problems(5, 8, [300, 512, 513, 200])
+    wire = sat.encode_inputs(probs)
+    a = _lib.Lowered(wire)
+    b = _lib.Lowered(wire, narrow=True, packed=True)
+    L = _lib.lib()
+    flags = set()
+    for p in range(a.n):
+        r = np.ascontiguousarray(b.record(p))
+        nv = int(r[1])
+        assert int(r[13]) == (6 if nv <= 512 else 5), (p, nv, int(r[13]))
+        if r[13] == 6:
+            f = int(r[14]) & 0xff
+            assert bool(f & 2) == (nv > 256)
+            flags.add(f)
+            assert (int(r[14]) >> 8) <= 4 * (len(r) - 16)
+        out = np.zeros(int(r[10]), np.int32)
+        assert L.dp_rec_widen(r.ctypes.data_as(_lib.c_i32p), len(r), out.ctypes.data_as(_lib.c_i32p)) == 0
+        np.testing.assert_array_equal(out, a.record(p))
+        np.testing.assert_array_equal(unpack_p16(r), a.record(p))
+        assert L.dp_rec_validate(r.ctypes.data_as(_lib.c_i32p), len(r)) == 0
+    assert any(f & 4 for f in flags) and any(not f & 4 for f in flags), flags  # nibble and byte lengths
+    assert any(not f & 1 for f in flags), flags                                # byte bounds
+
+
+def test_p8_is_the_p16d_record_in_fewer_bytes():
+    """DP_FMT_P8D decodes (independent restatement) to exactly the
+    DP_FMT_P16D record DP_LOWER_NO_P8 emits, and config 2's batch shrinks by
+    at least a third."""
+    from tests.gpu_common import unpack_p8
+    a = lowered_config(2, 300, 19, packed=True, p8=False)
+    b = lowered_config(2, 300, 19, packed=True)
+    for p in range(a.n):
+        r16, r8 = a.record(p), b.record(p)
+        assert r16[13] == 5 and r8[13] == 6
+        d = unpack_p8(np.ascontiguousarray(r8))
+        np.testing.assert_array_equal(d, r16[:len(d)])
+        assert not np.any(r16[len(d):])  # (the rest is padding)
+    assert b.rec_off[-1] < 0.67 * a.rec_off[-1], (b.rec_off[-1], a.rec_off[-1])
+
+
+def test_p8_malformed_is_rejected():
+    """An unknown flag bit, a body byte count shorter than its sections, a
+    list source marked nonzero that is zero, a variable past nv (the bit-8
+    plane), lengths that do not sum to the row total: dp_rec_validate rejects
+    each (the kernel checks the same, tests/test_gpu_parity.py)."""
+    from tests.gpu_common import p8_sections
+    b = lowered_config(2, 40, 43, packed=True)
+    L = _lib.lib()
+
+    def bad(r):
+        return L.dp_rec_validate(np.ascontiguousarray(r).ctypes.data_as(_lib.c_i32p), len(r)) != 0
+    p = next(p for p in range(b.n) if int(b.record(p)[14]) & 4 and int(b.record(p)[1]) < 256
+             and p8_sections(b.record(p))["nz"] > 0)
+    r0 = np.ascontiguousarray(b.record(p)).copy()
+    assert r0[13] == 6 and not bad(r0)
+    S = p8_sections(r0)
+    r = r0.copy(); r[14] |= 64                                                        # unknown flag
+    assert bad(r)
+    r = r0.copy(); r[14] = (r[14] & 0xff) | ((S["srcval"] - 1) << 8)                 # body too short
+    assert bad(r)
+    r = r0.copy(); t = r[16:].view(np.uint8); t[S["srcval"]] = 0                     # a nonzero source is 0
+    assert bad(r)
+    r = r0.copy(); t = r[16:].view(np.uint8); t[0] = 255                             # variable past nv
+    assert bad(r)
+    r = r0.copy(); t = r[16:].view(np.uint8); t[S["lens"]] ^= 1                      # a row length off by one
+    assert bad(r)
