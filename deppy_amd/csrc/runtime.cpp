@@ -112,6 +112,7 @@ constexpr int64_t kChunkBytes = 1ll << 30;
 // balance, and the smallest such chunk (config 2: 5000-problem chunks ran 3%
 // under whole 10k ones, 2500-problem ones 32%; profiles/r05_chunk_ab.txt)
 constexpr int32_t kChunksPerDevice = 3;
+constexpr int kCostClasses = 16;  // plan_chunk: dispatch classes of one-wavefront problems (anchors, capped)
 constexpr int32_t kMinSharedChunk = 4096;
 // D2H of the explanation pool per chunk: this many words per problem are
 // copied with the fixed outputs; a chunk whose cores need more fetches the
@@ -170,6 +171,7 @@ struct Head {
   bool direct;    // the record is its own staged form (16-bit, 16-byte aligned)
   int32_t lds, inst_words, nid;
   int64_t sw, rec_bytes;
+  uint8_t cls;    // cost class of a one-wavefront problem: its anchors (plan_chunk's dispatch order)
 };
 
 struct Plan {
@@ -215,6 +217,7 @@ void read_head(Head& H, const int32_t* h, int64_t avail, int32_t opt_flags, bool
   if (!header_ok(h, avail)) { H.place = -1; return; }
   H.inst_words = bits_words(h[DP_H_NV]);
   H.nid = h[DP_H_NID];
+  H.cls = (uint8_t)std::min<int32_t>(h[DP_H_NA], kCostClasses - 1);
   // lds_path, with the one-wavefront layout computed once; past
   // group_above(), a record whose 16-bit image fits a CU may go to the
   // all-LDS multi-wave group (ldsg_ok: plan_chunk decides per chunk;
@@ -431,23 +434,43 @@ void plan_chunk(Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0,
   // 10.9 -> 6.5 MB; config 5 and 6 unchanged (scripts/xcd_ab.sh,
   // profiles/r03_xcd_order_ab.txt).
   static const int64_t xcd_order = env_i64("DEPPY_XCD_ORDER", kMaxLdsBytes);
+  static const bool anchor_order = env_i64("DEPPY_ANCHOR_ORDER", 1) != 0;  // diagnostic A/B
   for (int r = 0; r < ng; ++r) {
     const int g = ix[r];
     if (xcd_order && bl[g].lds <= xcd_order) {
-      // XCD-contiguous: workgroup b runs on XCD b % kXcds, so the launch's
-      // members (in problem order) are cut into kXcds contiguous ranges and
-      // XCD x takes range x in problem order: neighbouring records (sharing
-      // their boundary lines) are read, and neighbouring results written,
-      // through one XCD's L2 at about the same time
+      // Dispatch order by cost class, the costliest first: a catalog's
+      // anchors (Mandatory roots, lit_mapping.go:163-174) start its search,
+      // and on config 2 they predict its steps (correlation 0.7 with their
+      // log; 89 of the 100 slowest of 10k catalogs have 3 or 4 of 4), so the
+      // slow ones start with the launch instead of forming its tail.
+      // Within a class XCD-contiguous: workgroup b runs on XCD b % kXcds,
+      // so XCD x takes the x-th contiguous range of the class's members in
+      // problem order: neighbouring records (sharing their boundary lines)
+      // are read, and neighbouring results written, through one XCD's L2 at
+      // about the same time
       int32_t* v = P.order.data() + bl[g].first;
-      const int32_t m = bl[g].count, base = m / kXcds, rem = m % kXcds;
-      P.tmp.assign(v, v + m);
-      int32_t start[kXcds];
-      for (int x = 0, s = 0; x < kXcds; ++x) {
-        start[x] = s;
-        s += base + (x < rem);
+      const int32_t m = bl[g].count;
+      P.tmp.resize((size_t)m);
+      int32_t ccnt[kCostClasses] = {}, cat[kCostClasses];
+      for (int32_t b = 0; b < m; ++b) ccnt[anchor_order ? head[v[b]].cls : 0]++;
+      for (int c = kCostClasses - 1, o2 = 0; c >= 0; --c) {
+        cat[c] = o2;
+        o2 += ccnt[c];
       }
-      for (int32_t b = 0; b < m; ++b) v[b] = P.tmp[(size_t)(start[b % kXcds] + b / kXcds)];
+      for (int32_t b = 0; b < m; ++b) P.tmp[(size_t)cat[anchor_order ? head[v[b]].cls : 0]++] = v[b];
+      for (int32_t pos = 0; pos < m;) {  // one class: [pos, end) of tmp
+        const int32_t c = anchor_order ? head[P.tmp[(size_t)pos]].cls : 0;
+        int32_t end = pos;
+        while (end < m && (!anchor_order || head[P.tmp[(size_t)end]].cls == c)) ++end;
+        int32_t cnt[kXcds] = {}, start[kXcds], k[kXcds] = {};
+        for (int32_t b = pos; b < end; ++b) cnt[b % kXcds]++;
+        for (int x = 0, s2 = pos; x < kXcds; ++x) {
+          start[x] = s2;
+          s2 += cnt[x];
+        }
+        for (int32_t b = pos; b < end; ++b) v[b] = P.tmp[(size_t)(start[b % kXcds] + k[b % kXcds]++)];
+        pos = end;
+      }
     } else {
       lpt(P.order.data() + bl[g].first, (size_t)bl[g].count);
     }
@@ -859,6 +882,10 @@ struct Lane {
   // the chunk in flight
   dp_job* job = nullptr;
   int32_t p0 = 0;
+  // its results being scattered by the device's finisher thread (under
+  // Device::fmu): the lane's buffers and plan are the finisher's until then
+  dp_job* fjob = nullptr;
+  bool scattering = false;
   Plan plan;
   OutLayout ol{};
   std::vector<uint8_t> bad;  // per-problem malformed marks of the chunk being started
@@ -910,6 +937,13 @@ struct Device {
   std::deque<Lane*> inflight;     // lanes holding a chunk, oldest first (worker only)
   dp::Pool* pool = nullptr;       // staging and planning threads of this device
   bool own_pool = false;
+  // -- the finisher's: chunks done on the GPU, their results scattered into
+  // their jobs' dp_result off the worker's path (finisher_main) --
+  std::thread finisher;
+  std::mutex fmu;
+  std::condition_variable fcv;
+  std::deque<Lane*> fq;
+  bool fstop = false;
   std::mutex smu;                 // st
   dp_stats st{};                  // this device's pipeline counters
 };
@@ -1106,10 +1140,57 @@ int finish_lane(dp_ctx* ctx, Device& D, Lane& L) {
     HIP_OK(hipStreamSynchronize(L.s));
     st.d2h_bytes += (int64_t)(need - L.ol.d2h);
   }
-  st.bcp_bytes += (int64_t)scatter(L.plan, L.ol, L.h_out.p, L.p0, &job->res, D.pool);
-  st.scatter_ms += now_ms() - t1;
   add_device_stats(D, st);
+  // the results to the caller on the finisher thread, so the worker goes on
+  // planning and enqueueing the next chunks (config 2: planning and scatter
+  // took 0.15 + 0.17 ms of the worker's 0.45 ms per 10k-catalog chunk)
+  {
+    std::lock_guard<std::mutex> lk(D.fmu);
+    L.fjob = job;
+    L.scattering = true;
+    D.fq.push_back(&L);
+  }
+  D.fcv.notify_all();
   return 0;
+}
+
+void chunk_done(dp_job* job, int rc);
+
+// Wait until lane L's results are scattered (the worker, before it reuses
+// the lane's buffers or plan).
+void wait_scatter(Device& D, Lane& L) {
+  std::unique_lock<std::mutex> lk(D.fmu);
+  D.fcv.wait(lk, [&] { return !L.scattering; });
+}
+
+// A device's finisher thread: scatters finished chunks' results into their
+// jobs (oldest first) and accounts them.  Exits once stopped and drained.
+void finisher_main(dp_ctx* ctx, Device* Dp) {
+  Device& D = *Dp;
+  std::unique_lock<std::mutex> lk(D.fmu);
+  for (;;) {
+    if (D.fq.empty()) {
+      if (D.fstop) return;
+      D.fcv.wait(lk);
+      continue;
+    }
+    Lane* L = D.fq.front();
+    D.fq.pop_front();
+    lk.unlock();
+    dp_stats st{};
+    const double t0 = now_ms();
+    dp_job* job = L->fjob;
+    st.bcp_bytes += (int64_t)scatter(L->plan, L->ol, L->h_out.p, L->p0, &job->res, D.pool);
+    st.scatter_ms += now_ms() - t0;
+    add_device_stats(D, st);
+    lk.lock();
+    L->scattering = false;
+    L->fjob = nullptr;
+    lk.unlock();
+    D.fcv.notify_all();
+    chunk_done(job, 0);  // (may free the job: not touched after this)
+    lk.lock();
+  }
 }
 
 // One chunk of `job` is over (delivered, failed or skipped).
@@ -1129,7 +1210,7 @@ void deliver(dp_ctx* ctx, Device& D, Lane& L) {
   auto it = std::find(D.inflight.begin(), D.inflight.end(), &L);
   if (it != D.inflight.end()) D.inflight.erase(it);
   const int rc = finish_lane(ctx, D, L);
-  chunk_done(job, rc);
+  if (rc) chunk_done(job, rc);  // (else the finisher completes the chunk)
 }
 
 // Planning storage of `dst` grown to (at least) the sizes `src` uses, with
@@ -1198,10 +1279,12 @@ int grow_device_lanes(dp_ctx* ctx, Device& D, Lane& L, const LaneNeed& need) {
   for (int li = 0; li < D.nlanes; ++li) {
     Lane& O = D.lanes[li];
     if (&O == &L) continue;
+    wait_scatter(D, O);
     grow_plan(O.plan, L.plan);
     grow_vec(O.bad, L.bad.size());
     if (need.fits(O)) continue;
     deliver(ctx, D, O);  // (an error of its chunk goes to that chunk's job)
+    wait_scatter(D, O);
     if (reserve_lane(ctx, O, need)) return -1;
   }
   return 0;
@@ -1214,6 +1297,21 @@ int start_chunk(dp_ctx* ctx, Device& D, Lane& L, dp_job* job, int32_t p0, int32_
   const int64_t allocs0 = g_buf_allocs.load(std::memory_order_relaxed);
   const size_t bad_cap = L.bad.capacity(), plan_cap0 = plan_cap(L.plan);
   const double t0 = now_ms();
+  // The records' DMA ahead of the plan (the plan adds only the tables after
+  // them): a page-locked batch whose first record is in a staged form sends
+  // its source range to the image's front at once when it fits the lane and
+  // its copy is not one the fill would chain (below), so the copy runs under
+  // the planning.  (A chunk that then turns out not to be direct stages its
+  // image over it, later on the same stream.)
+  static const int64_t chain_mb = env_i64("DEPPY_COPY_CHAIN_MB", 64);
+  static const bool early_dma = env_i64("DEPPY_EARLY_DMA", 1) != 0;  // diagnostic A/B
+  const int64_t W = job->rec_off[p0 + n] - job->rec_off[p0];
+  hipStream_t cs = L.cs ? L.cs : L.s;
+  const int32_t f0 = n > 0 && W >= DP_H_SIZE ? job->rec[job->rec_off[p0] + DP_H_FMT] : -1;
+  const bool early = early_dma && job->pinned && !ctx->zc_in && W > 0 && (size_t)4 * W <= L.d_in.cap &&
+                     (f0 == DP_FMT_U16 || dp_fmt_packed(f0)) &&
+                     !(chain_mb > 0 && (size_t)4 * W >= (size_t)chain_mb << 20);
+  if (early) HIP_OK(hipMemcpyAsync(L.d_in.p, job->rec + job->rec_off[p0], 4 * (size_t)W, hipMemcpyHostToDevice, cs));
   L.bad.assign((size_t)n, 0);
   std::vector<uint8_t>& bad = L.bad;
   dp::plan_chunk(L.plan, job->rec, job->rec_off, p0, n, ctx->flags, &bad, D.pool);
@@ -1226,7 +1324,6 @@ int start_chunk(dp_ctx* ctx, Device& D, Lane& L, dp_job* job, int32_t p0, int32_
   // offset, and only the other problems' records are staged, after it.
   // (Worth it while the others' source words, copied for nothing, are not
   // the larger part.)
-  const int64_t W = job->rec_off[p0 + n] - job->rec_off[p0];
   const bool direct = job->pinned && L.plan.n_direct > 0 && !ctx->zc_in && 2 * L.plan.other_words <= W;
   if (direct) {
     Plan& Q = L.plan;
@@ -1249,7 +1346,9 @@ int start_chunk(dp_ctx* ctx, Device& D, Lane& L, dp_job* job, int32_t p0, int32_
   const size_t rest = direct ? il.img + 4 * (size_t)W : 0;
   const LaneNeed need{il.end - rest, il.end, L.ol.end, L.ol.end,
                       (size_t)std::max<int64_t>(L.plan.scratch_words, 1) * 4};
+  const char* const d_in0 = L.d_in.p;
   if (!need.fits(L) && grow_device_lanes(ctx, D, L, need)) return -1;
+  const bool early_in = early && L.d_in.p == d_in0;  // (a grown lane has a new buffer: copy again)
   char* const hin = L.h_in.p - rest;  // (only offsets >= rest are used)
   const Plan& P = L.plan;
   if (!direct || P.n_direct < n) {  // stage the records (host pool)
@@ -1278,7 +1377,6 @@ int start_chunk(dp_ctx* ctx, Device& D, Lane& L, dp_job* job, int32_t p0, int32_
   char* dout = L.zc_out ? L.h_out.dev : L.d_out.p;
   size_t h2d = 0;
   // (lane buffers are free: finish_lane waited for the lane's last chunk)
-  hipStream_t cs = L.cs ? L.cs : L.s;
   // Filling an idle pipeline with large chunks, copies go in submission
   // order: the first chunks (one per stream) each wait for the previous
   // one's copy instead of sharing PCIe with all of them, so the first
@@ -1288,7 +1386,6 @@ int start_chunk(dp_ctx* ctx, Device& D, Lane& L, dp_job* job, int32_t p0, int32_
   // DEPPY_COPY_CHAIN_MB (default 64; 0: off): measured on one box, configs 4
   // and 5 (564 / 322 MB chunks) gain 10-11% host to host at 20 steps, while
   // configs 2 and 6 (19 / 10 MB) lose half (profiles/r03_copy_chain_ab_unsized.txt).
-  static const int64_t chain_mb = env_i64("DEPPY_COPY_CHAIN_MB", 64);
   const size_t copy_bytes = direct ? 4 * (size_t)W + (il.end - rest) : zc_in ? 0 : il.end;
   if (D.inflight.empty()) D.fill_left = D.nstreams;
   const bool chain = chain_mb > 0 && D.fill_left > 0 && copy_bytes >= (size_t)chain_mb << 20;
@@ -1298,14 +1395,14 @@ int start_chunk(dp_ctx* ctx, Device& D, Lane& L, dp_job* job, int32_t p0, int32_
   (void)hipGetLastError();  // (hipEventQuery's not-ready status)
   if (direct) {
     const size_t src_bytes = 4 * (size_t)W;
-    if (src_bytes)
+    if (src_bytes && !early_in)
       HIP_OK(hipMemcpyAsync(L.d_in.p + il.img, job->rec + job->rec_off[p0], src_bytes, hipMemcpyHostToDevice, cs));
     HIP_OK(hipMemcpyAsync(L.d_in.p + rest, L.h_in.p, il.end - rest, hipMemcpyHostToDevice, cs));
     h2d = src_bytes + il.end - rest;
     st.direct_chunks++;
   } else if (!zc_in) {
     HIP_OK(hipMemcpyAsync(L.d_in.p, L.h_in.p, il.end, hipMemcpyHostToDevice, cs));
-    h2d = il.end;
+    h2d = il.end + (early ? 4 * (size_t)W : 0);
   }
   if (cs != L.s || chain) HIP_OK(hipEventRecord(L.copied, cs));
   if (cs != L.s) HIP_OK(hipStreamWaitEvent(L.s, L.copied, 0));
@@ -1367,6 +1464,7 @@ void run_task(dp_ctx* ctx, Device& D, const Task& t) {
   Lane& L = D.lanes[D.cursor];
   D.cursor = (D.cursor + 1) % D.nlanes;
   deliver(ctx, D, L);
+  wait_scatter(D, L);
   if (start_chunk(ctx, D, L, job, t.p0, t.n)) {
     L.job = nullptr;
     chunk_done(job, -1);
@@ -1589,6 +1687,7 @@ dp_ctx* dp_create(const dp_opts* opts) {
     D.own_pool = cnt > 1;
     D.pool = D.own_pool ? new dp::Pool(per) : ctx->pool;
     D.worker = std::thread(worker_main, ctx, &D);
+    D.finisher = std::thread(finisher_main, ctx, &D);
   }
   return ctx;
 }
@@ -1603,6 +1702,14 @@ void dp_destroy(dp_ctx* ctx) {
     }
     D.qcv.notify_all();
     D.worker.join();
+    if (D.finisher.joinable()) {  // (the worker handed it every chunk it delivered)
+      {
+        std::lock_guard<std::mutex> lk(D.fmu);
+        D.fstop = true;
+      }
+      D.fcv.notify_all();
+      D.finisher.join();
+    }
     if (D.own_pool) delete D.pool;
     D.pool = nullptr;
   }
