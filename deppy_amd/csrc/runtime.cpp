@@ -174,6 +174,15 @@ struct Head {
   uint8_t cls;    // cost class of a one-wavefront problem: its anchors (plan_chunk's dispatch order)
 };
 
+// One block of plan_chunk's passes: its sums, then (after the scan) its
+// image and installed-word bases.
+constexpr int32_t kPlanBlock = 512;
+struct PlanBlock {
+  int64_t img = 0, inst = 0, core = 0, rbytes = 0, other = 0;
+  int32_t ndirect = 0, nother = 0, nok = 0;
+  int32_t bcount[kNBuckets] = {}, bmax[kNBuckets] = {};
+};
+
 struct Plan {
   int32_t n = 0;
   std::vector<int64_t> img_off;   // [n+1] staged word offsets
@@ -199,6 +208,7 @@ struct Plan {
   // planning scratch, kept across chunks (no allocation or page fault per
   // chunk once grown)
   std::vector<Head> head;
+  std::vector<PlanBlock> blk;
   std::vector<int32_t> big[5], cnt, tmp, grp;
 };
 
@@ -289,61 +299,123 @@ void plan_chunk(Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0,
   P.n_direct = 0;
   P.big_base = 0;
   Head* head = P.head.data();
-  auto rd = [&](int64_t i) {
-    // every header is a cache miss: keep the next ones in flight
-    if (i + 8 < n) {
-      const int32_t* h8 = rec + rec_off[p0 + i + 8];
-      __builtin_prefetch(h8);
-      __builtin_prefetch(h8 + 15);
-    }
-    read_head(head[i], rec + rec_off[p0 + i], rec_off[p0 + i + 1] - rec_off[p0 + i], opt_flags,
-              (rec_off[p0 + i] & 3) == 0);
+  // Three passes over blocks of kPlanBlock problems (on the pool when there
+  // are several blocks; the per-problem work is a header cache miss and its
+  // layout arithmetic, ~25 ns a header on one core): the headers, then each
+  // block's sums, then the offsets from the scanned sums.  The lists of
+  // multi-wave and skipped problems are built in problem order afterwards,
+  // only when the chunk has some.
+  const int32_t nblk = (n + kPlanBlock - 1) / kPlanBlock;
+  P.blk.resize((size_t)std::max(nblk, 1));
+  auto over_blocks = [&](const std::function<void(int64_t)>& fn) {
+    if (pool && nblk > 1) pool->run(nblk, fn, 1);
+    else for (int32_t b = 0; b < nblk; ++b) fn(b);
   };
-  if (pool && n > 256) pool->run(n, std::function<void(int64_t)>(rd), 64);
-  else for (int32_t i = 0; i < n; ++i) rd(i);
+  over_blocks([&](int64_t b) {
+    const int32_t i0 = (int32_t)b * kPlanBlock, i1 = std::min(n, i0 + kPlanBlock);
+    int32_t nok = 0;
+    for (int32_t i = i0; i < i1; ++i) {
+      // every header is a cache miss: keep the next ones in flight
+      if (i + 8 < i1) {
+        const int32_t* h8 = rec + rec_off[p0 + i + 8];
+        __builtin_prefetch(h8);
+        __builtin_prefetch(h8 + 15);
+      }
+      read_head(head[i], rec + rec_off[p0 + i], rec_off[p0 + i + 1] - rec_off[p0 + i], opt_flags,
+                (rec_off[p0 + i] & 3) == 0);
+      nok += head[i].ldsg_ok;
+    }
+    P.blk[(size_t)b].nok = nok;
+  });
   // mid-size catalogs onto the all-LDS group when the chunk holds few of
   // them (placement.hpp kLdsgMaxProblems), else the HBM-read 4-wave groups
   {
     const int lm = dp::ldsg_env();
     int32_t n_ok = 0;
-    for (int32_t i = 0; i < n; ++i) n_ok += head[i].ldsg_ok;
+    for (int32_t b = 0; b < nblk; ++b) n_ok += P.blk[(size_t)b].nok;
     if (n_ok > 0 && (lm == dp::LDSG_ALWAYS || (lm == dp::LDSG_AUTO && n_ok <= dp::kLdsgMaxProblems)))
       for (int32_t i = 0; i < n; ++i)
         if (head[i].ldsg_ok) place_ldsg(head[i], rec + rec_off[p0 + i], (rec_off[p0 + i] & 3) == 0);
   }
-  // one pass: offsets, totals and per-bucket counts / LDS maxima
+  // per block: totals and per-bucket counts / LDS maxima
+  const bool rec_aligned = ((uintptr_t)rec & 15) == 0;
+  over_blocks([&](int64_t b) {
+    PlanBlock& B = P.blk[(size_t)b];
+    const int32_t nok = B.nok;
+    B = PlanBlock{};
+    B.nok = nok;
+    const int32_t i0 = (int32_t)b * kPlanBlock, i1 = std::min(n, i0 + kPlanBlock);
+    for (int32_t i = i0; i < i1; ++i) {
+      const Head& H = head[i];
+      const bool d = rec_aligned && H.direct;
+      B.ndirect += d;
+      B.other += d ? 0 : rec_off[p0 + i + 1] - rec_off[p0 + i];
+      if (H.place == M_LDS) {
+        B.bcount[H.bucket]++;
+        B.bmax[H.bucket] = std::max(B.bmax[H.bucket], H.lds);
+      } else {
+        B.nother++;
+      }
+      if (H.place != -1) {
+        B.img += H.sw;
+        B.inst += H.inst_words;
+        B.core += H.nid;
+        B.rbytes += H.rec_bytes;
+      }
+    }
+  });
   for (auto& v : P.big) v.clear();
   int32_t bcount[kNBuckets] = {}, bmax[kNBuckets] = {};
-  const bool rec_aligned = ((uintptr_t)rec & 15) == 0;
   int64_t img = 0, inst = 0;
-  P.img_off[0] = P.inst_off[0] = 0;
-  for (int32_t i = 0; i < n; ++i) {
-    const Head& H = head[i];
-    const bool d = rec_aligned && H.direct;
-    P.direct[(size_t)i] = d;
-    P.n_direct += d;
-    P.other_words += d ? 0 : rec_off[p0 + i + 1] - rec_off[p0 + i];
-    P.narrow[(size_t)i] = H.place == M_LDS || H.place == M_LDSG;
-    if (H.place == M_LDS) {
-      bcount[H.bucket]++;
-      bmax[H.bucket] = std::max(bmax[H.bucket], H.lds);
-    } else if (H.place >= 0) {
-      P.big[(size_t)H.place].push_back(i);
-    } else {
-      if (H.place == -1 && bad) (*bad)[(size_t)i] = 1;
-      P.skip.push_back(i);
-      P.skip_flags.push_back(H.place == -1 ? DP_F_MALFORMED : DP_F_TOO_LARGE);
+  bool others = false;
+  for (int32_t b = 0; b < nblk; ++b) {  // the scan
+    PlanBlock& B = P.blk[(size_t)b];
+    const int64_t bi = B.img, bn = B.inst;
+    B.img = img;
+    B.inst = inst;
+    img += bi;
+    inst += bn;
+    P.n_direct += B.ndirect;
+    P.other_words += B.other;
+    P.core_cap += B.core;
+    P.rec_bytes += B.rbytes;
+    others |= B.nother > 0;
+    for (int k = 0; k < kNBuckets; ++k) {
+      bcount[k] += B.bcount[k];
+      bmax[k] = std::max(bmax[k], B.bmax[k]);
     }
-    if (H.place != -1) {
-      img += H.sw;
-      inst += H.inst_words;
-      P.core_cap += H.nid;
-      P.rec_bytes += H.rec_bytes;
-    }
-    P.img_off[(size_t)i + 1] = img;
-    P.inst_off[(size_t)i + 1] = inst;
   }
-  P.dev_off.assign(P.img_off.begin(), P.img_off.end() - 1);
+  P.dev_off.resize((size_t)n);
+  P.img_off[0] = P.inst_off[0] = 0;
+  over_blocks([&](int64_t b) {
+    const PlanBlock& B = P.blk[(size_t)b];
+    int64_t im = B.img, in = B.inst;
+    const int32_t i0 = (int32_t)b * kPlanBlock, i1 = std::min(n, i0 + kPlanBlock);
+    for (int32_t i = i0; i < i1; ++i) {
+      const Head& H = head[i];
+      P.direct[(size_t)i] = rec_aligned && H.direct;
+      P.narrow[(size_t)i] = H.place == M_LDS || H.place == M_LDSG;
+      P.dev_off[(size_t)i] = im;
+      if (H.place != -1) {
+        im += H.sw;
+        in += H.inst_words;
+      }
+      P.img_off[(size_t)i + 1] = im;
+      P.inst_off[(size_t)i + 1] = in;
+    }
+  });
+  if (others)
+    for (int32_t i = 0; i < n; ++i) {
+      const Head& H = head[i];
+      if (H.place == M_LDS) continue;
+      if (H.place >= 0) {
+        P.big[(size_t)H.place].push_back(i);
+      } else {
+        if (H.place == -1 && bad) (*bad)[(size_t)i] = 1;
+        P.skip.push_back(i);
+        P.skip_flags.push_back(H.place == -1 ? DP_F_MALFORMED : DP_F_TOO_LARGE);
+      }
+    }
   P.img_words = img;
   // Within a launch, workgroups are dispatched in blockIdx order: largest
   // record first (longest-processing-time-first), so the long solves do not
@@ -1235,7 +1307,8 @@ void grow_plan(Plan& dst, const Plan& src) {
   grow_vec(dst.dev_off, src.dev_off.size());
   grow_vec(dst.direct, src.direct.size());
   grow_vec(dst.head, src.head.size());
-  for (int k = 0; k < 4; ++k) grow_vec(dst.big[k], src.big[k].size());
+  grow_vec(dst.blk, src.blk.size());
+  for (int k = 0; k < 5; ++k) grow_vec(dst.big[k], src.big[k].size());
   grow_vec(dst.cnt, src.cnt.capacity());
   grow_vec(dst.tmp, src.tmp.capacity());
 }
@@ -1262,7 +1335,8 @@ int reserve_lane(dp_ctx* ctx, Lane& L, const LaneNeed& n) {
 size_t plan_cap(const Plan& P) {
   size_t c = P.img_off.capacity() + P.inst_off.capacity() + P.dev_off.capacity() + P.scratch_off.capacity() +
              P.narrow.capacity() + P.direct.capacity() + P.order.capacity() + P.launches.capacity() +
-             P.skip.capacity() + P.skip_flags.capacity() + P.head.capacity() + P.cnt.capacity() + P.tmp.capacity();
+             P.skip.capacity() + P.skip_flags.capacity() + P.head.capacity() + P.cnt.capacity() + P.tmp.capacity() +
+             P.blk.capacity();
   for (const auto& b : P.big) c += b.capacity();
   return c;
 }
@@ -1774,8 +1848,8 @@ int dp_device_bytes(const dp_batch* b, int32_t opt_flags, int64_t* rec_bytes, in
 
 int dp_plan_placements(const dp_batch* b, int32_t opt_flags, int8_t* place) {
   if (!b || !place || b->n_problems < 0 || (b->n_problems > 0 && (!b->rec || !b->rec_off))) return -1;
-  Plan P;
-  dp::plan_chunk(P, b->rec, b->rec_off, 0, b->n_problems, opt_flags, nullptr);
+  static thread_local Plan P;  // (reused, as a lane's: no allocation once grown)
+  dp::plan_chunk(P, b->rec, b->rec_off, 0, b->n_problems, opt_flags, nullptr, &dp::host_pool());
   for (int32_t i = 0; i < b->n_problems; ++i) place[i] = (int8_t)P.head[(size_t)i].place;
   return 0;
 }
