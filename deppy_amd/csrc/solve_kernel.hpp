@@ -115,16 +115,23 @@ __device__ __forceinline__ int wave_incl_max(int x) {
   return y;
 }
 
+// Whole-wave minimum and sum, wave-uniform: the DPP scans' lane 63.  (A
+// __shfl_xor butterfly takes a ds_bpermute address VGPR per step, which the
+// compiler keeps live across the search loop: six of the register-capped
+// build's spills.)
 __device__ __forceinline__ int wave_min(int x) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) x = min(x, __shfl_xor(x, d));
-  return x;
+  constexpr int I = 0x7fffffff;  // lanes a shift does not reach keep the identity (bound_ctrl off)
+  int y = x;
+  y = min(y, __builtin_amdgcn_update_dpp(I, x, 0x111, 0xf, 0xf, false));  // row_shr:1
+  y = min(y, __builtin_amdgcn_update_dpp(I, x, 0x112, 0xf, 0xf, false));  // row_shr:2
+  y = min(y, __builtin_amdgcn_update_dpp(I, x, 0x113, 0xf, 0xf, false));  // row_shr:3
+  y = min(y, __builtin_amdgcn_update_dpp(I, y, 0x114, 0xf, 0xe, false));  // row_shr:4, banks 1-3
+  y = min(y, __builtin_amdgcn_update_dpp(I, y, 0x118, 0xf, 0xc, false));  // row_shr:8, banks 2-3
+  y = min(y, __builtin_amdgcn_update_dpp(I, y, 0x142, 0xa, 0xf, false));  // row_bcast:15 -> rows 1, 3
+  y = min(y, __builtin_amdgcn_update_dpp(I, y, 0x143, 0xc, 0xf, false));  // row_bcast:31 -> rows 2, 3
+  return __builtin_amdgcn_readlane(y, 63);
 }
-__device__ __forceinline__ int wave_sum(int x) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
-  return x;
-}
+__device__ __forceinline__ int wave_sum(int x) { return __builtin_amdgcn_readlane(wave_incl_scan(x), 63); }
 
 __device__ __forceinline__ bool getb(const uint32_t* b, int i) { return (b[i >> 5] >> (i & 31)) & 1u; }
 
@@ -424,7 +431,7 @@ struct Group {
     } else {
       int b = 0;
       if (m && lane == 0) b = atomicAdd(&scal[S_APP], __popcll(m));
-      b = __shfl(b, 0);
+      b = __builtin_amdgcn_readlane(b, 0);
       return run + b + __popcll(m & lanemask_lt());
     }
   }
@@ -2451,12 +2458,8 @@ struct Group {
       const int l = i < tlen ? (int)trail[i] : 1;
       int s = 0, n = 0;
       if (!(l & 1)) { s = (int)w_off[l]; n = (int)w_off[l + 1] - s; }
-      int inc = n;
-      for (int d = 1; d < 64; d <<= 1) {
-        const int t = __shfl_up(inc, d);
-        if (lane >= d) inc += t;
-      }
-      const int total = __shfl(inc, 63);
+      const int inc = wave_incl_scan(n);
+      const int total = __builtin_amdgcn_readlane(inc, 63);
       for (int base = 0; base < total; base += 64) {
         const int f = base + lane;
         int j = 0;  // lowest lane whose inclusive count exceeds f
@@ -3078,7 +3081,7 @@ struct Group {
   // thread 0's x in every thread
   __device__ __forceinline__ int g_bcast0(int x) {
     if constexpr (NW == 1) {
-      return __shfl(x, 0);
+      return __builtin_amdgcn_readlane(x, 0);
     } else {
       return exchange(x, tid == 0)[0];
     }
