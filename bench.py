@@ -335,10 +335,10 @@ def main():
                     help="skip the host-to-host leg (profiling runs of the solve kernel)")
     ap.add_argument("--flags", type=int, default=0,
                     help="dp_opts.flags (diagnostic placements: 1 group, 2 HBM, 4 mid groups)")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r05_pmc_traffic.jsonl"),
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r06_pmc_traffic.jsonl"),
                     help="HBM bytes per solve kernel dispatch from separate rocprofv3 --pmc passes; "
                          "used for roofline.traffic when its config/problems match")
-    ap.add_argument("--sq-json", default=os.path.join(ROOT, "profiles", "r05_sq_split.json"),
+    ap.add_argument("--sq-json", default=os.path.join(ROOT, "profiles", "r06_sq_split.json"),
                     help="SQ instruction counts per wave of this build (scripts/pmc_sq_r02.sh + sq_summary.py), "
                          "for roofline.issue")
     args = ap.parse_args()

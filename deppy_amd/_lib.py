@@ -96,6 +96,7 @@ EXPORTS = [
     "dp_gen_free", "dp_upload_traced", "dp_download_trace", "dp_solve_traced", "dp_lowered_errors",
     "dp_device_bytes", "dp_lower_into", "dp_lowered_new", "dp_lowered_exact_count", "dp_lowered_pinned", "dp_rec_widen", "dp_submit", "dp_job_wait", "dp_get_stats", "dp_stage_roundtrip",
     "dp_stitch_selftest", "dp_partition", "dp_build_info", "dp_get_device_stats", "dp_plan_placements",
+    "dp_plan_order",
 ]
 
 
@@ -252,6 +253,7 @@ def lib():
     L.dp_gen_free.argtypes = [vp]
     L.dp_device_bytes.argtypes = [ctypes.POINTER(Batch), ctypes.c_int32, c_i64p, c_i64p]
     L.dp_plan_placements.argtypes = [ctypes.POINTER(Batch), ctypes.c_int32, c_i8p]
+    L.dp_plan_order.argtypes = [ctypes.POINTER(Batch), ctypes.c_int32, c_i32p, c_i32p]
     _lib = L
     return L
 
@@ -642,6 +644,19 @@ def plan_placements(rec_off, rec, flags: int = 0) -> np.ndarray:
     if lib().dp_plan_placements(ctypes.byref(_batch(rec_off, rec)), flags, _p(place, c_i8p)) != 0:
         raise RuntimeError("dp_plan_placements failed")
     return place[:len(rec_off) - 1]
+
+
+def plan_order(rec_off, rec, flags: int = 0):
+    """(order, launch_first): the workgroup order dp_submit plans for a batch
+    cut as one chunk (dp_plan_order)."""
+    rec_off = np.ascontiguousarray(rec_off, np.int64)
+    rec = np.ascontiguousarray(rec if len(rec) else np.zeros(1, np.int32), np.int32)
+    order = np.zeros(max(len(rec_off) - 1, 1), np.int32)
+    first = np.zeros(32, np.int32)
+    nl = lib().dp_plan_order(ctypes.byref(_batch(rec_off, rec)), flags, _p(order, c_i32p), _p(first, c_i32p))
+    if nl < 0:
+        raise RuntimeError("dp_plan_order failed")
+    return order, first[:nl]
 
 
 def stage_roundtrip(rec_off, rec, flags: int = 0, chunk_problems: int = 0, chunk_bytes: int = 0):

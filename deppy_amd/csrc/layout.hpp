@@ -66,64 +66,16 @@ __host__ __device__ constexpr int32_t mode_waves(int mode) {
   return mode == M_LDS ? 1 : mode == M_SPLIT4 ? MID_WAVES : mode == M_LDSG ? LDSG_WAVES : BIG_WAVES;
 }
 // work list of one propagation chunk (rows watched by <= 64*waves frontier literals)
-#ifndef DP_WBUF_LDS
-#define DP_WBUF_LDS 128
-#endif
-#ifndef DP_CQ_LDS
-#define DP_CQ_LDS 64
-#endif
 __host__ __device__ constexpr int32_t mode_wbuf(int mode) {
-  return mode == M_LDS ? DP_WBUF_LDS : mode == M_LDSG ? 1024 : 4096;
+  return mode == M_LDS ? 128 : mode == M_LDSG ? 1024 : 4096;
 }
 // AtMost rows queued for wave-cooperative evaluation in one round
-__host__ __device__ constexpr int32_t mode_cq(int mode) { return mode == M_LDS ? DP_CQ_LDS : mode == M_LDSG ? 256 : 512; }
-// M_LDS stores imp (the lowest implying row per literal) in 16 bits, updated
-// by a compare-and-swap, or in 32 bits, updated by atomicMin
-#ifndef DP_IMP16
-#define DP_IMP16 1
-#endif
-constexpr bool IMP16_LDS = DP_IMP16;
-// Two-watched-literal filter on the multi-wave placements (-DDP_2WL=1):
-// every clause row keeps the two literals it watches (Layout::wp); a round
-// reaches a row through the occurrence lists as before, but evaluates it only
-// when one of its watches is false, and then moves the watches
-// (solve_kernel.hpp clause_unit).  Bit-exact, and measured slower: config 4
-// kernel only 7.64k -> 6.50k res/s, config 5 720k -> 654k (the pair is one
-// more dependent read before a row, the rows it skips were short;
-// profiles/r03_c4_*.json, r03_c5_*.json).  Off: occurrence lists.
-#ifndef DP_2WL
-#define DP_2WL 0
-#endif
-__host__ __device__ constexpr bool mode_2wl(int mode) { return DP_2WL && !mode_n16(mode); }
-// Two-watched-literal propagation on the one-wavefront path (-DDP_TWL_LDS=1):
-// a clause row of 3..254 literals sits in the watch lists of two of its
-// positions only (Layout::wpos, a byte each); a round that falsifies one of
-// them moves that watch to another non-false position, so the row leaves
-// that literal's list and joins the new one's (per-literal live ends in
-// Layout::wend, within the occurrence-count capacity the lists already
-// have).  Row literals are never reordered (Solve()'s decision is the first
-// unassigned positive literal in row order).  Shorter and longer rows, and
-// AtMost rows, stay in every list they occur in.  Bit-exact with the
-// occurrence lists (solve_kernel.hpp visit_twl argues it).
-#ifndef DP_TWL_LDS
-#define DP_TWL_LDS 0
-#endif
-__host__ __device__ constexpr bool mode_twl_lds(int mode) { return DP_TWL_LDS && mode == M_LDS; }
-constexpr int32_t TWL_MIN_LEN = 3, TWL_MAX_LEN = 254;
-
-// Row slots on the multi-wave placements (-DDP_ROWSLOT=1; the compact hot
-// image of a clause row): 32 bytes per row in the HBM scratch, built during
-// init -- the row's watched pair, its length, and its literals inline when
-// it has at most five (else the row's offset into clause_lits).  A round
-// reaches a row from its watch entry with one 32-byte read instead of the
-// offsets-then-literals chain of the record.  Bit-exact, and measured
-// slower: config 4 kernel only 7.64k -> 7.30k res/s, with 2WL 6.41k (the
-// slots add 32 B a row to a working set that already misses L2).  Off.
-#ifndef DP_ROWSLOT
-#define DP_ROWSLOT 0
-#endif
-__host__ __device__ constexpr bool mode_rowslot(int mode) { return DP_ROWSLOT && !mode_n16(mode); }
-constexpr int32_t ROWSLOT_INLINE = 5;
+__host__ __device__ constexpr int32_t mode_cq(int mode) { return mode == M_LDS ? 64 : mode == M_LDSG ? 256 : 512; }
+// The one-wavefront image stores imp (the lowest implying row per literal)
+// in 16 bits, updated by a compare-and-swap; the multi-wave modes in 32
+// bits, updated by atomicMin.  Two-watched-literal filters, row slots and
+// 2-byte watch entries were built and measured slower on every placement
+// (DESIGN.md §5.3, §9); occurrence lists with 8-byte entries ship.
 
 // wave-shared scalars (S_*), then (multi-wave modes) per-wave reduction slots
 constexpr int32_t NSCAL = 64;
@@ -250,23 +202,6 @@ __host__ __device__ inline uint32_t row_info(int32_t a, int32_t len) {
   return a >= 0 && a < (1 << 24) && len >= 0 && len < 255 ? ((uint32_t)a << 8) | (uint32_t)len : ROW_INFO_NONE;
 }
 
-// Bytes per entry of the watch lists the device builds for a multi-wave
-// record (Layout::wl): 8 ({row, row_info(row)}, the row's literal range
-// carried in the entry), or with -DDP_WENT=2 (A/B) the row id alone when
-// every row id fits 16 bits.  The 2-byte entries shrink an OLM-scale
-// catalog's lists from ~2.1 MB to ~0.5 MB so its BCP working set fits one
-// XCD's 4 MB L2, at one more dependent read a visit (the row's offsets).
-// Measured (round 5, bit-exact): one config-4 catalog alone L2 hit rate
-// 69.7% -> 79.3%, but the 20-catalog kernel median 7.79-7.85 -> 7.85-7.94
-// ms and the 256-catalog batch unchanged (11.77k vs 11.82k res/s), with
-// more write requests (profiles/r05_c4_went_ab.txt).  8 stays.
-#ifndef DP_WENT
-#define DP_WENT 8
-#endif
-__host__ __device__ inline int32_t went_bytes(const int32_t* h) {
-  return DP_WENT == 2 && (int64_t)h[DP_H_NC] + h[DP_H_NK] <= 65535 ? 2 : 8;
-}
-
 struct ImgLayout {
   int32_t w_off, w, words;
 };
@@ -331,14 +266,8 @@ struct Layout {
   int32_t tl;        // u16[2hc] first implications, (slot << 1) | negative       [LDS]
   int32_t fr;        // i32[hc] trail ring: trail[i] at fr[i & (hc - 1)]          [LDS]
   int32_t hc;        // slots (a power of two; 0 when the mode keeps rounds in HBM)
-  int32_t wp;        // (mode_rowslot) i32[8][nc] row slots {watch x, watch y, len, l0 | offset, l1..l4};
-                     // else (mode_2wl) u64[nc] the two literals clause row r watches, low word first
   int32_t wl;        // multi-wave, DP_FMT_I32 records: device-built w_off[2nv+2], then
-                     // [ncl+nkl] entries: u16 rows, or int2 {row, row_info} (went_bytes)  [HBM]
-  int32_t wpos;      // (mode_twl_lds) u8[2nc] watched positions of each clause row
-  int32_t wend;      // (mode_twl_lds) u16[2nv] live end of each literal's watch list
-  int32_t wfi;       // (mode_twl_lds) u8[wbuf] frontier literal of each flattened work-list entry
-  int32_t fcur;      // (mode_twl_lds) i32[64] compaction cursor per frontier literal of a chunk
+                     // [ncl+nkl] int2 {row, row_info} entries  [HBM]
   int32_t bytes;     // HBM scratch bytes (0 for M_LDS / M_LDSG)
   int32_t lds_bytes; // LDS bytes
   int32_t cap, lcap;
@@ -425,18 +354,12 @@ __host__ __device__ inline Layout layout_hc(const int32_t* h, int32_t hc) {
   L.trail = take(nv * ix, COLD);
   L.touched = take(2 * nv * ix, COLD);
   L.d_mark = take(nv * ix, COLD);
-  L.imp = take(2 * nv * (N16 && IMP16_LDS ? 2 : 4), COLD);
+  L.imp = take(2 * nv * (N16 ? 2 : 4), COLD);
   L.l_off = take((L_MAX + 1) * ix, COLD);
   L.l_lits = take(L.lcap * ix, COLD);
   L.dq = take(2 * L.cap * ix, COLD);
   L.stk = take(3 * L.cap * ix, COLD);
-  L.wp = mode_rowslot(MODE) ? take(h[DP_H_NC] * 32, COLD) : mode_2wl(MODE) ? take(h[DP_H_NC] * 8, COLD) : 0;
-  L.wl = !N16 && h[DP_H_FMT] == DP_FMT_I32
-             ? take((2 * nv + 2) * 4 + (h[DP_H_NCL] + h[DP_H_NKL]) * went_bytes(h), COLD) : 0;
-  L.wpos = mode_twl_lds(MODE) ? take(2 * h[DP_H_NC], COLD) : 0;
-  L.wend = mode_twl_lds(MODE) ? take(4 * nv, COLD) : 0;
-  L.wfi = mode_twl_lds(MODE) ? take(mode_wbuf(MODE), COLD) : 0;
-  L.fcur = mode_twl_lds(MODE) ? take(64 * 4, COLD) : 0;
+  L.wl = !N16 && h[DP_H_FMT] == DP_FMT_I32 ? take((2 * nv + 2) * 4 + (h[DP_H_NCL] + h[DP_H_NKL]) * 8, COLD) : 0;
   L.bytes = og;
   L.lds_bytes = ol;
   return L;

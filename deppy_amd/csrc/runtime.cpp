@@ -209,6 +209,8 @@ struct Plan {
   // chunk once grown)
   std::vector<Head> head;
   std::vector<PlanBlock> blk;
+  std::vector<int32_t> segcnt;             // [block][segment] one-wavefront counts, then write cursors
+  std::vector<int64_t> segpos, segxs;       // segment starts in order; per segment, each XCD's first member
   std::vector<int32_t> big[5], cnt, tmp, grp;
 };
 
@@ -487,66 +489,116 @@ void plan_chunk(Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0,
   int ix[kNBuckets];
   for (int g = 0; g < ng; ++g) ix[g] = g;
   std::stable_sort(ix, ix + ng, [&](int x, int y) { return gsize[x] > gsize[y]; });
-  int64_t at[kNBuckets];
   int64_t o = (int64_t)P.order.size();
   for (int r = 0; r < ng; ++r) {
     const int g = ix[r];
     bl[g].first = (int)o;
     bl[g].count = (int)gsize[g];
-    at[g] = o;
     o += gsize[g];
   }
   P.order.resize((size_t)o);
-  for (int32_t i = 0; i < n; ++i)
-    if (head[i].place == M_LDS) P.order[(size_t)at[group_of[head[i].bucket]]++] = i;
   // XCD-contiguous order for one-wavefront launches up to this LDS request
   // (DEPPY_XCD_ORDER, bytes; 0: longest record first everywhere).  Measured
   // on one box against LPT: config 2 host to host 18.4-18.5M -> 20.3-20.6M
   // res/s, kernel only 22.4M -> 23.9-24.2M; config 3 PMC writes per run
   // 10.9 -> 6.5 MB; config 5 and 6 unchanged (scripts/xcd_ab.sh,
   // profiles/r03_xcd_order_ab.txt).
+  // Within such a launch, dispatch order by cost class, the costliest
+  // first: a catalog's anchors (Mandatory roots, lit_mapping.go:163-174)
+  // start its search, and on config 2 they predict its steps (correlation
+  // 0.7 with their log; 89 of the 100 slowest of 10k catalogs have 3 or 4
+  // of 4), so the slow ones start with the launch instead of forming its
+  // tail.  Within a class XCD-contiguous: workgroup b runs on XCD b % kXcds,
+  // so XCD x takes the x-th contiguous range of the class's members in
+  // problem order: neighbouring records (sharing their boundary lines) are
+  // read, and neighbouring results written, through one XCD's L2 at about
+  // the same time.
+  // Built as one stable counting sort of the one-wavefront problems by
+  // segment (launch rank, class) over the plan's blocks, then every segment
+  // dealt to the XCDs, both passes on the pool.
   static const int64_t xcd_order = env_i64("DEPPY_XCD_ORDER", kMaxLdsBytes);
   static const bool anchor_order = env_i64("DEPPY_ANCHOR_ORDER", 1) != 0;  // diagnostic A/B
-  for (int r = 0; r < ng; ++r) {
-    const int g = ix[r];
-    if (xcd_order && bl[g].lds <= xcd_order) {
-      // Dispatch order by cost class, the costliest first: a catalog's
-      // anchors (Mandatory roots, lit_mapping.go:163-174) start its search,
-      // and on config 2 they predict its steps (correlation 0.7 with their
-      // log; 89 of the 100 slowest of 10k catalogs have 3 or 4 of 4), so the
-      // slow ones start with the launch instead of forming its tail.
-      // Within a class XCD-contiguous: workgroup b runs on XCD b % kXcds,
-      // so XCD x takes the x-th contiguous range of the class's members in
-      // problem order: neighbouring records (sharing their boundary lines)
-      // are read, and neighbouring results written, through one XCD's L2 at
-      // about the same time
-      int32_t* v = P.order.data() + bl[g].first;
-      const int32_t m = bl[g].count;
-      P.tmp.resize((size_t)m);
-      int32_t ccnt[kCostClasses] = {}, cat[kCostClasses];
-      for (int32_t b = 0; b < m; ++b) ccnt[anchor_order ? head[v[b]].cls : 0]++;
-      for (int c = kCostClasses - 1, o2 = 0; c >= 0; --c) {
-        cat[c] = o2;
-        o2 += ccnt[c];
-      }
-      for (int32_t b = 0; b < m; ++b) P.tmp[(size_t)cat[anchor_order ? head[v[b]].cls : 0]++] = v[b];
-      for (int32_t pos = 0; pos < m;) {  // one class: [pos, end) of tmp
-        const int32_t c = anchor_order ? head[P.tmp[(size_t)pos]].cls : 0;
-        int32_t end = pos;
-        while (end < m && (!anchor_order || head[P.tmp[(size_t)end]].cls == c)) ++end;
-        int32_t cnt[kXcds] = {}, start[kXcds], k[kXcds] = {};
-        for (int32_t b = pos; b < end; ++b) cnt[b % kXcds]++;
-        for (int x = 0, s2 = pos; x < kXcds; ++x) {
-          start[x] = s2;
-          s2 += cnt[x];
-        }
-        for (int32_t b = pos; b < end; ++b) v[b] = P.tmp[(size_t)(start[b % kXcds] + k[b % kXcds]++)];
-        pos = end;
-      }
-    } else {
-      lpt(P.order.data() + bl[g].first, (size_t)bl[g].count);
+  if (ng > 0) {
+    int rank_of[kNBuckets];
+    bool xo[kNBuckets];
+    for (int r = 0; r < ng; ++r) {
+      rank_of[ix[r]] = r;
+      xo[ix[r]] = xcd_order && bl[ix[r]].lds <= xcd_order;
     }
-    P.launches.push_back(bl[g]);
+    const int nseg = ng * kCostClasses;
+    auto seg_of = [&](const Head& H) {
+      const int g = group_of[H.bucket];
+      const int c = anchor_order && xo[g] ? H.cls : 0;
+      return rank_of[g] * kCostClasses + (kCostClasses - 1 - c);
+    };
+    P.segcnt.assign((size_t)nblk * nseg, 0);
+    over_blocks([&](int64_t b) {
+      int32_t* c = P.segcnt.data() + (size_t)b * nseg;
+      const int32_t i0 = (int32_t)b * kPlanBlock, i1 = std::min(n, i0 + kPlanBlock);
+      for (int32_t i = i0; i < i1; ++i)
+        if (head[i].place == M_LDS) c[seg_of(head[i])]++;
+    });
+    P.segpos.resize((size_t)nseg + 1);
+    int64_t run = bl[ix[0]].first;  // (the one-wavefront launches follow the multi-wave ones)
+    for (int sg = 0; sg < nseg; ++sg) {
+      P.segpos[(size_t)sg] = run;
+      for (int32_t b = 0; b < nblk; ++b) {
+        int32_t& c = P.segcnt[(size_t)b * nseg + sg];
+        const int32_t x = c;
+        c = (int32_t)run;
+        run += x;
+      }
+    }
+    P.segpos[(size_t)nseg] = run;
+    P.tmp.resize((size_t)o);
+    over_blocks([&](int64_t b) {
+      int32_t* c = P.segcnt.data() + (size_t)b * nseg;
+      const int32_t i0 = (int32_t)b * kPlanBlock, i1 = std::min(n, i0 + kPlanBlock);
+      for (int32_t i = i0; i < i1; ++i)
+        if (head[i].place == M_LDS) P.tmp[(size_t)c[seg_of(head[i])]++] = i;
+    });
+    // each segment [pos, end): slot b (XCD x = b % kXcds) takes the next of
+    // XCD x's contiguous range of the segment's members
+    P.segxs.resize((size_t)nseg * kXcds);
+    // (XCDs count from the launch's first workgroup: slot t of launch g is
+    // workgroup t - bl[g].first)
+    auto first_on = [&](int sg, int64_t pos, int x) {  // the segment's first slot on XCD x
+      const int64_t rel = pos - bl[ix[sg / kCostClasses]].first;
+      return pos + ((x - rel % kXcds) % kXcds + kXcds) % kXcds;
+    };
+    for (int sg = 0; sg < nseg; ++sg) {
+      const int64_t pos = P.segpos[(size_t)sg], end = P.segpos[(size_t)sg + 1];
+      int64_t st = pos;
+      for (int x = 0; x < kXcds; ++x) {
+        P.segxs[(size_t)sg * kXcds + x] = st;
+        const int64_t first = first_on(sg, pos, x);
+        st += first < end ? (end - 1 - first) / kXcds + 1 : 0;
+      }
+    }
+    const int64_t o0 = bl[ix[0]].first, nslot = o - o0;
+    const int32_t sblk = (int32_t)((nslot + kPlanBlock - 1) / kPlanBlock);
+    auto deal = [&](int64_t b) {
+      const int64_t s0 = o0 + b * kPlanBlock, s1 = std::min<int64_t>(o, s0 + kPlanBlock);
+      int sg = (int)(std::upper_bound(P.segpos.begin(), P.segpos.end(), s0) - P.segpos.begin()) - 1;
+      for (int64_t t = s0; t < s1; ++t) {
+        while (P.segpos[(size_t)sg + 1] <= t) ++sg;
+        const int g = ix[sg / kCostClasses];
+        if (!xo[g]) {
+          P.order[(size_t)t] = P.tmp[(size_t)t];
+          continue;
+        }
+        const int x = (int)((t - bl[g].first) % kXcds);
+        const int64_t first = first_on(sg, P.segpos[(size_t)sg], x);
+        P.order[(size_t)t] = P.tmp[(size_t)(P.segxs[(size_t)sg * kXcds + x] + (t - first) / kXcds)];
+      }
+    };
+    if (pool && sblk > 1) pool->run(sblk, std::function<void(int64_t)>(deal), 1);
+    else for (int32_t b = 0; b < sblk; ++b) deal(b);
+    for (int r = 0; r < ng; ++r) {
+      const int g = ix[r];
+      if (!xo[g]) lpt(P.order.data() + bl[g].first, (size_t)bl[g].count);
+      P.launches.push_back(bl[g]);
+    }
   }
   static const int pad_kb = (int)env_i64("DEPPY_LDS_PAD_KB", 0);  // diagnostic (occupancy study)
   if (pad_kb > 0)
@@ -1308,6 +1360,9 @@ void grow_plan(Plan& dst, const Plan& src) {
   grow_vec(dst.direct, src.direct.size());
   grow_vec(dst.head, src.head.size());
   grow_vec(dst.blk, src.blk.size());
+  grow_vec(dst.segcnt, src.segcnt.size());
+  grow_vec(dst.segpos, src.segpos.size());
+  grow_vec(dst.segxs, src.segxs.size());
   for (int k = 0; k < 5; ++k) grow_vec(dst.big[k], src.big[k].size());
   grow_vec(dst.cnt, src.cnt.capacity());
   grow_vec(dst.tmp, src.tmp.capacity());
@@ -1336,7 +1391,7 @@ size_t plan_cap(const Plan& P) {
   size_t c = P.img_off.capacity() + P.inst_off.capacity() + P.dev_off.capacity() + P.scratch_off.capacity() +
              P.narrow.capacity() + P.direct.capacity() + P.order.capacity() + P.launches.capacity() +
              P.skip.capacity() + P.skip_flags.capacity() + P.head.capacity() + P.cnt.capacity() + P.tmp.capacity() +
-             P.blk.capacity();
+             P.blk.capacity() + P.segcnt.capacity() + P.segpos.capacity() + P.segxs.capacity();
   for (const auto& b : P.big) c += b.capacity();
   return c;
 }
@@ -1844,6 +1899,16 @@ int dp_device_bytes(const dp_batch* b, int32_t opt_flags, int64_t* rec_bytes, in
   if (rec_bytes) *rec_bytes = P.rec_bytes;
   if (img_bytes) *img_bytes = 4 * P.img_words;
   return 0;
+}
+
+int dp_plan_order(const dp_batch* b, int32_t opt_flags, int32_t* order, int32_t* launch_first) {
+  if (!b || !order || b->n_problems < 0 || (b->n_problems > 0 && (!b->rec || !b->rec_off))) return -1;
+  static thread_local Plan P;
+  dp::plan_chunk(P, b->rec, b->rec_off, 0, b->n_problems, opt_flags, nullptr, &dp::host_pool());
+  std::copy(P.order.begin(), P.order.end(), order);
+  if (launch_first)
+    for (size_t k = 0; k < P.launches.size(); ++k) launch_first[k] = P.launches[k].first;
+  return (int)P.launches.size();
 }
 
 int dp_plan_placements(const dp_batch* b, int32_t opt_flags, int8_t* place) {

@@ -52,36 +52,13 @@ constexpr int32_t R_EXTRA = -2;  // epilogue bound over the extras
 enum { CK_NONE = 0, CK_ROW, CK_VAR, CK_ASSUME, CK_EXTRA };
 enum { RS_SAT = 1, RS_UNSAT = -1, RS_BUDGET = 2 };
 
-// One wavefront: flush the AtMost queue before a visit that could overflow
-// it (1), or evaluate the overflowing rows in-lane (0).
-#ifndef DP_MAKE_ROOM
-#define DP_MAKE_ROOM 0
-#endif
-
-// BCP-visited bytes, counted per thread; -DDP_VIS=0 compiles
-// the counter out (register-pressure A/B).
-#ifndef DP_VIS
-#define DP_VIS 1
-#endif
-#if DP_VIS
+// BCP-visited bytes, counted per thread (Group::vis_add).
 #define DP_VIS_ADD(x) vis_add(x)
-#else
-#define DP_VIS_ADD(x) ((void)0)
-#endif
 
 // Lanes of the wave hand values to each other through the working set (LDS,
 // or HBM): complete every access before the next phase.
-#ifndef DP_WSYNC_FENCE
-#define DP_WSYNC_FENCE 1
-#endif
 __device__ __forceinline__ void wsync() {
-#if DP_WSYNC_FENCE == 2
-  // (A/B) wavefront scope: a compiler barrier only -- one wave's LDS
-  // operations execute in program order, so no s_waitcnt is emitted
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-#elif DP_WSYNC_FENCE
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-#endif
   __builtin_amdgcn_wave_barrier();
 }
 
@@ -180,11 +157,10 @@ struct Group {
   static constexpr int NT = 64 * NW;           // threads per problem
   static constexpr int WBUF = mode_wbuf(MODE);
   static constexpr int CQ = mode_cq(MODE);
-  static_assert(NW > 1 || !DP_MAKE_ROOM || CQ >= 64, "make_room: the AtMost queue holds one visit");
 
   // the lowest implying row per literal: 16-bit in LDS, 32-bit (global
   // atomics) in the multi-wave modes; IMP_NONE = no implication this round
-  static constexpr bool IMP16 = N16 && IMP16_LDS;
+  static constexpr bool IMP16 = N16;
   using IMP = typename std::conditional<IMP16, uint16_t, uint32_t>::type;
   static constexpr uint32_t IMP_NONE = IMP16 ? 0xffffu : (uint32_t)INF;
   // guess-stack flag: the choice was already satisfied by a guess (m = none)
@@ -246,7 +222,6 @@ struct Group {
   // reading its offsets (one dependent HBM read less per row; w is unused).
   // nullptr: 4-byte row entries in w.
   const int2* w8;
-  const uint16_t* w16;  // 2-byte entries (layout.hpp went_bytes): the row alone
   int nwatch, dthr;
   // BCP-visited bytes (this thread): the watch entries, row offsets, row
   // literals and their values that propagation reads
@@ -263,26 +238,6 @@ struct Group {
   int8_t* val;
   IX *reason, *rs, *trail, *touched, *d_mark, *l_off, *l_lits, *dq, *stk;
   IMP* imp;  // imp[l] = lowest row implying literal l this round
-  // two-watched-literal filter (mode_2wl): the watched pair of each clause
-  // row; `sweep` (base scope) evaluates the rows it names unfiltered
-  static constexpr bool TWL = mode_2wl(MODE);
-  static constexpr bool RSLOT = mode_rowslot(MODE);  // row slots (layout.hpp): the pair at wpair[4r]
-  static constexpr int WS = RSLOT ? 4 : 1;            // u64 words per row of wpair
-  uint64_t* wpair;
-  bool sweep;
-  // two-watched-literal lists of the one-wavefront path (mode_twl_lds):
-  // watched positions (a byte each) per clause row, live end per list, and
-  // for the flattened work list each entry's frontier literal and each
-  // frontier literal's compaction cursor.  twl_on: this problem's watch
-  // entries carry the slot in bit 15 (every row id below 32768).
-  static constexpr bool TWLL = mode_twl_lds(MODE);
-  uint8_t *wpos8, *wfi;
-  uint16_t* wend16;
-  int32_t* fcur;
-  bool twl_on;
-  __device__ __forceinline__ bool twl_dyn(int len) const {
-    return TWLL && twl_on && len >= TWL_MIN_LEN && len <= TWL_MAX_LEN;
-  }
   uint32_t *d_flip, *inS, *extra, *seen, *model, *used, *en, *en2, *crit, *dset, *fg;
   IX *wbuf, *cardq;
   int32_t* scal;
@@ -359,9 +314,6 @@ struct Group {
     }
     __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0)
     __syncthreads();
-#ifdef DP_BAR_INV
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // diagnostic: drop L1 after each barrier
-#endif
   }
   __device__ __forceinline__ void gsync() {
     if constexpr (NW == 1) wsync();
@@ -582,18 +534,7 @@ struct Group {
     touched = reinterpret_cast<IX*>(cold + L.touched);
     d_mark = reinterpret_cast<IX*>(cold + L.d_mark);
     imp = reinterpret_cast<IMP*>(cold + L.imp);
-    wpair = reinterpret_cast<uint64_t*>(cold + L.wp);
     w8 = nullptr;
-    w16 = nullptr;
-    sweep = false;
-    twl_on = false;
-    if constexpr (TWLL) {
-      wpos8 = reinterpret_cast<uint8_t*>(lds + L.wpos);
-      wend16 = reinterpret_cast<uint16_t*>(lds + L.wend);
-      wfi = reinterpret_cast<uint8_t*>(lds + L.wfi);
-      fcur = reinterpret_cast<int32_t*>(lds + L.fcur);
-      twl_on = nrows < 32768;
-    }
     d_flip = reinterpret_cast<uint32_t*>(hot + L.d_flip);
     inS = reinterpret_cast<uint32_t*>(hot + L.inS);
     extra = reinterpret_cast<uint32_t*>(hot + L.extra);
@@ -665,12 +606,10 @@ struct Group {
     } else {
       if (h[DP_H_FMT] == DP_FMT_I32) {  // plain int32 record: the lists in scratch (layout.hpp wl)
         IX* wo = reinterpret_cast<IX*>(hbm + L.wl);
-        const bool e2 = went_bytes(h) == 2;
-        if (device_watches(h)) build_watches_wide(wo, wo + 2 * nv + 2, e2, reinterpret_cast<uint32_t*>(lds + L.wbuf));
+        if (device_watches(h)) build_watches_wide(wo, wo + 2 * nv + 2, reinterpret_cast<uint32_t*>(lds + L.wbuf));
         // (else built by the passes before this launch, watch_build.hip)
         w_off = wo; w = nullptr;
-        if (e2) w16 = reinterpret_cast<const uint16_t*>(wo + 2 * nv + 2);
-        else w8 = reinterpret_cast<const int2*>(wo + 2 * nv + 2);
+        w8 = reinterpret_cast<const int2*>(wo + 2 * nv + 2);
       } else {
         w_off = rv(X.w_off); w = rv(X.w);  // host-built, staged after the record
       }
@@ -695,21 +634,6 @@ struct Group {
       l_off[0] = 0;
       scal[S_POSROWS] = h[DP_H_NVU] > 0;
     }
-    if constexpr (TWL || RSLOT)  // every row watches its first two literals (nothing is assigned yet)
-      for (int r = tid; r < nc; r += NT) {
-        const int a = clause_off[r], b = clause_off[r + 1], len = b - a;
-        const int x = len > 0 ? (int)clause_lits[a] : 0, y = len >= 2 ? (int)clause_lits[a + 1] : x;
-        if constexpr (RSLOT) {
-          int lt[ROWSLOT_INLINE];
-#pragma unroll
-          for (int k = 0; k < ROWSLOT_INLINE; ++k) lt[k] = k < len && len <= ROWSLOT_INLINE ? (int)clause_lits[a + k] : 0;
-          int4* sp = reinterpret_cast<int4*>(wpair + 4 * r);
-          sp[0] = make_int4(x, y, len, len <= ROWSLOT_INLINE ? lt[0] : a);
-          sp[1] = make_int4(lt[1], lt[2], lt[3], lt[4]);
-        } else {
-          wpair[r] = (uint64_t)(uint32_t)x | ((uint64_t)(uint32_t)y << 32);
-        }
-      }
     gsync();
     return true;
   }
@@ -1091,7 +1015,7 @@ struct Group {
   // cursors.  Row order within a list is left to the atomics, as in
   // build_watches.  Ends with a draining barrier: every wavefront reads the
   // lists after it.
-  __device__ __forceinline__ void build_watches_wide(IX* wo, IX* wlist, bool e2, uint32_t* cnt) {
+  __device__ __forceinline__ void build_watches_wide(IX* wo, IX* wlist, uint32_t* cnt) {
     static_assert(!N16, "LDS-image problems build theirs in LDS");
     const int n2 = 2 * nv + 1;
     for (int i = tid; i < n2; i += NT) cnt[i] = 0u;
@@ -1113,11 +1037,7 @@ struct Group {
     }
     gsync();
     int2* ww = reinterpret_cast<int2*>(wlist);
-    uint16_t* w2 = reinterpret_cast<uint16_t*>(wlist);
-    auto put = [&](uint32_t at, int row, int a, int len) {
-      if (e2) w2[at] = (uint16_t)row;
-      else ww[at] = make_int2(row, (int)row_info(a, len));
-    };
+    auto put = [&](uint32_t at, int row, int a, int len) { ww[at] = make_int2(row, (int)row_info(a, len)); };
     for (int r = tid; r < nc; r += NT) {
       const int a = clause_off[r], b = clause_off[r + 1];
       for (int j = a; j < b; ++j) put(atomicAdd(&cnt[(int)clause_lits[j] ^ 1], 1u), r, a, b - a);
@@ -1208,12 +1128,6 @@ struct Group {
 #endif
     for (int r = tid; r < nc; r += NT) {
       const int a = clause_off[r], b = clause_off[r + 1];
-      if (twl_dyn(b - a)) {  // two-watched: positions 0 and 1 (slot in bit 15)
-        ww[atomicAdd(&cnt[(int)clause_lits[a] ^ 1], 1u)] = enc(r);
-        ww[atomicAdd(&cnt[(int)clause_lits[a + 1] ^ 1], 1u)] = enc(r | 0x8000);
-        reinterpret_cast<uint16_t*>(wpos8)[r] = 0x0100;
-        continue;
-      }
       for (int j0 = a; j0 < b; j0 += 8) {
         int l[8];
 #pragma unroll
@@ -1236,10 +1150,6 @@ struct Group {
       }
     }
     gsync();
-    if constexpr (TWLL) {  // the cursors end where each list's entries end
-      for (int l = tid; l < 2 * nv; l += NT) wend16[l] = (uint16_t)cnt[l];
-      gsync();
-    }
 #ifdef DP_STAMPS
     sub[5] = stamp() - tb2;
 #endif
@@ -1255,7 +1165,6 @@ struct Group {
   // watch entry j: {row, row_info} (w8), or {row, ROW_INFO_NONE}
   __device__ __forceinline__ int2 went(int j) const {
     if constexpr (!N16) {
-      if (w16) return make_int2((int)w16[j], (int)ROW_INFO_NONE);
       if (w8) return w8[j];
     }
     return make_int2((int)w[j], (int)ROW_INFO_NONE);
@@ -1382,144 +1291,9 @@ struct Group {
     if (nun == 0) crow = min(crow, r);
     return nun == 1 ? ul : -1;
   }
-  // Two-watched-literal evaluation of clause row r, whose watched pair has a
-  // false literal: the row's outcome as eval_clause, and its new pair --
-  // its first two non-false literals, else its one non-false literal and its
-  // most recently falsified one, else its two most recently falsified ones
-  // (by rs, ties to row order).  Invariant: a row with two or more non-false
-  // literals watches two of them.  It holds at the start (nothing assigned),
-  // a round's falsifications are repaired in the next round before any
-  // other, and backtracking only ever returns to a propagation fixpoint,
-  // where a row with a false watch has at most one non-false literal unless
-  // that watch (its latest falsification) was undone too.  So a row whose
-  // pair is non-false has two non-false literals: not unit, not false, and
-  // skipped without reading it -- exactly the rows occurrence lists would
-  // have found unit or false are evaluated, and the round is unchanged.  Every
-  // lane that evaluates a row in one round writes the same pair.
-  __device__ __forceinline__ int eval_clause_twl(int r, int a, int b, int& crow) {
-    int nun = 0, ul = -1, n0 = -1, n1 = -1;
-    bool sat = false;
-    DP_VIS_ADD(2 * sizeof(IX));
-    for (int j = a; j < b && n1 < 0; j += 4) {
-      int l[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) l[k] = j + k < b ? (int)clause_lits[j + k] : -1;
-      int x[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) x[k] = l[k] >= 0 ? lit_val(l[k]) : -1;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (l[k] < 0 || n1 >= 0) continue;
-        DP_VIS_ADD(sizeof(IX) + 1);
-        if (x[k] > 0) sat = true;
-        if (x[k] == 0) { ++nun; ul = l[k]; }
-        if (x[k] >= 0) {
-          if (n0 < 0) n0 = l[k];
-          else n1 = l[k];
-        }
-      }
-    }
-    uint32_t px, py;
-    if (n1 >= 0) {
-      px = (uint32_t)n0; py = (uint32_t)n1;
-    } else {
-      // one or no non-false literal: the latest falsified ones
-      int f0 = -1, f1 = -1, r0 = -1, r1 = -1;
-      for (int j = a; j < b; ++j) {
-        const int l = clause_lits[j];
-        if (lit_val(l) >= 0) continue;
-        const int t = (int)rs[l >> 1];
-        DP_VIS_ADD(sizeof(IX));
-        if (t > r0) { f1 = f0; r1 = r0; f0 = l; r0 = t; }
-        else if (t > r1) { f1 = l; r1 = t; }
-      }
-      if (n0 >= 0) { px = (uint32_t)n0; py = (uint32_t)(f0 >= 0 ? f0 : n0); }
-      else { px = (uint32_t)f0; py = (uint32_t)(f1 >= 0 ? f1 : f0); }
-    }
-    __hip_atomic_store(&wpair[WS * r], (uint64_t)px | ((uint64_t)py << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (sat || n1 >= 0) return -1;
-    if (nun == 0) crow = min(crow, r);
-    return nun == 1 ? ul : -1;
-  }
-
-  // A row of at most ROWSLOT_INLINE literals from its slot (registers): the
-  // row's outcome (eval_clause), and with TWL its new pair (eval_clause_twl).
-  __device__ __forceinline__ int eval_inline(int r, const int (&lt)[ROWSLOT_INLINE], int len, int& crow) {
-    int nun = 0, ul = -1, n0 = -1, n1 = -1;
-    bool sat = false;
-    int x[ROWSLOT_INLINE];
-#pragma unroll
-    for (int k = 0; k < ROWSLOT_INLINE; ++k) x[k] = k < len ? lit_val(lt[k]) : -1;
-    DP_VIS_ADD((uint32_t)len * 1u);
-#pragma unroll
-    for (int k = 0; k < ROWSLOT_INLINE; ++k) {
-      if (k >= len) continue;
-      if (x[k] > 0) sat = true;
-      if (x[k] == 0) { ++nun; ul = lt[k]; }
-      if (x[k] >= 0) {
-        if (n0 < 0) n0 = lt[k];
-        else if (n1 < 0) n1 = lt[k];
-      }
-    }
-    if constexpr (TWL) {
-      uint32_t px, py;
-      if (n1 >= 0) {
-        px = (uint32_t)n0; py = (uint32_t)n1;
-      } else {
-        int f0 = -1, f1 = -1, r0 = -1, r1 = -1;
-        int t[ROWSLOT_INLINE];
-#pragma unroll
-        for (int k = 0; k < ROWSLOT_INLINE; ++k) t[k] = k < len && x[k] < 0 ? (int)rs[lt[k] >> 1] : -1;
-#pragma unroll
-        for (int k = 0; k < ROWSLOT_INLINE; ++k) {
-          if (t[k] < 0) continue;
-          DP_VIS_ADD(sizeof(IX));
-          if (t[k] > r0) { f1 = f0; r1 = r0; f0 = lt[k]; r0 = t[k]; }
-          else if (t[k] > r1) { f1 = lt[k]; r1 = t[k]; }
-        }
-        if (n0 >= 0) { px = (uint32_t)n0; py = (uint32_t)(f0 >= 0 ? f0 : n0); }
-        else { px = (uint32_t)f0; py = (uint32_t)(f1 >= 0 ? f1 : f0); }
-      }
-      __hip_atomic_store(&wpair[WS * r], (uint64_t)px | ((uint64_t)py << 32), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (sat || n1 >= 0) return -1;
-    if (nun == 0) crow = min(crow, r);
-    return nun == 1 ? ul : -1;
-  }
-
   // a clause row (r < nc) or a learned row (r >= nrows); info: the row's
   // literal range from its watch entry (row_info), or ROW_INFO_NONE
   __device__ __forceinline__ int clause_unit(int r, int& crow, uint32_t info = ROW_INFO_NONE) {
-    if constexpr (RSLOT) {
-      if (r < nc) {
-        // the slot: the pair (coherent: other wavefronts move it), then the
-        // row's length and literals (written once, at init) -- one hop
-        const int32_t* sp = reinterpret_cast<const int32_t*>(wpair + 4 * r);
-        uint64_t wv = 0;
-        if (TWL && !sweep) wv = __hip_atomic_load(&wpair[4 * r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int2 q = *reinterpret_cast<const int2*>(sp + 2);
-        const int4 t = *reinterpret_cast<const int4*>(sp + 4);
-        DP_VIS_ADD(32);
-        if (TWL && !sweep && lit_val((int)(uint32_t)wv) >= 0 && lit_val((int)(uint32_t)(wv >> 32)) >= 0) return -1;
-        if (q.x <= ROWSLOT_INLINE) {
-          const int lt[ROWSLOT_INLINE] = {q.y, t.x, t.y, t.z, t.w};
-          return eval_inline(r, lt, q.x, crow);
-        }
-        if constexpr (TWL) return eval_clause_twl(r, q.y, q.y + q.x, crow);
-        else return eval_clause(r, clause_lits, q.y, q.y + q.x, crow);
-      }
-    }
-    if constexpr (TWL) {
-      if (r < nc) {
-        if (!sweep) {
-          const uint64_t wv = __hip_atomic_load(&wpair[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          DP_VIS_ADD(8);
-          if (lit_val((int)(uint32_t)wv) >= 0 && lit_val((int)(uint32_t)(wv >> 32)) >= 0) return -1;
-        }
-        return eval_clause_twl(r, clause_off[r], clause_off[r + 1], crow);
-      }
-    }
     if constexpr (!N16) {
       if (r < nc && info != ROW_INFO_NONE) {
         const int a = (int)(info >> 8);
@@ -1555,17 +1329,6 @@ struct Group {
     }
   }
 
-  // One wavefront: before a visit, evaluate the AtMost queue if the visit
-  // might overflow it (the round's outcome does not depend on the order).
-  __device__ __forceinline__ void make_room(int& crow, int& ncq) {
-    if constexpr (NW == 1 && DP_MAKE_ROOM) {
-      if (ncq > CQ - 64) {
-        flush_cards(crow, ncq);
-        ncq = 0;
-      }
-    }
-  }
-
   // A watched row reached in a round: clause rows are evaluated by the thread
   // that reached them; AtMost rows are queued (ballot compaction) and later
   // evaluated by the whole wavefront that queued them, one row at a time
@@ -1579,198 +1342,17 @@ struct Group {
     const bool ok = r >= 0 && row_on(r);
     const bool card = ok && r >= nc && r < nrows;
     const uint64_t m = __ballot(card);
-    if constexpr (NW == 1 && DP_MAKE_ROOM) {
-      if (card) cardq[ncq + __popcll(m & lanemask_lt())] = enc(r);
-      note_all(ok && !card ? clause_unit(r, crow, info) : -1, r);
-      ncq += __popcll(m);
-    } else {
-      const bool q = ncq + __popcll(m) <= CQW;  // queue full: evaluate in-lane
-      const int pos = wid * CQW + ncq + __popcll(m & lanemask_lt());
-      if (card && q) {
-        cardq[pos] = enc(r);
-        if constexpr (NW > 1 && !N16) cardq[CQ + pos] = (IX)info;  // (IX = int32 here; M_LDSG entries carry no range)
-      } else if (card) card_serial(r, crow);
-      else if (ok) {
-        const int ul = clause_unit(r, crow, info);
-        if (ul >= 0) note(ul, r);
-      }
-      if (q) ncq += __popcll(m);
-    }
-  }
-
-  // ---- two-watched-literal rounds (mode_twl_lds) ----
-  // A clause row of TWL_MIN_LEN..TWL_MAX_LEN literals is in the lists of
-  // its two watched positions only (wpos8[2r], wpos8[2r + 1]; the entry in
-  // position p's list carries slot bit (p == the second watch) << 15).
-  // Visited through slot k, whose literal a round falsified, against the
-  // assignment at the start of the round (nothing is committed during it):
-  //  - the other watch true: nothing (the row is satisfied), keep the entry;
-  //  - else the row's outcome exactly as eval_clause -- with at most one
-  //    non-false position it is unit on that one (unassigned), satisfied
-  //    (true) or conflicting (none); with two or more, neither -- and slot k
-  //    moves to N[k] when the other watch is false too (both were falsified
-  //    by the last round, and each slot's visit takes its own one of the
-  //    first two non-false positions N[0], N[1]), else to the first of them
-  //    that is not the other watch.  Nothing to move to: keep the entry.
-  // The two visits of a row whose watches fell together may run in either
-  // order or in one instruction: a slot rewritten by the other visit holds
-  // N[j], non-false, and "the first of N not the other" then gives the same
-  // N[k].  A moved watch's literal z is non-false, so its list (~z) is not
-  // one this round iterates: it is appended to (atomicAdd on its live end),
-  // never compacted, within the occurrence-count capacity.
-  // Why every row that becomes unit or false is reached (so every round
-  // equals the occurrence lists' round, lowest rows and all): a row whose
-  // watches are both non-false has at most one of them falsified per round
-  // before it is visited; a row left with a false watch has its other watch
-  // true (assigned no later than the false one) or is unit / conflicting
-  // with the false watch among its latest falsified literals -- and every
-  // backtrack returns to a propagation fixpoint (a round boundary, where no
-  // row is unit), which un-assigns that watch whenever it would matter.
-  // Checked on the CPU against the occurrence lists, bit-exact on configs
-  // 2, 3, 5 and 6, and by the GPU parity tests.
-  __device__ __forceinline__ bool twl_row(int r, int k, int a, int b, int& crow) {
-    const uint32_t wp = reinterpret_cast<const uint16_t*>(wpos8)[r];
-    const int po = k ? (int)(wp & 0xffu) : (int)(wp >> 8);
-    const int vo = lit_val(clause_lits[a + po]);
-    DP_VIS_ADD(2 * sizeof(IX) + 2 + sizeof(IX) + 1);
-    if (vo > 0) return true;
-    // the first two non-false positions (and their literals)
-    int n0 = -1, n1 = -1, z0 = 0, z1 = 0;
-    for (int j = a; j < b && n1 < 0; j += 4) {
-      int l[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) l[q] = j + q < b ? (int)clause_lits[j + q] : -1;
-      int x[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) x[q] = l[q] >= 0 ? lit_val(l[q]) : -1;
-      DP_VIS_ADD(4 * (sizeof(IX) + 1));
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (x[q] >= 0) {
-          if (n0 < 0) { n0 = j + q - a; z0 = l[q]; }
-          else if (n1 < 0) { n1 = j + q - a; z1 = l[q]; }
-        }
-    }
-    if (n1 < 0) {
-      if (n0 < 0) crow = min(crow, r);           // every literal false
-      else if (lit_val(z0) == 0) note(z0, r);    // unit
-    }
-    int q, z;
-    if (vo < 0) { q = k ? n1 : n0; z = k ? z1 : z0; }
-    else if (n0 != po) { q = n0; z = z0; }
-    else { q = n1; z = z1; }
-    if (q < 0) return true;
-    wpos8[2 * r + k] = (uint8_t)q;
-    const int li = z ^ 1;
-    const uint32_t sh = 16u * (uint32_t)(li & 1);
-    const uint32_t old = atomicAdd(reinterpret_cast<uint32_t*>(wend16) + (li >> 1), 1u << sh);
-    const_cast<IX*>(w)[(old >> sh) & 0xffffu] = enc(r | (k << 15));
-    return false;
-  }
-
-  // visit() for a two-watched problem: entry e (or -1) -> keep it in its list?
-  __device__ __forceinline__ bool visit_twl(int e, int& crow, int& ncq) {
-    DP_VIS_ADD(e >= 0 ? sizeof(IX) : 0);  // the watch entry
-    const int r = e >= 0 ? (e & 0x7fff) : -1, k = (e >> 15) & 1;
-    const bool ok = r >= 0 && row_on(r);
-    const bool card = ok && r >= nc;
-    const uint64_t m = __ballot(card);
-    const bool fits = ncq + __popcll(m) <= CQ;  // queue full: evaluate in-lane
-    bool keep = true;
-    if (card && fits) cardq[ncq + __popcll(m & lanemask_lt())] = enc(r);
-    else if (card) card_serial(r, crow);
+    const bool q = ncq + __popcll(m) <= CQW;  // queue full: evaluate in-lane
+    const int pos = wid * CQW + ncq + __popcll(m & lanemask_lt());
+    if (card && q) {
+      cardq[pos] = enc(r);
+      if constexpr (NW > 1 && !N16) cardq[CQ + pos] = (IX)info;  // (IX = int32 here; M_LDSG entries carry no range)
+    } else if (card) card_serial(r, crow);
     else if (ok) {
-      const int a = clause_off[r], b = clause_off[r + 1];
-      if (twl_dyn(b - a)) {
-        keep = twl_row(r, k, a, b, crow);
-      } else {
-        const int ul = eval_clause(r, clause_lits, a, b, crow);
-        if (ul >= 0) note(ul, r);
-      }
+      const int ul = clause_unit(r, crow, info);
+      if (ul >= 0) note(ul, r);
     }
-    if (fits) ncq += __popcll(m);
-    return keep;
-  }
-
-  // One frontier literal's list [w_off[l], wend[l]): visited 64 entries at a
-  // time, the kept ones compacted to its front by ballot rank (a moved
-  // entry is written only once an earlier one left).
-  __device__ __forceinline__ int twl_list(int l, int& crow, int& ncq) {
-    IX* wm = const_cast<IX*>(w);
-    const int a = w_off[l], e = wend16[l];
-    int kept = 0;
-    for (int k0 = a; k0 < e; k0 += NT) {
-      const int j = k0 + tid;
-      const int ent = j < e ? (int)w[j] : -1;
-      const bool kk = visit_twl(ent, crow, ncq) && ent >= 0;
-      const uint64_t km = __ballot(kk);
-      const int at = a + kept + __popcll(km & lanemask_lt());
-      if (kk && at != j) wm[at] = enc(ent);
-      kept += __popcll(km);
-    }
-    if (tid == 0) wend16[l] = (uint16_t)(a + kept);
-    return e - a;
-  }
-
-  // The frontier trail[lo..hi) of a two-watched problem.  Larger frontiers
-  // are flattened as on the occurrence lists, each work-list entry tagged
-  // with its frontier literal (wfi); the entries of one list are contiguous,
-  // so each is compacted by its rank among the kept entries of its segment
-  // plus its list's cursor (fcur), which the segment's last lane advances.
-  template <class FR>
-  __device__ __forceinline__ void frontier_twl(int lo, int hi, int& crow, int& ncq, FR&& front) {
-    if (hi - lo == 1) {
-      const int n = twl_list(DP_CHK(front(lo), 0, 2 * nv, 10), crow, ncq);
-      (void)n;
-      DP_ACC(12, n);
-      return;
-    }
-    IX* wm = const_cast<IX*>(w);
-    for (int b = lo; b < hi; b += NT) {
-      const int i = b + tid;
-      int cnt = 0, a = 0, l = 0;
-      if (i < hi) {
-        l = DP_CHK(front(i), 0, 2 * nv, 11);
-        a = w_off[l];
-        cnt = (int)wend16[l] - a;
-      }
-      const int incl = wave_incl_scan(cnt);
-      const int total = __builtin_amdgcn_readlane(incl, 63);
-      DP_ACC(26, total);
-      if (total <= WBUF) {
-        for (int k = 0, at = incl - cnt; k < cnt; ++k) {
-          wbuf[at + k] = enc(a + k);
-          wfi[at + k] = (uint8_t)tid;
-        }
-        if (i < hi) fcur[tid] = a;
-        wsync();
-        for (int t0 = 0; t0 < total; t0 += NT) {
-          const int t = t0 + tid;
-          const bool valid = t < total;
-          const int pos = valid ? (int)wbuf[t] : 0;
-          const int f = valid ? (int)wfi[t] : -1;
-          const int ent = valid ? (int)w[pos] : -1;
-          const bool kk = visit_twl(ent, crow, ncq) && valid;
-          const int fp = __shfl_up(f, 1), fn = __shfl_down(f, 1);
-          const uint64_t sm = __ballot(valid && (lane == 0 || fp != f));
-          const uint64_t le = lanemask_lt() | (1ull << lane);
-          const uint64_t seg = ~((1ull << (63 - __clzll(sm & le))) - 1ull);  // (valid lanes: a start at or below)
-          const uint64_t km = __ballot(kk);
-          const int base = valid ? fcur[f] : 0;
-          const int at = base + __popcll(km & lanemask_lt() & seg);
-          if (kk && at != pos) wm[at] = enc(ent);
-          if (valid && (lane == 63 || t + 1 >= total || fn != f)) fcur[f] = at + (kk ? 1 : 0);
-          wsync();
-        }
-        if (i < hi) wend16[l] = (uint16_t)fcur[tid];
-        wsync();
-      } else {
-        // a very large chunk: one frontier literal at a time
-        const int n = min(NT, hi - b);
-        for (int e = 0; e < n; ++e) twl_list(front(b + e), crow, ncq);
-      }
-    }
-    DP_ACC(13, hi - lo);
+    if (q) ncq += __popcll(m);
   }
 
   // AtMost rows, one at a time per wavefront, lanes over positions (oracle:
@@ -2090,18 +1672,6 @@ struct Group {
       int ncq = 0;
       const int hint = pre_lo;  // (valid for this round only)
       pre_lo = -1;
-      if constexpr (TWLL) {
-        if (twl_on) {
-          frontier_twl(lo, hi, crow, ncq, front);
-          flush_cards(crow, ncq);
-          eval_learned(crow);
-#ifdef DP_STAMPS
-          DP_ACC(hi - lo == 1 ? 8 : 9, stamp() - t0);
-          DP_ACC(1, stamp() - t0);
-#endif
-          return;
-        }
-      }
       if (hi - lo == 1) {  // one new literal: threads over its watch list
         int a, e;
         if (lo == hint) {
@@ -2111,7 +1681,6 @@ struct Group {
           a = w_off[l]; e = w_off[l + 1];
         }
         for (int k0 = a; k0 < e; k0 += NT) {
-          make_room(crow, ncq);
           visit_at(k0 + tid < e ? k0 + tid : -1, crow, ncq);
         }
 #ifdef DP_STAMPS
@@ -2161,7 +1730,6 @@ struct Group {
             if constexpr (NW > 1) DP_ACC(28, tf2 - tf1);  // the work list
 #endif
             for (int t0 = 0; t0 < total; t0 += 64) {
-              make_room(crow, ncq);
               visit_at(t0 + lane < total ? DP_CHK((int)wb[t0 + lane], 0, nwatch, 12) : -1, crow, ncq);
             }
 #ifdef DP_STAMPS
@@ -2175,7 +1743,6 @@ struct Group {
               const int l = front(f0 + e);
               const int a2 = w_off[l], e2 = w_off[l + 1];
               for (int k0 = a2; k0 < e2; k0 += 64) {
-                make_room(crow, ncq);
                 visit_at(k0 + lane < e2 ? k0 + lane : -1, crow, ncq);
               }
             }
@@ -2234,15 +1801,12 @@ struct Group {
   __device__ __forceinline__ int base_propagate() {
     const int r = run_round([&](int& crow) {
       int ncq = 0;
-      sweep = true;  // (rows of one literal are unit on the empty assignment: no filter)
       for (int i0 = 0; i0 < nrows; i0 += NT) {
         const int row = i0 + tid;
         const bool f = row < nc ? (int)clause_off[row + 1] - (int)clause_off[row] <= 1
                                 : row < nrows && card_fires(row - nc);
-        make_room(crow, ncq);
         visit(f ? row : -1, crow, ncq);
       }
-      sweep = false;
       flush_cards(crow, ncq);
       eval_learned(crow);
     });
@@ -2435,7 +1999,7 @@ struct Group {
     int best = INF;
     // (two-watched lists no longer hold every row a true literal occurs in:
     // scan the rows)
-    if (nc <= 4 * NT || (TWLL && twl_on) || scal[S_POSROWS]) {
+    if (nc <= 4 * NT || scal[S_POSROWS]) {
       // few rows: every thread scans its rows in ascending order (the
       // oracle's scan, a short dependent chain per thread)
       for (int c = tid; c < nc; c += NT) {
@@ -2448,7 +2012,6 @@ struct Group {
       violated(best, fu);
       return fu;
     }
-#ifndef DP_FV_THREAD
     // Flattened: a wavefront takes 64 trail entries, scans their watch-list
     // lengths, and walks the concatenated (literal, entry) pairs 64 at a
     // time, so a long list does not hold the other lanes.  Loop bounds
@@ -2474,18 +2037,6 @@ struct Group {
         }
       }
     }
-#else
-    for (int i = tid; i < tlen; i += NT) {
-      const int l = trail[i];
-      if (l & 1) continue;  // only variables assigned true own violations
-      for (int k = w_off[l]; k < (int)w_off[l + 1]; ++k) {
-        const int2 e = went(k);
-        const int c = e.x;
-        int fu;
-        if (c < nc && c < best && row_on(c) && violated(c, fu, (uint32_t)e.y)) best = c;
-      }
-    }
-#endif
     best = g_min(best);
     if (best == INF) return -1;
     int fu;
@@ -3017,8 +2568,7 @@ struct Group {
   }
   // The one key of K violated among the rows holding v, or -1 (none or
   // several): the rows in v's two watch lists (every clause holding v or ~v,
-  // every AtMost row holding v), or a scan of all rows when the lists are
-  // two-watched.
+  // every AtMost row holding v).
   __device__ __forceinline__ int viol_key(int v) {
     int lo = INF, hi = -1;
     auto one = [&](int r) {
@@ -3028,17 +2578,10 @@ struct Group {
       lo = min(lo, k);
       hi = max(hi, k);
     };
-    if (TWLL && twl_on) {
-      for (int r0 = 0; r0 < nrows; r0 += NT) {
-        const int r = r0 + tid;
-        if (r < nrows && row_has(r, v)) one(r);
-      }
-    } else {
-      const int a = w_off[2 * v], b = w_off[2 * v + 2];
-      for (int j0 = a; j0 < b; j0 += NT) {
-        const int j = j0 + tid;
-        if (j < b) one(went(j).x);
-      }
+    const int a = w_off[2 * v], b = w_off[2 * v + 2];
+    for (int j0 = a; j0 < b; j0 += NT) {
+      const int j = j0 + tid;
+      if (j < b) one(went(j).x);
     }
     lo = g_min(lo);
     hi = -g_min(-hi);
@@ -3218,15 +2761,18 @@ struct Group {
 // working-set footprint; the multi-wave modes work partly in HBM scratch).
 // Outputs: status / flags / installed / core / steps (oracle_solve).
 #ifndef DP_LDS_MIN_WAVES
-#define DP_LDS_MIN_WAVES 4
+#define DP_LDS_MIN_WAVES 5
 #endif
 // (MINW: minimum waves per SIMD the kernel is compiled for.  The one-wavefront
-// kernel has two builds: unbounded (151 VGPRs, 3 waves per SIMD, no spills)
-// and DP_LDS_MIN_WAVES = 4 (128 VGPRs, 21 VGPRs + 338 SGPRs spilled to
-// scratch).  The capped build only pays where LDS would let more than 12
-// problems share a CU (small catalogs: config 3 70.8M -> 86.0M res/s); at 9
-// per CU (config 2) its spills are ~40 MB of extra scratch writes per run for
-// no throughput.  launch_solve picks the build per launch by footprint.)
+// kernel has two builds: unbounded (105 VGPRs: 4 waves per SIMD, 16 per CU)
+// and DP_LDS_MIN_WAVES = 5 (94 VGPRs: 20 per CU), neither with a spill
+// (tests/test_placement.py reads the code objects).  The capped build only
+// pays where LDS would let more than 16 problems share a CU (small
+// catalogs, config 3); launch_solve picks the build per launch by
+// footprint.  Before round 6 the whole-wave reductions were __shfl_xor
+// butterflies whose ds_bpermute addresses the compiler kept live across the
+// search loop: 163 VGPRs unbounded, and 13 spilled at a 128 cap.  A cap of 6
+// waves (80 VGPRs) spills 11.)
 // One problem's results as two 16-byte vector stores (kernel_api.hpp).
 __device__ __forceinline__ void put_out(ProblemOut* o, int status, int32_t flags, int32_t clen, int32_t cat,
                                         int64_t steps, uint64_t bcp) {

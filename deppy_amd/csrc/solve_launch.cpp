@@ -19,11 +19,11 @@ hipError_t launch_split4_configure(int);
 hipError_t launch_hbm_configure(int);
 hipError_t launch_ldsg_configure(int);
 
-// The unbounded one-wavefront build runs 3 waves per SIMD (12 per CU).  A
-// launch whose footprint lets LDS hold more problems than that per CU takes
-// the register-capped build (4 per SIMD, 16 per CU); larger footprints are
-// LDS-bound and keep the build without spills (solve_kernel.hpp).
-constexpr int kUnboundedWavesPerCU = 12;
+// The unbounded one-wavefront build runs 4 waves per SIMD (105 VGPRs, 16 per
+// CU).  A launch whose footprint lets LDS hold more problems than that per
+// CU takes the register-capped build (5 per SIMD, 20 per CU; 94 VGPRs);
+// larger footprints are LDS-bound (solve_kernel.hpp DP_LDS_MIN_WAVES).
+constexpr int kUnboundedWavesPerCU = 16;
 constexpr int kLdsPerCU = 160 * 1024;
 
 hipError_t launch_solve(const KernelArgs& a, int mode, int n_blocks, int lds_bytes, hipStream_t stream) {

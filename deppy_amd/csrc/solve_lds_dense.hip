@@ -1,9 +1,8 @@
 // M_LDS instantiation of the solve kernel (solve_kernel.hpp) capped at
 // DP_LDS_MIN_WAVES waves per SIMD: for small footprints, where LDS would let
 // more problems share a CU than the unbounded build's registers allow.
-// Clause rows evaluated two literals per step (the unbounded build: four):
-// with the BCP counter left out, the capped build then spills one VGPR
-// instead of 12 (Group::NO_VIS).
+// Clause rows evaluated two literals per step (the unbounded build: four),
+// and the BCP counter left out (Group::NO_VIS).
 #define DP_EVAL_UNROLL 2
 #include "solve_kernel.hpp"
 

@@ -11,9 +11,8 @@
 //          positive l the AtMost rows holding var(l), once per distinct
 //          variable; the same rows as build_watches_host),
 //   scan   the counts into list offsets (one workgroup per record),
-//   fill   the lists through the offsets as cursors: 2-byte entries (the
-//          row) when every row id fits 16 bits, else 8-byte entries {row,
-//          row_info(row)} (layout.hpp went_bytes).
+//   fill   the lists through the offsets as cursors: 8-byte entries {row,
+//          row_info(row)} (layout.hpp row_info).
 // Counts go to wo[l + 2] and cursors run on wo[l + 1], so when the fill ends
 // wo[l] is the start of list l (wo[2nv] their total) with no pass to shift
 // the offsets back.  Row order within a list is left to the atomics, as in
@@ -39,7 +38,6 @@ struct WbRec {
   const int32_t* h;
   int32_t* wo;  // [2nv + 2] counters / offsets, then the lists: [ncl + nkl] u16 rows or int2 {row, row_info}
   dp_rec_layout R;
-  bool e2;      // 2-byte entries (layout.hpp went_bytes)
 };
 
 // Item k of the launch, when its lists are built by these passes.
@@ -49,7 +47,6 @@ __device__ __forceinline__ bool wb_rec(const KernelArgs& a, int k, WbRec& x) {
   if (h[DP_H_FMT] != DP_FMT_I32 || device_watches(h)) return false;
   x.h = h;
   x.R = rec_layout(h);
-  x.e2 = went_bytes(h) == 2;
   x.wo = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(a.scratch + a.scratch_off[k]) + layout<MODE>(h).wl);
   return true;
 }
@@ -79,12 +76,9 @@ __global__ __launch_bounds__(kWbThreads) void wb_rows(KernelArgs a) {
   const int32_t* kl = h + x.R.card_lits;
   int32_t* wo = x.wo;
   int2* ww = reinterpret_cast<int2*>(wo + 2 * nv + 2);
-  uint16_t* w2 = reinterpret_cast<uint16_t*>(wo + 2 * nv + 2);
   const unsigned cap = (unsigned)(ncl + nkl), nl = (unsigned)(2 * nv);
   auto put = [&](unsigned at, int2 e) {
-    if (at >= cap) return;
-    if (x.e2) w2[at] = (uint16_t)e.x;
-    else ww[at] = e;
+    if (at < cap) ww[at] = e;
   };
   const int t = s * kWbThreads + (int)threadIdx.x, T = kWbSlices * kWbThreads;
   for (int r = t; r < nc; r += T) {

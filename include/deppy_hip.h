@@ -586,6 +586,11 @@ enum dp_place {
   DP_PLACE_TOO_LARGE = -2
 };
 int dp_plan_placements(const dp_batch* b, int32_t opt_flags, int8_t* place);
+/*   dp_plan_order: the launch order dp_submit plans for b as one chunk:
+ *     order[] (the problems, skipped ones left out, in workgroup order:
+ *     launch after launch) and launch_first[] (each launch's first index
+ *     into order; up to 21 launches).  Returns the number of launches or -1. */
+int dp_plan_order(const dp_batch* b, int32_t opt_flags, int32_t* order, int32_t* launch_first);
 
 /* Device time of the solve kernel(s) of the last waited launch (dp_run,
  * dp_wait, dp_solve), measured with HIP events on its stream (max over devices). */

@@ -262,9 +262,17 @@ def _network_rows(m, nv, aig, ident, clauses, aux):
     Every And gate in the cone of the gate literal m gets an auxiliary
     variable (after the input's variables, in ascending node order) and its
     three Tseitin clauses [~g a] [~g b] [g ~a ~b]; then the unit [m].  Unit
-    propagation over them derives exactly what gini's does over the gates
-    (the counting row is strictly stronger with repeated ids, DESIGN.md
-    §3.1).  Every row carries the AtMost's identity."""
+    propagation over one such network derives what gini's does over its
+    gates (the counting row is strictly stronger with repeated ids,
+    DESIGN.md §3.1).  Each AtMost gets its own copy of its cone: two
+    networks that share gates through the strash (the same ids with
+    different bounds) share no auxiliary variable here, where gini has one
+    variable per shared node -- a value forced on a shared gate by one
+    network does not reach the other, so propagation can be weaker than
+    gini's.  Sharing would need the gate rows always on (an identity's rows
+    are dropped with it during core search).  Parity with the reference is
+    unpinned for such inputs (no reference vector holds one).  Every row
+    carries the AtMost's identity."""
     rev = {g: ab for ab, g in aig.strash.items()}
     cone, todo = set(), [m & ~1]
     while todo:

@@ -342,3 +342,24 @@ def test_nvu_header_validated():
         r2 = r.copy()
         r2[H_NVU] = ok
         assert L.dp_rec_validate(r2.ctypes.data_as(_lib.c_i32p), len(r2)) == 0
+
+
+def test_two_networks_over_the_same_ids_get_their_own_gates():
+    """Two repeated-id AtMosts over the same ids with different bounds share
+    gates in gini's strash; here each lowers to its own copy of its cone
+    (lower.cpp network_rows, lower_ref.py _network_rows): the record holds
+    the auxiliaries of both networks side by side, the C++ lowering equals
+    the restatement, and the oracle's answer satisfies both bounds.  Whether
+    gini's shared gates would propagate more is parity-unpinned (no
+    reference vector holds such a pair)."""
+    vs = [V("a", sat.AtMost(1, "b", "b", "c"), sat.AtMost(2, "b", "b", "c"), sat.Mandatory()),
+          V("b", sat.Mandatory()), V("c")]
+    one = [V("a", sat.AtMost(1, "b", "b", "c"), sat.Mandatory()), V("b", sat.Mandatory()), V("c")]
+    lw = _lib.Lowered(sat.encode_inputs([vs, one]))
+    compare(lw, 0, _ref(vs))
+    compare(lw, 1, _ref(one))
+    r2, r1 = lw.record(0), lw.record(1)
+    aux2, aux1 = int(r2[H_NV]) - int(r2[H_NVU]), int(r1[H_NV]) - int(r1[H_NVU])
+    assert aux1 > 0 and aux2 > aux1  # the second network's gates are not the first one's
+    res = oracle.solve_batch(lw.rec_off, lw.rec)
+    assert list(res["status"]) == [-1, -1]  # b twice with b mandatory exceeds AtMost(1); a mandatory

@@ -130,3 +130,57 @@ def test_no_vgpr_spills():
     bad = [(k[".name"], k[".vgpr_count"], k[".vgpr_spill_count"], k[".private_segment_fixed_size"])
            for k in ks if k[".vgpr_spill_count"] or k[".private_segment_fixed_size"]]
     assert bad == [], bad
+
+
+# ---------------------------------------------------------------------------
+# dispatch order (runtime.cpp plan_chunk)
+# ---------------------------------------------------------------------------
+def _expected_lds_order(rec_off, rec, members, first_rel=0):
+    """A one-wavefront launch's workgroup order, restated: cost classes
+    (anchors, at most 15) costliest first, members in problem order within a
+    class, each class dealt XCD-contiguously (workgroup b on XCD b % 8 takes
+    the next of XCD (b % 8)'s contiguous range of the class)."""
+    cls = {p: min(int(rec[rec_off[p] + 5]), 15) for p in members}
+    srt = sorted(members, key=lambda p: (-cls[p], p))
+    out = [None] * len(srt)
+    pos = 0
+    while pos < len(srt):
+        end = pos
+        while end < len(srt) and cls[srt[end]] == cls[srt[pos]]:
+            end += 1
+        slots = {x: [b for b in range(pos, end) if (b + first_rel) % 8 == x] for x in range(8)}
+        at = pos
+        for x in range(8):
+            for k, b in enumerate(slots[x]):
+                out[b] = srt[at + k]
+            at += len(slots[x])
+        pos = end
+    return out
+
+
+def test_plan_order_one_wavefront():
+    """Config 2 (one launch of one-wavefront problems): the planned order is
+    the costliest anchor class first, XCD-contiguous within each class."""
+    lw = lowered_config(2, 3000, 7, narrow=True, packed=True)
+    order, first = _lib.plan_order(lw.rec_off, lw.rec)
+    assert list(first) == [0]
+    assert list(order) == _expected_lds_order(lw.rec_off, lw.rec, list(range(lw.n)))
+
+
+def test_plan_order_mixed_launches():
+    """Config 5 (multi-wave launches first, then the one-wavefront ones):
+    every problem once, each launch's members of one placement, and each
+    one-wavefront launch in the restated order (its XCDs counted from its
+    first workgroup)."""
+    lw = lowered_config(5, 2000, 9, narrow=True, packed=True)
+    place = _lib.plan_placements(lw.rec_off, lw.rec)
+    order, first = _lib.plan_order(lw.rec_off, lw.rec)
+    assert sorted(order.tolist()) == list(range(lw.n))
+    bounds = list(first) + [lw.n]
+    assert len(first) >= 2
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        seg = order[a:b].tolist()
+        kinds = set(place[seg].tolist())
+        assert len(kinds) == 1, kinds
+        if kinds == {LDS}:
+            assert seg == _expected_lds_order(lw.rec_off, lw.rec, sorted(seg), first_rel=0), (a, b)
