@@ -521,67 +521,114 @@ int p8_to_p16d(const int32_t* rec, int64_t avail, std::vector<int32_t>& p16) {
   return 0;
 }
 
+// DP_FMT_P8D's body (include/deppy_hip.h) from a record's arrays given by
+// accessors -- clause literal j, AtMost variable j, bound k, anchor i, the
+// length of row i (clause rows, then AtMost rows), list source k, and the
+// identity of AtMost row k -- in two steps: p8_plan (the flags and the body's
+// bytes; false when the form does not apply: more than DP_P8_MAX_VARS
+// variables or a bound above 255), then p8_write into `o` (the body, zeroed,
+// plan.bytes long; sets h's DP_H_FMT and DP_H_P8).  pack8 feeds them a
+// DP_FMT_P16D record, the fast lowering its own arrays (Lowerer::emit_p16d).
+struct P8Plan {
+  int32_t flags;
+  int64_t bytes;
+};
+template <class KB, class LEN, class SRC>
+bool p8_plan(const int32_t* h, KB kb, LEN len, SRC src, P8Plan& P) {
+  if (h[DP_H_NV] > DP_P8_MAX_VARS) return false;
+  const int64_t nk = h[DP_H_NK], rows = (int64_t)h[DP_H_NC] + nk, nch = h[DP_H_NCH];
+  bool b1 = true, nib = true;
+  for (int64_t k = 0; k < nk; ++k) {
+    const int32_t b = kb(k);
+    if (b < 0 || b > 255) return false;
+    b1 = b1 && b == 1;
+  }
+  for (int64_t i = 0; i < rows && nib; ++i) nib = len(i) <= 15;
+  int64_t nz = 0;
+  for (int64_t k = 0; k < nch; ++k) nz += src(k) != 0;
+  P.flags = (h[DP_H_NV] > 256 ? DP_P8_HI : 0) | (b1 ? DP_P8_B1 : 0) | (nib ? DP_P8_NIB : 0);
+  int32_t t[DP_H_SIZE];
+  std::memcpy(t, h, sizeof t);
+  t[DP_H_P8] = P.flags;
+  P.bytes = dp_p8_body_bytes(t, nz);
+  return true;
+}
+template <class CL, class KL, class KB, class AN, class LEN, class SRC, class KID>
+void p8_write(int32_t* h, const P8Plan& P, uint8_t* o, CL cl, KL kl, KB kb, AN an, LEN len, SRC src, KID kid) {
+  const int32_t f = P.flags;
+  h[DP_H_FMT] = DP_FMT_P8D;
+  h[DP_H_P8] = f;
+  const dp_p8_layout L = dp_p8_layout_of(h);
+  const int64_t ncl = h[DP_H_NCL], nkl = h[DP_H_NKL], nk = h[DP_H_NK], na = h[DP_H_NA];
+  const int64_t rows = (int64_t)h[DP_H_NC] + nk, nch = h[DP_H_NCH];
+  const bool hi = f & DP_P8_HI;
+  auto setbit = [&](int64_t at, int64_t j) { o[at + (j >> 3)] |= (uint8_t)(1u << (j & 7)); };
+  // eight positions a step: their low bytes, then their bit-plane bytes
+  // whole (no read-modify-write per bit)
+  auto vars = [&](auto get, int64_t n, int64_t lo, int64_t neg, int64_t hp, int sh) {
+    for (int64_t j0 = 0; j0 < n; j0 += 8) {
+      uint32_t nb = 0, hb = 0;
+      const int q1 = (int)std::min<int64_t>(8, n - j0);
+      for (int q = 0; q < q1; ++q) {
+        const int32_t x = get(j0 + q);
+        o[lo + j0 + q] = (uint8_t)(x >> sh);
+        nb |= (uint32_t)(x & sh) << q;  // (sh = 1: the literal's sign; 0: none)
+        hb |= (uint32_t)((x >> (8 + sh)) & 1) << q;
+      }
+      if (neg >= 0) o[neg + (j0 >> 3)] = (uint8_t)nb;
+      if (hi) o[hp + (j0 >> 3)] = (uint8_t)hb;
+    }
+  };
+  vars(cl, ncl, L.cvar, L.neg, L.chi, 1);
+  vars(kl, nkl, L.kvar, -1, L.khi, 0);
+  vars(an, na, L.avar, -1, L.ahi, 0);
+  if (!(f & DP_P8_B1))
+    for (int64_t k = 0; k < nk; ++k) o[L.bound + k] = (uint8_t)kb(k);
+  if (f & DP_P8_NIB) {
+    for (int64_t i = 0; i < rows; i += 2)
+      o[L.lens + (i >> 1)] = (uint8_t)(len(i) | (i + 1 < rows ? len(i + 1) << 4 : 0));
+  } else {
+    for (int64_t i = 0; i < rows; ++i) o[L.lens + i] = (uint8_t)len(i);
+  }
+  int64_t q = L.srcval;
+  for (int64_t k = 0; k < nch; ++k)
+    if (const int32_t x = src(k)) {
+      setbit(L.srcnz, k);
+      o[q++] = (uint8_t)x;
+    }
+  for (int64_t k = 0; k < nk; ++k) setbit(q, kid(k));
+  h[DP_H_P8] = (int32_t)((uint32_t)f | ((uint32_t)P.bytes << 8));
+}
+
 // The DP_FMT_P16D record r in the DP_FMT_P8D form, in place, when it applies
-// (at most DP_P8_MAX_VARS variables, every AtMost bound below 256).  Returns
-// its words as it lies (dp_rec_phys_words), or 0 with r unchanged.
+// (p8_plan).  Returns its words as it lies (dp_rec_phys_words), or 0 with r
+// unchanged.
 int64_t pack8(int32_t* r) {
-  if (r[DP_H_FMT] != DP_FMT_P16D || r[DP_H_NV] > DP_P8_MAX_VARS) return 0;
-  const int64_t ncl = r[DP_H_NCL], nkl = r[DP_H_NKL], nk = r[DP_H_NK], na = r[DP_H_NA];
-  const int64_t nc = r[DP_H_NC], nch = r[DP_H_NCH], nid = r[DP_H_NID];
+  if (r[DP_H_FMT] != DP_FMT_P16D) return 0;
+  const int64_t ncl = r[DP_H_NCL], nkl = r[DP_H_NKL], nk = r[DP_H_NK], nc = r[DP_H_NC], nch = r[DP_H_NCH];
   const uint16_t* u = reinterpret_cast<const uint16_t*>(r + DP_H_SIZE);
   const uint16_t *cl = u, *kl = cl + ncl, *kb = kl + nkl, *an = kb + nk;
   const uint8_t* t = reinterpret_cast<const uint8_t*>(r + DP_H_SIZE) + dp_p16_tail_at(r);
   const uint8_t *lens = t, *src = t + nc + nk, *mask = src + nch;
-  int32_t f = r[DP_H_NV] > 256 ? DP_P8_HI : 0;
-  bool b1 = true, nib = true;
-  for (int64_t k = 0; k < nk; ++k) {
-    if (kb[k] > 255) return 0;
-    b1 = b1 && kb[k] == 1;
-  }
-  for (int64_t i = 0; i < nc + nk; ++i) nib = nib && lens[i] <= 15;
-  f |= (b1 ? DP_P8_B1 : 0) | (nib ? DP_P8_NIB : 0);
+  auto KB = [&](int64_t k) { return (int32_t)kb[k]; };
+  auto LEN = [&](int64_t i) { return (int32_t)lens[i]; };
+  auto SRC = [&](int64_t k) { return (int32_t)src[k]; };
+  P8Plan P;
+  if (!p8_plan(r, KB, LEN, SRC, P)) return 0;
+  static thread_local std::vector<int32_t> kid;  // the AtMost identities, from the mask
+  kid.clear();
+  for (int32_t i = 0; i < r[DP_H_NID]; ++i)
+    if ((mask[i >> 3] >> (i & 7)) & 1) kid.push_back(i);
+  static thread_local std::vector<uint8_t> o;
+  o.assign((size_t)P.bytes, 0);
   int32_t h[DP_H_SIZE];
   std::memcpy(h, r, sizeof h);
-  h[DP_H_FMT] = DP_FMT_P8D;
-  h[DP_H_P8] = f;
-  const dp_p8_layout P = dp_p8_layout_of(h);
-  int64_t nz = 0;
-  for (int64_t k = 0; k < nch; ++k) nz += src[k] != 0;
-  const int64_t bytes = dp_p8_body_bytes(h, nz);
-  static thread_local std::vector<uint8_t> o;
-  o.assign((size_t)bytes, 0);
-  auto setbit = [&](int64_t at, int64_t j) { o[(size_t)(at + (j >> 3))] |= (uint8_t)(1u << (j & 7)); };
-  for (int64_t j = 0; j < ncl; ++j) {
-    o[(size_t)(P.cvar + j)] = (uint8_t)(cl[j] >> 1);
-    if (cl[j] & 1) setbit(P.neg, j);
-    if ((f & DP_P8_HI) && (cl[j] >> 9)) setbit(P.chi, j);
-  }
-  for (int64_t j = 0; j < nkl; ++j) {
-    o[(size_t)(P.kvar + j)] = (uint8_t)kl[j];
-    if ((f & DP_P8_HI) && (kl[j] >> 8)) setbit(P.khi, j);
-  }
-  for (int64_t i = 0; i < na; ++i) {
-    o[(size_t)(P.avar + i)] = (uint8_t)an[i];
-    if ((f & DP_P8_HI) && (an[i] >> 8)) setbit(P.ahi, i);
-  }
-  if (!b1)
-    for (int64_t k = 0; k < nk; ++k) o[(size_t)(P.bound + k)] = (uint8_t)kb[k];
-  for (int64_t i = 0; i < nc + nk; ++i) {
-    if (nib) o[(size_t)(P.lens + (i >> 1))] |= (uint8_t)(lens[i] << (4 * (i & 1)));
-    else o[(size_t)(P.lens + i)] = lens[i];
-  }
-  int64_t q = 0;
-  for (int64_t k = 0; k < nch; ++k)
-    if (src[k]) {
-      setbit(P.srcnz, k);
-      o[(size_t)(P.srcval + q++)] = src[k];
-    }
-  std::memcpy(o.data() + P.srcval + nz, mask, (size_t)((nid + 7) / 8));
-  h[DP_H_P8] = (int32_t)((uint32_t)f | ((uint32_t)bytes << 8));
+  p8_write(h, P, o.data(), [&](int64_t j) { return (int32_t)cl[j]; }, [&](int64_t j) { return (int32_t)kl[j]; }, KB,
+           [&](int64_t i) { return (int32_t)an[i]; }, LEN, SRC, [&](int64_t k) { return kid[(size_t)k]; });
   std::memcpy(r, h, sizeof h);
   uint8_t* b = reinterpret_cast<uint8_t*>(r + DP_H_SIZE);
-  std::memcpy(b, o.data(), (size_t)bytes);
-  std::memset(b + bytes, 0, (size_t)((4 - bytes % 4) % 4));  // to the last word's end
+  std::memcpy(b, o.data(), (size_t)P.bytes);
+  std::memset(b + P.bytes, 0, (size_t)((4 - P.bytes % 4) % 4));  // to the last word's end
   return dp_rec_phys_words(r);
 }
 
@@ -750,6 +797,28 @@ struct Lowerer {
     hdr[DP_H_FMT] = DP_FMT_P16D;
     const int64_t tb = dp_p16_tail_bytes(hdr);
     if (tb > DP_P16_TAIL_MAX) return false;
+    auto len = [&](int64_t i) {
+      return i < F.nc ? F.clause_off[i + 1] - F.clause_off[i] : F.card_off[i - F.nc + 1] - F.card_off[i - F.nc];
+    };
+    auto kb = [&](int64_t k) { return F.card_bound[k]; };
+    auto srcv = [&](int64_t k) { return (int32_t)F.src[k]; };
+    P8Plan P8;
+    if (p8 && p8_plan(hdr, kb, len, srcv, P8)) {  // DP_FMT_P8D straight from the arrays
+      const int64_t phys = DP_H_SIZE + (P8.bytes + 3) / 4, padded = (phys + 3) & ~3LL;
+      int32_t* r = O.extend((size_t)padded);
+      uint8_t* b = reinterpret_cast<uint8_t*>(r + DP_H_SIZE);
+      std::memset(b, 0, (size_t)(4 * (padded - DP_H_SIZE)));
+      p8_write(hdr, P8, b, [&](int64_t j) { return F.clause_lits[j]; }, [&](int64_t j) { return F.card_lits[j]; }, kb,
+               [&](int64_t i) { return F.anchors[i]; }, len, srcv, [&](int64_t k) { return F.card_id[k]; });
+      std::memcpy(r, hdr, sizeof hdr);
+      O.rec_len.push_back(padded);
+      O.ivar.insert(O.ivar.end(), F.owner_v, F.owner_v + F.nid);
+      O.icon.insert(O.icon.end(), F.owner_c, F.owner_c + F.nid);
+      O.ident_len.push_back(F.nid);
+      O.err.push_back(DP_LOWER_OK);
+      O.msg.emplace_back();
+      return true;
+    }
     const int64_t at = dp_p16_tail_at(hdr);
     const int64_t phys = DP_H_SIZE + (at + tb + 3) / 4, padded = (phys + 3) & ~3LL;
     int32_t* r = O.extend((size_t)padded);
@@ -773,16 +842,7 @@ struct Lowerer {
     t += F.nch;
     std::memset(t, 0, (size_t)(reinterpret_cast<uint8_t*>(r + padded) - t));  // mask, then the padding
     for (int32_t k = 0; k < F.nk; ++k) t[F.card_id[k] >> 3] |= (uint8_t)(1u << (F.card_id[k] & 7));
-    int64_t len = padded;
-    if (p8) {
-      const int64_t p8w = pack8(r);
-      if (p8w) {  // the record shrank in place: give the rest back
-        len = (p8w + 3) & ~3LL;
-        for (int64_t j = p8w; j < len; ++j) r[j] = 0;
-        O.nrec -= (size_t)(padded - len);
-      }
-    }
-    O.rec_len.push_back(len);
+    O.rec_len.push_back(padded);
     O.ivar.insert(O.ivar.end(), F.owner_v, F.owner_v + F.nid);
     O.icon.insert(O.icon.end(), F.owner_c, F.owner_c + F.nid);
     O.ident_len.push_back(F.nid);
