@@ -31,7 +31,7 @@ with open("gpurun_out/r06_final/pmc_traffic.jsonl", "w") as f:
 PY
   cat $OUT/pmc_traffic.jsonl
   rm -rf gpurun_out/sq
-  bash scripts/pmc_sq_r02.sh "2 3 6" > $OUT/sq.log 2>&1 || exit 1
+  bash scripts/pmc_sq_r02.sh "2 3 6 4" > $OUT/sq.log 2>&1 || exit 1
   python3 scripts/sq_summary.py gpurun_out/sq > $OUT/sq_split.json || exit 1
   head -c 600 $OUT/sq_split.json
   exit 0
