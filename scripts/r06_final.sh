@@ -8,7 +8,10 @@
 #   bash scripts/r06_final.sh bench  GPU parity tests, smoke(), the driver's
 #                                    command for configs 2-6, the rocprofv3
 #                                    kernel-trace stats of the config-2 driver
-#                                    command and of the config 4 / 5 kernels alone
+#                                    command and of the config 2 / 4 / 5 kernels
+#                                    alone, config 4's single-catalog latency
+#                                    (c4_latency.py) and the served path's
+#                                    pieces (pipe_timing.py)
 # Every GPU step has its own time limit; the first failure ends the call.
 set -o pipefail
 export TMPDIR=/tmp
@@ -51,4 +54,7 @@ for c in 2 4 5; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/ktrace_c$c -o run -- \
     python3 bench.py --config $c --kernel-only --kernel-steps $ks --no-cpu > $OUT/ktrace_c$c.json 2> $OUT/ktrace_c$c.err || exit 1
 done
+timeout -k 10 300 python -u scripts/c4_latency.py 20 > $OUT/c4_latency.jsonl 2> $OUT/c4_latency.err || exit 1
+tail -1 $OUT/c4_latency.jsonl
+timeout -k 10 300 python -u scripts/pipe_timing.py 2 10000 > $OUT/pipe_timing.txt 2>&1 || exit 1
 echo "closing run done"
