@@ -517,16 +517,24 @@ def _batch(rec_off, rec):
 
 
 def result_arrays(rec_off, rec) -> dict:
-    """Caller-allocated dp_result arrays for a batch (dp_result_layout)."""
+    """Caller-allocated dp_result arrays for a batch (dp_result_layout),
+    their pages touched here: np.zeros maps large arrays lazily, and the
+    pipeline's scatter would otherwise take the page faults of a buffer's
+    first use (config 6: 0.23 instead of 0.055 ms per 10k results)."""
     rec_off = np.ascontiguousarray(rec_off, np.int64)
     n = len(rec_off) - 1
     inst_off = np.zeros(n + 1, np.int64)
     core_off = np.zeros(n + 1, np.int64)
     lib().dp_result_layout(ctypes.byref(_batch(rec_off, rec)), _p(inst_off, c_i64p), _p(core_off, c_i64p))
-    return dict(status=np.zeros(max(n, 1), np.int8), flags=np.zeros(max(n, 1), np.int32),
-                installed=np.zeros(max(1, int(inst_off[-1])), np.uint32), inst_off=inst_off,
-                core=np.zeros(max(1, int(core_off[-1])), np.int32), core_off=core_off,
-                core_len=np.zeros(max(n, 1), np.int32), steps=np.zeros(max(n, 1), np.int64))
+
+    def zeros(m, dt):
+        a = np.empty(m, dt)
+        a.fill(0)
+        return a
+    return dict(status=zeros(max(n, 1), np.int8), flags=zeros(max(n, 1), np.int32),
+                installed=zeros(max(1, int(inst_off[-1])), np.uint32), inst_off=inst_off,
+                core=zeros(max(1, int(core_off[-1])), np.int32), core_off=core_off,
+                core_len=zeros(max(n, 1), np.int32), steps=zeros(max(n, 1), np.int64))
 
 
 def _result_struct(out: dict) -> Result:
