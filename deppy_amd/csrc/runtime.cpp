@@ -186,6 +186,7 @@ struct PlanBlock {
 
 struct Plan {
   int32_t n = 0;
+  int32_t n_ldsg = 0;             // problems placed on M_LDSG
   std::vector<int64_t> img_off;   // [n+1] staged word offsets
   std::vector<uint8_t> narrow;    // [n] staged in 16-bit form
   std::vector<int32_t> order;     // workgroup -> local problem
@@ -285,9 +286,12 @@ void read_head(Head& H, const int32_t* h, int64_t avail, int32_t opt_flags, bool
 // rec + rec_off[p0 + i] is local problem i.  Problems whose header is not
 // well formed are planned as skipped (the caller reports them).  pool (may
 // be null) reads the headers in parallel.
+// ldsg_busy: M_LDSG problems already in flight on the device (the
+// pipeline's other lanes), counted against kLdsgMaxProblems with the chunk's.
 void plan_chunk(Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0, int32_t n,
-                int32_t opt_flags, std::vector<uint8_t>* bad, Pool* pool = nullptr) {
+                int32_t opt_flags, std::vector<uint8_t>* bad, Pool* pool = nullptr, int32_t ldsg_busy = 0) {
   P.n = n;
+  P.n_ldsg = 0;
   P.img_off.resize((size_t)n + 1);
   P.inst_off.resize((size_t)n + 1);
   P.narrow.resize((size_t)n);
@@ -342,9 +346,15 @@ void plan_chunk(Plan& P, const int32_t* rec, const int64_t* rec_off, int32_t p0,
     const int lm = dp::ldsg_env();
     int32_t n_ok = 0;
     for (int32_t b = 0; b < nblk; ++b) n_ok += P.blk[(size_t)b].nok;
-    if (n_ok > 0 && (lm == dp::LDSG_ALWAYS || (lm == dp::LDSG_AUTO && n_ok <= dp::kLdsgMaxProblems)))
+    // (with other M_LDSG chunks in flight on the device -- concurrent small
+    // jobs -- their problems count too: the rule is per device load, so many
+    // small chunks do not each take the all-LDS group, the regime measured
+    // slower under load)
+    if (n_ok > 0 && (lm == dp::LDSG_ALWAYS || (lm == dp::LDSG_AUTO && n_ok + ldsg_busy <= dp::kLdsgMaxProblems))) {
       for (int32_t i = 0; i < n; ++i)
         if (head[i].ldsg_ok) place_ldsg(head[i], rec + rec_off[p0 + i], (rec_off[p0 + i] & 3) == 0);
+      P.n_ldsg = n_ok;
+    }
   }
   // per block: totals and per-bucket counts / LDS maxima
   const bool rec_aligned = ((uintptr_t)rec & 15) == 0;
@@ -1451,7 +1461,9 @@ int start_chunk(dp_ctx* ctx, Device& D, Lane& L, dp_job* job, int32_t p0, int32_
   if (early) HIP_OK(hipMemcpyAsync(L.d_in.p, job->rec + job->rec_off[p0], 4 * (size_t)W, hipMemcpyHostToDevice, cs));
   L.bad.assign((size_t)n, 0);
   std::vector<uint8_t>& bad = L.bad;
-  dp::plan_chunk(L.plan, job->rec, job->rec_off, p0, n, ctx->flags, &bad, D.pool);
+  int32_t ldsg_busy = 0;  // M_LDSG problems of the chunks in flight on this device
+  for (const Lane* o : D.inflight) ldsg_busy += o->plan.n_ldsg;
+  dp::plan_chunk(L.plan, job->rec, job->rec_off, p0, n, ctx->flags, &bad, D.pool, ldsg_busy);
   const double t_plan = now_ms();
   st.plan_ms += t_plan - t0;
   // Direct: records already in their staged form (16-bit, on a 16-byte
