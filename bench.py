@@ -144,6 +144,51 @@ def end_to_end(ctx, wa, n, steps, depth=2):
     return n * steps / (time.perf_counter() - t0)
 
 
+def end_to_end_device(ctx, wa, lw_host, n, steps, depth=2):
+    """end_to_end with the lowering on the GPU (dp_lower_device): the 32-bit
+    wire in page-locked memory crosses PCIe, one wavefront per problem lowers
+    it (lower_device.hip) into records that come back to page-locked host
+    memory byte-identical to dp_lower_into's, and they are submitted as in
+    end_to_end; `depth` batches in flight."""
+    from deppy_amd import _lib
+    dl = _lib.DeviceLowerer(ctx)
+    w32 = _lib.Wire32Arrays(wa)
+    lws = [dl.lower(w32, _lib.Lowered.empty()) for _ in range(depth)]
+    same = bool(np.array_equal(lws[0].rec_off, lw_host.rec_off) and np.array_equal(lws[0].rec, lw_host.rec)
+                and np.array_equal(lws[0].ident_var, lw_host.ident_var)
+                and np.array_equal(lws[0].ident_con, lw_host.ident_con))
+    outs = [_lib.result_arrays(x.rec_off, x.rec) for x in lws]
+    t0 = time.perf_counter()
+    for _ in range(3):
+        dl.lower(w32, lws[0])
+    t_lower = (time.perf_counter() - t0) / 3
+
+    def run(k):
+        jobs = []
+        for i in range(k):
+            j = i % depth
+            if len(jobs) == depth:
+                jobs.pop(0).wait()
+            dl.lower(w32, lws[j])
+            jobs.append(ctx.submit(lws[j].rec_off, lws[j].rec, outs[j]))
+        for job in jobs:
+            job.wait()
+
+    run(depth)
+    t0 = time.perf_counter()
+    run(steps)
+    rate = n * steps / (time.perf_counter() - t0)
+    out = {"res_per_s": round(rate, 1), "steps": steps,
+           "lowering_res_per_s": round(n / t_lower, 1), "lowering_ms": round(t_lower * 1e3, 3),
+           "host_lowered_problems": dl.host_count, "wire_bytes": w32.nbytes(),
+           "records_equal_host_lowering": same,
+           "note": "wire (dp_wire32, page-locked) -> dp_lower_device (one wavefront per problem, "
+                   "lower_device.hip; records back in page-locked host memory, byte-identical to "
+                   "dp_lower_into) -> dp_submit/dp_job_wait -> results, 2 batches in flight; not value"}
+    dl.close()
+    return out
+
+
 def solve_batch_api(ctx, wa, n, steps):
     """The shipped API path, one batch at a time: deppy_amd.sat.solve_wire (the
     wire -> results half of SolveBatch, what the cgo shim does): dp_lower_into
@@ -461,6 +506,7 @@ def main():
             "note": "wire format -> dp_lower_into -> dp_submit/dp_job_wait -> results, 2 batches in flight "
                     "(lowering of batch i+1 overlaps the solve of batch i); what BenchmarkSolve times "
                     "(NewSolver(WithInput)+Solve, bench_test.go:66-77); not value"}
+        line["end_to_end_device"] = end_to_end_device(ctx, wa, lw, n, args.e2e_steps)
         line["solve_batch_api"] = {
             "res_per_s": round(solve_batch_api(ctx, wa, n, max(2, args.e2e_steps // 2)), 1),
             "steps": max(2, args.e2e_steps // 2),

@@ -96,7 +96,8 @@ EXPORTS = [
     "dp_gen_free", "dp_upload_traced", "dp_download_trace", "dp_solve_traced", "dp_lowered_errors",
     "dp_device_bytes", "dp_lower_into", "dp_lowered_new", "dp_lowered_exact_count", "dp_lowered_pinned", "dp_rec_widen", "dp_submit", "dp_job_wait", "dp_get_stats", "dp_stage_roundtrip",
     "dp_stitch_selftest", "dp_partition", "dp_build_info", "dp_get_device_stats", "dp_plan_placements",
-    "dp_plan_order",
+    "dp_plan_order", "dp_dlower_new", "dp_dlower_free", "dp_lower_device", "dp_dlower_host_count",
+    "dp_host_alloc", "dp_host_free",
 ]
 
 
@@ -114,6 +115,22 @@ class Wire(ctypes.Structure):
         ("str_off", c_i64p),
         ("str_bytes", ctypes.c_char_p),
         ("interned", ctypes.c_int32),
+    ]
+
+
+class Wire32(ctypes.Structure):
+    _fields_ = [
+        ("n_problems", ctypes.c_int32),
+        ("prob_var_off", c_i32p),
+        ("var_id", c_i32p),
+        ("var_con_off", c_i32p),
+        ("con_kind", c_i32p),
+        ("con_n", c_i32p),
+        ("con_arg_off", c_i32p),
+        ("con_arg", c_i32p),
+        ("n_strs", ctypes.c_int64),
+        ("str_off", c_i64p),
+        ("str_bytes", ctypes.c_char_p),
     ]
 
 
@@ -252,6 +269,15 @@ def lib():
     L.dp_gen_wire.restype = ctypes.POINTER(Wire)
     L.dp_gen_free.argtypes = [vp]
     L.dp_device_bytes.argtypes = [ctypes.POINTER(Batch), ctypes.c_int32, c_i64p, c_i64p]
+    L.dp_dlower_new.argtypes = [vp]
+    L.dp_dlower_new.restype = vp
+    L.dp_dlower_free.argtypes = [vp]
+    L.dp_lower_device.argtypes = [vp, ctypes.POINTER(Wire32), ctypes.c_int32, vp]
+    L.dp_dlower_host_count.argtypes = [vp]
+    L.dp_dlower_host_count.restype = ctypes.c_int64
+    L.dp_host_alloc.argtypes = [ctypes.c_int64]
+    L.dp_host_alloc.restype = vp
+    L.dp_host_free.argtypes = [vp]
     L.dp_plan_placements.argtypes = [ctypes.POINTER(Batch), ctypes.c_int32, c_i8p]
     L.dp_plan_order.argtypes = [ctypes.POINTER(Batch), ctypes.c_int32, c_i32p, c_i32p]
     _lib = L
@@ -421,6 +447,121 @@ class Lowered:
 
     def record(self, p: int) -> np.ndarray:
         return self.rec[self.rec_off[p]:self.rec_off[p + 1]]
+
+    @classmethod
+    def empty(cls, narrow: bool = True, pinned: bool = True, packed: bool = True, p8: bool = True) -> "Lowered":
+        """An empty result for another lowering to fill (DeviceLowerer.lower)."""
+        self = cls.__new__(cls)
+        self.narrow = narrow
+        self._flags = (1 if narrow else 0) | (2 if pinned else 0) | (4 if packed else 0) | (0 if p8 else 8)
+        self._owner = _LoweredHandle(ctypes.c_void_p(lib().dp_lowered_new()))
+        self._fetch()
+        return self
+
+
+class HostArray:
+    """n elements of page-locked host memory (dp_host_alloc) as a numpy array,
+    or ordinary numpy memory when there is no device."""
+
+    def __init__(self, n: int, dtype):
+        dt = np.dtype(dtype)
+        nb = max(int(n), 1) * dt.itemsize
+        self._p = lib().dp_host_alloc(nb)  # NULL without a device
+        if self._p:
+            buf = (ctypes.c_char * nb).from_address(self._p)
+            self.a = np.frombuffer(buf, dt, count=max(int(n), 1))[:int(n)]
+        else:
+            self.a = np.zeros(max(int(n), 1), dt)[:int(n)]
+
+    def __del__(self):
+        try:
+            if self._p:
+                self.a = None
+                lib().dp_host_free(self._p)
+                self._p = None
+        except Exception:
+            pass
+
+
+class Wire32Arrays:
+    """A dp_wire32 (include/deppy_hip.h): the wire's index arrays in 32 bits,
+    in page-locked memory when a device is present, so dp_lower_device's
+    copy to the device runs by DMA from where they lie."""
+
+    INT = ("prob_var_off", "var_id", "var_con_off", "con_kind", "con_n", "con_arg_off", "con_arg")
+
+    def __init__(self, wire: WireArrays, pinned: bool = True):
+        self._bufs = {}
+        self.a = {}
+        for k in self.INT:
+            src = wire.a[k]
+            if len(src) and (src.max() > np.iinfo(np.int32).max or src.min() < np.iinfo(np.int32).min):
+                raise ValueError("dp_wire32: %s does not fit 32 bits" % k)
+            if pinned:
+                b = HostArray(len(src), np.int32)
+                b.a[:] = src
+                self._bufs[k] = b
+                self.a[k] = b.a
+            else:
+                self.a[k] = np.ascontiguousarray(src, np.int32)
+        self.a["str_off"] = wire.a["str_off"]
+        self.a["str_bytes"] = wire.a["str_bytes"]
+        self._pad = np.zeros(1, np.int32)
+
+    @property
+    def n_problems(self) -> int:
+        return len(self.a["prob_var_off"]) - 1
+
+    def nbytes(self) -> int:
+        return int(sum(self.a[k].nbytes for k in self.INT))
+
+    def struct(self) -> Wire32:
+        a = self.a
+        w = Wire32()
+        w.n_problems = len(a["prob_var_off"]) - 1
+        for k in self.INT:
+            setattr(w, k, _p(a[k] if len(a[k]) else self._pad, c_i32p))
+        w.n_strs = len(a["str_off"]) - 1
+        w.str_off = _p(a["str_off"], c_i64p)
+        w.str_bytes = ctypes.cast(a["str_bytes"].ctypes.data, ctypes.c_char_p)
+        return w
+
+
+class DeviceLowerer:
+    """dp_dlower: lowering on the context's first device (dp_lower_device),
+    the same records as dp_lower_into, byte for byte."""
+
+    def __init__(self, ctx: "Context"):
+        h = lib().dp_dlower_new(ctx.h)
+        if not h:
+            raise RuntimeError(lib().dp_last_global_error().decode())
+        self.h = h
+        self.ctx = ctx  # (outlives the lowering object)
+
+    def lower(self, w32: Wire32Arrays, lw: Lowered | None = None, pinned: bool = True) -> Lowered:
+        if lw is None:
+            lw = Lowered.empty(pinned=pinned)
+        ws = w32.struct()
+        if lib().dp_lower_device(self.h, ctypes.byref(ws), lw._flags, lw._owner.h) != 0:
+            raise ValueError(lib().dp_last_global_error().decode())
+        lw._fetch()
+        return lw
+
+    @property
+    def host_count(self) -> int:
+        """Problems of the last call lowered on the host."""
+        return int(lib().dp_dlower_host_count(self.h))
+
+    def close(self):
+        if self.h:
+            lib().dp_dlower_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 # ---------------------------------------------------------------------------

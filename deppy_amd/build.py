@@ -16,7 +16,7 @@ OBJ = os.path.join(HERE, "_obj")
 STAMPS_LIB = os.path.join(HERE, "libdeppy_hip_stamps.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
-SOURCES = ["solve_lds.hip", "solve_lds_dense.hip", "solve_split.hip", "solve_split4.hip", "solve_ldsg.hip", "solve_hbm.hip", "watch_build.hip", "solve_launch.cpp", "runtime.cpp",
+SOURCES = ["solve_lds.hip", "solve_lds_dense.hip", "solve_split.hip", "solve_split4.hip", "solve_ldsg.hip", "solve_hbm.hip", "watch_build.hip", "lower_device.hip", "solve_launch.cpp", "runtime.cpp",
            "lower.cpp", "gen.cpp"]
 FLAGS = ["-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function",
          "--offload-arch=" + ARCH, "-I" + os.path.join(HERE, "..", "include")]

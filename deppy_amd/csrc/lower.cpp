@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <new>
 #include <atomic>
+#include <memory>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -21,6 +22,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "dlower.hpp"
 #include "hostmem.hpp"
 #include "placement.hpp"
 #include "pool.hpp"
@@ -1451,41 +1453,55 @@ struct Lowerer {
 }  // namespace
 }  // namespace dp
 
-// The records of a dp_lowered: grown, never shrunk, contents not preserved
-// across a resize (every call rewrites them); page-locked when asked and a
-// HIP device is present (dp_submit then copies them to the device as they
-// are), else ordinary 64-byte aligned memory.
-struct RecStore {
-  int32_t* p = nullptr;
+// The records (and identity arrays) of a dp_lowered: grown, never shrunk,
+// contents not preserved across a resize (every call rewrites them);
+// page-locked when asked and a HIP device is present (dp_submit then copies
+// the records to the device as they are, and dp_lower_device copies into
+// them by DMA), else ordinary 64-byte aligned memory.
+template <class T>
+struct HostStore {
+  T* p = nullptr;
   size_t n = 0, cap = 0;
   bool pinned = false;
   void resize(size_t m, bool want_pinned) {
     if (m > cap || want_pinned != pinned) {
       release();
       const size_t c = std::max<size_t>(m + m / 8, 1024);
-      void* q = want_pinned ? dp::pinned_alloc(4 * c) : nullptr;
+      void* q = want_pinned ? dp::pinned_alloc(sizeof(T) * c) : nullptr;
       pinned = q != nullptr;
-      if (!q) q = std::aligned_alloc(64, (4 * c + 63) & ~(size_t)63);
+      if (!q) q = std::aligned_alloc(64, (sizeof(T) * c + 63) & ~(size_t)63);
       if (!q) throw std::bad_alloc();
-      p = static_cast<int32_t*>(q);
+      p = static_cast<T*>(q);
       cap = c;
     }
     n = m;
   }
+  T* data() { return p; }
+  const T* data() const { return p; }
+  size_t size() const { return n; }
+  T* begin() { return p; }
   void release() {
     if (p) pinned ? dp::pinned_free(p) : std::free(p);
     p = nullptr;
     cap = n = 0;
     pinned = false;
   }
-  ~RecStore() { release(); }
+  void swap(HostStore& o) {
+    std::swap(p, o.p);
+    std::swap(n, o.n);
+    std::swap(cap, o.cap);
+    std::swap(pinned, o.pinned);
+  }
+  ~HostStore() { release(); }
 };
+using RecStore = HostStore<int32_t>;
 
 struct dp_lowered {
   int32_t n = 0;
   std::vector<int64_t> rec_off, ident_off;
   RecStore rec;
-  std::vector<int32_t> ivar, icon, err;
+  HostStore<int32_t> ivar, icon;
+  std::vector<int32_t> err;
   std::vector<std::string> msg;
   // scratch kept across dp_lower_into calls (once grown, no allocation or
   // page fault per call): per pool thread, and chunk c's slices of outs[t]
@@ -1498,6 +1514,11 @@ struct dp_lowered {
   std::vector<Piece> pieces;
   std::vector<size_t> at_rec, at_id, at_p;
   std::atomic<int64_t> n_exact{0};  // problems the last call lowered through the full AIG
+  // dp_lower_device's problems lowered on the host (dp::lowered_splice):
+  // their own result, and the spliced arrays before they are swapped in
+  std::unique_ptr<dp_lowered> sub;
+  RecStore rec2;
+  HostStore<int32_t> ivar2, icon2;
 };
 
 extern "C" {
@@ -1639,8 +1660,8 @@ int dp_lower_into(const dp_wire* wire, int32_t flags, dp_lowered* lw) {
     ap[(size_t)c + 1] = ap[(size_t)c] + (pc.q1 - pc.q0);
   }
   lw->rec.resize(ar.back(), (flags & DP_LOWER_PINNED) != 0);
-  lw->ivar.resize(ai.back());
-  lw->icon.resize(ai.back());
+  lw->ivar.resize(ai.back(), (flags & DP_LOWER_PINNED) != 0);
+  lw->icon.resize(ai.back(), (flags & DP_LOWER_PINNED) != 0);
   lw->rec_off.resize((size_t)P + 1);
   lw->ident_off.resize((size_t)P + 1);
   lw->err.resize((size_t)P);
@@ -1670,6 +1691,97 @@ int dp_lower_into(const dp_wire* wire, int32_t flags, dp_lowered* lw) {
     pool.run(nchunks, std::function<void(int64_t)>(merge), 1);
   return 0;
 }
+
+}  // extern "C"
+
+namespace dp {
+
+// dp_lower_device's hand-over (lower_device.hip): lw sized for P problems,
+// rec_words record words and n_ident identities, every problem without an
+// error; the caller fills the arrays.
+LoweredOut lowered_prepare(dp_lowered* lw, int32_t P, int64_t rec_words, int64_t n_ident, bool pinned) {
+  lw->n = P;
+  lw->n_exact.store(0);
+  lw->rec.resize((size_t)rec_words, pinned);
+  lw->ivar.resize((size_t)n_ident, pinned);
+  lw->icon.resize((size_t)n_ident, pinned);
+  lw->rec_off.resize((size_t)P + 1);
+  lw->ident_off.resize((size_t)P + 1);
+  lw->err.assign((size_t)P, DP_LOWER_OK);
+  if (lw->msg.size() != (size_t)P) lw->msg.resize((size_t)P);
+  for (auto& m : lw->msg)
+    if (!m.empty()) m.clear();
+  return {lw->rec_off.data(), lw->ident_off.data(), lw->rec.data(), lw->ivar.data(), lw->icon.data()};
+}
+
+// The problems `which` (ascending; lw gives them no record words and no
+// identities) lowered on the host from `sub` (exactly those problems, in
+// that order) and spliced into lw: records, identities and errors, as
+// dp_lower_into gives them.  Returns 0, or -1 for a malformed problem.
+int lowered_splice(dp_lowered* lw, const dp_wire* sub, int32_t flags, const int32_t* which, int32_t nw) {
+  if (!lw->sub) lw->sub.reset(new dp_lowered);
+  dp_lowered& t = *lw->sub;
+  if (dp_lower_into(sub, flags & ~DP_LOWER_PINNED, &t) != 0) return -1;
+  lw->n_exact.store(t.n_exact.load());
+  const int32_t P = lw->n;
+  const bool pinned = lw->rec.pinned;
+  // new offsets in place, from the old lengths (a running copy of the old
+  // offsets: ro / io are rewritten from the front)
+  int64_t r = 0, d = 0, old_r = 0, old_d = 0;
+  int32_t j = 0;
+  std::vector<int64_t>& ro = lw->rec_off;
+  std::vector<int64_t>& io = lw->ident_off;
+  // pass 1: sizes
+  for (int32_t p = 0; p < P; ++p) {
+    if (j < nw && which[j] == p) {
+      r += t.rec_off[(size_t)j + 1] - t.rec_off[(size_t)j];
+      d += t.ident_off[(size_t)j + 1] - t.ident_off[(size_t)j];
+      ++j;
+    } else {
+      r += ro[(size_t)p + 1] - ro[(size_t)p];
+      d += io[(size_t)p + 1] - io[(size_t)p];
+    }
+  }
+  lw->rec2.resize((size_t)r, pinned);
+  lw->ivar2.resize((size_t)d, pinned);
+  lw->icon2.resize((size_t)d, pinned);
+  // pass 2: copies, then the offsets
+  r = d = 0;
+  j = 0;
+  for (int32_t p = 0; p < P; ++p) {
+    const int64_t ro1 = ro[(size_t)p + 1], io1 = io[(size_t)p + 1];
+    if (j < nw && which[j] == p) {
+      const int64_t a = t.rec_off[(size_t)j], b = t.rec_off[(size_t)j + 1];
+      std::copy(t.rec.p + a, t.rec.p + b, lw->rec2.p + r);
+      const int64_t ia = t.ident_off[(size_t)j], ib = t.ident_off[(size_t)j + 1];
+      std::copy(t.ivar.p + ia, t.ivar.p + ib, lw->ivar2.p + d);
+      std::copy(t.icon.p + ia, t.icon.p + ib, lw->icon2.p + d);
+      r += b - a;
+      d += ib - ia;
+      lw->err[(size_t)p] = t.err[(size_t)j];
+      lw->msg[(size_t)p] = t.msg[(size_t)j];
+      ++j;
+    } else {
+      std::copy(lw->rec.p + old_r, lw->rec.p + ro1, lw->rec2.p + r);
+      std::copy(lw->ivar.p + old_d, lw->ivar.p + io1, lw->ivar2.p + d);
+      std::copy(lw->icon.p + old_d, lw->icon.p + io1, lw->icon2.p + d);
+      r += ro1 - old_r;
+      d += io1 - old_d;
+    }
+    old_r = ro1;
+    old_d = io1;
+    ro[(size_t)p + 1] = r;
+    io[(size_t)p + 1] = d;
+  }
+  lw->rec.swap(lw->rec2);
+  lw->ivar.swap(lw->ivar2);
+  lw->icon.swap(lw->icon2);
+  return 0;
+}
+
+}  // namespace dp
+
+extern "C" {
 
 void dp_lowered_free(dp_lowered* lw) { delete lw; }
 dp_lowered* dp_lowered_new(void) { return new dp_lowered; }

@@ -41,6 +41,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "dlower.hpp"
 #include "kernel_api.hpp"
 #include "layout.hpp"
 #include "hostmem.hpp"
@@ -1756,6 +1757,10 @@ int lane_streams() {
 
 }  // namespace
 
+namespace dp {
+int ctx_first_ordinal(const dp_ctx* ctx) { return ctx && !ctx->dev.empty() ? ctx->dev[0].ordinal : -1; }
+}  // namespace dp
+
 extern "C" {
 
 dp_ctx* dp_create(const dp_opts* opts) {
@@ -1906,6 +1911,10 @@ const char* dp_last_error(const dp_ctx* ctx) {
 }
 int32_t dp_num_devices(const dp_ctx* ctx) { return ctx ? (int32_t)ctx->dev.size() : 0; }
 int32_t dp_lanes(const dp_ctx* ctx) { return ctx && !ctx->dev.empty() ? (int32_t)ctx->dev[0].nlanes : 0; }
+void* dp_host_alloc(int64_t bytes) { return bytes > 0 ? dp::pinned_alloc((size_t)bytes) : nullptr; }
+void dp_host_free(void* p) {
+  if (p) dp::pinned_free(p);
+}
 
 int dp_result_layout(const dp_batch* b, int64_t* inst_off, int64_t* core_off) {
   if (!b || !inst_off || !core_off || b->n_problems < 0) return -1;

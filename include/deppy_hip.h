@@ -367,6 +367,49 @@ int32_t dp_lowered_error(const dp_lowered* lw, int32_t p, const char** msg);
 int32_t dp_lowered_errors(const dp_lowered* lw, int32_t* err);
 
 /* ------------------------------------------------------------------------ */
+/* Lowering on the device: compact wire -> records                          */
+/* ------------------------------------------------------------------------ */
+/* dp_wire with 32-bit arrays, always interned (equal string index <=> equal
+ * identifier): half the bytes of dp_wire to cross PCIe.  Offsets are
+ * absolute, as dp_wire's; the string table is read only for error texts. */
+typedef struct dp_wire32 {
+  int32_t n_problems;
+  const int32_t* prob_var_off; /* [n_problems+1] -> variables          */
+  const int32_t* var_id;       /* [n_vars]   string index of Identifier  */
+  const int32_t* var_con_off;  /* [n_vars+1] -> constraints             */
+  const int32_t* con_kind;     /* [n_cons]   enum dp_kind               */
+  const int32_t* con_n;        /* [n_cons]   AtMost bound               */
+  const int32_t* con_arg_off;  /* [n_cons+1] -> con_arg                  */
+  const int32_t* con_arg;      /* [n_args]   string index               */
+  int64_t n_strs;
+  const int64_t* str_off;      /* [n_strs+1] -> str_bytes (error texts)  */
+  const char* str_bytes;
+} dp_wire32;
+
+/* The device lowering of a context's first device: a stream, device buffers
+ * and page-locked staging of its own, grown on demand and reused by every
+ * call (a serving loop keeps one).  NULL on failure (dp_last_error(ctx)). */
+typedef struct dp_ctx dp_ctx;
+typedef struct dp_dlower dp_dlower;
+dp_dlower* dp_dlower_new(dp_ctx* ctx);
+void dp_dlower_free(dp_dlower* d);
+/* dp_lower_into on the GPU: the same dp_lowered, byte for byte, for flags
+ * DP_LOWER_NARROW | DP_LOWER_PACKED (| DP_LOWER_PINNED).  One wavefront per
+ * problem runs the canonical-key lowering (lower.cpp lower_fast) in LDS and
+ * writes the DP_FMT_P8D record; a problem it does not take (one the keys
+ * cannot decide, an error to report, a record in another form, past the
+ * kernel's sizes) is flagged and lowered on the host pool, and its record is
+ * spliced in.  Other flags lower every problem on the host.  Synchronous.
+ * Returns 0, or -1 (text in dp_last_global_error()). */
+int dp_lower_device(dp_dlower* d, const dp_wire32* wire, int32_t flags, dp_lowered* lw);
+/* Problems of the last dp_lower_device call lowered on the host. */
+int64_t dp_dlower_host_count(const dp_dlower* d);
+/* Page-locked host memory for wire batches (the H2D copy then runs by DMA
+ * from where they lie).  NULL without a device. */
+void* dp_host_alloc(int64_t bytes);
+void dp_host_free(void* p);
+
+/* ------------------------------------------------------------------------ */
 /* 3. Solving                                                                 */
 /* ------------------------------------------------------------------------ */
 

@@ -1,0 +1,145 @@
+"""Lowering on the device (dp_lower_device, deppy_amd/csrc/lower_device.hip):
+the compact 32-bit wire lowered by one wavefront per problem gives the same
+dp_lowered as dp_lower_into(NARROW | PACKED) on the host, byte for byte --
+records, offsets, identity owners (the reported AppliedConstraint,
+lit_mapping.go:69-72), errors and their texts -- with the problems the kernel
+does not take lowered on the host and spliced in."""
+import numpy as np
+import pytest
+
+from deppy_amd import _lib, sat
+from tests import fixtures
+from tests.test_lowering import EDGE, V, _random_problems, all_golden_variable_sets, variables_of
+
+
+def wire_of(config, n, seed):
+    w = _lib.generate(config, n, seed)
+    return _lib.WireArrays(**{k: w[k] for k in (
+        "prob_var_off", "var_id", "var_con_off", "con_kind", "con_n", "con_arg_off", "con_arg",
+        "str_off")}, str_bytes=w["str_bytes"].tobytes())
+
+
+def assert_same(dev, host):
+    assert dev.n == host.n
+    np.testing.assert_array_equal(dev.rec_off, host.rec_off)
+    np.testing.assert_array_equal(dev.rec, host.rec)
+    np.testing.assert_array_equal(dev.ident_off, host.ident_off)
+    np.testing.assert_array_equal(dev.ident_var, host.ident_var)
+    np.testing.assert_array_equal(dev.ident_con, host.ident_con)
+    np.testing.assert_array_equal(dev.err, host.err)
+    assert dev.msg == host.msg
+
+
+def test_wire32_arrays_without_device():
+    """The 32-bit wire keeps every index of the 64-bit one (numpy memory when
+    no device gives page-locked memory) and refuses what does not fit."""
+    w = wire_of(2, 30, 5)
+    w32 = _lib.Wire32Arrays(w)
+    for k in _lib.Wire32Arrays.INT:
+        np.testing.assert_array_equal(w32.a[k], w.a[k])
+        assert w32.a[k].dtype == np.int32
+    s = w32.struct()
+    assert s.n_problems == 30 and s.n_strs == len(w.a["str_off"]) - 1
+    big = _lib.WireArrays(**{k: v.copy() for k, v in w.a.items() if k != "str_bytes"},
+                          str_bytes=w.a["str_bytes"][:-1].tobytes())
+    big.a["con_arg"][0] = 1 << 40
+    with pytest.raises(ValueError, match="32 bits"):
+        _lib.Wire32Arrays(big)
+
+
+@pytest.fixture(scope="module")
+def dl():
+    ctx = _lib.Context(0, 1)
+    d = _lib.DeviceLowerer(ctx)
+    yield d
+    d.close()
+    ctx.close()
+
+
+def lower_both(dl, wire, **kw):
+    host = _lib.Lowered(wire, narrow=True, pinned=True, packed=True, **kw)
+    dev = dl.lower(_lib.Wire32Arrays(wire), _lib.Lowered.empty(pinned=True, **kw))
+    return dev, host
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config,n", [(2, 10000), (3, 20000), (6, 5000), (5, 300)])
+def test_device_records_equal_host(dl, config, n):
+    """Configs 2 and 3 lower entirely on the device; config 6's Dependencies
+    on their own subject (choice lists without rows: not P16D) and config 5's
+    multi-wave catalogs go to the host; every byte equals dp_lower_into's."""
+    dev, host = lower_both(dl, wire_of(config, n, 77))
+    assert_same(dev, host)
+    forms = np.unique(dev.rec[dev.rec_off[:-1] + 13], return_counts=True)
+    print("config", config, "host-lowered", dl.host_count, "of", n, "forms", forms)
+    if config in (2, 3):
+        assert dl.host_count == 0
+
+
+@pytest.mark.gpu
+def test_device_records_of_colliding_problems(dl):
+    """Small random problems where identity keys collide (Conflict vs
+    AtMost(1;a,b), repeated Dependencies, AtMosts over one set in two orders,
+    multiplicities, tautologies, lookup errors) -- the kernel takes what its
+    keys decide and the host the rest; the result equals the host's."""
+    probs = []
+    for seed in (1, 2, 3, 5, 11):
+        probs += _random_problems(seed, 400)
+    probs += EDGE + [variables_of(vs) for vs in all_golden_variable_sets()]
+    probs += [
+        [V("a", sat.Dependency("b", "c"), sat.Dependency("c"), sat.Dependency("b", "c")), V("b", sat.Dependency("c")),
+         V("c")],
+        [V("a", sat.Conflict("b"), sat.AtMost(1, "b", "a")), V("b", sat.AtMost(1, "a", "b"), sat.Conflict("a"))],
+        [V("a", sat.AtMost(1, "a", "b", "c"), sat.AtMost(1, "a", "b", "c"), sat.AtMost(2, "c", "b", "a")), V("b"),
+         V("c", sat.AtMost(0, "a", "b"), sat.AtMost(0, "b", "a"))],
+    ]
+    wire = sat.encode_inputs(probs)
+    dev, host = lower_both(dl, wire)
+    assert_same(dev, host)
+    # both paths were exercised
+    assert 0 < dl.host_count < len(probs), dl.host_count
+
+
+@pytest.mark.gpu
+def test_device_lowering_other_flags_and_reuse(dl):
+    """Flags the kernel does not emit (P16D kept by DP_LOWER_NO_P8) lower on
+    the host through the same call; one result object serves batch after
+    batch of different shapes."""
+    wire = wire_of(2, 500, 3)
+    dev, host = lower_both(dl, wire, p8=False)
+    assert_same(dev, host)
+    assert dl.host_count == 500
+    lw = _lib.Lowered.empty()
+    for cfg, n, seed in ((2, 3000, 1), (3, 5000, 2), (2, 700, 3), (6, 2000, 4)):
+        w = wire_of(cfg, n, seed)
+        dl.lower(_lib.Wire32Arrays(w), lw)
+        assert_same(lw, _lib.Lowered(w, narrow=True, pinned=True, packed=True))
+
+
+@pytest.mark.gpu
+def test_device_lowered_batch_solves_like_host(dl):
+    """The device-lowered batch goes to dp_submit as it lies (page-locked,
+    staged forms) and solves to the host-lowered batch's results."""
+    wire = wire_of(2, 4000, 9)
+    dev, host = lower_both(dl, wire)
+    ctx = dl.ctx
+    a = ctx.submit(dev.rec_off, dev.rec).wait()
+    b = ctx.submit(host.rec_off, host.rec).wait()
+    for k in ("status", "flags", "installed", "core_len", "core"):
+        np.testing.assert_array_equal(a[k], b[k])
+
+
+@pytest.mark.gpu
+def test_device_lowering_malformed_wire(dl):
+    """A malformed problem fails the whole call, as dp_lower_into does."""
+    wire = wire_of(2, 50, 4)
+    bad = _lib.WireArrays(**{k: v.copy() for k, v in wire.a.items() if k != "str_bytes"},
+                          str_bytes=wire.a["str_bytes"][:-1].tobytes())
+    bad.a["con_arg"][5] = len(bad.a["str_off"]) + 3  # a string index past the table
+    with pytest.raises(ValueError, match="malformed"):
+        _lib.Lowered(bad, narrow=True, packed=True)
+    with pytest.raises(ValueError, match="malformed"):
+        dl.lower(_lib.Wire32Arrays(bad))
+    # the object still works after a failed call
+    dev, host = lower_both(dl, wire)
+    assert_same(dev, host)
