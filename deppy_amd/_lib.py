@@ -122,11 +122,12 @@ class Wire32(ctypes.Structure):
     _fields_ = [
         ("n_problems", ctypes.c_int32),
         ("prob_var_off", c_i32p),
+        ("prob_con_off", c_i32p),
+        ("prob_arg_off", c_i32p),
         ("var_id", c_i32p),
-        ("var_con_off", c_i32p),
-        ("con_kind", c_i32p),
-        ("con_n", c_i32p),
-        ("con_arg_off", c_i32p),
+        ("var_ncon", ctypes.POINTER(ctypes.c_uint16)),
+        ("con_kn", c_i32p),
+        ("con_nargs", ctypes.POINTER(ctypes.c_uint16)),
         ("con_arg", c_i32p),
         ("n_strs", ctypes.c_int64),
         ("str_off", c_i64p),
@@ -455,7 +456,10 @@ class Lowered:
         self.narrow = narrow
         self._flags = (1 if narrow else 0) | (2 if pinned else 0) | (4 if packed else 0) | (0 if p8 else 8)
         self._owner = _LoweredHandle(ctypes.c_void_p(lib().dp_lowered_new()))
-        self._fetch()
+        self.n, self.n_exact, self.pinned = 0, 0, False
+        self.rec_off = self.ident_off = np.zeros(1, np.int64)
+        self.rec = self.ident_var = self.ident_con = self.err = np.zeros(0, np.int32)
+        self.msg = []
         return self
 
 
@@ -484,43 +488,64 @@ class HostArray:
 
 
 class Wire32Arrays:
-    """A dp_wire32 (include/deppy_hip.h): the wire's index arrays in 32 bits,
-    in page-locked memory when a device is present, so dp_lower_device's
-    copy to the device runs by DMA from where they lie."""
+    """A dp_wire32 (include/deppy_hip.h), the compact wire: per problem the
+    absolute offsets of its variables, constraints and arguments, per
+    variable and constraint a 16-bit count, a constraint's kind and bound in
+    one word.  In page-locked memory when a device is present, so
+    dp_lower_device's copy to the device runs by DMA from where it lies."""
 
-    INT = ("prob_var_off", "var_id", "var_con_off", "con_kind", "con_n", "con_arg_off", "con_arg")
+    ARRAYS = (("prob_var_off", np.int32), ("prob_con_off", np.int32), ("prob_arg_off", np.int32),
+              ("var_id", np.int32), ("var_ncon", np.uint16), ("con_kn", np.int32), ("con_nargs", np.uint16),
+              ("con_arg", np.int32))
 
     def __init__(self, wire: WireArrays, pinned: bool = True):
+        w = wire.a
+        pvo = w["prob_var_off"]
+        vco, cao = w["var_con_off"], w["con_arg_off"]
+        pco = vco[pvo] if len(vco) else np.zeros(len(pvo), np.int64)
+        pao = cao[pco] if len(cao) else np.zeros(len(pvo), np.int64)
+        n = w["con_n"].astype(np.int64)
+        src = dict(prob_var_off=pvo, prob_con_off=pco, prob_arg_off=pao, var_id=w["var_id"],
+                   var_ncon=np.diff(vco) if len(vco) > 1 else np.zeros(0, np.int64),
+                   con_kn=w["con_kind"].astype(np.int64) | (n << 3),
+                   con_nargs=np.diff(cao) if len(cao) > 1 else np.zeros(0, np.int64),
+                   con_arg=w["con_arg"])
         self._bufs = {}
         self.a = {}
-        for k in self.INT:
-            src = wire.a[k]
-            if len(src) and (src.max() > np.iinfo(np.int32).max or src.min() < np.iinfo(np.int32).min):
-                raise ValueError("dp_wire32: %s does not fit 32 bits" % k)
+        for k, dt in self.ARRAYS:
+            x = np.asarray(src[k])
+            info = np.iinfo(dt)
+            if len(x) and (x.max() > info.max or x.min() < info.min) or (k == "con_kn" and len(n) and (
+                    n.max() >= 1 << 28 or n.min() < -(1 << 28))):
+                raise ValueError("dp_wire32: %s does not fit %d bits" % (k, 8 * np.dtype(dt).itemsize))
             if pinned:
-                b = HostArray(len(src), np.int32)
-                b.a[:] = src
+                b = HostArray(len(x), dt)
+                b.a[:] = x
                 self._bufs[k] = b
                 self.a[k] = b.a
             else:
-                self.a[k] = np.ascontiguousarray(src, np.int32)
-        self.a["str_off"] = wire.a["str_off"]
-        self.a["str_bytes"] = wire.a["str_bytes"]
-        self._pad = np.zeros(1, np.int32)
+                self.a[k] = np.ascontiguousarray(x, dt)
+        self.a["str_off"] = w["str_off"]
+        self.a["str_bytes"] = w["str_bytes"]
+        self._pad32 = np.zeros(1, np.int32)
+        self._pad16 = np.zeros(1, np.uint16)
 
     @property
     def n_problems(self) -> int:
         return len(self.a["prob_var_off"]) - 1
 
     def nbytes(self) -> int:
-        return int(sum(self.a[k].nbytes for k in self.INT))
+        return int(sum(self.a[k].nbytes for k, _ in self.ARRAYS))
 
     def struct(self) -> Wire32:
         a = self.a
         w = Wire32()
         w.n_problems = len(a["prob_var_off"]) - 1
-        for k in self.INT:
-            setattr(w, k, _p(a[k] if len(a[k]) else self._pad, c_i32p))
+        for k, dt in self.ARRAYS:
+            if dt == np.uint16:
+                setattr(w, k, _p(a[k] if len(a[k]) else self._pad16, ctypes.POINTER(ctypes.c_uint16)))
+            else:
+                setattr(w, k, _p(a[k] if len(a[k]) else self._pad32, c_i32p))
         w.n_strs = len(a["str_off"]) - 1
         w.str_off = _p(a["str_off"], c_i64p)
         w.str_bytes = ctypes.cast(a["str_bytes"].ctypes.data, ctypes.c_char_p)

@@ -26,6 +26,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -43,7 +46,7 @@ namespace {
 // the kernel's sizes (a problem past them is lowered on the host)
 constexpr int DL_NV = 512;   // variables (DP_P8_MAX_VARS)
 constexpr int DL_C = 512;    // constraints
-constexpr int DL_A = 2048;   // constraint arguments
+constexpr int DL_A = 1536;   // constraint arguments
 constexpr int DL_VH = 1024;  // identifier hash slots (>= 2 DL_NV)
 constexpr int DL_KH = 1024;  // identity-key slots (>= 2 DL_C)
 // a record's words: header + the largest DP_FMT_P8D body these sizes allow
@@ -79,26 +82,40 @@ __device__ __forceinline__ bool m_list(uint32_t m) { return (m & 8u) != 0; }
 __device__ __forceinline__ int m_kind(uint32_t m) { return (int)((m >> 4) & 15u); }
 __device__ __forceinline__ int m_len(uint32_t m) { return (int)(m >> 8); }
 
+// Arrays live in phases: the identifier table (1) shares its words with the
+// rows (3-4), the key table (2-3) with the record (4), which keeps the
+// working set at 4 workgroups per CU.
 struct DlShared {
-  int32_t vkey[DL_VH];  // string id + 1 (0: empty)
-  int16_t vval[DL_VH];
+  union {
+    struct {
+      int32_t vkey[DL_VH];  // string id + 1 (0: empty)
+      int16_t vval[DL_VH];
+    };
+    struct {
+      int16_t clit[DL_A + DL_C];  // clause literals
+      int16_t kv[DL_A];           // AtMost variables
+    };
+  };
+  union {
+    struct {
+      unsigned long long kkey[DL_KH];  // key + 1 (0: empty)
+      int32_t kfirst[DL_KH], klast[DL_KH];
+    };
+    uint32_t rec[DL_SLOT];
+  };
   int16_t vstart[DL_NV + 2];  // constraints of variable i: [vstart[i], vstart[i+1])
   int16_t cs[DL_C];           // constraint -> subject variable
   int16_t ca[DL_A];           // argument -> variable
   int16_t cslot[DL_C];        // constraint -> key slot (-1: none)
+  int16_t castart[DL_C + 1];  // arguments of constraint c: [castart[c], castart[c+1])
   uint32_t cmeta[DL_C];
   int16_t cid[DL_C];    // identity of a first writer
   int16_t clist[DL_C];  // choice list of a Dependency with candidates
-  unsigned long long kkey[DL_KH];  // key + 1 (0: empty)
-  int32_t kfirst[DL_KH], klast[DL_KH];
-  int16_t clit[DL_A + DL_C];  // clause literals
-  int16_t kv[DL_A];           // AtMost variables
   int16_t kb[DL_C];           // AtMost bounds
   uint8_t clen[DL_C], klen[DL_C], src[DL_C];
   uint32_t mask[DL_C / 32];   // identity is an AtMost row's
   uint32_t aflag[DL_NV / 32];  // variable has a Mandatory constraint
   int16_t av[DL_NV];
-  uint32_t rec[DL_SLOT];
   int32_t fb;  // the host lowers this problem
   int32_t big;  // a bound or row length past the packed forms'
 };
@@ -123,12 +140,14 @@ __device__ __forceinline__ bool fits16_dev(const int32_t* h) {
 }
 
 struct DlArgs {
-  const int32_t *pvo, *vid, *vco, *kind, *cn, *cao, *arg;  // the batch's ranges on the device
+  // the batch's dp_wire32 ranges on the device
+  const int32_t *pvo, *pco, *pao, *vid, *ckn, *arg;
+  const uint16_t *vnc, *cna;
   int32_t pbase, cbase, abase;  // absolute index of each range's first element
   int32_t nvars, ncons, nargs;
   int64_t n_strs;
   int64_t group_above;  // placement.hpp one_wave's bound
-  int32_t P;
+  int32_t p0;           // first problem of this launch
   int32_t* words;  // [P] padded record words, 0: lowered on the host
   int32_t* nid;    // [P]
   int32_t* slots;  // [P * DL_SLOT]
@@ -138,7 +157,7 @@ struct DlArgs {
 
 __global__ void __launch_bounds__(DL_T) lower_kernel(DlArgs a) {
   __shared__ DlShared S;
-  const int p = blockIdx.x;
+  const int p = a.p0 + (int)blockIdx.x;
   const int lane = (int)threadIdx.x;
   auto give_up = [&]() {
     if (lane == 0) {
@@ -149,12 +168,36 @@ __global__ void __launch_bounds__(DL_T) lower_kernel(DlArgs a) {
   const int v0 = a.pvo[p] - a.pbase, v1 = a.pvo[p + 1] - a.pbase;
   const int nv = v1 - v0;
   if (nv <= 0 || nv > DL_NV || v0 < 0 || v1 > a.nvars) return give_up();
-  const int cb = a.vco[v0] - a.cbase, ce = a.vco[v1] - a.cbase;
+  const int cb = a.pco[p] - a.cbase, ce = a.pco[p + 1] - a.cbase;
   const int C = ce - cb;
   if (cb < 0 || C < 0 || ce > a.ncons || C > DL_C) return give_up();
-  const int ab = C ? a.cao[cb] - a.abase : 0, ae = C ? a.cao[ce] - a.abase : 0;
+  const int ab = a.pao[p] - a.abase, ae = a.pao[p + 1] - a.abase;
   const int A = ae - ab;
   if (ab < 0 || A < 0 || ae > a.nargs || A > DL_A) return give_up();
+  // the counts -> offsets within the problem (their sums must be C and A)
+  {
+    int run = 0;
+    for (int i0 = 0; i0 < nv && run <= C; i0 += DL_T) {
+      const int i = i0 + lane;
+      int tot;
+      const int ex = excl_scan(i < nv ? (int)a.vnc[v0 + i] : 0, tot);
+      if (i < nv) S.vstart[i] = (int16_t)min(run + ex, 0x7fff);
+      run += tot;
+    }
+    int arun = 0;
+    for (int c0 = 0; c0 < C && arun <= A; c0 += DL_T) {
+      const int c = c0 + lane;
+      int tot;
+      const int ex = excl_scan(c < C ? (int)a.cna[cb + c] : 0, tot);
+      if (c < C) S.castart[c] = (int16_t)min(arun + ex, 0x7fff);
+      arun += tot;
+    }
+    if (run != C || arun != A) return give_up();  // inconsistent counts: the host reports them
+    if (lane == 0) {
+      S.vstart[nv] = (int16_t)C;
+      S.castart[C] = (int16_t)A;
+    }
+  }
 
   // ---- 0. tables ----
   for (int i = lane; i < DL_VH; i += DL_T) S.vkey[i] = 0;
@@ -174,13 +217,11 @@ __global__ void __launch_bounds__(DL_T) lower_kernel(DlArgs a) {
   // ---- 1. identifiers -> variables (lit_mapping.go:50-57) ----
   for (int i = lane; i < nv; i += DL_T) {
     const int32_t sid = a.vid[v0 + i];
-    const int c0 = a.vco[v0 + i] - a.cbase, c1 = a.vco[v0 + i + 1] - a.cbase;
-    if (sid < 0 || (int64_t)sid >= a.n_strs || c0 < cb || c1 > ce || c1 < c0) {
+    if (sid < 0 || (int64_t)sid >= a.n_strs) {
       S.fb = 1;  // malformed: the host reports it
       continue;
     }
-    S.vstart[i] = (int16_t)(c0 - cb);
-    for (int c = c0; c < c1; ++c) S.cs[c - cb] = (int16_t)i;
+    for (int c = S.vstart[i], c1 = S.vstart[i] + (int)a.vnc[v0 + i]; c < c1; ++c) S.cs[c] = (int16_t)i;
     uint32_t h = ((uint32_t)sid * 2654435761u) >> 22;  // log2(DL_VH) bits
     for (;;) {
       const int32_t old = atomicCAS(&S.vkey[h], 0, sid + 1);
@@ -195,7 +236,6 @@ __global__ void __launch_bounds__(DL_T) lower_kernel(DlArgs a) {
       h = (h + 1) & (DL_VH - 1);
     }
   }
-  if (lane == 0) S.vstart[nv] = (int16_t)C;
   __syncthreads();
   if (S.fb) return give_up();
   // arguments (LitOf, lit_mapping.go:81-88: an unknown one is an error the host reports)
@@ -224,9 +264,10 @@ __global__ void __launch_bounds__(DL_T) lower_kernel(DlArgs a) {
 
   // ---- 2. identity keys (lower.cpp lower_fast's switch) ----
   for (int c = lane; c < C; c += DL_T) {
-    const int kind = a.kind[cb + c];
-    const int n = a.cn[cb + c];
-    const int a0 = a.cao[cb + c] - a.abase - ab, a1 = a.cao[cb + c + 1] - a.abase - ab;
+    const int32_t kn = a.ckn[cb + c];
+    const int kind = kn & 7;
+    const int n = kn >> 3;
+    const int a0 = S.castart[c], a1 = S.castart[c + 1];
     const int ns = a1 - a0;
     const int vi = S.cs[c];
     bool bad = a0 < 0 || a1 > A || ns < 0;
@@ -349,16 +390,16 @@ __global__ void __launch_bounds__(DL_T) lower_kernel(DlArgs a) {
     const int first = s >= 0 ? S.kfirst[s] : -1;
     const bool isf = s >= 0 && first == c;
     const int kind = m_kind(m);
-    const int a0 = act ? a.cao[cb + c] - a.abase - ab : 0;
-    const int ns = act ? a.cao[cb + c + 1] - a.abase - ab - a0 : 0;
+    const int a0 = act ? S.castart[c] : 0;
+    const int ns = act ? S.castart[c + 1] - a0 : 0;
     const int vi = act ? S.cs[c] : 0;
     // an equal hashed key names the same term only for the same subject
     // (Dependency), bound (AtMost) and sequence (lower.cpp same_term)
     bool bad = false;
     if (s >= 0 && !isf && m_hashed(m)) {
-      const int f0 = a.cao[cb + first] - a.abase - ab, fns = a.cao[cb + first + 1] - a.abase - ab - f0;
+      const int f0 = S.castart[first], fns = S.castart[first + 1] - f0;
       bad = fns != ns || (kind == DP_DEPENDENCY && S.cs[first] != vi) ||
-            (kind == DP_ATMOST && a.cn[cb + first] != a.cn[cb + c]) || m_kind(S.cmeta[first]) != kind;
+            (kind == DP_ATMOST && a.ckn[cb + first] != a.ckn[cb + c]) || m_kind(S.cmeta[first]) != kind;
       for (int j = 0; j < ns && !bad; ++j) bad = S.ca[f0 + j] != S.ca[a0 + j];
     }
     if (__ballot(bad)) {
@@ -415,7 +456,7 @@ __global__ void __launch_bounds__(DL_T) lower_kernel(DlArgs a) {
     }
     bool kb1 = true;
     if (isk) {
-      const int n = a.cn[cb + c];
+      const int n = a.ckn[cb + c] >> 3;
       S.klen[krow] = (uint8_t)rlen;
       S.kb[krow] = (int16_t)n;
       kb1 = n == 1;
@@ -554,14 +595,17 @@ __global__ void __launch_bounds__(DL_T) lower_kernel(DlArgs a) {
   }
 }
 
-// Record and identity offsets: one workgroup, a contiguous segment per thread.
+// Record and identity offsets of problems [q0, q1): one workgroup, a
+// contiguous segment per thread, continuing from rec_off[q0] / ident_off[q0]
+// (the previous piece's, on the same stream; 0 for the first).
 constexpr int SCAN_T = 1024;
-__global__ void __launch_bounds__(SCAN_T) scan_kernel(const int32_t* words, const int32_t* nid, int32_t P,
+__global__ void __launch_bounds__(SCAN_T) scan_kernel(const int32_t* words, const int32_t* nid, int32_t q0, int32_t q1,
                                                      int64_t* rec_off, int64_t* ident_off) {
   __shared__ int64_t sw[SCAN_T], si[SCAN_T];
   const int t = (int)threadIdx.x;
-  const int seg = (P + SCAN_T - 1) / SCAN_T;
-  const int b = min(P, t * seg), e = min(P, b + seg);
+  const int n = q1 - q0;
+  const int seg = (n + SCAN_T - 1) / SCAN_T;
+  const int b = q0 + min(n, t * seg), e = min(q1, b + seg);
   int64_t w = 0, d = 0;
   for (int i = b; i < e; ++i) {
     w += words[i];
@@ -577,9 +621,11 @@ __global__ void __launch_bounds__(SCAN_T) scan_kernel(const int32_t* words, cons
     si[t] += xd;
     __syncthreads();
   }
-  w = sw[t] - w;
-  d = si[t] - d;
-  if (t == 0) {
+  const int64_t w0 = q0 ? rec_off[q0] : 0, d0 = q0 ? ident_off[q0] : 0;
+  w = w0 + sw[t] - w;
+  d = d0 + si[t] - d;
+  __syncthreads();  // (every thread read the bases before any writes)
+  if (t == 0 && q0 == 0) {
     rec_off[0] = 0;
     ident_off[0] = 0;
   }
@@ -591,12 +637,14 @@ __global__ void __launch_bounds__(SCAN_T) scan_kernel(const int32_t* words, cons
   }
 }
 
-// The slots packed into the batch (records 16-byte aligned, as every offset is).
-__global__ void __launch_bounds__(DL_T) pack_kernel(const int32_t* words, const int32_t* nid, const int32_t* slots,
-                                                    const int32_t* ivs, const int32_t* ics, const int64_t* rec_off,
-                                                    const int64_t* ident_off, int32_t* rec, int32_t* ivar,
-                                                    int32_t* icon) {
-  const int p = blockIdx.x, lane = (int)threadIdx.x;
+// The slots of problems p0.. packed into the batch (records 16-byte aligned,
+// as every offset is): device memory, or the caller's page-locked host
+// memory through its device mapping (the copy back is the kernel's writes).
+__global__ void __launch_bounds__(DL_T) pack_kernel(int32_t p0, const int32_t* words, const int32_t* nid,
+                                                    const int32_t* slots, const int32_t* ivs, const int32_t* ics,
+                                                    const int64_t* rec_off, const int64_t* ident_off, int32_t* rec,
+                                                    int32_t* ivar, int32_t* icon) {
+  const int p = p0 + (int)blockIdx.x, lane = (int)threadIdx.x;
   const int w4 = words[p] >> 2;
   const int4* s = reinterpret_cast<const int4*>(slots + (int64_t)p * DL_SLOT);
   int4* d = reinterpret_cast<int4*>(rec + rec_off[p]);
@@ -632,8 +680,13 @@ struct DevBuf {
 
 struct dp_dlower {
   int dev = 0;
-  hipStream_t st = nullptr;
-  DevBuf<int32_t> pvo, vid, vco, kind, cn, cao, arg, words, nid, slots, ivs, ics, rec, ivar, icon;
+  hipStream_t st = nullptr;   // kernels and the copies back
+  hipStream_t cst = nullptr;  // the wire's copies to the device
+  hipStream_t pst = nullptr;  // the packing (its writes to host memory run under the next piece's lowering)
+  static constexpr int kMaxPieces = 8;
+  hipEvent_t ev[kMaxPieces] = {}, es[kMaxPieces] = {};
+  DevBuf<int32_t> pvo, pco, pao, vid, ckn, arg, words, nid, slots, ivs, ics, rec, ivar, icon;
+  DevBuf<uint16_t> vnc, cna;
   DevBuf<int64_t> ro, io;
   int64_t* h_off = nullptr;  // page-locked: rec_off then ident_off
   size_t h_cap = 0;
@@ -645,7 +698,13 @@ struct dp_dlower {
   std::mutex mu;  // one call at a time
   ~dp_dlower() {
     if (h_off) dp::pinned_free(h_off);
+    for (auto e : ev)
+      if (e) (void)hipEventDestroy(e);
+    for (auto e : es)
+      if (e) (void)hipEventDestroy(e);
+    if (pst) (void)hipStreamDestroy(pst);
     if (st) (void)hipStreamDestroy(st);
+    if (cst) (void)hipStreamDestroy(cst);
   }
 };
 
@@ -660,7 +719,9 @@ std::string hip_err(const char* what, hipError_t e) { return std::string("dp_low
     }                                                \
   } while (0)
 
-// Problem range [p0, p1) of w as int64 arrays of their own (rebased).
+// The problems d->which of w as a dp_wire of their own (64-bit, offsets
+// from 0).  Inconsistent counts stay malformed (a negative identifier), so
+// the host lowering reports the batch as dp_lower_into does.
 void host_subwire(dp_dlower* d, const dp_wire32* w, dp_wire* sub) {
   d->s_pvo.assign(1, 0);
   d->s_vid.clear();
@@ -672,21 +733,32 @@ void host_subwire(dp_dlower* d, const dp_wire32* w, dp_wire* sub) {
   int64_t nc = 0, na = 0;
   for (const int32_t p : d->which) {
     const int32_t v0 = w->prob_var_off[p], v1 = w->prob_var_off[p + 1];
+    int64_t c = w->prob_con_off[p], x = w->prob_arg_off[p];
+    const int64_t ce = w->prob_con_off[p + 1], xe = w->prob_arg_off[p + 1];
+    // the counts must add up to the problem's ranges
+    int64_t sc = 0, sx = 0;
+    for (int32_t v = v0; v < v1; ++v) sc += w->var_ncon[v];
+    bool bad = sc != ce - c;
+    if (!bad)
+      for (int64_t k = c; k < ce; ++k) sx += w->con_nargs[k];
+    bad = bad || sx != xe - x;
     for (int32_t v = v0; v < v1; ++v) {
       d->s_vid.push_back(w->var_id[v]);
-      const int32_t c0 = w->var_con_off[v], c1 = w->var_con_off[v + 1];
       d->s_vco.push_back(nc);
-      for (int32_t c = c0; c < std::max(c0, c1); ++c) {
-        d->s_kind.push_back(w->con_kind[c]);
-        d->s_cn.push_back(w->con_n[c]);
+      for (int32_t k = 0; k < (int32_t)w->var_ncon[v] && !bad; ++k, ++c) {
+        const int32_t kn = w->con_kn[c];
+        d->s_kind.push_back(kn & 7);
+        d->s_cn.push_back(kn >> 3);
         d->s_cao.push_back(na);
-        const int32_t a0 = w->con_arg_off[c], a1 = w->con_arg_off[c + 1];
-        for (int32_t x = a0; x < std::max(a0, a1); ++x) d->s_arg.push_back(w->con_arg[x]);
-        na += std::max(0, a1 - a0);
-        if (a1 < a0) d->s_arg.push_back(-1);  // stays malformed (a negative id)
+        for (int32_t j = 0; j < (int32_t)w->con_nargs[c]; ++j, ++x, ++na) d->s_arg.push_back(w->con_arg[x]);
+        ++nc;
       }
-      nc += std::max(0, c1 - c0);
-      if (c1 < c0) d->s_vid.back() = -1;  // stays malformed
+    }
+    if (bad && d->s_vid.size() > (size_t)d->s_pvo.back()) {
+      d->s_vid.back() = -1;
+    } else if (bad) {  // no variable to mark: one malformed variable
+      d->s_vid.push_back(-1);
+      d->s_vco.push_back(nc);
     }
     d->s_pvo.push_back((int64_t)d->s_vid.size());
   }
@@ -719,6 +791,25 @@ int lower_on_host(const dp_wire32* w, int32_t flags, dp_lowered* lw, dp_dlower* 
   d->host_count = w->n_problems;
   return dp_lower_into(&sub, flags, lw);
 }
+
+double dl_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+// DEPPY_DL_TIMES=1 (diagnostic): each call's phases on stderr
+bool dl_times() {
+  static const bool on = [] {
+    const char* e = std::getenv("DEPPY_DL_TIMES");
+    return e && *e && *e != '0';
+  }();
+  return on;
+}
+
+bool monotone(const int32_t* o, int32_t P) {
+  if (!o || o[0] < 0) return false;
+  for (int32_t p = 0; p < P; ++p)
+    if (o[p + 1] < o[p]) return false;
+  return true;
+}
 }  // namespace
 
 extern "C" {
@@ -731,7 +822,12 @@ dp_dlower* dp_dlower_new(dp_ctx* ctx) {
   }
   auto* d = new dp_dlower;
   d->dev = dev;
-  if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking) != hipSuccess) {
+  bool ok = hipSetDevice(dev) == hipSuccess && hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking) == hipSuccess &&
+            hipStreamCreateWithFlags(&d->cst, hipStreamNonBlocking) == hipSuccess &&
+            hipStreamCreateWithFlags(&d->pst, hipStreamNonBlocking) == hipSuccess;
+  for (auto& e : d->ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+  for (auto& e : d->es) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
     dp::set_global_error("dp_dlower_new: stream creation failed");
     delete d;
     return nullptr;
@@ -743,45 +839,32 @@ void dp_dlower_free(dp_dlower* d) { delete d; }
 int64_t dp_dlower_host_count(const dp_dlower* d) { return d ? d->host_count : 0; }
 
 int dp_lower_device(dp_dlower* d, const dp_wire32* w, int32_t flags, dp_lowered* lw) {
-  if (!d || !lw || !w || w->n_problems < 0 || !w->prob_var_off) {
-    dp::set_global_error("dp_lower_device: malformed wire batch");
+  if (!d || !lw || !w || w->n_problems < 0 || !monotone(w->prob_var_off, w->n_problems) ||
+      !monotone(w->prob_con_off, w->n_problems) || !monotone(w->prob_arg_off, w->n_problems)) {
+    dp::set_global_error("dp_lower: malformed wire batch");
     return -1;
   }
   std::lock_guard<std::mutex> lk(d->mu);
+  const double t0 = dl_ms();
   const int32_t P = w->n_problems;
-  for (int32_t p = 0; p < P; ++p)
-    if (w->prob_var_off[p + 1] < w->prob_var_off[p] || w->prob_var_off[p] < 0) {
-      dp::set_global_error("dp_lower: malformed wire batch");
-      return -1;
-    }
   const bool ours = (flags & (DP_LOWER_NARROW | DP_LOWER_PACKED)) == (DP_LOWER_NARROW | DP_LOWER_PACKED) &&
                     !(flags & DP_LOWER_NO_P8) && dp::ldsg_env() != dp::LDSG_ALWAYS && P > 0;
   if (!ours) return lower_on_host(w, flags, lw, d);
-  const int32_t pv0 = w->prob_var_off[0], pvN = w->prob_var_off[P];
-  const int32_t nvars = pvN - pv0;
-  if (nvars > 0 && (!w->var_id || !w->var_con_off)) {
-    dp::set_global_error("dp_lower: malformed wire batch");
-    return -1;
-  }
-  const int32_t cb0 = nvars ? w->var_con_off[pv0] : 0, ceN = nvars ? w->var_con_off[pvN] : cb0;
-  const int32_t ncons = std::max(0, ceN - cb0);
-  if (ncons > 0 && (!w->con_kind || !w->con_n || !w->con_arg_off || cb0 < 0)) {
-    dp::set_global_error("dp_lower: malformed wire batch");
-    return -1;
-  }
-  const int32_t ab0 = ncons ? w->con_arg_off[cb0] : 0, aeN = ncons ? w->con_arg_off[ceN] : ab0;
-  const int32_t nargs = std::max(0, aeN - ab0);
-  if (nargs > 0 && (!w->con_arg || ab0 < 0)) {
+  const int32_t pv0 = w->prob_var_off[0], cb0 = w->prob_con_off[0], ab0 = w->prob_arg_off[0];
+  const int32_t nvars = w->prob_var_off[P] - pv0, ncons = w->prob_con_off[P] - cb0, nargs = w->prob_arg_off[P] - ab0;
+  if ((nvars > 0 && (!w->var_id || !w->var_ncon)) || (ncons > 0 && (!w->con_kn || !w->con_nargs)) ||
+      (nargs > 0 && !w->con_arg)) {
     dp::set_global_error("dp_lower: malformed wire batch");
     return -1;
   }
   DL_OK(hipSetDevice(d->dev));
   DL_OK(d->pvo.need((size_t)P + 1));
+  DL_OK(d->pco.need((size_t)P + 1));
+  DL_OK(d->pao.need((size_t)P + 1));
   DL_OK(d->vid.need((size_t)nvars + 1));
-  DL_OK(d->vco.need((size_t)nvars + 1));
-  DL_OK(d->kind.need((size_t)ncons + 1));
-  DL_OK(d->cn.need((size_t)ncons + 1));
-  DL_OK(d->cao.need((size_t)ncons + 1));
+  DL_OK(d->vnc.need((size_t)nvars + 1));
+  DL_OK(d->ckn.need((size_t)ncons + 1));
+  DL_OK(d->cna.need((size_t)ncons + 1));
   DL_OK(d->arg.need((size_t)nargs + 1));
   DL_OK(d->words.need((size_t)P));
   DL_OK(d->nid.need((size_t)P));
@@ -800,28 +883,21 @@ int dp_lower_device(dp_dlower* d, const dp_wire32* w, int32_t flags, dp_lowered*
       return -1;
     }
   }
-  hipStream_t st = d->st;
-  auto h2d = [&](int32_t* dst, const int32_t* src, size_t n) {
-    return n ? hipMemcpyAsync(dst, src, n * sizeof(int32_t), hipMemcpyHostToDevice, st) : hipSuccess;
+  hipStream_t st = d->st, cst = d->cst;
+  auto h2d = [&](auto* dst, const auto* src, int64_t n) {
+    return n > 0 ? hipMemcpyAsync(dst, src, (size_t)n * sizeof(*src), hipMemcpyHostToDevice, cst) : hipSuccess;
   };
-  DL_OK(h2d(d->pvo.p, w->prob_var_off, (size_t)P + 1));
-  if (nvars) {
-    DL_OK(h2d(d->vid.p, w->var_id + pv0, (size_t)nvars));
-    DL_OK(h2d(d->vco.p, w->var_con_off + pv0, (size_t)nvars + 1));
-  }
-  if (ncons) {
-    DL_OK(h2d(d->kind.p, w->con_kind + cb0, (size_t)ncons));
-    DL_OK(h2d(d->cn.p, w->con_n + cb0, (size_t)ncons));
-    DL_OK(h2d(d->cao.p, w->con_arg_off + cb0, (size_t)ncons + 1));
-  }
-  if (nargs) DL_OK(h2d(d->arg.p, w->con_arg + ab0, (size_t)nargs));
+  DL_OK(h2d(d->pvo.p, w->prob_var_off, (int64_t)P + 1));
+  DL_OK(h2d(d->pco.p, w->prob_con_off, (int64_t)P + 1));
+  DL_OK(h2d(d->pao.p, w->prob_arg_off, (int64_t)P + 1));
   DlArgs a{};
   a.pvo = d->pvo.p;
+  a.pco = d->pco.p;
+  a.pao = d->pao.p;
   a.vid = d->vid.p;
-  a.vco = d->vco.p;
-  a.kind = d->kind.p;
-  a.cn = d->cn.p;
-  a.cao = d->cao.p;
+  a.vnc = d->vnc.p;
+  a.ckn = d->ckn.p;
+  a.cna = d->cna.p;
   a.arg = d->arg.p;
   a.pbase = pv0;
   a.cbase = cb0;
@@ -831,49 +907,103 @@ int dp_lower_device(dp_dlower* d, const dp_wire32* w, int32_t flags, dp_lowered*
   a.nargs = nargs;
   a.n_strs = w->n_strs;
   a.group_above = dp::group_above();
-  a.P = P;
   a.words = d->words.p;
   a.nid = d->nid.p;
   a.slots = d->slots.p;
   a.ivs = d->ivs.p;
   a.ics = d->ics.p;
-  hipLaunchKernelGGL(lower_kernel, dim3((unsigned)P), dim3(DL_T), 0, st, a);
-  DL_OK(hipGetLastError());
-  hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(SCAN_T), 0, st, d->words.p, d->nid.p, P, d->ro.p, d->io.p);
-  DL_OK(hipGetLastError());
+  // Every size bounded from the batch's totals (a record's words: at most
+  // 23 + (2 (args + constraints) + 2 variables + 4 constraints) / 4, an
+  // identity per constraint), so the result is sized before the kernels run
+  // and each piece is packed straight into place.
+  const int64_t bound_words = 24 * (int64_t)P + (2 * ((int64_t)nargs + ncons) + 2 * (int64_t)nvars + 4 * (int64_t)ncons) / 4;
+  const dp::LoweredOut O = dp::lowered_prepare(lw, P, bound_words, (int64_t)ncons + 1, (flags & DP_LOWER_PINNED) != 0);
+  // page-locked results are written by the pack kernel through their device
+  // mapping; otherwise into device buffers and copied back
+  int32_t *trec = nullptr, *tivar = nullptr, *ticon = nullptr;
+  if (flags & DP_LOWER_PINNED) {
+    void *r = nullptr, *iv = nullptr, *ic = nullptr;
+    if (hipHostGetDevicePointer(&r, O.rec, 0) == hipSuccess && hipHostGetDevicePointer(&iv, O.ivar, 0) == hipSuccess &&
+        hipHostGetDevicePointer(&ic, O.icon, 0) == hipSuccess) {
+      trec = static_cast<int32_t*>(r);
+      tivar = static_cast<int32_t*>(iv);
+      ticon = static_cast<int32_t*>(ic);
+    }
+    (void)hipGetLastError();
+  }
+  const bool mapped = trec != nullptr;
+  if (!mapped) {
+    DL_OK(d->rec.need((size_t)bound_words + 4));
+    DL_OK(d->ivar.need((size_t)ncons + 1));
+    DL_OK(d->icon.need((size_t)ncons + 1));
+    trec = d->rec.p;
+    tivar = d->ivar.p;
+    ticon = d->icon.p;
+  }
+  // pieces: the wire's copy of piece k+1 runs under the lowering and packing
+  // of piece k
+  const int pieces = (int)std::min<int64_t>(dp_dlower::kMaxPieces, std::max<int64_t>(1, P / 2048));
+  for (int k = 0; k < pieces; ++k) {
+    const int32_t q0 = (int32_t)((int64_t)P * k / pieces), q1 = (int32_t)((int64_t)P * (k + 1) / pieces);
+    const int32_t v0 = w->prob_var_off[q0], v1 = w->prob_var_off[q1];
+    const int32_t c0 = w->prob_con_off[q0], c1 = w->prob_con_off[q1];
+    const int32_t x0 = w->prob_arg_off[q0], x1 = w->prob_arg_off[q1];
+    DL_OK(h2d(d->vid.p + (v0 - pv0), w->var_id + v0, v1 - v0));
+    DL_OK(h2d(d->vnc.p + (v0 - pv0), w->var_ncon + v0, v1 - v0));
+    DL_OK(h2d(d->ckn.p + (c0 - cb0), w->con_kn + c0, c1 - c0));
+    DL_OK(h2d(d->cna.p + (c0 - cb0), w->con_nargs + c0, c1 - c0));
+    DL_OK(h2d(d->arg.p + (x0 - ab0), w->con_arg + x0, x1 - x0));
+    DL_OK(hipEventRecord(d->ev[k], cst));
+    DL_OK(hipStreamWaitEvent(st, d->ev[k], 0));
+    if (q1 == q0) continue;
+    a.p0 = q0;
+    hipLaunchKernelGGL(lower_kernel, dim3((unsigned)(q1 - q0)), dim3(DL_T), 0, st, a);
+    DL_OK(hipGetLastError());
+    hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(SCAN_T), 0, st, d->words.p, d->nid.p, q0, q1, d->ro.p, d->io.p);
+    DL_OK(hipGetLastError());
+    DL_OK(hipEventRecord(d->es[k], st));
+    DL_OK(hipStreamWaitEvent(d->pst, d->es[k], 0));
+    hipLaunchKernelGGL(pack_kernel, dim3((unsigned)(q1 - q0)), dim3(DL_T), 0, d->pst, q0, d->words.p, d->nid.p,
+                       d->slots.p, d->ivs.p, d->ics.p, d->ro.p, d->io.p, trec, tivar, ticon);
+    DL_OK(hipGetLastError());
+  }
   int64_t* h_ro = d->h_off;
   int64_t* h_io = d->h_off + P + 1;
   DL_OK(hipMemcpyAsync(h_ro, d->ro.p, ((size_t)P + 1) * sizeof(int64_t), hipMemcpyDeviceToHost, st));
   DL_OK(hipMemcpyAsync(h_io, d->io.p, ((size_t)P + 1) * sizeof(int64_t), hipMemcpyDeviceToHost, st));
   DL_OK(hipStreamSynchronize(st));
+  const double t_dev = dl_ms();
   const int64_t rw = h_ro[P], ni = h_io[P];
-  DL_OK(d->rec.need((size_t)rw + 4));
-  DL_OK(d->ivar.need((size_t)ni + 1));
-  DL_OK(d->icon.need((size_t)ni + 1));
-  hipLaunchKernelGGL(pack_kernel, dim3((unsigned)P), dim3(DL_T), 0, st, d->words.p, d->nid.p, d->slots.p, d->ivs.p,
-                     d->ics.p, d->ro.p, d->io.p, d->rec.p, d->ivar.p, d->icon.p);
-  DL_OK(hipGetLastError());
-  const dp::LoweredOut O = dp::lowered_prepare(lw, P, rw, ni, (flags & DP_LOWER_PINNED) != 0);
   std::memcpy(O.rec_off, h_ro, ((size_t)P + 1) * sizeof(int64_t));
   std::memcpy(O.ident_off, h_io, ((size_t)P + 1) * sizeof(int64_t));
-  if (rw) DL_OK(hipMemcpyAsync(O.rec, d->rec.p, (size_t)rw * sizeof(int32_t), hipMemcpyDeviceToHost, st));
-  if (ni) {
-    DL_OK(hipMemcpyAsync(O.ivar, d->ivar.p, (size_t)ni * sizeof(int32_t), hipMemcpyDeviceToHost, st));
-    DL_OK(hipMemcpyAsync(O.icon, d->icon.p, (size_t)ni * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+  if (!mapped) {  // (after the packs, on their stream)
+    if (rw) DL_OK(hipMemcpyAsync(O.rec, d->rec.p, (size_t)rw * sizeof(int32_t), hipMemcpyDeviceToHost, d->pst));
+    if (ni) {
+      DL_OK(hipMemcpyAsync(O.ivar, d->ivar.p, (size_t)ni * sizeof(int32_t), hipMemcpyDeviceToHost, d->pst));
+      DL_OK(hipMemcpyAsync(O.icon, d->icon.p, (size_t)ni * sizeof(int32_t), hipMemcpyDeviceToHost, d->pst));
+    }
   }
   // the problems the kernel left to the host, found while the copies run
   d->which.clear();
   for (int32_t p = 0; p < P; ++p)
     if (h_ro[p + 1] == h_ro[p]) d->which.push_back(p);
   d->host_count = (int64_t)d->which.size();
-  DL_OK(hipStreamSynchronize(st));
-  if (d->which.empty()) return 0;
+  DL_OK(hipStreamSynchronize(d->pst));
+  const double t_pack = dl_ms();
+  if (d->which.empty()) {
+    if (dl_times()) std::fprintf(stderr, "dp_lower_device: P %d device %.3f pack %.3f ms\n", P, t_dev - t0, t_pack - t0);
+    return 0;
+  }
   dp_wire sub{};
   host_subwire(d, w, &sub);
+  const double t_sub = dl_ms();
   if (dp::lowered_splice(lw, &sub, flags, d->which.data(), (int32_t)d->which.size()) != 0) {
     dp::set_global_error("dp_lower: malformed wire batch");
     return -1;
   }
+  if (dl_times())
+    std::fprintf(stderr, "dp_lower_device: P %d device %.3f pack %.3f sub-wire %.3f splice %.3f ms (%d on the host)\n", P,
+                 t_dev - t0, t_pack - t0, t_sub - t_pack, dl_ms() - t_sub, (int)d->which.size());
   return 0;
 }
 

@@ -369,20 +369,27 @@ int32_t dp_lowered_errors(const dp_lowered* lw, int32_t* err);
 /* ------------------------------------------------------------------------ */
 /* Lowering on the device: compact wire -> records                          */
 /* ------------------------------------------------------------------------ */
-/* dp_wire with 32-bit arrays, always interned (equal string index <=> equal
- * identifier): half the bytes of dp_wire to cross PCIe.  Offsets are
- * absolute, as dp_wire's; the string table is read only for error texts. */
+/* The compact wire: dp_wire's content in about 45% of its bytes, the form
+ * that crosses PCIe to the device lowering.  Always interned (equal string
+ * index <=> equal identifier).  Per problem, absolute offsets of its first
+ * variable, constraint and argument; per variable and per constraint a
+ * 16-bit count instead of an offset; a constraint's kind and AtMost bound in
+ * one word.  Problem p's constraints are the counts of its variables in
+ * order (their sum is prob_con_off[p+1] - prob_con_off[p]), and likewise its
+ * arguments.  The string table is read only for error texts. */
 typedef struct dp_wire32 {
   int32_t n_problems;
-  const int32_t* prob_var_off; /* [n_problems+1] -> variables          */
-  const int32_t* var_id;       /* [n_vars]   string index of Identifier  */
-  const int32_t* var_con_off;  /* [n_vars+1] -> constraints             */
-  const int32_t* con_kind;     /* [n_cons]   enum dp_kind               */
-  const int32_t* con_n;        /* [n_cons]   AtMost bound               */
-  const int32_t* con_arg_off;  /* [n_cons+1] -> con_arg                  */
-  const int32_t* con_arg;      /* [n_args]   string index               */
+  const int32_t* prob_var_off;  /* [n_problems+1] -> variables            */
+  const int32_t* prob_con_off;  /* [n_problems+1] -> constraints          */
+  const int32_t* prob_arg_off;  /* [n_problems+1] -> arguments            */
+  const int32_t* var_id;        /* [n_vars]  string index of Identifier    */
+  const uint16_t* var_ncon;     /* [n_vars]  constraints of the variable   */
+  const int32_t* con_kn;        /* [n_cons]  enum dp_kind | bound << 3 (the
+                                   AtMost bound, arithmetic shift)        */
+  const uint16_t* con_nargs;    /* [n_cons]  arguments of the constraint   */
+  const int32_t* con_arg;       /* [n_args]  string index                  */
   int64_t n_strs;
-  const int64_t* str_off;      /* [n_strs+1] -> str_bytes (error texts)  */
+  const int64_t* str_off;       /* [n_strs+1] -> str_bytes (error texts)   */
   const char* str_bytes;
 } dp_wire32;
 

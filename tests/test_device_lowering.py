@@ -31,20 +31,31 @@ def assert_same(dev, host):
 
 
 def test_wire32_arrays_without_device():
-    """The 32-bit wire keeps every index of the 64-bit one (numpy memory when
+    """The compact wire holds the 64-bit wire's content (numpy memory when
     no device gives page-locked memory) and refuses what does not fit."""
     w = wire_of(2, 30, 5)
     w32 = _lib.Wire32Arrays(w)
-    for k in _lib.Wire32Arrays.INT:
-        np.testing.assert_array_equal(w32.a[k], w.a[k])
-        assert w32.a[k].dtype == np.int32
+    a, b = w32.a, w.a
+    np.testing.assert_array_equal(a["prob_var_off"], b["prob_var_off"])
+    np.testing.assert_array_equal(a["prob_con_off"], b["var_con_off"][b["prob_var_off"]])
+    np.testing.assert_array_equal(a["prob_arg_off"], b["con_arg_off"][a["prob_con_off"]])
+    np.testing.assert_array_equal(a["var_id"], b["var_id"])
+    np.testing.assert_array_equal(np.concatenate([[0], np.cumsum(a["var_ncon"])]), b["var_con_off"])
+    np.testing.assert_array_equal(np.concatenate([[0], np.cumsum(a["con_nargs"])]), b["con_arg_off"])
+    np.testing.assert_array_equal(a["con_kn"] & 7, b["con_kind"])
+    np.testing.assert_array_equal(a["con_kn"] >> 3, b["con_n"])
+    np.testing.assert_array_equal(a["con_arg"], b["con_arg"])
+    assert w32.nbytes() < 0.5 * sum(b[k].nbytes for k in ("prob_var_off", "var_id", "var_con_off", "con_kind",
+                                                           "con_n", "con_arg_off", "con_arg"))
     s = w32.struct()
-    assert s.n_problems == 30 and s.n_strs == len(w.a["str_off"]) - 1
-    big = _lib.WireArrays(**{k: v.copy() for k, v in w.a.items() if k != "str_bytes"},
-                          str_bytes=w.a["str_bytes"][:-1].tobytes())
+    assert s.n_problems == 30 and s.n_strs == len(b["str_off"]) - 1
+    big = _lib.WireArrays(**{k: v.copy() for k, v in b.items() if k != "str_bytes"},
+                          str_bytes=b["str_bytes"][:-1].tobytes())
     big.a["con_arg"][0] = 1 << 40
     with pytest.raises(ValueError, match="32 bits"):
         _lib.Wire32Arrays(big)
+    e = _lib.Lowered.empty()
+    assert e.n == 0 and list(e.rec_off) == [0] and e._flags == 1 | 2 | 4
 
 
 @pytest.fixture(scope="module")

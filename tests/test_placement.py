@@ -184,3 +184,38 @@ def test_plan_order_mixed_launches():
         assert len(kinds) == 1, kinds
         if kinds == {LDS}:
             assert seg == _expected_lds_order(lw.rec_off, lw.rec, sorted(seg), first_rel=0), (a, b)
+
+
+@pytest.mark.gpu
+def test_ldsg_rule_counts_the_device_load():
+    """M_LDSG holds a whole CU's LDS per catalog, so the pipeline puts
+    mid-size catalogs there only while the device's M_LDSG problems in flight
+    (every lane's chunk, not the new chunk's alone) stay within
+    kLdsgMaxProblems (runtime.cpp start_chunk).  A batch of
+    120 such catalogs alone goes to M_LDSG; 16 of them submitted at once
+    mostly do not, and every result equals the one-job result."""
+    ldsg = _lib.PLACES.index("ldsg")
+    lw = lowered_config(5, 1500, 21)
+    pl = _lib.plan_placements(lw.rec_off, lw.rec)
+    pf = _lib.plan_placements(lw.rec_off, lw.rec, _lib.OPT_FORCE_LDSG)
+    mid = [p for p in range(lw.n) if pl[p] != LDS and pf[p] == ldsg][:120]
+    assert len(mid) == 120
+    recs = [lw.rec[lw.rec_off[p]:lw.rec_off[p + 1]] for p in mid]
+    rec = np.concatenate(recs).astype(np.int32)
+    rec_off = np.concatenate([[0], np.cumsum([len(r) for r in recs])]).astype(np.int64)
+    assert (_lib.plan_placements(rec_off, rec) == ldsg).all()
+    ctx = _lib.Context(0, 1)
+    try:
+        ctx.stats(reset=True)
+        one = ctx.submit(rec_off, rec).wait()
+        assert ctx.stats(reset=True)["placed"]["ldsg"] == 120
+        jobs = [ctx.submit(rec_off, rec) for _ in range(16)]
+        outs = [j.wait() for j in jobs]
+        st = ctx.stats(reset=True)["placed"]
+        assert st["ldsg"] + st["split4"] == 16 * 120, st
+        assert st["ldsg"] <= 8 * 120, st
+        for o in outs:
+            for k in ("status", "flags", "installed", "core_len", "core", "steps"):
+                np.testing.assert_array_equal(o[k], one[k])
+    finally:
+        ctx.close()
