@@ -129,6 +129,8 @@ class Wire32(ctypes.Structure):
         ("con_kn", c_i32p),
         ("con_nargs", ctypes.POINTER(ctypes.c_uint16)),
         ("con_arg", c_i32p),
+        ("var_id16", ctypes.POINTER(ctypes.c_uint16)),
+        ("con_arg16", ctypes.POINTER(ctypes.c_uint16)),
         ("n_strs", ctypes.c_int64),
         ("str_off", c_i64p),
         ("str_bytes", ctypes.c_char_p),
@@ -491,14 +493,15 @@ class Wire32Arrays:
     """A dp_wire32 (include/deppy_hip.h), the compact wire: per problem the
     absolute offsets of its variables, constraints and arguments, per
     variable and constraint a 16-bit count, a constraint's kind and bound in
-    one word.  In page-locked memory when a device is present, so
+    one word; with at most 65,536 strings (and ids16) the string indices in
+    16 bits.  In page-locked memory when a device is present, so
     dp_lower_device's copy to the device runs by DMA from where it lies."""
 
     ARRAYS = (("prob_var_off", np.int32), ("prob_con_off", np.int32), ("prob_arg_off", np.int32),
               ("var_id", np.int32), ("var_ncon", np.uint16), ("con_kn", np.int32), ("con_nargs", np.uint16),
               ("con_arg", np.int32))
 
-    def __init__(self, wire: WireArrays, pinned: bool = True):
+    def __init__(self, wire: WireArrays, pinned: bool = True, ids16: bool = True):
         w = wire.a
         pvo = w["prob_var_off"]
         vco, cao = w["var_con_off"], w["con_arg_off"]
@@ -510,9 +513,12 @@ class Wire32Arrays:
                    con_kn=w["con_kind"].astype(np.int64) | (n << 3),
                    con_nargs=np.diff(cao) if len(cao) > 1 else np.zeros(0, np.int64),
                    con_arg=w["con_arg"])
+        self.ids16 = ids16 and len(w["str_off"]) - 1 <= 65536
+        if self.ids16:
+            src["var_id16"], src["con_arg16"] = src.pop("var_id"), src.pop("con_arg")
         self._bufs = {}
         self.a = {}
-        for k, dt in self.ARRAYS:
+        for k, dt in self.arrays():
             x = np.asarray(src[k])
             info = np.iinfo(dt)
             if len(x) and (x.max() > info.max or x.min() < info.min) or (k == "con_kn" and len(n) and (
@@ -530,18 +536,24 @@ class Wire32Arrays:
         self._pad32 = np.zeros(1, np.int32)
         self._pad16 = np.zeros(1, np.uint16)
 
+    def arrays(self):
+        if not self.ids16:
+            return self.ARRAYS
+        wide = {"var_id": "var_id16", "con_arg": "con_arg16"}
+        return tuple((wide[k], np.uint16) if k in wide else (k, dt) for k, dt in self.ARRAYS)
+
     @property
     def n_problems(self) -> int:
         return len(self.a["prob_var_off"]) - 1
 
     def nbytes(self) -> int:
-        return int(sum(self.a[k].nbytes for k, _ in self.ARRAYS))
+        return int(sum(self.a[k].nbytes for k, _ in self.arrays()))
 
     def struct(self) -> Wire32:
         a = self.a
         w = Wire32()
         w.n_problems = len(a["prob_var_off"]) - 1
-        for k, dt in self.ARRAYS:
+        for k, dt in self.arrays():
             if dt == np.uint16:
                 setattr(w, k, _p(a[k] if len(a[k]) else self._pad16, ctypes.POINTER(ctypes.c_uint16)))
             else:

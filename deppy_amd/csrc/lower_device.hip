@@ -49,12 +49,10 @@ constexpr int DL_C = 512;    // constraints
 constexpr int DL_A = 1536;   // constraint arguments
 constexpr int DL_VH = 1024;  // identifier hash slots (>= 2 DL_NV)
 constexpr int DL_KH = 1024;  // identity-key slots (>= 2 DL_C)
-// a record's words: header + the largest DP_FMT_P8D body these sizes allow
-// (literals and AtMost positions <= DL_A + DL_C, their planes, anchors,
-// bounds, lengths, sources, mask), padded to 16 bytes
-constexpr int DL_BODY_MAX = (DL_A + DL_C) + DL_NV + DL_C + 3 * ((DL_A + DL_C) / 8) + DL_NV / 8 + DL_C + DL_C / 8 +
-                            DL_C + DL_C / 8 + 16;
-constexpr int DL_SLOT = (DP_H_SIZE + (DL_BODY_MAX + 3) / 4 + 3) & ~3;
+// a record's words at most: the LDS words the key table leaves to the record
+// (the largest DP_FMT_P8D body these sizes allow is ~4.6 KB; a DP_FMT_P16
+// record past 16 KB goes to the host)
+constexpr int DL_SLOT = (DL_KH * 16) / 4;
 constexpr int DL_T = 64;  // one wavefront per problem
 
 // canonical keys, as lower.cpp's
@@ -116,8 +114,10 @@ struct DlShared {
   uint32_t mask[DL_C / 32];   // identity is an AtMost row's
   uint32_t aflag[DL_NV / 32];  // variable has a Mandatory constraint
   int16_t av[DL_NV];
+  uint8_t vcl[DL_NV];  // choice lists per variable (DP_FMT_P16)
   int32_t fb;  // the host lowers this problem
   int32_t big;  // a bound or row length past the packed forms'
+  int32_t p16;  // the rows do not imply the choice lists: DP_FMT_P16
 };
 
 __device__ __forceinline__ uint64_t lt_mask() { return (1ull << __lane_id()) - 1ull; }
@@ -142,7 +142,8 @@ __device__ __forceinline__ bool fits16_dev(const int32_t* h) {
 struct DlArgs {
   // the batch's dp_wire32 ranges on the device
   const int32_t *pvo, *pco, *pao, *vid, *ckn, *arg;
-  const uint16_t *vnc, *cna;
+  const uint16_t *vnc, *cna, *vid16, *arg16;  // (16-bit string indices when ids16)
+  int32_t ids16;
   int32_t pbase, cbase, abase;  // absolute index of each range's first element
   int32_t nvars, ncons, nargs;
   int64_t n_strs;
@@ -211,12 +212,13 @@ __global__ void __launch_bounds__(DL_T) lower_kernel(DlArgs a) {
   if (lane == 0) {
     S.fb = 0;
     S.big = 0;
+    S.p16 = 0;
   }
   __syncthreads();
 
   // ---- 1. identifiers -> variables (lit_mapping.go:50-57) ----
   for (int i = lane; i < nv; i += DL_T) {
-    const int32_t sid = a.vid[v0 + i];
+    const int32_t sid = a.ids16 ? (int32_t)a.vid16[v0 + i] : a.vid[v0 + i];
     if (sid < 0 || (int64_t)sid >= a.n_strs) {
       S.fb = 1;  // malformed: the host reports it
       continue;
@@ -240,7 +242,7 @@ __global__ void __launch_bounds__(DL_T) lower_kernel(DlArgs a) {
   if (S.fb) return give_up();
   // arguments (LitOf, lit_mapping.go:81-88: an unknown one is an error the host reports)
   for (int j = lane; j < A; j += DL_T) {
-    const int32_t sid = a.arg[ab + j];
+    const int32_t sid = a.ids16 ? (int32_t)a.arg16[ab + j] : a.arg[ab + j];
     if (sid < 0 || (int64_t)sid >= a.n_strs) {
       S.fb = 1;
       continue;
@@ -275,18 +277,32 @@ __global__ void __launch_bounds__(DL_T) lower_kernel(DlArgs a) {
     uint32_t m = 0;
     if (!bad) {
       if (kind == DP_DEPENDENCY && ns > 0) {
-        // the row (~s, d1..dn); a list without a row (s among d) or a
-        // repeated candidate leaves P16D's implied lists: the host
-        uint64_t h = hmix(0x646570ULL, (uint64_t)vi);
-        for (int j = 0; j < ns && !bad; ++j) {
-          const int d = S.ca[a0 + j];
-          bad = d == vi;
-          for (int q = 0; q < j && !bad; ++q) bad = S.ca[a0 + q] == d;
-          h = hmix(h, (uint64_t)d);
+        if (ns + 1 > 255) {
+          bad = true;
+        } else if (S.ca[a0] == vi) {
+          // Or(~x_s, x_s) = T: a choice list with no identity and no row
+          // (lower.cpp: list_id -1); the lists are then not implied by the
+          // rows, so the record is DP_FMT_P16 with the lists explicit
+          m = meta(RT_SKIP, false, true, kind, 0);
+          S.p16 = 1;
+        } else {
+          // the row (~s, d1..dn), each candidate once; s among the later
+          // candidates folds the row to T while the identity stays (not a
+          // packed form: the host)
+          uint64_t h = hmix(0x646570ULL, (uint64_t)vi);
+          int len = 1;
+          for (int j = 0; j < ns && !bad; ++j) {
+            const int d = S.ca[a0 + j];
+            bad = d == vi;
+            bool rep = false;
+            for (int q = 0; q < j && !rep; ++q) rep = S.ca[a0 + q] == d;
+            len += rep ? 0 : 1;
+            h = hmix(h, (uint64_t)d);
+          }
+          if (len < ns + 1) S.p16 = 1;  // a repeated candidate: the row is shorter than its list
+          key = keyh(K_DEP, h);
+          m = meta(RT_CLAUSE, true, true, kind, len);
         }
-        if (ns + 1 > 255) bad = true;
-        key = keyh(K_DEP, h);
-        m = meta(RT_CLAUSE, true, true, kind, ns + 1);
       } else {
         switch (kind) {
           case DP_MANDATORY:
@@ -433,19 +449,21 @@ __global__ void __launch_bounds__(DL_T) lower_kernel(DlArgs a) {
     __syncthreads();  // the chunk's cid / clist before their readers
     bool far = false;
     if (isl) {
-      const int d = isf ? 0 : k - S.clist[first];
+      const int d = isf || s < 0 ? 0 : k - S.clist[first];
       far = d > 255;
       S.src[k] = (uint8_t)d;
     }
-    if (__ballot(far)) {
-      if (lane == 0) S.fb = 1;
-      break;
-    }
+    if (__ballot(far) && lane == 0) S.p16 = 1;  // a repeat too far back for a source byte
     if (isc) {
       S.clen[crow] = (uint8_t)rlen;
       if (kind == DP_DEPENDENCY && ns > 0) {
         S.clit[cat] = (int16_t)(2 * vi + 1);
-        for (int j = 0; j < ns; ++j) S.clit[cat + 1 + j] = (int16_t)(2 * S.ca[a0 + j]);
+        for (int j = 0, o = 1; j < ns; ++j) {
+          const int d = S.ca[a0 + j];
+          bool rep = false;
+          for (int q = 0; q < j && !rep; ++q) rep = S.ca[a0 + q] == d;
+          if (!rep) S.clit[cat + o++] = (int16_t)(2 * d);
+        }
       } else if (rlen == 1) {
         const uint64_t key = S.kkey[s] - 1ull;
         S.clit[cat] = (int16_t)(2 * (int)(key & 0x3fffffffULL) + ((key >> 60) == K_NEG ? 1 : 0));
@@ -500,10 +518,73 @@ __global__ void __launch_bounds__(DL_T) lower_kernel(DlArgs a) {
   h[DP_H_NKL] = nkl;
   h[DP_H_NCHL] = nchl;
   h[DP_H_WORDS] = DP_H_SIZE + (nc + 1) + ncl + nc + (nk + 1) + nkl + 2 * nk + (nv + 1) + (nch + 1) + nchl + na;
-  // one wavefront per problem (placement.hpp lds_image), P16D's tail bound
-  if (!fits16_dev(h) || (int64_t)dp::layout<dp::M_LDS>(h).lds_bytes > a.group_above ||
-      (int64_t)nc + nk + nch + (nid + 7) / 8 > DP_P16_TAIL_MAX)
-    return give_up();
+  // one wavefront per problem (placement.hpp lds_image)
+  if (!fits16_dev(h) || (int64_t)dp::layout<dp::M_LDS>(h).lds_bytes > a.group_above) return give_up();
+  auto put_header = [&]() {
+    for (int i = lane; i < DL_SLOT; i += DL_T) S.rec[i] = 0u;
+    __syncthreads();
+    if (lane < DP_H_SIZE) {
+      int32_t x = 0;
+#pragma unroll
+      for (int i = 0; i < DP_H_SIZE; ++i)
+        if (i == lane) x = h[i];
+      S.rec[lane] = (uint32_t)x;
+    }
+  };
+  auto put_out = [&](int padded) {
+    __syncthreads();
+    int32_t* out = a.slots + (int64_t)p * DL_SLOT;
+    for (int i = lane; i < padded; i += DL_T) out[i] = (int32_t)S.rec[i];
+    if (lane == 0) {
+      a.words[p] = padded;
+      a.nid[p] = nid;
+    }
+  };
+  if (S.p16) {
+    // DP_FMT_P16, the choice lists explicit (lower.cpp narrow_last -> pack16
+    // when the rows do not imply them)
+    bool bad16 = false;
+    for (int i = lane; i < nv; i += DL_T) {
+      int cnt = 0;
+      for (int c = S.vstart[i]; c < S.vstart[i + 1]; ++c) cnt += m_list(S.cmeta[c]) ? 1 : 0;
+      bad16 = bad16 || cnt > 255;
+      S.vcl[i] = (uint8_t)cnt;
+    }
+    const int tb = nc + nk + nv + nch + (nid + 7) / 8;
+    const int at = (2 * (ncl + nkl + nk + nchl + na) + 15) & ~15;
+    const int phys = DP_H_SIZE + (at + tb + 3) / 4, padded = (phys + 3) & ~3;
+    if (__ballot(bad16) || tb > DP_P16_TAIL_MAX || padded > DL_SLOT) return give_up();
+    h[DP_H_FMT] = DP_FMT_P16;
+    put_header();
+    uint16_t* const u = reinterpret_cast<uint16_t*>(S.rec + DP_H_SIZE);
+    uint8_t* const t = reinterpret_cast<uint8_t*>(S.rec + DP_H_SIZE) + at;
+    for (int j = lane; j < ncl; j += DL_T) u[j] = (uint16_t)S.clit[j];
+    for (int j = lane; j < nkl; j += DL_T) u[ncl + j] = (uint16_t)S.kv[j];
+    for (int j = lane; j < nk; j += DL_T) u[ncl + nkl + j] = (uint16_t)S.kb[j];
+    // the lists in list (= constraint) order, each its Dependency's candidates
+    int run = 0;
+    for (int c0 = 0; c0 < C; c0 += DL_T) {
+      const int c = c0 + lane;
+      const bool isl = c < C && m_list(S.cmeta[c]);
+      const int ns = isl ? S.castart[c + 1] - S.castart[c] : 0;
+      int tot;
+      const int ex = excl_scan(ns, tot);
+      if (isl) {
+        for (int j = 0; j < ns; ++j) u[ncl + nkl + nk + run + ex + j] = (uint16_t)S.ca[S.castart[c] + j];
+        t[nc + nk + nv + S.clist[c]] = (uint8_t)ns;
+      }
+      run += tot;
+    }
+    for (int j = lane; j < na; j += DL_T) u[ncl + nkl + nk + nchl + j] = (uint16_t)S.av[j];
+    for (int i = lane; i < nc; i += DL_T) t[i] = S.clen[i];
+    for (int i = lane; i < nk; i += DL_T) t[nc + i] = S.klen[i];
+    for (int i = lane; i < nv; i += DL_T) t[nc + nk + i] = S.vcl[i];
+    for (int b = lane; b < ((nid + 7) >> 3); b += DL_T)
+      t[nc + nk + nv + nch + b] = (uint8_t)(S.mask[b >> 2] >> ((b & 3) * 8));
+    put_out(padded);
+    return;
+  }
+  if ((int64_t)nc + nk + nch + (nid + 7) / 8 > DP_P16_TAIL_MAX) return give_up();  // P16D's tail bound
   const int f = (nv > 256 ? DP_P8_HI : 0) | (b1 ? DP_P8_B1 : 0) | (nib ? DP_P8_NIB : 0);
   const bool hi = f & DP_P8_HI;
   // dp_p8_layout_of
@@ -528,15 +609,7 @@ __global__ void __launch_bounds__(DL_T) lower_kernel(DlArgs a) {
   if (padded > DL_SLOT) return give_up();
   h[DP_H_FMT] = DP_FMT_P8D;
   h[DP_H_P8] = (int32_t)((uint32_t)f | ((uint32_t)bytes << 8));
-  for (int i = lane; i < padded; i += DL_T) S.rec[i] = 0u;
-  __syncthreads();
-  if (lane < DP_H_SIZE) {
-    int32_t x = 0;
-#pragma unroll
-    for (int i = 0; i < DP_H_SIZE; ++i)
-      if (i == lane) x = h[i];
-    S.rec[lane] = (uint32_t)x;
-  }
+  put_header();
   uint8_t* const rb = reinterpret_cast<uint8_t*>(S.rec + DP_H_SIZE);
   for (int j = lane; j < ncl; j += DL_T) rb[L_cvar + j] = (uint8_t)(S.clit[j] >> 1);
   for (int j = lane; j < nkl; j += DL_T) rb[L_kvar + j] = (uint8_t)S.kv[j];
@@ -586,13 +659,7 @@ __global__ void __launch_bounds__(DL_T) lower_kernel(DlArgs a) {
     q += __popcll(bm);
   }
   for (int b = lane; b < ((nid + 7) >> 3); b += DL_T) rb[L_mask + b] = (uint8_t)(S.mask[b >> 2] >> ((b & 3) * 8));
-  __syncthreads();
-  int32_t* out = a.slots + (int64_t)p * DL_SLOT;
-  for (int i = lane; i < padded; i += DL_T) out[i] = (int32_t)S.rec[i];
-  if (lane == 0) {
-    a.words[p] = padded;
-    a.nid[p] = nid;
-  }
+  put_out(padded);
 }
 
 // Record and identity offsets of problems [q0, q1): one workgroup, a
@@ -686,7 +753,7 @@ struct dp_dlower {
   static constexpr int kMaxPieces = 8;
   hipEvent_t ev[kMaxPieces] = {}, es[kMaxPieces] = {};
   DevBuf<int32_t> pvo, pco, pao, vid, ckn, arg, words, nid, slots, ivs, ics, rec, ivar, icon;
-  DevBuf<uint16_t> vnc, cna;
+  DevBuf<uint16_t> vnc, cna, vid16, arg16;
   DevBuf<int64_t> ro, io;
   int64_t* h_off = nullptr;  // page-locked: rec_off then ident_off
   size_t h_cap = 0;
@@ -695,6 +762,7 @@ struct dp_dlower {
   std::vector<int32_t> which;
   std::vector<int64_t> s_pvo, s_vid, s_vco, s_cao, s_arg;
   std::vector<int32_t> s_kind, s_cn;
+  std::vector<uint8_t> s_bad;
   std::mutex mu;  // one call at a time
   ~dp_dlower() {
     if (h_off) dp::pinned_free(h_off);
@@ -723,59 +791,82 @@ std::string hip_err(const char* what, hipError_t e) { return std::string("dp_low
 // from 0).  Inconsistent counts stay malformed (a negative identifier), so
 // the host lowering reports the batch as dp_lower_into does.
 void host_subwire(dp_dlower* d, const dp_wire32* w, dp_wire* sub) {
-  d->s_pvo.assign(1, 0);
-  d->s_vid.clear();
-  d->s_vco.clear();
-  d->s_kind.clear();
-  d->s_cn.clear();
-  d->s_cao.clear();
-  d->s_arg.clear();
-  int64_t nc = 0, na = 0;
-  for (const int32_t p : d->which) {
+  const size_t nw = d->which.size();
+  // sizes: a problem whose counts do not add up to its ranges becomes one
+  // malformed variable
+  std::vector<uint8_t>& bad = d->s_bad;
+  bad.assign(nw, 0);
+  int64_t tv = 0, tc = 0, ta = 0;
+  for (size_t i = 0; i < nw; ++i) {
+    const int32_t p = d->which[i];
     const int32_t v0 = w->prob_var_off[p], v1 = w->prob_var_off[p + 1];
-    int64_t c = w->prob_con_off[p], x = w->prob_arg_off[p];
-    const int64_t ce = w->prob_con_off[p + 1], xe = w->prob_arg_off[p + 1];
-    // the counts must add up to the problem's ranges
+    const int64_t c0 = w->prob_con_off[p], ce = w->prob_con_off[p + 1];
+    const int64_t x0 = w->prob_arg_off[p], xe = w->prob_arg_off[p + 1];
     int64_t sc = 0, sx = 0;
     for (int32_t v = v0; v < v1; ++v) sc += w->var_ncon[v];
-    bool bad = sc != ce - c;
-    if (!bad)
-      for (int64_t k = c; k < ce; ++k) sx += w->con_nargs[k];
-    bad = bad || sx != xe - x;
+    if (sc == ce - c0)
+      for (int64_t k = c0; k < ce; ++k) sx += w->con_nargs[k];
+    bad[i] = sc != ce - c0 || sx != xe - x0;
+    tv += bad[i] ? std::max(1, v1 - v0) : v1 - v0;
+    if (!bad[i]) {
+      tc += ce - c0;
+      ta += xe - x0;
+    }
+  }
+  d->s_pvo.resize(nw + 1);
+  d->s_vid.resize((size_t)tv + 1);
+  d->s_vco.resize((size_t)tv + 1);
+  d->s_kind.resize((size_t)tc + 1);
+  d->s_cn.resize((size_t)tc + 1);
+  d->s_cao.resize((size_t)tc + 1);
+  d->s_arg.resize((size_t)ta + 1);
+  int64_t* const pvo = d->s_pvo.data();
+  int64_t* const vid = d->s_vid.data();
+  int64_t* const vco = d->s_vco.data();
+  int32_t* const kind = d->s_kind.data();
+  int32_t* const cn = d->s_cn.data();
+  int64_t* const cao = d->s_cao.data();
+  int64_t* const arg = d->s_arg.data();
+  int64_t nv = 0, nc = 0, na = 0;
+  pvo[0] = 0;
+  for (size_t i = 0; i < nw; ++i) {
+    const int32_t p = d->which[i];
+    const int32_t v0 = w->prob_var_off[p], v1 = w->prob_var_off[p + 1];
+    if (bad[i]) {
+      for (int32_t v = v0; v < std::max(v1, v0 + 1); ++v) {
+        vid[nv] = -1;  // (a negative identifier: dp_lower_into reports the batch malformed)
+        vco[nv++] = nc;
+      }
+      pvo[i + 1] = nv;
+      continue;
+    }
+    int64_t c = w->prob_con_off[p];
+    const int64_t xb = w->prob_arg_off[p];
+    int64_t x = 0;
     for (int32_t v = v0; v < v1; ++v) {
-      d->s_vid.push_back(w->var_id[v]);
-      d->s_vco.push_back(nc);
-      for (int32_t k = 0; k < (int32_t)w->var_ncon[v] && !bad; ++k, ++c) {
+      vid[nv] = w->var_id16 ? (int64_t)w->var_id16[v] : (int64_t)w->var_id[v];
+      vco[nv++] = nc;
+      for (int32_t k = 0; k < (int32_t)w->var_ncon[v]; ++k, ++c) {
         const int32_t kn = w->con_kn[c];
-        d->s_kind.push_back(kn & 7);
-        d->s_cn.push_back(kn >> 3);
-        d->s_cao.push_back(na);
-        for (int32_t j = 0; j < (int32_t)w->con_nargs[c]; ++j, ++x, ++na) d->s_arg.push_back(w->con_arg[x]);
-        ++nc;
+        kind[nc] = kn & 7;
+        cn[nc] = kn >> 3;
+        cao[nc++] = na;
+        for (int32_t j = 0; j < (int32_t)w->con_nargs[c]; ++j, ++x)
+          arg[na++] = w->con_arg16 ? (int64_t)w->con_arg16[xb + x] : (int64_t)w->con_arg[xb + x];
       }
     }
-    if (bad && d->s_vid.size() > (size_t)d->s_pvo.back()) {
-      d->s_vid.back() = -1;
-    } else if (bad) {  // no variable to mark: one malformed variable
-      d->s_vid.push_back(-1);
-      d->s_vco.push_back(nc);
-    }
-    d->s_pvo.push_back((int64_t)d->s_vid.size());
+    pvo[i + 1] = nv;
   }
-  d->s_vco.push_back(nc);
-  d->s_cao.push_back(na);
-  d->s_kind.push_back(0);
-  d->s_cn.push_back(0);
-  d->s_arg.push_back(0);
-  d->s_vid.push_back(0);
-  sub->n_problems = (int32_t)d->which.size();
-  sub->prob_var_off = d->s_pvo.data();
-  sub->var_id = d->s_vid.data();
-  sub->var_con_off = d->s_vco.data();
-  sub->con_kind = d->s_kind.data();
-  sub->con_n = d->s_cn.data();
-  sub->con_arg_off = d->s_cao.data();
-  sub->con_arg = d->s_arg.data();
+  vco[nv] = nc;
+  cao[nc] = na;
+  sub->n_problems = (int32_t)nw;
+  sub->prob_var_off = pvo;
+  sub->var_id = vid;
+  sub->var_con_off = vco;
+  sub->con_kind = kind;
+  sub->con_n = cn;
+  sub->con_arg_off = cao;
+  sub->con_arg = arg;
   sub->n_strs = w->n_strs;
   sub->str_off = w->str_off;
   sub->str_bytes = w->str_bytes;
@@ -812,6 +903,17 @@ bool monotone(const int32_t* o, int32_t P) {
 }
 }  // namespace
 
+// The packing's stream at the highest priority: a queue of its own, so its
+// writes to host memory run beside the next piece's lowering instead of
+// behind it (DEPPY_DL_PACK_PRIORITY=0: a normal stream, A/B).
+hipError_t dl_pack_stream(hipStream_t* s) {
+  const char* e = std::getenv("DEPPY_DL_PACK_PRIORITY");
+  int lo = 0, hi = 0;
+  if ((e && *e == '0') || hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess)
+    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+  return hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi);
+}
+
 extern "C" {
 
 dp_dlower* dp_dlower_new(dp_ctx* ctx) {
@@ -824,7 +926,7 @@ dp_dlower* dp_dlower_new(dp_ctx* ctx) {
   d->dev = dev;
   bool ok = hipSetDevice(dev) == hipSuccess && hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking) == hipSuccess &&
             hipStreamCreateWithFlags(&d->cst, hipStreamNonBlocking) == hipSuccess &&
-            hipStreamCreateWithFlags(&d->pst, hipStreamNonBlocking) == hipSuccess;
+            dl_pack_stream(&d->pst) == hipSuccess;
   for (auto& e : d->ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
   for (auto& e : d->es) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
   if (!ok) {
@@ -852,8 +954,11 @@ int dp_lower_device(dp_dlower* d, const dp_wire32* w, int32_t flags, dp_lowered*
   if (!ours) return lower_on_host(w, flags, lw, d);
   const int32_t pv0 = w->prob_var_off[0], cb0 = w->prob_con_off[0], ab0 = w->prob_arg_off[0];
   const int32_t nvars = w->prob_var_off[P] - pv0, ncons = w->prob_con_off[P] - cb0, nargs = w->prob_arg_off[P] - ab0;
-  if ((nvars > 0 && (!w->var_id || !w->var_ncon)) || (ncons > 0 && (!w->con_kn || !w->con_nargs)) ||
-      (nargs > 0 && !w->con_arg)) {
+  const bool ids16 = w->var_id16 != nullptr;
+  if ((nvars > 0 && (!(ids16 ? (const void*)w->var_id16 : (const void*)w->var_id) || !w->var_ncon)) ||
+      (ncons > 0 && (!w->con_kn || !w->con_nargs)) ||
+      (nargs > 0 && !(ids16 ? (const void*)w->con_arg16 : (const void*)w->con_arg)) ||
+      (ids16 && w->n_strs > 65536)) {
     dp::set_global_error("dp_lower: malformed wire batch");
     return -1;
   }
@@ -861,11 +966,16 @@ int dp_lower_device(dp_dlower* d, const dp_wire32* w, int32_t flags, dp_lowered*
   DL_OK(d->pvo.need((size_t)P + 1));
   DL_OK(d->pco.need((size_t)P + 1));
   DL_OK(d->pao.need((size_t)P + 1));
-  DL_OK(d->vid.need((size_t)nvars + 1));
+  if (ids16) {
+    DL_OK(d->vid16.need((size_t)nvars + 1));
+    DL_OK(d->arg16.need((size_t)nargs + 1));
+  } else {
+    DL_OK(d->vid.need((size_t)nvars + 1));
+    DL_OK(d->arg.need((size_t)nargs + 1));
+  }
   DL_OK(d->vnc.need((size_t)nvars + 1));
   DL_OK(d->ckn.need((size_t)ncons + 1));
   DL_OK(d->cna.need((size_t)ncons + 1));
-  DL_OK(d->arg.need((size_t)nargs + 1));
   DL_OK(d->words.need((size_t)P));
   DL_OK(d->nid.need((size_t)P));
   DL_OK(d->slots.need((size_t)P * DL_SLOT));
@@ -899,6 +1009,9 @@ int dp_lower_device(dp_dlower* d, const dp_wire32* w, int32_t flags, dp_lowered*
   a.ckn = d->ckn.p;
   a.cna = d->cna.p;
   a.arg = d->arg.p;
+  a.vid16 = d->vid16.p;
+  a.arg16 = d->arg16.p;
+  a.ids16 = ids16 ? 1 : 0;
   a.pbase = pv0;
   a.cbase = cb0;
   a.abase = ab0;
@@ -941,19 +1054,32 @@ int dp_lower_device(dp_dlower* d, const dp_wire32* w, int32_t flags, dp_lowered*
     ticon = d->icon.p;
   }
   // pieces: the wire's copy of piece k+1 runs under the lowering and packing
-  // of piece k
+  // of piece k.  Every copy and its event is enqueued first: an event marker
+  // may share a hardware queue with the packing's stream, and one enqueued
+  // after pack(k) would hold lower(k+1) behind it.
   const int pieces = (int)std::min<int64_t>(dp_dlower::kMaxPieces, std::max<int64_t>(1, P / 2048));
+  auto piece = [&](int k, int32_t& q0, int32_t& q1) {
+    q0 = (int32_t)((int64_t)P * k / pieces);
+    q1 = (int32_t)((int64_t)P * (k + 1) / pieces);
+  };
   for (int k = 0; k < pieces; ++k) {
-    const int32_t q0 = (int32_t)((int64_t)P * k / pieces), q1 = (int32_t)((int64_t)P * (k + 1) / pieces);
+    int32_t q0, q1;
+    piece(k, q0, q1);
     const int32_t v0 = w->prob_var_off[q0], v1 = w->prob_var_off[q1];
     const int32_t c0 = w->prob_con_off[q0], c1 = w->prob_con_off[q1];
     const int32_t x0 = w->prob_arg_off[q0], x1 = w->prob_arg_off[q1];
-    DL_OK(h2d(d->vid.p + (v0 - pv0), w->var_id + v0, v1 - v0));
+    if (ids16) DL_OK(h2d(d->vid16.p + (v0 - pv0), w->var_id16 + v0, v1 - v0));
+    else DL_OK(h2d(d->vid.p + (v0 - pv0), w->var_id + v0, v1 - v0));
     DL_OK(h2d(d->vnc.p + (v0 - pv0), w->var_ncon + v0, v1 - v0));
     DL_OK(h2d(d->ckn.p + (c0 - cb0), w->con_kn + c0, c1 - c0));
     DL_OK(h2d(d->cna.p + (c0 - cb0), w->con_nargs + c0, c1 - c0));
-    DL_OK(h2d(d->arg.p + (x0 - ab0), w->con_arg + x0, x1 - x0));
+    if (ids16) DL_OK(h2d(d->arg16.p + (x0 - ab0), w->con_arg16 + x0, x1 - x0));
+    else DL_OK(h2d(d->arg.p + (x0 - ab0), w->con_arg + x0, x1 - x0));
     DL_OK(hipEventRecord(d->ev[k], cst));
+  }
+  for (int k = 0; k < pieces; ++k) {
+    int32_t q0, q1;
+    piece(k, q0, q1);
     DL_OK(hipStreamWaitEvent(st, d->ev[k], 0));
     if (q1 == q0) continue;
     a.p0 = q0;

@@ -369,7 +369,7 @@ int32_t dp_lowered_errors(const dp_lowered* lw, int32_t* err);
 /* ------------------------------------------------------------------------ */
 /* Lowering on the device: compact wire -> records                          */
 /* ------------------------------------------------------------------------ */
-/* The compact wire: dp_wire's content in about 45% of its bytes, the form
+/* The compact wire: dp_wire's content in about 30-45% of its bytes, the form
  * that crosses PCIe to the device lowering.  Always interned (equal string
  * index <=> equal identifier).  Per problem, absolute offsets of its first
  * variable, constraint and argument; per variable and per constraint a
@@ -382,12 +382,18 @@ typedef struct dp_wire32 {
   const int32_t* prob_var_off;  /* [n_problems+1] -> variables            */
   const int32_t* prob_con_off;  /* [n_problems+1] -> constraints          */
   const int32_t* prob_arg_off;  /* [n_problems+1] -> arguments            */
-  const int32_t* var_id;        /* [n_vars]  string index of Identifier    */
+  const int32_t* var_id;        /* [n_vars]  string index of Identifier
+                                   (NULL when var_id16 is given)          */
   const uint16_t* var_ncon;     /* [n_vars]  constraints of the variable   */
   const int32_t* con_kn;        /* [n_cons]  enum dp_kind | bound << 3 (the
                                    AtMost bound, arithmetic shift)        */
   const uint16_t* con_nargs;    /* [n_cons]  arguments of the constraint   */
-  const int32_t* con_arg;       /* [n_args]  string index                  */
+  const int32_t* con_arg;       /* [n_args]  string index (NULL when
+                                   con_arg16 is given)                    */
+  /* With at most 65,536 strings, the string indices in 16 bits instead
+   * (about a third fewer bytes on config 2); both or neither. */
+  const uint16_t* var_id16;     /* [n_vars]                                */
+  const uint16_t* con_arg16;    /* [n_args]                                */
   int64_t n_strs;
   const int64_t* str_off;       /* [n_strs+1] -> str_bytes (error texts)   */
   const char* str_bytes;

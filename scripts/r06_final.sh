@@ -15,14 +15,15 @@
 # Every GPU step has its own time limit; the first failure ends the call.
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/r06_final
+OUT=gpurun_out/${2:-r06_final}
 mkdir -p $OUT
 if [ "$1" = pmc ]; then
   bash scripts/pmc_fetch_split.sh "2 3 6 5 4" $OUT/fetch_split || exit 1
-  python3 - <<'PY' || exit 1
-import json
-d = json.load(open("gpurun_out/r06_final/fetch_split/fetch_split.json"))
-with open("gpurun_out/r06_final/pmc_traffic.jsonl", "w") as f:
+  OUT=$OUT python3 - <<'PY' || exit 1
+import json, os
+out = os.environ["OUT"]
+d = json.load(open(out + "/fetch_split/fetch_split.json"))
+with open(out + "/pmc_traffic.jsonl", "w") as f:
     for c, v in d.items():
         f.write(json.dumps({"config": int(c), "problems": v["problems"],
                             "hbm_bytes_per_dispatch": v["read_bytes_by_size"] + v["write_bytes"],
@@ -45,7 +46,7 @@ timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/s
 cat $OUT/smoke.log
 for c in 2 3 4 5 6; do
   timeout -k 10 400 python -u bench.py --gpus 1 --steps 20 --warmup 5 --config $c > $OUT/bench_c$c.json 2> $OUT/bench_c$c.err || exit 1
-  python3 -c "import json; d=json.loads(open('$OUT/bench_c$c.json').read().strip().splitlines()[-1]); print('config $c', d['value'], 'kernel_only', d['kernel_only']['res_per_s'], 'cpu', d['cpu_baseline']['value'], 'frac', d['roofline']['frac'], 't/a', d['roofline']['traffic_over_algorithmic'], 'lat', d['latency']['gpu_ms_median'], d['latency']['cpu_1thread_ms_median'], 'e2e', d.get('end_to_end', {}).get('res_per_s'), 'api', d.get('solve_batch_api', {}).get('res_per_s'), 'exact', d['verified_bit_exact_vs_oracle'])"
+  python3 -c "import json; d=json.loads(open('$OUT/bench_c$c.json').read().strip().splitlines()[-1]); print('config $c', d['value'], 'kernel_only', d['kernel_only']['res_per_s'], 'cpu', d['cpu_baseline']['value'], 'frac', d['roofline']['frac'], 't/a', d['roofline']['traffic_over_algorithmic'], 'lat', d['latency']['gpu_ms_median'], d['latency']['cpu_1thread_ms_median'], 'e2e', d.get('end_to_end', {}).get('res_per_s'), 'e2e_dev', d.get('end_to_end_device', {}).get('res_per_s'), 'dev_lower', d.get('end_to_end_device', {}).get('lowering_res_per_s'), 'api', d.get('solve_batch_api', {}).get('res_per_s'), 'exact', d['verified_bit_exact_vs_oracle'])"
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_c2 -o run -- \
   python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu --e2e-steps 0 > $OUT/trace_c2.json 2> $OUT/trace_c2.err || exit 1

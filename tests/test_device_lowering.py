@@ -34,7 +34,7 @@ def test_wire32_arrays_without_device():
     """The compact wire holds the 64-bit wire's content (numpy memory when
     no device gives page-locked memory) and refuses what does not fit."""
     w = wire_of(2, 30, 5)
-    w32 = _lib.Wire32Arrays(w)
+    w32 = _lib.Wire32Arrays(w, ids16=False)
     a, b = w32.a, w.a
     np.testing.assert_array_equal(a["prob_var_off"], b["prob_var_off"])
     np.testing.assert_array_equal(a["prob_con_off"], b["var_con_off"][b["prob_var_off"]])
@@ -48,11 +48,21 @@ def test_wire32_arrays_without_device():
     assert w32.nbytes() < 0.5 * sum(b[k].nbytes for k in ("prob_var_off", "var_id", "var_con_off", "con_kind",
                                                            "con_n", "con_arg_off", "con_arg"))
     s = w32.struct()
-    assert s.n_problems == 30 and s.n_strs == len(b["str_off"]) - 1
+    assert s.n_problems == 30 and s.n_strs == len(b["str_off"]) - 1 and not s.var_id16
+    # 16-bit string indices where the table allows them
+    w16 = _lib.Wire32Arrays(w)
+    assert w16.ids16 and "var_id" not in w16.a and w16.a["con_arg16"].dtype == np.uint16
+    np.testing.assert_array_equal(w16.a["var_id16"], b["var_id"])
+    np.testing.assert_array_equal(w16.a["con_arg16"], b["con_arg"])
+    assert w16.nbytes() < 0.75 * w32.nbytes()
+    s16 = w16.struct()
+    assert s16.var_id16 and s16.con_arg16 and not s16.var_id and not s16.con_arg
     big = _lib.WireArrays(**{k: v.copy() for k, v in b.items() if k != "str_bytes"},
                           str_bytes=b["str_bytes"][:-1].tobytes())
     big.a["con_arg"][0] = 1 << 40
     with pytest.raises(ValueError, match="32 bits"):
+        _lib.Wire32Arrays(big, ids16=False)
+    with pytest.raises(ValueError, match="16 bits"):
         _lib.Wire32Arrays(big)
     e = _lib.Lowered.empty()
     assert e.n == 0 and list(e.rec_off) == [0] and e._flags == 1 | 2 | 4
@@ -67,23 +77,25 @@ def dl():
     ctx.close()
 
 
-def lower_both(dl, wire, **kw):
+def lower_both(dl, wire, ids16=True, **kw):
     host = _lib.Lowered(wire, narrow=True, pinned=True, packed=True, **kw)
-    dev = dl.lower(_lib.Wire32Arrays(wire), _lib.Lowered.empty(pinned=True, **kw))
+    dev = dl.lower(_lib.Wire32Arrays(wire, ids16=ids16), _lib.Lowered.empty(pinned=True, **kw))
     return dev, host
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("config,n", [(2, 10000), (3, 20000), (6, 5000), (5, 300)])
-def test_device_records_equal_host(dl, config, n):
-    """Configs 2 and 3 lower entirely on the device; config 6's Dependencies
-    on their own subject (choice lists without rows: not P16D) and config 5's
-    multi-wave catalogs go to the host; every byte equals dp_lower_into's."""
-    dev, host = lower_both(dl, wire_of(config, n, 77))
+@pytest.mark.parametrize("config,n,ids16", [(2, 10000, True), (2, 3000, False), (3, 20000, True), (6, 5000, True),
+                                            (5, 300, True)])
+def test_device_records_equal_host(dl, config, n, ids16):
+    """Configs 2, 3 and 6 lower entirely on the device (config 6's
+    Dependencies on their own subject give DP_FMT_P16 records: choice lists
+    without rows); config 5's multi-wave catalogs go to the host; every byte
+    equals dp_lower_into's, with 16- and 32-bit string indices."""
+    dev, host = lower_both(dl, wire_of(config, n, 77), ids16=ids16)
     assert_same(dev, host)
     forms = np.unique(dev.rec[dev.rec_off[:-1] + 13], return_counts=True)
     print("config", config, "host-lowered", dl.host_count, "of", n, "forms", forms)
-    if config in (2, 3):
+    if config in (2, 3, 6):
         assert dl.host_count == 0
 
 
