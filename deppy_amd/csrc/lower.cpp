@@ -1519,6 +1519,8 @@ struct dp_lowered {
   std::unique_ptr<dp_lowered> sub;
   RecStore rec2;
   HostStore<int32_t> ivar2, icon2;
+  std::vector<int64_t> ro2, io2;
+  std::vector<int32_t> src2;
 };
 
 extern "C" {
@@ -1725,54 +1727,42 @@ int lowered_splice(dp_lowered* lw, const dp_wire* sub, int32_t flags, const int3
   lw->n_exact.store(t.n_exact.load());
   const int32_t P = lw->n;
   const bool pinned = lw->rec.pinned;
-  // new offsets in place, from the old lengths (a running copy of the old
-  // offsets: ro / io are rewritten from the front)
-  int64_t r = 0, d = 0, old_r = 0, old_d = 0;
-  int32_t j = 0;
+  // the new offsets (serial, O(P)), then the copies on the host pool
   std::vector<int64_t>& ro = lw->rec_off;
   std::vector<int64_t>& io = lw->ident_off;
-  // pass 1: sizes
+  std::vector<int64_t>& nro = lw->ro2;
+  std::vector<int64_t>& nio = lw->io2;
+  std::vector<int32_t>& src = lw->src2;  // problem -> its index in `which`, or -1
+  nro.resize((size_t)P + 1);
+  nio.resize((size_t)P + 1);
+  src.assign((size_t)P, -1);
+  nro[0] = nio[0] = 0;
+  for (int32_t j = 0; j < nw; ++j) src[(size_t)which[j]] = j;
   for (int32_t p = 0; p < P; ++p) {
-    if (j < nw && which[j] == p) {
-      r += t.rec_off[(size_t)j + 1] - t.rec_off[(size_t)j];
-      d += t.ident_off[(size_t)j + 1] - t.ident_off[(size_t)j];
-      ++j;
-    } else {
-      r += ro[(size_t)p + 1] - ro[(size_t)p];
-      d += io[(size_t)p + 1] - io[(size_t)p];
-    }
+    const int32_t j = src[(size_t)p];
+    nro[(size_t)p + 1] = nro[(size_t)p] + (j >= 0 ? t.rec_off[(size_t)j + 1] - t.rec_off[(size_t)j]
+                                                    : ro[(size_t)p + 1] - ro[(size_t)p]);
+    nio[(size_t)p + 1] = nio[(size_t)p] + (j >= 0 ? t.ident_off[(size_t)j + 1] - t.ident_off[(size_t)j]
+                                                    : io[(size_t)p + 1] - io[(size_t)p]);
   }
-  lw->rec2.resize((size_t)r, pinned);
-  lw->ivar2.resize((size_t)d, pinned);
-  lw->icon2.resize((size_t)d, pinned);
-  // pass 2: copies, then the offsets
-  r = d = 0;
-  j = 0;
-  for (int32_t p = 0; p < P; ++p) {
-    const int64_t ro1 = ro[(size_t)p + 1], io1 = io[(size_t)p + 1];
-    if (j < nw && which[j] == p) {
-      const int64_t a = t.rec_off[(size_t)j], b = t.rec_off[(size_t)j + 1];
-      std::copy(t.rec.p + a, t.rec.p + b, lw->rec2.p + r);
-      const int64_t ia = t.ident_off[(size_t)j], ib = t.ident_off[(size_t)j + 1];
-      std::copy(t.ivar.p + ia, t.ivar.p + ib, lw->ivar2.p + d);
-      std::copy(t.icon.p + ia, t.icon.p + ib, lw->icon2.p + d);
-      r += b - a;
-      d += ib - ia;
-      lw->err[(size_t)p] = t.err[(size_t)j];
-      lw->msg[(size_t)p] = t.msg[(size_t)j];
-      ++j;
-    } else {
-      std::copy(lw->rec.p + old_r, lw->rec.p + ro1, lw->rec2.p + r);
-      std::copy(lw->ivar.p + old_d, lw->ivar.p + io1, lw->ivar2.p + d);
-      std::copy(lw->icon.p + old_d, lw->icon.p + io1, lw->icon2.p + d);
-      r += ro1 - old_r;
-      d += io1 - old_d;
-    }
-    old_r = ro1;
-    old_d = io1;
-    ro[(size_t)p + 1] = r;
-    io[(size_t)p + 1] = d;
+  lw->rec2.resize((size_t)nro[(size_t)P], pinned);
+  lw->ivar2.resize((size_t)nio[(size_t)P], pinned);
+  lw->icon2.resize((size_t)nio[(size_t)P], pinned);
+  dp::host_pool().run(P, std::function<void(int64_t)>([&](int64_t p) {
+    const int32_t j = src[(size_t)p];
+    const int32_t* r = j >= 0 ? t.rec.p + t.rec_off[(size_t)j] : lw->rec.p + ro[(size_t)p];
+    const int32_t* iv = j >= 0 ? t.ivar.p + t.ident_off[(size_t)j] : lw->ivar.p + io[(size_t)p];
+    const int32_t* ic = j >= 0 ? t.icon.p + t.ident_off[(size_t)j] : lw->icon.p + io[(size_t)p];
+    std::copy(r, r + (nro[(size_t)p + 1] - nro[(size_t)p]), lw->rec2.p + nro[(size_t)p]);
+    std::copy(iv, iv + (nio[(size_t)p + 1] - nio[(size_t)p]), lw->ivar2.p + nio[(size_t)p]);
+    std::copy(ic, ic + (nio[(size_t)p + 1] - nio[(size_t)p]), lw->icon2.p + nio[(size_t)p]);
+  }), 256);
+  for (int32_t j = 0; j < nw; ++j) {
+    lw->err[(size_t)which[j]] = t.err[(size_t)j];
+    lw->msg[(size_t)which[j]] = t.msg[(size_t)j];
   }
+  ro.swap(nro);
+  io.swap(nio);
   lw->rec.swap(lw->rec2);
   lw->ivar.swap(lw->ivar2);
   lw->icon.swap(lw->icon2);

@@ -763,6 +763,7 @@ struct dp_dlower {
   std::vector<int64_t> s_pvo, s_vid, s_vco, s_cao, s_arg;
   std::vector<int32_t> s_kind, s_cn;
   std::vector<uint8_t> s_bad;
+  std::vector<int64_t> s_sz, s_off;
   std::mutex mu;  // one call at a time
   ~dp_dlower() {
     if (h_off) dp::pinned_free(h_off);
@@ -791,14 +792,16 @@ std::string hip_err(const char* what, hipError_t e) { return std::string("dp_low
 // from 0).  Inconsistent counts stay malformed (a negative identifier), so
 // the host lowering reports the batch as dp_lower_into does.
 void host_subwire(dp_dlower* d, const dp_wire32* w, dp_wire* sub) {
-  const size_t nw = d->which.size();
-  // sizes: a problem whose counts do not add up to its ranges becomes one
-  // malformed variable
+  const int64_t nw = (int64_t)d->which.size();
+  dp::Pool& pool = dp::host_pool();
+  // sizes (on the host pool): a problem whose counts do not add up to its
+  // ranges becomes one malformed variable
+  std::vector<int64_t>& sz = d->s_sz;  // [3 nw]: variables, constraints, arguments
+  sz.resize((size_t)(3 * nw + 3));
   std::vector<uint8_t>& bad = d->s_bad;
-  bad.assign(nw, 0);
-  int64_t tv = 0, tc = 0, ta = 0;
-  for (size_t i = 0; i < nw; ++i) {
-    const int32_t p = d->which[i];
+  bad.assign((size_t)nw, 0);
+  pool.run(nw, std::function<void(int64_t)>([&](int64_t i) {
+    const int32_t p = d->which[(size_t)i];
     const int32_t v0 = w->prob_var_off[p], v1 = w->prob_var_off[p + 1];
     const int64_t c0 = w->prob_con_off[p], ce = w->prob_con_off[p + 1];
     const int64_t x0 = w->prob_arg_off[p], xe = w->prob_arg_off[p + 1];
@@ -806,14 +809,20 @@ void host_subwire(dp_dlower* d, const dp_wire32* w, dp_wire* sub) {
     for (int32_t v = v0; v < v1; ++v) sc += w->var_ncon[v];
     if (sc == ce - c0)
       for (int64_t k = c0; k < ce; ++k) sx += w->con_nargs[k];
-    bad[i] = sc != ce - c0 || sx != xe - x0;
-    tv += bad[i] ? std::max(1, v1 - v0) : v1 - v0;
-    if (!bad[i]) {
-      tc += ce - c0;
-      ta += xe - x0;
-    }
-  }
-  d->s_pvo.resize(nw + 1);
+    const bool b = sc != ce - c0 || sx != xe - x0;
+    bad[(size_t)i] = b;
+    sz[(size_t)(3 * i)] = b ? std::max(1, v1 - v0) : v1 - v0;
+    sz[(size_t)(3 * i + 1)] = b ? 0 : ce - c0;
+    sz[(size_t)(3 * i + 2)] = b ? 0 : xe - x0;
+  }), 64);
+  // offsets (serial), then the arrays (on the pool)
+  std::vector<int64_t>& off = d->s_off;  // [3 (nw+1)]
+  off.resize((size_t)(3 * nw + 3));
+  off[0] = off[1] = off[2] = 0;
+  for (int64_t i = 0; i < nw; ++i)
+    for (int q = 0; q < 3; ++q) off[(size_t)(3 * (i + 1) + q)] = off[(size_t)(3 * i + q)] + sz[(size_t)(3 * i + q)];
+  const int64_t tv = off[(size_t)(3 * nw)], tc = off[(size_t)(3 * nw + 1)], ta = off[(size_t)(3 * nw + 2)];
+  d->s_pvo.resize((size_t)nw + 1);
   d->s_vid.resize((size_t)tv + 1);
   d->s_vco.resize((size_t)tv + 1);
   d->s_kind.resize((size_t)tc + 1);
@@ -827,18 +836,17 @@ void host_subwire(dp_dlower* d, const dp_wire32* w, dp_wire* sub) {
   int32_t* const cn = d->s_cn.data();
   int64_t* const cao = d->s_cao.data();
   int64_t* const arg = d->s_arg.data();
-  int64_t nv = 0, nc = 0, na = 0;
-  pvo[0] = 0;
-  for (size_t i = 0; i < nw; ++i) {
-    const int32_t p = d->which[i];
+  for (int64_t i = 0; i <= nw; ++i) pvo[i] = off[(size_t)(3 * i)];
+  pool.run(nw, std::function<void(int64_t)>([&](int64_t i) {
+    const int32_t p = d->which[(size_t)i];
     const int32_t v0 = w->prob_var_off[p], v1 = w->prob_var_off[p + 1];
-    if (bad[i]) {
+    int64_t nv = off[(size_t)(3 * i)], nc = off[(size_t)(3 * i + 1)], na = off[(size_t)(3 * i + 2)];
+    if (bad[(size_t)i]) {
       for (int32_t v = v0; v < std::max(v1, v0 + 1); ++v) {
         vid[nv] = -1;  // (a negative identifier: dp_lower_into reports the batch malformed)
         vco[nv++] = nc;
       }
-      pvo[i + 1] = nv;
-      continue;
+      return;
     }
     int64_t c = w->prob_con_off[p];
     const int64_t xb = w->prob_arg_off[p];
@@ -855,10 +863,9 @@ void host_subwire(dp_dlower* d, const dp_wire32* w, dp_wire* sub) {
           arg[na++] = w->con_arg16 ? (int64_t)w->con_arg16[xb + x] : (int64_t)w->con_arg[xb + x];
       }
     }
-    pvo[i + 1] = nv;
-  }
-  vco[nv] = nc;
-  cao[nc] = na;
+  }), 64);
+  vco[tv] = tc;
+  cao[tc] = ta;
   sub->n_problems = (int32_t)nw;
   sub->prob_var_off = pvo;
   sub->var_id = vid;
@@ -952,6 +959,19 @@ int dp_lower_device(dp_dlower* d, const dp_wire32* w, int32_t flags, dp_lowered*
   const bool ours = (flags & (DP_LOWER_NARROW | DP_LOWER_PACKED)) == (DP_LOWER_NARROW | DP_LOWER_PACKED) &&
                     !(flags & DP_LOWER_NO_P8) && dp::ldsg_env() != dp::LDSG_ALWAYS && P > 0;
   if (!ours) return lower_on_host(w, flags, lw, d);
+  // problems past the kernel's sizes are lowered on the host: when they
+  // hold most of the batch's arguments, the whole batch is (a device pass and
+  // a splice would only add to the host's work)
+  {
+    int64_t fit_args = 0, all_args = (int64_t)w->prob_arg_off[P] - w->prob_arg_off[0];
+    for (int32_t p = 0; p < P; ++p) {
+      const int32_t nv = w->prob_var_off[p + 1] - w->prob_var_off[p];
+      const int32_t nc = w->prob_con_off[p + 1] - w->prob_con_off[p];
+      const int32_t na = w->prob_arg_off[p + 1] - w->prob_arg_off[p];
+      if (nv >= 1 && nv <= DL_NV && nc <= DL_C && na <= DL_A) fit_args += na + 1;
+    }
+    if (2 * fit_args < all_args + P) return lower_on_host(w, flags, lw, d);
+  }
   const int32_t pv0 = w->prob_var_off[0], cb0 = w->prob_con_off[0], ab0 = w->prob_arg_off[0];
   const int32_t nvars = w->prob_var_off[P] - pv0, ncons = w->prob_con_off[P] - cb0, nargs = w->prob_arg_off[P] - ab0;
   const bool ids16 = w->var_id16 != nullptr;
