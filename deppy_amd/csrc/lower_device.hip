@@ -794,6 +794,8 @@ std::string hip_err(const char* what, hipError_t e) { return std::string("dp_low
 void host_subwire(dp_dlower* d, const dp_wire32* w, dp_wire* sub) {
   const int64_t nw = (int64_t)d->which.size();
   dp::Pool& pool = dp::host_pool();
+  // (a few large problems still spread over the pool: config 4's catalogs)
+  const int64_t blk = std::max<int64_t>(1, std::min<int64_t>(64, nw / (4 * (int64_t)pool.size())));
   // sizes (on the host pool): a problem whose counts do not add up to its
   // ranges becomes one malformed variable
   std::vector<int64_t>& sz = d->s_sz;  // [3 nw]: variables, constraints, arguments
@@ -814,7 +816,7 @@ void host_subwire(dp_dlower* d, const dp_wire32* w, dp_wire* sub) {
     sz[(size_t)(3 * i)] = b ? std::max(1, v1 - v0) : v1 - v0;
     sz[(size_t)(3 * i + 1)] = b ? 0 : ce - c0;
     sz[(size_t)(3 * i + 2)] = b ? 0 : xe - x0;
-  }), 64);
+  }), blk);
   // offsets (serial), then the arrays (on the pool)
   std::vector<int64_t>& off = d->s_off;  // [3 (nw+1)]
   off.resize((size_t)(3 * nw + 3));
@@ -863,7 +865,7 @@ void host_subwire(dp_dlower* d, const dp_wire32* w, dp_wire* sub) {
           arg[na++] = w->con_arg16 ? (int64_t)w->con_arg16[xb + x] : (int64_t)w->con_arg[xb + x];
       }
     }
-  }), 64);
+  }), blk);
   vco[tv] = tc;
   cao[tc] = ta;
   sub->n_problems = (int32_t)nw;
