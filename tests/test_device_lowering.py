@@ -4,6 +4,8 @@ dp_lowered as dp_lower_into(NARROW | PACKED) on the host, byte for byte --
 records, offsets, identity owners (the reported AppliedConstraint,
 lit_mapping.go:69-72), errors and their texts -- with the problems the kernel
 does not take lowered on the host and spliced in."""
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -164,5 +166,35 @@ def test_device_lowering_malformed_wire(dl):
     with pytest.raises(ValueError, match="malformed"):
         dl.lower(_lib.Wire32Arrays(bad))
     # the object still works after a failed call
+    dev, host = lower_both(dl, wire)
+    assert_same(dev, host)
+
+
+def test_device_lowering_entry_points_refuse_null():
+    """Without a context the entry points fail cleanly (no device touched):
+    dp_dlower_new(NULL) gives NULL with a reason, dp_lower_device(NULL, ...)
+    -1."""
+    L = _lib.lib()
+    assert not L.dp_dlower_new(None)
+    assert b"no context" in L.dp_last_global_error()
+    w32 = _lib.Wire32Arrays(wire_of(2, 3, 1))
+    ws = w32.struct()
+    lw = _lib.Lowered.empty()
+    assert L.dp_lower_device(None, ctypes.byref(ws), lw._flags, lw._owner.h) == -1
+    assert b"malformed" in L.dp_last_global_error()
+
+
+@pytest.mark.gpu
+def test_device_lowering_inconsistent_counts(dl):
+    """The compact wire's counts must add up to each problem's ranges: a
+    variable claiming one constraint more (or a constraint one argument more)
+    makes the batch malformed, as dp_lower_into reports a malformed wire;
+    the kernel leaves such a problem to the host, which reports it."""
+    wire = wire_of(2, 200, 6)
+    for key in ("var_ncon", "con_nargs"):
+        w32 = _lib.Wire32Arrays(wire)
+        w32.a[key][5] += 1
+        with pytest.raises(ValueError, match="malformed"):
+            dl.lower(w32)
     dev, host = lower_both(dl, wire)
     assert_same(dev, host)
