@@ -427,26 +427,39 @@ class Lowered:
         self._fetch()
         return self
 
+    def _cview(self, key, ptr, n: int, ctype, dtype) -> np.ndarray:
+        """_view, reused while the storage stays where it is (a serving loop
+        lowers batch after batch into the same storage: no new views)."""
+        addr = ctypes.cast(ptr, ctypes.c_void_p).value if n else 0
+        vc = self.__dict__.setdefault("_vc", {})
+        c = vc.get(key)
+        if c is not None and c[0] == addr and c[1] == n:
+            return c[2]
+        v = _view(self._owner, ptr, n, ctype, dtype)
+        vc[key] = (addr, n, v)
+        return v
+
     def _fetch(self):
-        L, h, o = lib(), self._owner.h, self._owner
+        L, h = lib(), self._owner.h
         P = L.dp_lowered_num_problems(h)
         self.n = P
         self.n_exact = int(L.dp_lowered_exact_count(h))
         self.pinned = bool(L.dp_lowered_pinned(h))
-        self.rec_off = _view(o, L.dp_lowered_rec_off(h), P + 1, ctypes.c_int64, np.int64)
-        self.rec = _view(o, L.dp_lowered_rec(h), int(self.rec_off[-1]), ctypes.c_int32, np.int32)
-        self.ident_off = _view(o, L.dp_lowered_ident_off(h), P + 1, ctypes.c_int64, np.int64)
+        self.rec_off = self._cview("rec_off", L.dp_lowered_rec_off(h), P + 1, ctypes.c_int64, np.int64)
+        self.rec = self._cview("rec", L.dp_lowered_rec(h), int(self.rec_off[-1]), ctypes.c_int32, np.int32)
+        self.ident_off = self._cview("ident_off", L.dp_lowered_ident_off(h), P + 1, ctypes.c_int64, np.int64)
         ni = int(self.ident_off[-1])
-        self.ident_var = _view(o, L.dp_lowered_ident_var(h), ni, ctypes.c_int32, np.int32)
-        self.ident_con = _view(o, L.dp_lowered_ident_con(h), ni, ctypes.c_int32, np.int32)
-        self.err = np.zeros(max(P, 1), np.int32)
-        self.msg = [None] * P
+        self.ident_var = self._cview("ident_var", L.dp_lowered_ident_var(h), ni, ctypes.c_int32, np.int32)
+        self.ident_con = self._cview("ident_con", L.dp_lowered_ident_con(h), ni, ctypes.c_int32, np.int32)
+        err = np.zeros(max(P, 1), np.int32)
+        msg = [None] * P
         m = ctypes.c_char_p()
-        if L.dp_lowered_errors(h, _p(self.err, c_i32p)):
-            for p in np.nonzero(self.err[:P])[0]:
+        if L.dp_lowered_errors(h, _p(err, c_i32p)):
+            for p in np.nonzero(err[:P])[0]:
                 L.dp_lowered_error(h, int(p), ctypes.byref(m))
-                self.msg[p] = m.value.decode("utf-8", "surrogateescape")
-        self.err = self.err[:P]
+                msg[p] = m.value.decode("utf-8", "surrogateescape")
+        self.err = err[:P]
+        self.msg = msg
 
     def record(self, p: int) -> np.ndarray:
         return self.rec[self.rec_off[p]:self.rec_off[p + 1]]
@@ -550,6 +563,9 @@ class Wire32Arrays:
         return int(sum(self.a[k].nbytes for k, _ in self.arrays()))
 
     def struct(self) -> Wire32:
+        """The dp_wire32 over these arrays (built once: they do not move)."""
+        if getattr(self, "_struct", None) is not None:
+            return self._struct
         a = self.a
         w = Wire32()
         w.n_problems = len(a["prob_var_off"]) - 1
@@ -561,6 +577,7 @@ class Wire32Arrays:
         w.n_strs = len(a["str_off"]) - 1
         w.str_off = _p(a["str_off"], c_i64p)
         w.str_bytes = ctypes.cast(a["str_bytes"].ctypes.data, ctypes.c_char_p)
+        self._struct = w
         return w
 
 
