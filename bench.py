@@ -189,6 +189,19 @@ def end_to_end_device(ctx, wa, lw_host, n, steps, depth=2):
     return out
 
 
+def solve_batch_api_device(ctx, wa, n, steps):
+    """solve_batch_api from the compact wire: deppy_amd.sat.solve_wire on a
+    _lib.Wire32Arrays lowers on the GPU (dp_lower_device), then dp_solve;
+    one batch at a time."""
+    from deppy_amd import _lib, sat
+    w32 = _lib.Wire32Arrays(wa)
+    sat.solve_wire(w32, ctx)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        sat.solve_wire(w32, ctx)
+    return n * steps / (time.perf_counter() - t0)
+
+
 def solve_batch_api(ctx, wa, n, steps):
     """The shipped API path, one batch at a time: deppy_amd.sat.solve_wire (the
     wire -> results half of SolveBatch, what the cgo shim does): dp_lower_into
@@ -513,6 +526,10 @@ def main():
             "note": "deppy_amd.sat.solve_wire (SolveBatch from the wire format to host results, as the cgo "
                     "shim calls the library): dp_lower_into NARROW|PACKED|PINNED into reused storage + dp_solve, "
                     "one batch at a time; not value"}
+        line["solve_batch_api"]["device_lowering_res_per_s"] = round(
+            solve_batch_api_device(ctx, wa, n, max(2, args.e2e_steps // 2)), 1)
+        line["solve_batch_api"]["device_lowering_note"] = (
+            "the same from the compact wire (sat.solve_wire on a Wire32Arrays: dp_lower_device + dp_solve)")
 
     if args.kernel_steps > 0:
         # the solve kernel alone, records resident in HBM (dp_upload): serial

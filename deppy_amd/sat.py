@@ -470,6 +470,8 @@ def release_lowering() -> None:
     """Free this thread's reused lowering storage (page-locked memory)."""
     _lowering.lw = None
     _lowering.pipe = None
+    _lowering.dlw = None
+    _lowering.dl = None
 
 
 # With SUB_BATCH > 0, a batch of at least 2 * SUB_BATCH problems is lowered
@@ -485,7 +487,22 @@ def release_lowering() -> None:
 SUB_BATCH = int(os.environ.get("DEPPY_SUB_BATCH", "0"))
 
 
-def solve_wire(wire: _lib.WireArrays, context: Optional[_lib.Context] = None, trace_cap: int = 0):
+def _device_lowered(w32: "_lib.Wire32Arrays", ctx: _lib.Context) -> _lib.Lowered:
+    """dp_lower_device into this thread's reused storage (its own from the
+    host path's), with a device lowering per context kept per thread."""
+    dls = getattr(_lowering, "dl", None)
+    if dls is None:
+        dls = _lowering.dl = {}
+    dl = dls.get(id(ctx))
+    if dl is None or dl.ctx is not ctx:
+        dl = dls[id(ctx)] = _lib.DeviceLowerer(ctx)
+    lw = getattr(_lowering, "dlw", None)
+    if lw is None:
+        lw = _lowering.dlw = _lib.Lowered.empty(**LOWER_FLAGS)
+    return dl.lower(w32, lw)
+
+
+def solve_wire(wire, context: Optional[_lib.Context] = None, trace_cap: int = 0):
     """The shipped path of SolveBatch from the wire format to host results:
     dp_lower_into(NARROW | PACKED | PINNED) into this thread's reused,
     page-locked storage, then dp_solve on the batch as it lies (dp_submit +
@@ -496,7 +513,15 @@ def solve_wire(wire: _lib.WireArrays, context: Optional[_lib.Context] = None, tr
     large untraced batch goes through _solve_pipelined (the same records,
     lowered and solved in overlapping sub-batches).
     Returns (lowered, results); both stay valid until this thread's next
-    call.  trace_cap > 0 solves through the traced device-resident form."""
+    call.  trace_cap > 0 solves through the traced device-resident form.
+    A compact wire (_lib.Wire32Arrays, include/deppy_hip.h dp_wire32) is
+    lowered on the GPU instead (dp_lower_device, the same records)."""
+    if isinstance(wire, _lib.Wire32Arrays):
+        with (contextlib.nullcontext() if context else _ctx_lock):
+            ctx = context or device_context()
+            lw = _device_lowered(wire, ctx)
+            res = ctx.solve(lw.rec_off, lw.rec, trace_cap)
+        return lw, res
     if trace_cap <= 0 and SUB_BATCH > 0 and wire.n_problems >= 2 * SUB_BATCH:
         return _solve_pipelined(wire, context)
     lw = _reused_lowered(wire)

@@ -198,3 +198,18 @@ def test_device_lowering_inconsistent_counts(dl):
             dl.lower(w32)
     dev, host = lower_both(dl, wire)
     assert_same(dev, host)
+
+
+@pytest.mark.gpu
+def test_solve_wire_takes_the_compact_wire(dl):
+    """sat.solve_wire (SolveBatch's wire-to-results half) lowers a compact
+    wire on the GPU: the same records and results as from the 64-bit wire."""
+    wire = wire_of(2, 3000, 12)
+    lw_h, rh = sat.solve_wire(wire, dl.ctx)
+    rec_h, off_h = lw_h.rec.copy(), lw_h.rec_off.copy()
+    rh = {k: v.copy() for k, v in rh.items()}
+    lw_d, rd = sat.solve_wire(_lib.Wire32Arrays(wire), dl.ctx)
+    np.testing.assert_array_equal(lw_d.rec_off, off_h)
+    np.testing.assert_array_equal(lw_d.rec, rec_h)
+    for k in ("status", "flags", "installed", "core_len", "core", "steps"):
+        np.testing.assert_array_equal(rd[k], rh[k])
