@@ -519,15 +519,22 @@ def main():
             "note": "wire format -> dp_lower_into -> dp_submit/dp_job_wait -> results, 2 batches in flight "
                     "(lowering of batch i+1 overlaps the solve of batch i); what BenchmarkSolve times "
                     "(NewSolver(WithInput)+Solve, bench_test.go:66-77); not value"}
-        line["end_to_end_device"] = end_to_end_device(ctx, wa, lw, n, args.e2e_steps)
+        try:  # (a leg beside value: its failure must not cost the line)
+            line["end_to_end_device"] = end_to_end_device(ctx, wa, lw, n, args.e2e_steps)
+        except Exception as e:  # noqa: BLE001
+            line["end_to_end_device"] = {"res_per_s": None, "error": repr(e)}
         line["solve_batch_api"] = {
             "res_per_s": round(solve_batch_api(ctx, wa, n, max(2, args.e2e_steps // 2)), 1),
             "steps": max(2, args.e2e_steps // 2),
             "note": "deppy_amd.sat.solve_wire (SolveBatch from the wire format to host results, as the cgo "
                     "shim calls the library): dp_lower_into NARROW|PACKED|PINNED into reused storage + dp_solve, "
                     "one batch at a time; not value"}
-        line["solve_batch_api"]["device_lowering_res_per_s"] = round(
-            solve_batch_api_device(ctx, wa, n, max(2, args.e2e_steps // 2)), 1)
+        try:
+            line["solve_batch_api"]["device_lowering_res_per_s"] = round(
+                solve_batch_api_device(ctx, wa, n, max(2, args.e2e_steps // 2)), 1)
+        except Exception as e:  # noqa: BLE001
+            line["solve_batch_api"]["device_lowering_res_per_s"] = None
+            line["solve_batch_api"]["device_lowering_error"] = repr(e)
         line["solve_batch_api"]["device_lowering_note"] = (
             "the same from the compact wire (sat.solve_wire on a Wire32Arrays: dp_lower_device + dp_solve)")
 
